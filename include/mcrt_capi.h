@@ -1,0 +1,339 @@
+/*
+ * mcrt_capi.h -- C ABI of the MI355X-native Monte-Carlo path-tracing core.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (compix/Monte-Carlo-Raytracer).  Every entry point names the reference
+ * interface it replaces (paths relative to the reference repo root):
+ *
+ *   RR  = third_party/RadeonRays/RadeonRays
+ *   APP = source/application/PathTracer
+ *   KRN = assets/kernels
+ *
+ * Plain C: opaque handles, plain pointers and sizes, no C++ or torch types.
+ * Every call returns an mcrt_status; mcrt_last_error() gives the message
+ * (the reference threw std::exception / Calc::Exception and the passes caught
+ * them: APP/raytracing/renderPasses/RTPathTracingPass.cpp:89-104).
+ *
+ * All structs below are byte-identical to the OpenCL device structs of
+ * KRN/kernel_data.h (sizes/offsets: SURVEY.md Appendix B), so the scene
+ * arrays the reference's RTScene builds (APP/raytracing/scene/RTScene.cpp)
+ * can be passed unchanged.
+ */
+#ifndef MCRT_CAPI_H
+#define MCRT_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCRT_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------ */
+/* Status codes                                                             */
+/* ------------------------------------------------------------------------ */
+typedef int mcrt_status;
+#define MCRT_OK                   0
+#define MCRT_ERROR_INVALID_ARG    1
+#define MCRT_ERROR_OUT_OF_MEMORY  2
+#define MCRT_ERROR_DEVICE         3
+#define MCRT_ERROR_NOT_READY      4  /* e.g. trace before mcrt_accel_build */
+#define MCRT_ERROR_NO_DEVICE      5
+
+/* ------------------------------------------------------------------------ */
+/* Device-layout value types (OpenCL float3 = 16 B, float2 = 8 B)           */
+/* ------------------------------------------------------------------------ */
+typedef struct __attribute__((aligned(16))) { float x, y, z, w; } mcrt_float4;
+typedef mcrt_float4 mcrt_float3;                      /* OpenCL float3: 16 B */
+typedef struct __attribute__((aligned(8))) { float x, y; } mcrt_float2;
+typedef struct __attribute__((aligned(16))) { mcrt_float4 m0, m1, m2, m3; } mcrt_mat4; /* row major, KRN/matrix.cl:4-11 */
+
+/* RTShape, KRN/kernel_data.h:36-52 (160 B) */
+typedef struct __attribute__((aligned(16))) {
+    mcrt_mat4 toWorldTransform;
+    mcrt_mat4 toWorldInverseTranspose;
+    uint32_t  startIdx;
+    uint32_t  startVertex;
+    uint32_t  numTriangles;
+    int32_t   materialId;   /* -1 = none */
+    int32_t   lightID;      /* -1 = not an emitter */
+    float     area;
+    int32_t   pad[2];
+} mcrt_shape;
+
+/* RTMaterial (uber material), KRN/kernel_data.h:87-113 (128 B) */
+typedef struct __attribute__((aligned(16))) {
+    mcrt_float3 uber_kd;
+    mcrt_float3 uber_ks;
+    mcrt_float3 uber_kr;
+    mcrt_float4 uber_kt;        /* w >= 0.5: glossy, else perfect specular transmission */
+    mcrt_float3 uber_opacity;
+    mcrt_float2 uber_roughness;
+    float       uber_eta;
+    int32_t     type;           /* 0 = RT_UBER_MATERIAL */
+    int32_t     uber_normalMapId;
+    int32_t     uber_diffuseTexId;
+    int32_t     uber_glossyTexId;
+    int32_t     uber_specReflectionTexId;
+    int32_t     uber_transmissionTexId;
+    int32_t     uber_opacityTexId;
+    int32_t     uber_roughnessTexId;
+    int32_t     uber_iorTexId;
+} mcrt_material;
+
+/* RTLight, KRN/kernel_data.h:137-152 (80 B) */
+#define MCRT_DIRECTIONAL_LIGHT        0
+#define MCRT_POINT_LIGHT              1
+#define MCRT_DISK_AREA_LIGHT          2
+#define MCRT_TRIANGLE_MESH_AREA_LIGHT 3
+#define MCRT_LIGHT_FLAG_DELTA_POSITION  (1 << 1)
+#define MCRT_LIGHT_FLAG_DELTA_DIRECTION (1 << 2)
+#define MCRT_LIGHT_FLAG_AREA            (1 << 3)
+typedef struct __attribute__((aligned(16))) {
+    mcrt_float3 d;
+    mcrt_float3 p;
+    mcrt_float3 intensity;
+    float   radius;
+    float   area;
+    float   choicePdf;
+    int32_t shapeId;
+    int32_t type;
+    int32_t flags;
+    int32_t pad[2];
+} mcrt_light;
+
+/* RTPinholeCamera, KRN/kernel_data.h:246-264 (176 B) */
+typedef struct __attribute__((aligned(16))) {
+    mcrt_mat4   worldToClip;
+    mcrt_float3 r00, r10, r11, r01;   /* corner directions, APP/.../RTPrimaryRaysPass.cpp:96-99 */
+    mcrt_float3 pos;
+    mcrt_float3 direction;
+    uint32_t    width;
+    uint32_t    height;
+    float       area;
+    int32_t     padding;
+} mcrt_camera;
+
+/* TextureDesc2D, KRN/kernel_data.h:317-326 (16 B); texels are RGBA8 */
+typedef struct {
+    uint16_t width, height, numMipLevels, format, wrap, pad;
+    uint32_t memOffset;       /* byte offset into tex_data */
+} mcrt_texture_desc;
+
+/* RadeonRays ray, RR/src/kernels/CL/common.cl:53-60 and KRN/kernel_data.h:407-417 (48 B) */
+typedef struct __attribute__((aligned(16))) {
+    mcrt_float4 o;            /* xyz origin, w = max range */
+    mcrt_float4 d;            /* xyz direction, w = time (unused) */
+    int32_t extra[2];         /* [0] = mask (-1: all shapes), [1] = active flag (0: inactive) */
+    int32_t doBackfaceCulling;
+    int32_t padding;
+} mcrt_ray;
+
+/* RadeonRays Intersection, RR/src/kernels/CL/common.cl:63-70 (32 B) */
+typedef struct __attribute__((aligned(16))) {
+    int32_t shapeid;          /* -1 on miss */
+    int32_t primid;           /* -1 on miss */
+    int32_t padding[2];
+    mcrt_float4 uvwt;         /* (u, v, 0, t); left untouched on miss */
+} mcrt_intersection;
+
+/* RTFilterProperties with the DEVICE layout (56 B): KRN/kernel_data.h:63-80.
+ * The reference host struct is 48 B (RadeonRays::float2 is 4-byte aligned),
+ * so the reference device read shifted fields; this ABI
+ * uses the explicit, correctly laid-out device struct. */
+#define MCRT_BOX_FILTER          0
+#define MCRT_TRIANGLE_FILTER     1
+#define MCRT_GAUSSIAN_FILTER     2
+#define MCRT_MITCHELL_FILTER     3
+#define MCRT_LANCZOS_SINC_FILTER 4
+typedef struct __attribute__((aligned(8))) {
+    int32_t     filterType;
+    int32_t     _align0;
+    mcrt_float2 radius;
+    float       mitchellB;
+    float       mitchellC;
+    float       lanczosSincTau;
+    float       gaussianAlpha;
+    float       gaussianExpX;
+    float       gaussianExpY;
+    mcrt_float2 pixelOffset;
+    float       pad;
+    int32_t     _align1;
+} mcrt_filter;
+
+/* ------------------------------------------------------------------------ */
+/* Scene description = the 15 SCENE_PARAMS arrays (KRN/kernel_data.h:338-352,
+ * filled by RTScene::setSceneArgs, APP/raytracing/scene/RTScene.cpp:178-197).
+ * Host pointers; they are COPIED to HBM and may be freed after the call.     */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const mcrt_shape*        shapes;        uint32_t num_shapes;
+    const uint32_t*          indices;       uint32_t num_indices;   /* per-shape local vertex indices */
+    const mcrt_float3*       positions;     uint32_t num_vertices;  /* all per-vertex arrays have num_vertices */
+    const mcrt_float2*       uvs;
+    const mcrt_float3*       normals;
+    const mcrt_float3*       tangents;
+    const mcrt_float3*       binormals;
+    const mcrt_float3*       colors;        /* may be NULL */
+    const mcrt_texture_desc* textures;      uint32_t num_textures;
+    const uint8_t*           tex_data;      uint64_t tex_data_bytes;
+    const uint32_t*          sobol_matrices; uint32_t num_sobol_words; /* 1024 x 52 (APP/raytracing/sampling/sobol.h:34); may be NULL for the random sampler */
+    const mcrt_light*        lights;        uint32_t num_lights;
+    const mcrt_material*     materials;     uint32_t num_materials;
+} mcrt_scene_desc;
+
+/* BVH build options: RTScene::commit SetOption calls (APP/raytracing/scene/RTScene.cpp:203-238)
+ * and IntersectorLDS::Process (RR/src/intersector/intersector_lds.cpp:176-196). */
+typedef struct {
+    float traversal_cost;   /* "bvh.sah.traversal_cost", default 10 */
+    int   num_bins;         /* "bvh.sah.num_bins", default 64 */
+    int   use_sah;          /* "bvh.builder" == "sah", default 1 */
+} mcrt_accel_opts;
+
+#define MCRT_SAMPLER_SOBOL  0   /* KRN/samplers.cl:16 */
+#define MCRT_SAMPLER_RANDOM 1   /* KRN/samplers.cl:17 (reference default) */
+
+/* One frame = one sample per pixel (RTPathTracingPass::update, APP/.../RTPathTracingPass.cpp:40-114). */
+typedef struct {
+    int32_t frame_index;        /* integrator_frameNum */
+    int32_t max_depth;          /* PathTracerSettings::GI.maxDepth (default 2) */
+    int32_t sampler;            /* MCRT_SAMPLER_* */
+    int32_t russian_roulette;   /* 0 = off (parity mode; the reference has none) */
+    int32_t rr_start_depth;     /* first bounce at which RR may terminate */
+    /* Tile split for multi-GPU: rows y with (y / band_rows) % num_bands == band_index
+     * are rendered; others are left untouched.  num_bands = 1 renders everything. */
+    int32_t band_rows;
+    int32_t num_bands;
+    int32_t band_index;
+} mcrt_frame_params;
+
+typedef struct mcrt_ctx_s*         mcrt_ctx;
+typedef struct mcrt_scene_s*       mcrt_scene;
+typedef struct mcrt_framebuffer_s* mcrt_framebuffer;
+
+/* ------------------------------------------------------------------------ */
+/* Context (replaces PlatformManager/KernelManager/RTBufferManager,
+ * APP/raytracing/system/*.cpp, and RadeonRays::CreateFromOpenClContext,
+ * RR/src/api/radeon_rays.cpp:288-318).  One context per GPU.               */
+/* ------------------------------------------------------------------------ */
+MCRT_API mcrt_status mcrt_ctx_create(int device, mcrt_ctx* out);
+MCRT_API mcrt_status mcrt_ctx_destroy(mcrt_ctx ctx);
+MCRT_API const char* mcrt_last_error(mcrt_ctx ctx);   /* ctx may be NULL: last global error */
+MCRT_API mcrt_status mcrt_ctx_synchronize(mcrt_ctx ctx);
+/* stream: a hipStream_t (as void*) all work of this context is enqueued on; NULL = the context's own stream. */
+MCRT_API mcrt_status mcrt_ctx_set_stream(mcrt_ctx ctx, void* stream);
+/* Per-kernel HIP-event timing (replaces QueryManager GPU timers, source/engine/util/QueryManager.h:141-164). */
+MCRT_API mcrt_status mcrt_ctx_set_profiling(mcrt_ctx ctx, int enable);
+/* Fills up to max entries; returns the number of kernels with stats in *count. */
+MCRT_API mcrt_status mcrt_ctx_kernel_stats(mcrt_ctx ctx, int max, const char** names,
+                                           double* total_ms, int64_t* launches,
+                                           double* alg_bytes, int* count);
+MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx);
+
+/* ------------------------------------------------------------------------ */
+/* Scene (replaces RTScene upload + RadeonRays CreateMesh/AttachShape/SetId/
+ * SetTransform/Commit: APP/raytracing/scene/RTScene.cpp:28-56,199-267,564-809;
+ * RR/include/radeon_rays.h:214-237).                                        */
+/* ------------------------------------------------------------------------ */
+MCRT_API mcrt_status mcrt_scene_create(mcrt_ctx ctx, const mcrt_scene_desc* desc, mcrt_scene* out);
+MCRT_API mcrt_status mcrt_scene_destroy(mcrt_scene scene);
+/* Dynamic updates (RTScene::update, APP/raytracing/scene/RTScene.cpp:317-391). Shapes
+ * whose transforms change require mcrt_accel_build again. */
+MCRT_API mcrt_status mcrt_scene_update_lights(mcrt_scene scene, const mcrt_light* lights, uint32_t n);
+MCRT_API mcrt_status mcrt_scene_update_materials(mcrt_scene scene, const mcrt_material* m, uint32_t n);
+MCRT_API mcrt_status mcrt_scene_update_shapes(mcrt_scene scene, const mcrt_shape* s, uint32_t n);
+/* BVH build over all shapes in world space (IntersectionApi::Commit ->
+ * IntersectorLDS::Process -> Bvh2::Build, RR/src/accelerator/bvh2.h:206-315).
+ * Hit shapeid = index into the shapes array (RTScene assigns SetId(nextShapeId++)
+ * in shape order, RTScene.cpp:592,668). opts may be NULL (defaults). */
+MCRT_API mcrt_status mcrt_accel_build(mcrt_scene scene, const mcrt_accel_opts* opts);
+/* Build statistics: node count, bytes on device, host build milliseconds. */
+MCRT_API mcrt_status mcrt_accel_info(mcrt_scene scene, uint64_t* num_nodes, uint64_t* device_bytes,
+                                     double* build_ms, uint32_t* num_triangles);
+
+/* ------------------------------------------------------------------------ */
+/* Ray queries on DEVICE buffers (IntersectionApi::QueryIntersection /
+ * QueryOcclusion, RR/include/radeon_rays.h:267-277 -> IntersectorLDS::Intersect/
+ * Occluded, RR/src/intersector/intersector_lds.cpp:266-326).
+ * Semantics of intersect_main/occluded_main (RR/src/kernels/CL/intersect_bvh2_lds.cl):
+ *  - rays with extra[1] == 0 leave their output untouched;
+ *  - a leaf is skipped when ray mask (extra[0]) == shape id (RR_RAY_MASK);
+ *  - closest: miss -> shapeid = primid = -1 (uvwt untouched), hit -> uvwt = (u,v,0,t);
+ *  - any: 1 = occluded, -1 = not occluded.                                 */
+/* ------------------------------------------------------------------------ */
+MCRT_API mcrt_status mcrt_trace_closest(mcrt_scene scene, const mcrt_ray* d_rays, int32_t n,
+                                        mcrt_intersection* d_hits);
+MCRT_API mcrt_status mcrt_trace_any(mcrt_scene scene, const mcrt_ray* d_rays, int32_t n,
+                                    int32_t* d_hits);
+
+/* ------------------------------------------------------------------------ */
+/* Frame buffer + integrator (RTPrimaryRaysPass, RTPathTracingPass,
+ * RTReconstructionPass: APP/raytracing/renderPasses/*.cpp; kernels
+ * KRN/PathTracing.cl, KRN/reconstruction.cl).                              */
+/* ------------------------------------------------------------------------ */
+MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint32_t height,
+                                             mcrt_framebuffer* out);
+MCRT_API mcrt_status mcrt_framebuffer_destroy(mcrt_framebuffer fb);
+/* Renders one 1-spp frame: PrimaryRays + maxDepth x (shade, shadow, extend).
+ * Result: per-pixel frame radiance ("RadianceBufferCL"). */
+MCRT_API mcrt_status mcrt_render_frame(mcrt_scene scene, mcrt_framebuffer fb, const mcrt_camera* camera,
+                                       const mcrt_frame_params* params);
+/* ReconstructionPass (KRN/reconstruction.cl:6-60): clamp [0,1000] (NaN->0),
+ * frame_index 0 overwrites, else accumulates sum(w*L), sum(w); image = ratio. */
+MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* filter, int32_t frame_index);
+/* Device pointers of the frame buffer's arrays (float4 x W*H, float x W*H). */
+MCRT_API mcrt_status mcrt_framebuffer_device_ptrs(mcrt_framebuffer fb, void** radiance, void** weighted_sum,
+                                                  void** weight_sum, void** image);
+/* Copies device -> host (RGBA32F, W*H*4 floats).  which: 0 radiance, 1 weighted sum, 2 image. */
+MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float* host_rgba);
+/* Per-frame path statistics of the last render (paths, closest rays, any rays, ...). */
+MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closest_rays, int64_t* any_rays,
+                                            int64_t* shaded_paths);
+
+/* ------------------------------------------------------------------------ */
+/* Host helpers                                                              */
+/* ------------------------------------------------------------------------ */
+/* RTPrimaryRaysPass::generatePrimaryRays + RTUtil::screenToRay + Camera::screenToNDC
+ * (APP/.../RTPrimaryRaysPass.cpp:81-104, APP/raytracing/util/RTUtil.cpp:9-41,
+ * source/engine/camera/Camera.cpp:139-145) for a perspective camera with a
+ * glm-style left-handed view (x right, y up, z forward).  pixel_offset is
+ * the TAA jitter in pixels (PathTracingApp.cpp:208-215). */
+MCRT_API mcrt_status mcrt_make_pinhole_camera(const float pos[3], const float forward[3], const float up[3],
+                                              float fov_y_deg, float near_z, float far_z,
+                                              uint32_t width, uint32_t height,
+                                              const float pixel_offset[2], mcrt_camera* out);
+/* Library version / build string. */
+MCRT_API const char* mcrt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#ifdef __cplusplus
+static_assert(sizeof(mcrt_shape) == 160, "RTShape is 160 B");
+static_assert(sizeof(mcrt_material) == 128, "RTMaterial is 128 B");
+static_assert(sizeof(mcrt_light) == 80, "RTLight is 80 B");
+static_assert(sizeof(mcrt_camera) == 176, "RTPinholeCamera is 176 B");
+static_assert(sizeof(mcrt_texture_desc) == 16, "TextureDesc2D is 16 B");
+static_assert(sizeof(mcrt_ray) == 48, "RR ray is 48 B");
+static_assert(sizeof(mcrt_intersection) == 32, "RR Intersection is 32 B");
+static_assert(sizeof(mcrt_filter) == 56, "RTFilterProperties (device) is 56 B");
+static_assert(offsetof(mcrt_material, uber_roughness) == 80, "roughness @80");
+static_assert(offsetof(mcrt_material, uber_normalMapId) == 96, "normalMapId @96");
+static_assert(offsetof(mcrt_camera, width) == 160, "width @160");
+static_assert(offsetof(mcrt_filter, radius) == 8, "radius @8 (device)");
+static_assert(offsetof(mcrt_filter, mitchellB) == 16, "B @16 (device)");
+static_assert(offsetof(mcrt_filter, pixelOffset) == 40, "pixelOffset @40 (device)");
+#else
+_Static_assert(sizeof(mcrt_shape) == 160, "RTShape is 160 B");
+_Static_assert(sizeof(mcrt_material) == 128, "RTMaterial is 128 B");
+_Static_assert(sizeof(mcrt_light) == 80, "RTLight is 80 B");
+_Static_assert(sizeof(mcrt_camera) == 176, "RTPinholeCamera is 176 B");
+_Static_assert(sizeof(mcrt_ray) == 48, "RR ray is 48 B");
+_Static_assert(sizeof(mcrt_intersection) == 32, "RR Intersection is 32 B");
+_Static_assert(sizeof(mcrt_filter) == 56, "RTFilterProperties (device) is 56 B");
+#endif
+
+#endif /* MCRT_CAPI_H */

@@ -1,0 +1,259 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes bindings of the oracle (CPU restatement,
+oracle/libmcrt_oracle.so) and of oracle/_ref (the reference's own RadeonRays
+sources compiled in place, oracle/_ref/librrref.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_c = ctypes
+_vp = _c.c_void_p
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built (run __graft_entry__.build() or make -C oracle)")
+    return _c.CDLL(path)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = _load(os.path.join(HERE, "libmcrt_oracle.so"))
+        L.orc_wang_hash.restype = _c.c_uint32
+        L.orc_wang_hash.argtypes = [_c.c_uint32]
+        L.orc_xorshift.restype = _c.c_uint32
+        L.orc_xorshift.argtypes = [_c.POINTER(_c.c_uint32)]
+        L.orc_rand_float.restype = _c.c_float
+        L.orc_rand_float.argtypes = [_c.POINTER(_c.c_uint32)]
+        L.orc_sobol_sample.restype = _c.c_float
+        L.orc_sobol_sample.argtypes = [_c.c_uint32, _c.c_uint32, _c.c_uint32, _vp]
+        L.orc_sampler_draws.argtypes = [_c.c_int, _c.c_uint32, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _vp, _vp]
+        L.orc_scene_create.restype = _vp
+        L.orc_scene_create.argtypes = [_vp]
+        L.orc_scene_destroy.argtypes = [_vp]
+        L.orc_bvh_build.restype = _c.c_int64
+        L.orc_bvh_build.argtypes = [_vp, _c.c_float, _c.c_int, _c.c_int]
+        L.orc_bvh_nodes.restype = _c.c_int64
+        L.orc_bvh_nodes.argtypes = [_vp, _vp, _c.c_int64]
+        L.orc_trace_closest.argtypes = [_vp, _vp, _c.c_int, _vp, _vp, _c.c_int]
+        L.orc_trace_any.argtypes = [_vp, _vp, _c.c_int, _vp, _vp, _c.c_int]
+        L.orc_brute_closest.argtypes = [_vp, _vp, _c.c_int, _vp]
+        L.orc_brute_any.argtypes = [_vp, _vp, _c.c_int, _vp]
+        L.orc_render_frame.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _vp, _vp]
+        L.orc_render_rows.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _c.c_int, _c.c_int, _vp, _vp]
+        L.orc_accumulate.argtypes = [_c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp, _vp]
+        L.orc_sample_uber.argtypes = [_vp] * 6 + [_c.c_float, _vp, _vp, _vp]
+        L.orc_eval_uber.argtypes = [_vp] * 5 + [_c.c_float, _vp, _vp, _vp]
+        L.orc_pdf_uber.restype = _c.c_float
+        L.orc_pdf_uber.argtypes = [_vp] * 6 + [_c.c_float, _vp, _vp]
+        L.orc_roughness_to_alpha.restype = _c.c_float
+        L.orc_roughness_to_alpha.argtypes = [_c.c_float]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class OracleScene:
+    """Oracle view of an mcrt.scenes.Scene (keeps the numpy arrays alive)."""
+
+    def __init__(self, scene):
+        self.scene = scene
+        self._desc = scene.desc()
+        self.h = lib().orc_scene_create(ctypes.byref(self._desc))
+        self.num_nodes = 0
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().orc_scene_destroy(self.h)
+        except Exception:
+            pass
+
+    def build(self, cost=10.0, bins=64, sah=True):
+        self.num_nodes = lib().orc_bvh_build(self.h, cost, bins, 1 if sah else 0)
+        return self.num_nodes
+
+    def nodes(self):
+        from mcrt.types import RRNODE_DTYPE
+        out = np.zeros(self.num_nodes, RRNODE_DTYPE)
+        lib().orc_bvh_nodes(self.h, _p(out), self.num_nodes)
+        return out
+
+    def closest(self, rays, threads=8, visits=False):
+        from mcrt.types import ISECT_DTYPE
+        hits = np.zeros(len(rays), ISECT_DTYPE)
+        hits["shapeid"] = -7
+        hits["primid"] = -7
+        v = np.zeros(len(rays), np.int32) if visits else None
+        lib().orc_trace_closest(self.h, _p(rays), len(rays), _p(hits), _p(v), threads)
+        return (hits, v) if visits else hits
+
+    def any(self, rays, threads=8, visits=False):
+        out = np.full(len(rays), -7, np.int32)
+        v = np.zeros(len(rays), np.int32) if visits else None
+        lib().orc_trace_any(self.h, _p(rays), len(rays), _p(out), _p(v), threads)
+        return (out, v) if visits else out
+
+    def brute_closest(self, rays):
+        from mcrt.types import ISECT_DTYPE
+        hits = np.zeros(len(rays), ISECT_DTYPE)
+        lib().orc_brute_closest(self.h, _p(rays), len(rays), _p(hits))
+        return hits
+
+    def brute_any(self, rays):
+        out = np.zeros(len(rays), np.int32)
+        lib().orc_brute_any(self.h, _p(rays), len(rays), _p(out))
+        return out
+
+    def render(self, cam, frame=0, max_depth=2, sampler=1, y0=0, y1=None, threads=8, radiance=None):
+        W, H = int(cam["width"][0]), int(cam["height"][0])
+        if y1 is None:
+            y1 = H
+        if radiance is None:
+            radiance = np.zeros((H, W, 4), np.float32)
+        stats = np.zeros(4, np.int64)
+        lib().orc_render_frame(self.h, _p(cam), frame, max_depth, sampler, y0, y1, threads, _p(radiance), _p(stats))
+        return radiance, stats
+
+    def render_rows(self, cam, rows, frame=0, max_depth=2, sampler=1, threads=8, radiance=None):
+        W, H = int(cam["width"][0]), int(cam["height"][0])
+        rows = np.ascontiguousarray(rows, np.int32)
+        if radiance is None:
+            radiance = np.zeros((H, W, 4), np.float32)
+        stats = np.zeros(4, np.int64)
+        lib().orc_render_rows(self.h, _p(cam), frame, max_depth, sampler, _p(rows), len(rows), threads,
+                              _p(radiance), _p(stats))
+        return radiance, stats
+
+
+def accumulate(radiance, frame, filt, wsum=None, wts=None):
+    H, W = radiance.shape[:2]
+    if wsum is None:
+        wsum = np.zeros((H, W, 4), np.float32)
+        wts = np.zeros((H, W), np.float32)
+    image = np.zeros((H, W, 4), np.float32)
+    lib().orc_accumulate(W, H, frame, _p(filt), _p(radiance), _p(wsum), _p(wts), _p(image))
+    return wsum, wts, image
+
+
+def wang_hash(x):
+    return lib().orc_wang_hash(x)
+
+
+def sampler_draws(kind, pix, frame, bounce, W, H, sobol=None):
+    out = np.zeros(5, np.float32)
+    lib().orc_sampler_draws(kind, pix, frame, bounce, W, H, _p(sobol), _p(out))
+    return out
+
+
+def sample_uber(kd, ks, kr, kt, alpha, opacity, eta, wo, u):
+    a = [np.asarray(x, np.float32) for x in (kd, ks, kr, kt, alpha, opacity)]
+    wo = np.asarray(wo, np.float32)
+    u = np.asarray(u, np.float32)
+    out = np.zeros(8, np.float32)
+    lib().orc_sample_uber(*[_p(x) for x in a], eta, _p(wo), _p(u), _p(out))
+    return out
+
+
+# --------------------------------------------------------------------------
+# oracle/_ref: the reference's own RadeonRays C++ (bvh2.cpp, mesh.cpp, utils.cpp)
+# --------------------------------------------------------------------------
+REF_LIB = os.path.join(HERE, "_ref", "librrref.so")
+_ref = None
+
+
+def ref_available():
+    return os.path.exists(REF_LIB)
+
+
+def ref():
+    global _ref
+    if _ref is None:
+        L = _load(REF_LIB)
+        L.rr_bvh_build.restype = _c.c_int64
+        L.rr_bvh_build.argtypes = [_c.c_int, _vp, _vp, _c.c_int, _vp, _vp, _vp, _c.c_float, _c.c_int, _c.c_int,
+                                   _vp, _c.c_int64]
+        L.rr_test_intersections.argtypes = [_c.c_int, _vp, _vp, _c.c_int, _vp, _vp, _vp, _vp, _c.c_int, _vp]
+        L.rr_test_occlusions.argtypes = [_c.c_int, _vp, _vp, _c.c_int, _vp, _vp, _vp, _vp, _c.c_int, _vp]
+        L.rr_load_obj.restype = _vp
+        L.rr_load_obj.argtypes = [_c.c_char_p, _c.c_char_p]
+        L.rr_obj_num_shapes.restype = _c.c_int
+        L.rr_obj_num_shapes.argtypes = [_vp]
+        L.rr_obj_shape.argtypes = [_vp, _c.c_int, _vp, _vp, _vp, _vp]
+        L.rr_obj_free.argtypes = [_vp]
+        _ref = L
+    return _ref
+
+
+class _RefShapes:
+    """Per-shape arrays of an mcrt.scenes.Scene in the layout RadeonRays' CreateMesh takes."""
+
+    def __init__(self, scene):
+        self.P, self.I, self.M = [], [], []
+        for s in scene.shapes:
+            v0, n = int(s["startVertex"]), 0
+            idx = scene.indices[s["startIdx"]: s["startIdx"] + 3 * s["numTriangles"]].astype(np.int32)
+            n = int(idx.max()) + 1 if idx.size else 0
+            self.P.append(np.ascontiguousarray(scene.positions[v0:v0 + n]))   # stride 16
+            self.I.append(np.ascontiguousarray(idx))
+            self.M.append(s["toWorldTransform"].astype(np.float32))
+        self.nv = np.array([p.shape[0] for p in self.P], np.int32)
+        self.nf = np.array([i.size // 3 for i in self.I], np.int32)
+        self.pp = (_c.c_void_p * len(self.P))(*[p.ctypes.data for p in self.P])
+        self.ip = (_c.c_void_p * len(self.I))(*[i.ctypes.data for i in self.I])
+        self.mt = np.ascontiguousarray(np.stack(self.M)) if self.M else np.zeros((0, 4, 4), np.float32)
+
+    def args(self):
+        return (len(self.P), self.pp, _p(self.nv), 16, self.ip, _p(self.nf), _p(self.mt))
+
+
+def ref_bvh_nodes(scene, cost=10.0, bins=64, sah=True):
+    from mcrt.types import RRNODE_DTYPE
+    sh = _RefShapes(scene)
+    n = ref().rr_bvh_build(*sh.args(), cost, bins, 1 if sah else 0, None, 0)
+    out = np.zeros(n, RRNODE_DTYPE)
+    ref().rr_bvh_build(*sh.args(), cost, bins, 1 if sah else 0, _p(out), n)
+    return out
+
+
+def ref_brute_closest(scene, rays):
+    from mcrt.types import ISECT_DTYPE
+    sh = _RefShapes(scene)
+    out = np.zeros(len(rays), ISECT_DTYPE)
+    ref().rr_test_intersections(*sh.args(), _p(rays), len(rays), _p(out))
+    return out
+
+
+def ref_brute_any(scene, rays):
+    sh = _RefShapes(scene)
+    out = np.zeros(len(rays), np.int32)
+    ref().rr_test_occlusions(*sh.args(), _p(rays), len(rays), _p(out))
+    return out
+
+
+def ref_load_obj(path):
+    L = ref()
+    base = os.path.dirname(path) + "/"
+    h = L.rr_load_obj(path.encode(), base.encode())
+    if not h:
+        raise RuntimeError(f"tinyobj failed on {path}")
+    shapes = []
+    for i in range(L.rr_obj_num_shapes(h)):
+        pp, npf, ip, ni = _c.c_void_p(), _c.c_int(), _c.c_void_p(), _c.c_int()
+        L.rr_obj_shape(h, i, _c.byref(pp), _c.byref(npf), _c.byref(ip), _c.byref(ni))
+        P = np.ctypeslib.as_array(_c.cast(pp, _c.POINTER(_c.c_float)), (npf.value,)).copy().reshape(-1, 3)
+        I = np.ctypeslib.as_array(_c.cast(ip, _c.POINTER(_c.c_int)), (ni.value,)).copy().reshape(-1, 3)
+        shapes.append((P, I))
+    L.rr_obj_free(h)
+    return shapes
