@@ -215,7 +215,7 @@ typedef struct mcrt_framebuffer_s* mcrt_framebuffer;
 
 /* ------------------------------------------------------------------------ */
 /* Context (replaces PlatformManager/KernelManager/RTBufferManager,
- * APP/raytracing/system/*.cpp, and RadeonRays::CreateFromOpenClContext,
+ * APP/raytracing/system/{Kernel,Platform}Manager.cpp, and RadeonRays::CreateFromOpenClContext,
  * RR/src/api/radeon_rays.cpp:288-318).  One context per GPU.               */
 /* ------------------------------------------------------------------------ */
 MCRT_API mcrt_status mcrt_ctx_create(int device, mcrt_ctx* out);
@@ -226,10 +226,11 @@ MCRT_API mcrt_status mcrt_ctx_synchronize(mcrt_ctx ctx);
 MCRT_API mcrt_status mcrt_ctx_set_stream(mcrt_ctx ctx, void* stream);
 /* Per-kernel HIP-event timing (replaces QueryManager GPU timers, source/engine/util/QueryManager.h:141-164). */
 MCRT_API mcrt_status mcrt_ctx_set_profiling(mcrt_ctx ctx, int enable);
-/* Fills up to max entries; returns the number of kernels with stats in *count. */
+/* Synchronizes, then fills up to max entries: kernel name, summed HIP-event time (ms),
+ * launch count and items processed (pixels / rays / paths); *count = kernels with stats. */
 MCRT_API mcrt_status mcrt_ctx_kernel_stats(mcrt_ctx ctx, int max, const char** names,
                                            double* total_ms, int64_t* launches,
-                                           double* alg_bytes, int* count);
+                                           int64_t* items, int* count);
 MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx);
 
 /* ------------------------------------------------------------------------ */
@@ -270,7 +271,7 @@ MCRT_API mcrt_status mcrt_trace_any(mcrt_scene scene, const mcrt_ray* d_rays, in
 
 /* ------------------------------------------------------------------------ */
 /* Frame buffer + integrator (RTPrimaryRaysPass, RTPathTracingPass,
- * RTReconstructionPass: APP/raytracing/renderPasses/*.cpp; kernels
+ * RTReconstructionPass: APP/raytracing/renderPasses/RT*Pass.cpp; kernels
  * KRN/PathTracing.cl, KRN/reconstruction.cl).                              */
 /* ------------------------------------------------------------------------ */
 MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint32_t height,

@@ -1,0 +1,835 @@
+// mcrt_capi.cpp -- host runtime behind include/mcrt_capi.h.
+//
+// Replaces the reference's OpenCL host plumbing (PlatformManager / KernelManager /
+// RTBufferManager, RTScene uploads, RadeonRays IntersectionApi, and the per-pass
+// launch + clFinish sequence of RTPrimaryRaysPass / RTPathTracingPass /
+// RTReconstructionPass) with: one HIP stream per context, all per-frame work enqueued
+// without host synchronisation (queue sizes stay on the device), one memset per frame.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mcrt_internal.h"
+
+namespace {
+
+thread_local std::string g_lastError;
+
+#define MCRT_MAX_BOUNCES 32
+
+enum KernelId { K_PRIMARY, K_SHADE0, K_SHADEN, K_SHADOW, K_EXTEND, K_ACCUM, K_TRACE_CLOSEST, K_TRACE_ANY, K_COUNT };
+const char* kKernelNames[K_COUNT] = {"k_primary", "k_shade0", "k_shadeN", "k_shadow",
+                                     "k_extend",  "k_accumulate", "k_trace_closest", "k_trace_any"};
+
+}  // namespace
+
+struct mcrt_ctx_s {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    int numCUs = 256;
+    bool profiling = false;
+    std::string error;
+    struct Pending {
+        int kernel;
+        hipEvent_t a, b;
+        const int* countDev;   // device counter holding the item count (or nullptr)
+        int64_t items;
+    };
+    std::vector<Pending> pending;
+    double totalMs[K_COUNT] = {};
+    int64_t launches[K_COUNT] = {};
+    int64_t items[K_COUNT] = {};
+};
+
+struct mcrt_scene_s {
+    mcrt_ctx ctx = nullptr;
+    // host copies needed for the BVH build and dynamic updates
+    std::vector<mcrt_shape> shapes;
+    std::vector<uint32_t> indices;
+    std::vector<mcrt_float4> positions;
+    // device arrays
+    void* dShapes = nullptr;
+    void* dIndices = nullptr;
+    void* dPositions = nullptr;
+    void* dUvs = nullptr;
+    void* dNormals = nullptr;
+    void* dTextures = nullptr;
+    void* dTexData = nullptr;
+    void* dSobol = nullptr;
+    void* dLights = nullptr;
+    void* dMaterials = nullptr;
+    uint32_t numLights = 0, numMaterials = 0, numTextures = 0;
+    bool hasSobol = false;
+    // BVH
+    void* dNodes = nullptr;
+    void* dTris = nullptr;
+    uint64_t numNodes = 0;
+    uint32_t numTris = 0;
+    double buildMs = 0.0;
+    int bvhDepth = 0;
+    // traversal scratch
+    uint32_t* dSpill = nullptr;
+    int spillCap = 0;
+    int traceGrid = 0;
+    int* dScratch = nullptr;   // [0] overflow flag, [1..] work counters for API queries
+};
+
+struct mcrt_framebuffer_s {
+    mcrt_ctx ctx = nullptr;
+    uint32_t W = 0, H = 0;
+    size_t N = 0;
+    float4* radiance = nullptr;
+    float4* wsum = nullptr;
+    float* wts = nullptr;
+    float4* image = nullptr;
+    float4* hitsP = nullptr;     // primary hits by pixel
+    float4* hitsE = nullptr;     // extension hits by queue slot
+    float4* eO[2] = {};
+    float4* eD[2] = {};
+    float4* eT[2] = {};
+    float4 *sO = nullptr, *sD = nullptr, *sL = nullptr;
+    int* counters = nullptr;     // [0..31] shadow counts, [32..63] ext counts, [64..] work counters
+    int lastMaxDepth = 0;
+    int64_t lastPixels = 0;
+    FrameArgs bands{};      // band layout of the last mcrt_render_frame (used by mcrt_accumulate)
+    bool haveBands = false;
+};
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+static mcrt_status fail(mcrt_ctx ctx, mcrt_status code, const std::string& msg) {
+    g_lastError = msg;
+    if (ctx) ctx->error = msg;
+    return code;
+}
+#define HIPCHK(ctx, expr)                                                                                   \
+    do {                                                                                                    \
+        hipError_t e_ = (expr);                                                                             \
+        if (e_ != hipSuccess)                                                                               \
+            return fail(ctx, e_ == hipErrorOutOfMemory ? MCRT_ERROR_OUT_OF_MEMORY : MCRT_ERROR_DEVICE,      \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                                 \
+    } while (0)
+
+template <class T>
+static hipError_t upload(void** dst, const T* src, size_t count, hipStream_t st) {
+    *dst = nullptr;
+    if (!src || count == 0) return hipSuccess;
+    hipError_t e = hipMalloc(dst, sizeof(T) * count);
+    if (e != hipSuccess) return e;
+    return hipMemcpyAsync(*dst, src, sizeof(T) * count, hipMemcpyHostToDevice, st);
+}
+
+struct Timed {
+    mcrt_ctx c;
+    int k;
+    hipEvent_t a = nullptr, b = nullptr;
+    const int* countDev;
+    int64_t items;
+    Timed(mcrt_ctx ctx, int kernel, const int* countDev_, int64_t items_) : c(ctx), k(kernel), countDev(countDev_), items(items_) {
+        if (c->profiling) {
+            hipEventCreate(&a);
+            hipEventCreate(&b);
+            hipEventRecord(a, c->stream);
+        }
+    }
+    ~Timed() {
+        if (c->profiling) {
+            hipEventRecord(b, c->stream);
+            c->pending.push_back({k, a, b, countDev, items});
+        }
+    }
+};
+
+static void drain_pending(mcrt_ctx ctx) {
+    if (ctx->pending.empty()) return;
+    hipStreamSynchronize(ctx->stream);
+    for (auto& p : ctx->pending) {
+        float ms = 0.0f;
+        hipEventElapsedTime(&ms, p.a, p.b);
+        ctx->totalMs[p.kernel] += ms;
+        ctx->launches[p.kernel] += 1;
+        int64_t it = p.items;
+        if (p.countDev) {
+            int v = 0;
+            hipMemcpy(&v, p.countDev, sizeof(int), hipMemcpyDeviceToHost);
+            it = v;
+        }
+        ctx->items[p.kernel] += it;
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    ctx->pending.clear();
+}
+
+// RR transform_point (RR/include/math/mathutils.h:111-118) for the BVH's world-space triangles
+static inline void xformPoint(const mcrt_mat4& m, const mcrt_float4& p, float* o) {
+    const mcrt_float4* r[3] = {&m.m0, &m.m1, &m.m2};
+    for (int i = 0; i < 3; ++i) {
+        float acc = 0.0f;
+        acc += r[i]->x * p.x;
+        acc += r[i]->y * p.y;
+        acc += r[i]->z * p.z;
+        acc += r[i]->w * 0.0f;
+        o[i] = acc + r[i]->w;
+    }
+}
+
+// filters.cl:12-69 (uniform per frame: the reference evaluates one pixelOffset per frame)
+static float filter_weight(const mcrt_filter& f) {
+    const float px = f.pixelOffset.x, py = f.pixelOffset.y;
+    auto mitchell1D = [](float x, float B, float C) {
+        x = std::fabs(2.0f * x);
+        if (x > 1.0f) return ((-B - 6 * C) * x * x * x + (6 * B + 30 * C) * x * x + (-12 * B - 48 * C) * x + (8 * B + 24 * C)) * (1.f / 6.f);
+        return ((12 - 9 * B - 6 * C) * x * x * x + (-18 + 12 * B + 6 * C) * x * x + (6 - 2 * B)) * (1.f / 6.f);
+    };
+    auto sinc = [](float x) { x = std::fabs(x); return x < 1e-5 ? 1.0f : std::sin(3.14159265359f * x) / (3.14159265359f * x); };
+    auto wsinc = [&](float x, float r, float tau) { x = std::fabs(x); return x > r ? 0.0f : sinc(x) * sinc(x / tau); };
+    switch (f.filterType) {
+    case MCRT_TRIANGLE_FILTER:
+        return std::fmax(0.0f, f.radius.x - std::fabs(px)) * std::fmax(0.0f, f.radius.y - std::fabs(py));
+    case MCRT_GAUSSIAN_FILTER:
+        return std::fmax(0.0f, std::exp(-f.gaussianAlpha * px * px) - f.gaussianExpX) *
+               std::fmax(0.0f, std::exp(-f.gaussianAlpha * py * py) - f.gaussianExpY);
+    case MCRT_MITCHELL_FILTER:
+        return mitchell1D(px / f.radius.x, f.mitchellB, f.mitchellC) * mitchell1D(py / f.radius.y, f.mitchellB, f.mitchellC);
+    case MCRT_LANCZOS_SINC_FILTER:
+        return wsinc(px, f.radius.x, f.lanczosSincTau) * wsinc(py, f.radius.y, f.lanczosSincTau);
+    default:
+        return 1.0f;
+    }
+}
+
+static TraceCtx trace_ctx(mcrt_scene s) {
+    TraceCtx c;
+    c.nodes = (const float4*)s->dNodes;
+    c.tris = (const float4*)s->dTris;
+    c.spill = s->dSpill;
+    c.spillCap = s->spillCap;
+    c.overflow = s->dScratch;
+    return c;
+}
+
+static SceneArgs scene_args(mcrt_scene s) {
+    SceneArgs a;
+    a.shapes = (const mcrt_shape*)s->dShapes;
+    a.indices = (const uint32_t*)s->dIndices;
+    a.positions = (const float4*)s->dPositions;
+    a.uvs = (const float2*)s->dUvs;
+    a.normals = (const float4*)s->dNormals;
+    a.textures = (const mcrt_texture_desc*)s->dTextures;
+    a.texData = (const uint8_t*)s->dTexData;
+    a.sobol = (const uint32_t*)s->dSobol;
+    a.lights = (const mcrt_light*)s->dLights;
+    a.materials = (const mcrt_material*)s->dMaterials;
+    a.tris = (const float4*)s->dTris;
+    a.numLights = (int)s->numLights;
+    return a;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+extern "C" {
+
+MCRT_API const char* mcrt_version(void) { return "mcrt-mi355x 0.1 (gfx950, HIP)"; }
+
+MCRT_API const char* mcrt_last_error(mcrt_ctx ctx) { return ctx ? ctx->error.c_str() : g_lastError.c_str(); }
+
+MCRT_API mcrt_status mcrt_ctx_create(int device, mcrt_ctx* out) {
+    if (!out) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "out is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(nullptr, MCRT_ERROR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= n) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "device index out of range");
+    auto* c = new mcrt_ctx_s();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess) { delete c; return fail(nullptr, MCRT_ERROR_DEVICE, "hipSetDevice failed"); }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(nullptr, MCRT_ERROR_DEVICE, "hipStreamCreate failed");
+    }
+    c->stream = c->own;
+    *out = c;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_ctx_destroy(mcrt_ctx ctx) {
+    if (!ctx) return MCRT_OK;
+    hipSetDevice(ctx->device);
+    drain_pending(ctx);
+    hipStreamSynchronize(ctx->stream);
+    hipStreamDestroy(ctx->own);
+    delete ctx;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_ctx_synchronize(mcrt_ctx ctx) {
+    if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_ctx_set_stream(mcrt_ctx ctx, void* stream) {
+    if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
+    ctx->stream = stream ? (hipStream_t)stream : ctx->own;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_ctx_set_profiling(mcrt_ctx ctx, int enable) {
+    if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
+    ctx->profiling = enable != 0;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_ctx_kernel_stats(mcrt_ctx ctx, int max, const char** names, double* total_ms,
+                                           int64_t* launches, int64_t* items, int* count) {
+    if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
+    hipSetDevice(ctx->device);
+    drain_pending(ctx);
+    int k = 0;
+    for (int i = 0; i < K_COUNT && k < max; ++i) {
+        if (ctx->launches[i] == 0) continue;
+        if (names) names[k] = kKernelNames[i];
+        if (total_ms) total_ms[k] = ctx->totalMs[i];
+        if (launches) launches[k] = ctx->launches[i];
+        if (items) items[k] = ctx->items[i];
+        ++k;
+    }
+    if (count) *count = k;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx) {
+    if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
+    drain_pending(ctx);
+    for (int i = 0; i < K_COUNT; ++i) { ctx->totalMs[i] = 0.0; ctx->launches[i] = 0; ctx->items[i] = 0; }
+    return MCRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// scene
+// ---------------------------------------------------------------------------
+static void scene_free_device(mcrt_scene s) {
+    void** ptrs[] = {&s->dShapes, &s->dIndices, &s->dPositions, &s->dUvs, &s->dNormals, &s->dTextures,
+                     &s->dTexData, &s->dSobol, &s->dLights, &s->dMaterials, &s->dNodes, &s->dTris};
+    for (void** p : ptrs) {
+        if (*p) hipFree(*p);
+        *p = nullptr;
+    }
+    if (s->dSpill) hipFree(s->dSpill);
+    if (s->dScratch) hipFree(s->dScratch);
+    s->dSpill = nullptr;
+    s->dScratch = nullptr;
+}
+
+MCRT_API mcrt_status mcrt_scene_create(mcrt_ctx ctx, const mcrt_scene_desc* d, mcrt_scene* out) {
+    if (!ctx || !d || !out) return fail(ctx, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    if (d->num_shapes == 0 || !d->shapes) return fail(ctx, MCRT_ERROR_INVALID_ARG, "scene has no shapes");
+    if (!d->indices || !d->positions || !d->uvs || !d->normals)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "indices/positions/uvs/normals are required");
+    for (uint32_t i = 0; i < d->num_shapes; ++i) {
+        const mcrt_shape& s = d->shapes[i];
+        if ((uint64_t)s.startIdx + 3ull * s.numTriangles > d->num_indices)
+            return fail(ctx, MCRT_ERROR_INVALID_ARG, "shape " + std::to_string(i) + " indexes past the index array");
+        if (s.materialId >= (int)d->num_materials)
+            return fail(ctx, MCRT_ERROR_INVALID_ARG, "shape " + std::to_string(i) + " has an invalid material id");
+        if (s.lightID >= (int)d->num_lights) return fail(ctx, MCRT_ERROR_INVALID_ARG, "invalid light id");
+    }
+    for (uint32_t i = 0; i < d->num_shapes; ++i) {
+        const mcrt_shape& s = d->shapes[i];
+        for (uint32_t k = 0; k < 3u * s.numTriangles; ++k)
+            if ((uint64_t)s.startVertex + d->indices[s.startIdx + k] >= d->num_vertices)
+                return fail(ctx, MCRT_ERROR_INVALID_ARG, "vertex index out of range in shape " + std::to_string(i));
+    }
+    for (uint32_t i = 0; i < d->num_lights; ++i) {
+        const mcrt_light& L = d->lights[i];
+        if (L.type == MCRT_TRIANGLE_MESH_AREA_LIGHT && (L.shapeId < 0 || L.shapeId >= (int)d->num_shapes ||
+                                                        d->shapes[L.shapeId].numTriangles == 0))
+            return fail(ctx, MCRT_ERROR_INVALID_ARG, "mesh light " + std::to_string(i) + " has an invalid shape");
+    }
+    for (uint32_t i = 0; i < d->num_textures; ++i) {
+        const mcrt_texture_desc& t = d->textures[i];
+        if (t.width == 0 || t.height == 0 || (uint64_t)t.memOffset + 4ull * t.width * t.height > d->tex_data_bytes)
+            return fail(ctx, MCRT_ERROR_INVALID_ARG, "texture " + std::to_string(i) + " is out of the texel buffer");
+    }
+    hipSetDevice(ctx->device);
+    auto* s = new mcrt_scene_s();
+    s->ctx = ctx;
+    s->shapes.assign(d->shapes, d->shapes + d->num_shapes);
+    s->indices.assign(d->indices, d->indices + d->num_indices);
+    s->positions.assign(d->positions, d->positions + d->num_vertices);
+    hipStream_t st = ctx->stream;
+    hipError_t e = hipSuccess;
+#define UP(dst, src, cnt) if (e == hipSuccess) e = upload(&s->dst, src, cnt, st)
+    UP(dShapes, d->shapes, d->num_shapes);
+    UP(dIndices, d->indices, d->num_indices);
+    UP(dPositions, d->positions, d->num_vertices);
+    UP(dUvs, d->uvs, d->num_vertices);
+    UP(dNormals, d->normals, d->num_vertices);
+    UP(dTextures, d->textures, d->num_textures);
+    UP(dTexData, d->tex_data, d->tex_data_bytes);
+    UP(dSobol, d->sobol_matrices, d->num_sobol_words);
+    UP(dLights, d->lights, d->num_lights);
+    UP(dMaterials, d->materials, d->num_materials);
+#undef UP
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        scene_free_device(s);
+        delete s;
+        return fail(ctx, e == hipErrorOutOfMemory ? MCRT_ERROR_OUT_OF_MEMORY : MCRT_ERROR_DEVICE,
+                    std::string("scene upload: ") + hipGetErrorString(e));
+    }
+    s->numLights = d->num_lights;
+    s->numMaterials = d->num_materials;
+    s->numTextures = d->num_textures;
+    s->hasSobol = d->sobol_matrices != nullptr && d->num_sobol_words >= 1024u * 52u;
+    *out = s;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_scene_destroy(mcrt_scene s) {
+    if (!s) return MCRT_OK;
+    hipSetDevice(s->ctx->device);
+    hipStreamSynchronize(s->ctx->stream);
+    scene_free_device(s);
+    delete s;
+    return MCRT_OK;
+}
+
+static mcrt_status replace_array(mcrt_scene s, void** dst, const void* src, size_t bytes) {
+    mcrt_ctx ctx = s->ctx;
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (*dst) HIPCHK(ctx, hipFree(*dst));
+    *dst = nullptr;
+    if (bytes) {
+        HIPCHK(ctx, hipMalloc(dst, bytes));
+        HIPCHK(ctx, hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    }
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_scene_update_lights(mcrt_scene s, const mcrt_light* lights, uint32_t n) {
+    if (!s || (n && !lights)) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "invalid lights");
+    mcrt_status st = replace_array(s, &s->dLights, lights, sizeof(mcrt_light) * n);
+    if (st == MCRT_OK) s->numLights = n;
+    return st;
+}
+
+MCRT_API mcrt_status mcrt_scene_update_materials(mcrt_scene s, const mcrt_material* m, uint32_t n) {
+    if (!s || (n && !m)) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "invalid materials");
+    mcrt_status st = replace_array(s, &s->dMaterials, m, sizeof(mcrt_material) * n);
+    if (st == MCRT_OK) s->numMaterials = n;
+    return st;
+}
+
+MCRT_API mcrt_status mcrt_scene_update_shapes(mcrt_scene s, const mcrt_shape* sh, uint32_t n) {
+    if (!s || !sh || n != s->shapes.size())
+        return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "shape count must not change");
+    for (uint32_t i = 0; i < n; ++i)
+        if (sh[i].startIdx != s->shapes[i].startIdx || sh[i].numTriangles != s->shapes[i].numTriangles)
+            return fail(s->ctx, MCRT_ERROR_INVALID_ARG, "shape topology must not change");
+    s->shapes.assign(sh, sh + n);
+    return replace_array(s, &s->dShapes, sh, sizeof(mcrt_shape) * n);
+}
+
+MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts) {
+    if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
+    mcrt_ctx ctx = s->ctx;
+    const float cost = opts ? opts->traversal_cost : 10.0f;
+    const int bins = opts ? opts->num_bins : 64;
+    const bool sah = opts ? opts->use_sah != 0 : true;
+    if (bins < 2 || bins > 4096) return fail(ctx, MCRT_ERROR_INVALID_ARG, "num_bins out of range");
+    auto t0 = std::chrono::steady_clock::now();
+    size_t n = 0;
+    for (auto& sh : s->shapes) n += sh.numTriangles;
+    if (n == 0) return fail(ctx, MCRT_ERROR_INVALID_ARG, "scene has no triangles (RR: Commit on empty scene throws)");
+    if (n > (size_t)0x7fffffff) return fail(ctx, MCRT_ERROR_INVALID_ARG, "too many triangles");
+    std::vector<float> tri(9 * n);
+    std::vector<int32_t> shapeOf(n), primOf(n);
+    size_t k = 0;
+    for (size_t si = 0; si < s->shapes.size(); ++si) {
+        const mcrt_shape& sh = s->shapes[si];
+        for (uint32_t f = 0; f < sh.numTriangles; ++f, ++k) {
+            for (int c = 0; c < 3; ++c)
+                xformPoint(sh.toWorldTransform, s->positions[sh.startVertex + s->indices[sh.startIdx + 3 * f + c]],
+                           &tri[9 * k + 3 * c]);
+            shapeOf[k] = (int32_t)si;
+            primOf[k] = (int32_t)f;
+        }
+    }
+    int threads = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+    mcrt::BvhOut bvh;
+    if (!mcrt::build_bvh(tri.data(), shapeOf.data(), primOf.data(), n, cost, bins, sah, threads, bvh))
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "BVH build failed");
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (s->dNodes) hipFree(s->dNodes);
+    if (s->dTris) hipFree(s->dTris);
+    s->dNodes = s->dTris = nullptr;
+    hipError_t e = hipMalloc(&s->dNodes, 64 * bvh.numNodes);
+    if (e == hipSuccess) e = hipMalloc(&s->dTris, 48 * bvh.numTris);
+    if (e == hipSuccess) e = hipMemcpy(s->dNodes, bvh.nodes, 64 * bvh.numNodes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(s->dTris, bvh.tris, 48 * bvh.numTris, hipMemcpyHostToDevice);
+    s->numNodes = bvh.numNodes;
+    s->numTris = (uint32_t)bvh.numTris;
+    s->bvhDepth = bvh.depth;
+    mcrt::free_bvh(bvh);
+    if (e != hipSuccess) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, std::string("BVH upload: ") + hipGetErrorString(e));
+    // traversal scratch: persistent grid = CUs x 8 blocks of 256 threads; spill deep enough for the tree
+    if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
+    HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
+    s->traceGrid = ctx->numCUs * 8;
+    const int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;
+    if (needCap > s->spillCap) {
+        if (s->dSpill) hipFree(s->dSpill);
+        s->spillCap = std::max(needCap, 32);
+        HIPCHK(ctx, hipMalloc(&s->dSpill, (size_t)s->traceGrid * 256 * s->spillCap * sizeof(uint32_t)));
+    }
+    s->buildMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_accel_info(mcrt_scene s, uint64_t* num_nodes, uint64_t* device_bytes, double* build_ms,
+                                     uint32_t* num_triangles) {
+    if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
+    if (num_nodes) *num_nodes = s->numNodes;
+    if (device_bytes) *device_bytes = 64ull * s->numNodes + 48ull * s->numTris;
+    if (build_ms) *build_ms = s->buildMs;
+    if (num_triangles) *num_triangles = s->numTris;
+    return MCRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RadeonRays-style queries
+// ---------------------------------------------------------------------------
+static mcrt_status trace_common(mcrt_scene s, const mcrt_ray* rays, int32_t n, mcrt_intersection* hits, int32_t* occl,
+                                bool any) {
+    if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
+    mcrt_ctx ctx = s->ctx;
+    if (!s->dNodes) return fail(ctx, MCRT_ERROR_NOT_READY, "mcrt_accel_build has not been called");
+    if (n < 0 || (n > 0 && !rays) || (n > 0 && !any && !hits) || (n > 0 && any && !occl))
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "invalid ray query arguments");
+    if (n == 0) return MCRT_OK;
+    hipSetDevice(ctx->device);
+    int* work = s->dScratch + (any ? 2 : 1);
+    HIPCHK(ctx, hipMemsetAsync(work, 0, sizeof(int), ctx->stream));
+    {
+        Timed t(ctx, any ? K_TRACE_ANY : K_TRACE_CLOSEST, nullptr, n);
+        int grid = std::min(s->traceGrid, (n + 255) / 256);
+        mcrt::launch_trace_rays(any, trace_ctx(s), rays, n, work, hits, occl, std::max(grid, 1), ctx->stream);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_trace_closest(mcrt_scene s, const mcrt_ray* d_rays, int32_t n, mcrt_intersection* d_hits) {
+    return trace_common(s, d_rays, n, d_hits, nullptr, false);
+}
+
+MCRT_API mcrt_status mcrt_trace_any(mcrt_scene s, const mcrt_ray* d_rays, int32_t n, int32_t* d_hits) {
+    return trace_common(s, d_rays, n, nullptr, d_hits, true);
+}
+
+// ---------------------------------------------------------------------------
+// frame buffer + integrator
+// ---------------------------------------------------------------------------
+static void fb_free(mcrt_framebuffer fb) {
+    void* ptrs[] = {fb->radiance, fb->wsum, fb->wts, fb->image, fb->hitsP, fb->hitsE, fb->eO[0], fb->eO[1],
+                    fb->eD[0],    fb->eD[1], fb->eT[0], fb->eT[1], fb->sO,   fb->sD,   fb->sL,    fb->counters};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint32_t height, mcrt_framebuffer* out) {
+    if (!ctx || !out || width == 0 || height == 0 || (uint64_t)width * height > (1ull << 30))
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "invalid frame buffer size");
+    hipSetDevice(ctx->device);
+    auto* fb = new mcrt_framebuffer_s();
+    fb->ctx = ctx;
+    fb->W = width;
+    fb->H = height;
+    fb->N = (size_t)width * height;
+    const size_t N = fb->N;
+    hipError_t e = hipSuccess;
+    auto A = [&](auto** p, size_t bytes) {
+        if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
+    };
+    A(&fb->radiance, 16 * N);
+    A(&fb->wsum, 16 * N);
+    A(&fb->wts, 4 * N);
+    A(&fb->image, 16 * N);
+    A(&fb->hitsP, 16 * N);
+    A(&fb->hitsE, 16 * N);
+    for (int i = 0; i < 2; ++i) { A(&fb->eO[i], 16 * N); A(&fb->eD[i], 16 * N); A(&fb->eT[i], 16 * N); }
+    A(&fb->sO, 16 * N);
+    A(&fb->sD, 16 * N);
+    A(&fb->sL, 16 * N);
+    A(&fb->counters, 256 * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(fb->radiance, 0, 16 * N);
+    if (e == hipSuccess) e = hipMemset(fb->wsum, 0, 16 * N);
+    if (e == hipSuccess) e = hipMemset(fb->wts, 0, 4 * N);
+    if (e == hipSuccess) e = hipMemset(fb->image, 0, 16 * N);
+    if (e == hipSuccess) e = hipMemset(fb->counters, 0, 256 * sizeof(int));
+    if (e != hipSuccess) {
+        fb_free(fb);
+        delete fb;
+        return fail(ctx, e == hipErrorOutOfMemory ? MCRT_ERROR_OUT_OF_MEMORY : MCRT_ERROR_DEVICE,
+                    std::string("frame buffer: ") + hipGetErrorString(e));
+    }
+    *out = fb;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_destroy(mcrt_framebuffer fb) {
+    if (!fb) return MCRT_OK;
+    hipSetDevice(fb->ctx->device);
+    hipStreamSynchronize(fb->ctx->stream);
+    fb_free(fb);
+    delete fb;
+    return MCRT_OK;
+}
+
+static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArgs& f, std::string& err) {
+    f.W = fb->W;
+    f.H = fb->H;
+    f.frame = p->frame_index;
+    f.maxDepth = p->max_depth;
+    f.sampler = p->sampler;
+    f.russianRoulette = p->russian_roulette;
+    f.rrStartDepth = p->rr_start_depth;
+    f.numBands = p->num_bands <= 0 ? 1 : p->num_bands;
+    f.bandIndex = p->band_index;
+    f.bandRows = f.numBands == 1 ? 8 : p->band_rows;
+    if (f.bandRows <= 0 || (f.bandRows & 7) != 0) { err = "band_rows must be a positive multiple of 8"; return false; }
+    if (f.bandIndex < 0 || f.bandIndex >= f.numBands) { err = "band_index out of range"; return false; }
+    f.tilesX = (int)((fb->W + 7) / 8);
+    // row-blocks (8 rows) of this band set inside the image
+    const int blocksTotal = (int)((fb->H + 7) / 8);
+    const int bpb = f.bandRows / 8;
+    int myBlocks = 0;
+    for (int gb = 0; gb < blocksTotal; ++gb)
+        if ((gb / bpb) % f.numBands == f.bandIndex) ++myBlocks;
+    // tile ids are dealt in the kernel as tb -> gb; count the band-local blocks that map inside
+    f.numTiles = myBlocks * f.tilesX;
+    return true;
+}
+
+MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cam,
+                                       const mcrt_frame_params* p) {
+    if (!s || !fb || !cam || !p) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    mcrt_ctx ctx = s->ctx;
+    if (fb->ctx != ctx) return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame buffer belongs to another context");
+    if (!s->dNodes) return fail(ctx, MCRT_ERROR_NOT_READY, "mcrt_accel_build has not been called");
+    if (cam->width != fb->W || cam->height != fb->H)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "camera size differs from the frame buffer");
+    if (p->max_depth < 1 || p->max_depth > MCRT_MAX_BOUNCES) return fail(ctx, MCRT_ERROR_INVALID_ARG, "max_depth out of range");
+    if (p->sampler != MCRT_SAMPLER_RANDOM && p->sampler != MCRT_SAMPLER_SOBOL)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "unknown sampler");
+    if (p->sampler == MCRT_SAMPLER_SOBOL && !s->hasSobol)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "Sobol sampler requires the 1024x52 Sobol matrices in the scene");
+    FrameArgs f;
+    std::string err;
+    if (!frame_args(fb, p, f, err)) return fail(ctx, MCRT_ERROR_INVALID_ARG, err);
+    hipSetDevice(ctx->device);
+    hipStream_t st = ctx->stream;
+    fb->lastMaxDepth = p->max_depth;
+    fb->lastPixels = 0;
+    fb->bands = f;
+    fb->haveBands = true;
+    // camera goes to device through a kernel argument copy (no host sync, no staging race)
+    mcrt_camera* dCam = reinterpret_cast<mcrt_camera*>(fb->counters + 128);   // 176 B slot after the counters
+    HIPCHK(ctx, hipMemcpyAsync(dCam, cam, sizeof(mcrt_camera), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemsetAsync(fb->counters, 0, 128 * sizeof(int), st));
+    int* shadowCnt = fb->counters;          // [b]
+    int* extCnt = fb->counters + 32;        // [b]
+    int* work = fb->counters + 64;          // [0] primary, [1+2b] shadow, [2+2b] extend
+    const TraceCtx tc = trace_ctx(s);
+    const SceneArgs sa = scene_args(s);
+    if (s->numLights == 0) {   // RTPathTracingPass.cpp:42: no lights -> pass skipped; radiance = 0 here
+        HIPCHK(ctx, hipMemsetAsync(fb->radiance, 0, 16 * fb->N, st));
+        return MCRT_OK;
+    }
+    const int grid = s->traceGrid;
+    {
+        Timed t(ctx, K_PRIMARY, nullptr, (int64_t)f.numTiles * 64);
+        mcrt::launch_primary(tc, f, dCam, work + 0, fb->hitsP, grid, st);
+    }
+    for (int b = 0; b < p->max_depth; ++b) {
+        QueueArgs q;
+        q.shadowCount = shadowCnt + b;
+        q.sO = fb->sO; q.sD = fb->sD; q.sL = fb->sL;
+        q.extCountOut = extCnt + b;
+        q.eOout = fb->eO[b & 1]; q.eDout = fb->eD[b & 1]; q.eTout = fb->eT[b & 1];
+        if (b == 0) {
+            Timed t(ctx, K_SHADE0, nullptr, (int64_t)f.numTiles * 64);
+            mcrt::launch_shade0(sa, f, dCam, fb->hitsP, fb->radiance, q, st);
+        } else {
+            {
+                Timed t(ctx, K_EXTEND, extCnt + b - 1, 0);
+                mcrt::launch_extend(tc, extCnt + b - 1, work + 2 + 2 * b, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1],
+                                    fb->hitsE, grid, st);
+            }
+            Timed t(ctx, K_SHADEN, extCnt + b - 1, 0);
+            mcrt::launch_shadeN(sa, f, b, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1],
+                                fb->eT[(b - 1) & 1], fb->hitsE, fb->radiance, q, (int)fb->N, st);
+        }
+        {
+            Timed t(ctx, K_SHADOW, shadowCnt + b, 0);
+            mcrt::launch_shadow(tc, shadowCnt + b, work + 1 + 2 * b, fb->sO, fb->sD, fb->sL, fb->radiance, grid, st);
+        }
+    }
+    HIPCHK(ctx, hipGetLastError());
+    fb->lastPixels = (int64_t)f.numTiles * 64;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* filter, int32_t frame_index) {
+    if (!fb || !filter) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    mcrt_ctx ctx = fb->ctx;
+    if (!fb->haveBands) {   // no frame rendered yet: whole image
+        mcrt_frame_params p;
+        std::memset(&p, 0, sizeof(p));
+        p.num_bands = 1;
+        std::string err;
+        frame_args(fb, &p, fb->bands, err);
+        fb->haveBands = true;
+    }
+    hipSetDevice(ctx->device);
+    {
+        Timed t(ctx, K_ACCUM, nullptr, (int64_t)fb->bands.numTiles * 64);
+        mcrt::launch_accumulate(fb->bands, frame_index, filter_weight(*filter), fb->radiance, fb->wsum, fb->wts,
+                                fb->image, ctx->stream);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_device_ptrs(mcrt_framebuffer fb, void** radiance, void** weighted_sum,
+                                                  void** weight_sum, void** image) {
+    if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
+    if (radiance) *radiance = fb->radiance;
+    if (weighted_sum) *weighted_sum = fb->wsum;
+    if (weight_sum) *weight_sum = fb->wts;
+    if (image) *image = fb->image;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float* host_rgba) {
+    if (!fb || !host_rgba || which < 0 || which > 2) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    const void* src = which == 0 ? (const void*)fb->radiance : which == 1 ? (const void*)fb->wsum : (const void*)fb->image;
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpy(host_rgba, src, 16 * fb->N, hipMemcpyDeviceToHost));
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closest_rays, int64_t* any_rays,
+                                            int64_t* shaded_paths) {
+    if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    int c[64];
+    HIPCHK(ctx, hipMemcpy(c, fb->counters, sizeof(c), hipMemcpyDeviceToHost));
+    int64_t cl = fb->lastPixels, an = 0, sh = fb->lastPixels;
+    for (int b = 0; b < fb->lastMaxDepth; ++b) {
+        an += c[b];
+        if (b + 1 < fb->lastMaxDepth) { cl += c[32 + b]; sh += c[32 + b]; }
+    }
+    if (closest_rays) *closest_rays = cl;
+    if (any_rays) *any_rays = an;
+    if (shaded_paths) *shaded_paths = sh;
+    return MCRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// host camera helper (RTPrimaryRaysPass::generatePrimaryRays + RTUtil::screenToRay)
+// ---------------------------------------------------------------------------
+MCRT_API mcrt_status mcrt_make_pinhole_camera(const float pos[3], const float forward[3], const float up[3],
+                                              float fov_y_deg, float near_z, float far_z, uint32_t width,
+                                              uint32_t height, const float pixel_offset[2], mcrt_camera* out) {
+    if (!pos || !forward || !up || !out || width == 0 || height == 0 || !(far_z > near_z))
+        return fail(nullptr, MCRT_ERROR_INVALID_ARG, "invalid camera");
+    double f[3] = {forward[0], forward[1], forward[2]};
+    double fl = std::sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+    for (double& x : f) x /= fl;
+    double u0[3] = {up[0], up[1], up[2]};
+    double s[3] = {u0[1] * f[2] - u0[2] * f[1], u0[2] * f[0] - u0[0] * f[2], u0[0] * f[1] - u0[1] * f[0]};
+    double sl = std::sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+    for (double& x : s) x /= sl;
+    double u[3] = {f[1] * s[2] - f[2] * s[1], f[2] * s[0] - f[0] * s[2], f[0] * s[1] - f[1] * s[0]};
+    double V[4][4] = {{s[0], s[1], s[2], -(s[0] * pos[0] + s[1] * pos[1] + s[2] * pos[2])},
+                      {u[0], u[1], u[2], -(u[0] * pos[0] + u[1] * pos[1] + u[2] * pos[2])},
+                      {f[0], f[1], f[2], -(f[0] * pos[0] + f[1] * pos[1] + f[2] * pos[2])},
+                      {0, 0, 0, 1}};
+    const double t = std::tan(fov_y_deg * 3.14159265358979323846 / 360.0), aspect = (double)width / height;
+    double P[4][4] = {{1.0 / (aspect * t), 0, 0, 0}, {0, 1.0 / t, 0, 0},
+                      {0, 0, (far_z + near_z) / (far_z - near_z), -(2.0 * far_z * near_z) / (far_z - near_z)},
+                      {0, 0, 1, 0}};
+    double VP[4][4], M[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            VP[i][j] = 0;
+            for (int k = 0; k < 4; ++k) VP[i][j] += P[i][k] * V[k][j];
+        }
+    const double ox = pixel_offset ? pixel_offset[0] / width : 0.0, oy = pixel_offset ? pixel_offset[1] / height : 0.0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) M[i][j] = VP[i][j] + (i == 0 ? ox * VP[3][j] : i == 1 ? oy * VP[3][j] : 0.0);
+    // invert M (Gauss-Jordan)
+    double A[4][8];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 8; ++j) A[i][j] = j < 4 ? M[i][j] : (j - 4 == i ? 1.0 : 0.0);
+    for (int c = 0; c < 4; ++c) {
+        int pr = c;
+        for (int r = c + 1; r < 4; ++r)
+            if (std::fabs(A[r][c]) > std::fabs(A[pr][c])) pr = r;
+        for (int j = 0; j < 8; ++j) std::swap(A[c][j], A[pr][j]);
+        const double d = A[c][c];
+        if (d == 0.0) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "singular camera matrix");
+        for (int j = 0; j < 8; ++j) A[c][j] /= d;
+        for (int r = 0; r < 4; ++r)
+            if (r != c) {
+                const double m = A[r][c];
+                for (int j = 0; j < 8; ++j) A[r][j] -= m * A[c][j];
+            }
+    }
+    auto ray = [&](double sx, double sy, mcrt_float4& o) {
+        const double nx = sx / width * 2.0 - 1.0, ny = sy / height * 2.0 - 1.0;
+        double a[4] = {nx, ny, -1.0, 1.0}, b[4] = {nx, ny, 1.0, 1.0}, ra[4] = {}, rb[4] = {};
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) { ra[i] += A[i][4 + j] * a[j]; rb[i] += A[i][4 + j] * b[j]; }
+        double d[3];
+        for (int i = 0; i < 3; ++i) d[i] = rb[i] / rb[3] - ra[i] / ra[3];
+        const double l = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+        o.x = (float)(d[0] / l); o.y = (float)(d[1] / l); o.z = (float)(d[2] / l); o.w = 0.0f;
+    };
+    std::memset(out, 0, sizeof(*out));
+    float* wc = &out->worldToClip.m0.x;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) wc[4 * i + j] = (float)VP[i][j];
+    ray(0, 0, out->r00);
+    ray(width, 0, out->r10);
+    ray(width, height, out->r11);
+    ray(0, height, out->r01);
+    out->pos.x = pos[0]; out->pos.y = pos[1]; out->pos.z = pos[2];
+    out->direction.x = (float)f[0]; out->direction.y = (float)f[1]; out->direction.z = (float)f[2];
+    out->width = width;
+    out->height = height;
+    out->area = (float)((2.0 * t * aspect) * (2.0 * t));
+    return MCRT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,81 @@
+// mcrt_internal.h -- structures shared by the host runtime (mcrt_capi.cpp) and the
+// HIP kernels (mcrt_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <cstddef>
+
+#include "../../include/mcrt_capi.h"
+
+// Device view of the scene (the 15 SCENE_PARAMS arrays + our BVH).
+struct SceneArgs {
+    const mcrt_shape* shapes;
+    const uint32_t* indices;
+    const float4* positions;
+    const float2* uvs;
+    const float4* normals;
+    const mcrt_texture_desc* textures;
+    const uint8_t* texData;
+    const uint32_t* sobol;
+    const mcrt_light* lights;
+    const mcrt_material* materials;
+    const float4* tris;   // 3 float4 per triangle: (v0, shape), (e1, prim), (e2, -)
+    int numLights;
+};
+
+struct FrameArgs {
+    uint32_t W, H;
+    int frame, maxDepth, sampler;
+    int russianRoulette, rrStartDepth;
+    int bandRows, numBands, bandIndex;
+    int tilesX, numTiles;   // 8x8 tiles of this rank's bands
+};
+
+struct QueueArgs {
+    int* shadowCount;
+    float4 *sO, *sD, *sL;
+    int* extCountOut;
+    float4 *eOout, *eDout, *eTout;
+};
+
+struct TraceCtx {
+    const float4* nodes;   // 4 float4 per node: x-slabs c0, x/y c1, z c0|c1, children
+    const float4* tris;
+    uint32_t* spill;
+    int spillCap;           // spill entries per lane
+    int* overflow;
+};
+
+namespace mcrt {
+void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, int* work, mcrt_intersection* hits,
+                       int* occl, int grid, hipStream_t st);
+void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, int* work, float4* hits, int grid,
+                    hipStream_t st);
+void launch_extend(const TraceCtx& c, const int* count, int* work, const float4* qO, const float4* qD, float4* hits,
+                   int grid, hipStream_t st);
+void launch_shadow(const TraceCtx& c, const int* count, int* work, const float4* sO, const float4* sD,
+                   const float4* sL, float4* radiance, int grid, hipStream_t st);
+void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
+                   float4* radiance, const QueueArgs& q, hipStream_t st);
+void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,
+                   const float4* qD, const float4* qT, const float4* hits, float4* radiance, const QueueArgs& q,
+                   int maxCount, hipStream_t st);
+void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* radiance, float4* wsum, float* wts,
+                       float4* image, hipStream_t st);
+}  // namespace mcrt
+
+// Host BVH builder (mcrt_bvh.cpp)
+namespace mcrt {
+struct BvhOut {
+    // GPU layout
+    std::size_t numNodes = 0;
+    std::size_t numTris = 0;
+    float* nodes = nullptr;   // 16 floats per node
+    float* tris = nullptr;    // 12 floats per triangle
+    int depth = 0;
+};
+// world-space triangles (9 floats each), shape id / prim id per triangle
+bool build_bvh(const float* tri, const int32_t* shapeOf, const int32_t* primOf, std::size_t n, float cost, int bins,
+               bool sah, int threads, BvhOut& out);
+void free_bvh(BvhOut& out);
+}  // namespace mcrt

@@ -1,0 +1,230 @@
+"""ctypes binding of libmcrt.so (include/mcrt_capi.h) -- the product path.
+
+There is deliberately no fallback: if the HIP library is missing or no GPU is present,
+the calls raise.  Device memory for ray queries comes from torch tensors on cuda
+(torch is plumbing here), everything else lives inside the library.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import PKG_DIR
+from . import types as T
+
+LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libmcrt.so")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), "include", "mcrt_capi.h")
+
+_c = ctypes
+_vp = _c.c_void_p
+_lib = None
+
+# every entry point of include/mcrt_capi.h: name -> (restype, argtypes)
+SIGNATURES = {
+    "mcrt_version": (_c.c_char_p, []),
+    "mcrt_last_error": (_c.c_char_p, [_vp]),
+    "mcrt_ctx_create": (_c.c_int, [_c.c_int, _c.POINTER(_vp)]),
+    "mcrt_ctx_destroy": (_c.c_int, [_vp]),
+    "mcrt_ctx_synchronize": (_c.c_int, [_vp]),
+    "mcrt_ctx_set_stream": (_c.c_int, [_vp, _vp]),
+    "mcrt_ctx_set_profiling": (_c.c_int, [_vp, _c.c_int]),
+    "mcrt_ctx_kernel_stats": (_c.c_int, [_vp, _c.c_int, _vp, _vp, _vp, _vp, _c.POINTER(_c.c_int)]),
+    "mcrt_ctx_reset_stats": (_c.c_int, [_vp]),
+    "mcrt_scene_create": (_c.c_int, [_vp, _vp, _c.POINTER(_vp)]),
+    "mcrt_scene_destroy": (_c.c_int, [_vp]),
+    "mcrt_scene_update_lights": (_c.c_int, [_vp, _vp, _c.c_uint32]),
+    "mcrt_scene_update_materials": (_c.c_int, [_vp, _vp, _c.c_uint32]),
+    "mcrt_scene_update_shapes": (_c.c_int, [_vp, _vp, _c.c_uint32]),
+    "mcrt_accel_build": (_c.c_int, [_vp, _vp]),
+    "mcrt_accel_info": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "mcrt_trace_closest": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
+    "mcrt_trace_any": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
+    "mcrt_framebuffer_create": (_c.c_int, [_vp, _c.c_uint32, _c.c_uint32, _c.POINTER(_vp)]),
+    "mcrt_framebuffer_destroy": (_c.c_int, [_vp]),
+    "mcrt_render_frame": (_c.c_int, [_vp, _vp, _vp, _vp]),
+    "mcrt_accumulate": (_c.c_int, [_vp, _vp, _c.c_int32]),
+    "mcrt_framebuffer_device_ptrs": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "mcrt_framebuffer_read": (_c.c_int, [_vp, _c.c_int, _vp]),
+    "mcrt_framebuffer_stats": (_c.c_int, [_vp, _vp, _vp, _vp]),
+    "mcrt_make_pinhole_camera": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _c.c_float, _c.c_float, _c.c_uint32,
+                                            _c.c_uint32, _vp, _vp]),
+}
+
+
+class MCRTError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MCRTError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                            "(make -C monte-carlo-raytracer_amd/csrc); there is no CPU fallback")
+        L = _c.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(status, ctx=None):
+    if status != 0:
+        msg = lib().mcrt_last_error(ctx)
+        raise MCRTError(f"mcrt status {status}: {msg.decode() if msg else ''}")
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class Context:
+    def __init__(self, device=0, profiling=False):
+        h = _vp()
+        _check(lib().mcrt_ctx_create(device, _c.byref(h)))
+        self.h = h
+        if profiling:
+            self.set_profiling(True)
+
+    def close(self):
+        if self.h:
+            lib().mcrt_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        _check(lib().mcrt_ctx_synchronize(self.h), self.h)
+
+    def set_stream(self, stream_ptr):
+        _check(lib().mcrt_ctx_set_stream(self.h, stream_ptr), self.h)
+
+    def set_profiling(self, on=True):
+        _check(lib().mcrt_ctx_set_profiling(self.h, 1 if on else 0), self.h)
+
+    def reset_stats(self):
+        _check(lib().mcrt_ctx_reset_stats(self.h), self.h)
+
+    def kernel_stats(self):
+        n = 16
+        names = (_c.c_char_p * n)()
+        ms = np.zeros(n, np.float64)
+        launches = np.zeros(n, np.int64)
+        items = np.zeros(n, np.int64)
+        cnt = _c.c_int()
+        _check(lib().mcrt_ctx_kernel_stats(self.h, n, names, _p(ms), _p(launches), _p(items), _c.byref(cnt)), self.h)
+        return {names[i].decode(): {"ms": float(ms[i]), "launches": int(launches[i]), "items": int(items[i])}
+                for i in range(cnt.value)}
+
+
+class DeviceScene:
+    def __init__(self, ctx, scene, build=True, cost=10.0, bins=64, sah=True):
+        self.ctx = ctx
+        self.scene = scene
+        self._desc = scene.desc()
+        h = _vp()
+        _check(lib().mcrt_scene_create(ctx.h, _c.byref(self._desc), _c.byref(h)), ctx.h)
+        self.h = h
+        if build:
+            self.build(cost, bins, sah)
+
+    def build(self, cost=10.0, bins=64, sah=True):
+        opts = T.AccelOpts(cost, bins, 1 if sah else 0)
+        _check(lib().mcrt_accel_build(self.h, _c.byref(opts)), self.ctx.h)
+
+    def info(self):
+        nn, nb, ms, nt = _c.c_uint64(), _c.c_uint64(), _c.c_double(), _c.c_uint32()
+        _check(lib().mcrt_accel_info(self.h, _c.byref(nn), _c.byref(nb), _c.byref(ms), _c.byref(nt)), self.ctx.h)
+        return {"nodes": nn.value, "bytes": nb.value, "build_ms": ms.value, "triangles": nt.value}
+
+    def update_lights(self, lights):
+        self._lights = np.ascontiguousarray(lights)
+        _check(lib().mcrt_scene_update_lights(self.h, _p(self._lights), len(self._lights)), self.ctx.h)
+
+    def update_materials(self, mats):
+        self._mats = np.ascontiguousarray(mats)
+        _check(lib().mcrt_scene_update_materials(self.h, _p(self._mats), len(self._mats)), self.ctx.h)
+
+    def trace_closest(self, rays_dev_ptr, n, hits_dev_ptr):
+        _check(lib().mcrt_trace_closest(self.h, rays_dev_ptr, n, hits_dev_ptr), self.ctx.h)
+
+    def trace_any(self, rays_dev_ptr, n, out_dev_ptr):
+        _check(lib().mcrt_trace_any(self.h, rays_dev_ptr, n, out_dev_ptr), self.ctx.h)
+
+    def close(self):
+        if self.h:
+            lib().mcrt_scene_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class FrameBuffer:
+    def __init__(self, ctx, width, height):
+        self.ctx = ctx
+        self.W, self.H = width, height
+        h = _vp()
+        _check(lib().mcrt_framebuffer_create(ctx.h, width, height, _c.byref(h)), ctx.h)
+        self.h = h
+
+    def render(self, dscene, cam, frame=0, max_depth=2, sampler=T.SAMPLER_RANDOM, rr=False, rr_start=3,
+               band_rows=8, num_bands=1, band_index=0):
+        p = T.FrameParams(frame, max_depth, sampler, 1 if rr else 0, rr_start, band_rows, num_bands, band_index)
+        cam = np.ascontiguousarray(cam)
+        _check(lib().mcrt_render_frame(dscene.h, self.h, _p(cam), _c.byref(p)), self.ctx.h)
+
+    def accumulate(self, filt, frame):
+        filt = np.ascontiguousarray(filt)
+        _check(lib().mcrt_accumulate(self.h, _p(filt), frame), self.ctx.h)
+
+    def read(self, which=0):
+        out = np.zeros((self.H, self.W, 4), np.float32)
+        _check(lib().mcrt_framebuffer_read(self.h, which, _p(out)), self.ctx.h)
+        return out
+
+    def device_ptrs(self):
+        r, s, w, i = _vp(), _vp(), _vp(), _vp()
+        _check(lib().mcrt_framebuffer_device_ptrs(self.h, _c.byref(r), _c.byref(s), _c.byref(w), _c.byref(i)),
+               self.ctx.h)
+        return r.value, s.value, w.value, i.value
+
+    def stats(self):
+        a, b, c = _c.c_int64(), _c.c_int64(), _c.c_int64()
+        _check(lib().mcrt_framebuffer_stats(self.h, _c.byref(a), _c.byref(b), _c.byref(c)), self.ctx.h)
+        return {"closest_rays": a.value, "any_rays": b.value, "shaded_paths": c.value}
+
+    def close(self):
+        if self.h:
+            lib().mcrt_framebuffer_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_pinhole_camera(pos, forward, up, fovy, near, far, width, height, pixel_offset=(0.0, 0.0)):
+    cam = np.zeros(1, T.CAMERA_DTYPE)
+    a = [np.asarray(v, np.float32) for v in (pos, forward, up, pixel_offset)]
+    _check(lib().mcrt_make_pinhole_camera(_p(a[0]), _p(a[1]), _p(a[2]), fovy, near, far, width, height, _p(a[3]),
+                                          _p(cam)))
+    return cam
+
+
+def header_symbols():
+    """Entry points declared in include/mcrt_capi.h (MCRT_API lines)."""
+    import re
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"MCRT_API\s+[\w\s\*]+?\b(mcrt_\w+)\s*\(", txt)))

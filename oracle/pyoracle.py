@@ -257,3 +257,81 @@ def ref_load_obj(path):
         shapes.append((P, I))
     L.rr_obj_free(h)
     return shapes
+
+
+# --------------------------------------------------------------------------
+# oracle/_ref on the GPU box: the reference's OpenCL kernels (PathTracing.cl,
+# reconstruction.cl, RadeonRays intersect_bvh2_lds.cl) compiled for gfx950,
+# run through the ROCm OpenCL runtime by oracle/_ref/clref_runner.so.
+# --------------------------------------------------------------------------
+CLREF_LIB = os.path.join(HERE, "_ref", "clref_runner.so")
+_clref = None
+
+
+def clref_available():
+    return os.path.exists(CLREF_LIB)
+
+
+def clref(variant="ieee"):
+    global _clref
+    if _clref is None:
+        L = _load(CLREF_LIB)
+        L.clref_error.restype = _c.c_char_p
+        L.clref_device.restype = _c.c_char_p
+        L.clref_init.argtypes = [_c.c_char_p, _c.c_char_p]
+        L.clref_scene_create.restype = _vp
+        L.clref_scene_create.argtypes = [_vp, _vp, _c.c_int64]
+        L.clref_render.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _vp, _vp]
+        L.clref_accumulate.argtypes = [_vp, _c.c_int, _vp, _vp]
+        L.clref_trace.argtypes = [_vp, _vp, _c.c_int, _vp, _c.c_int]
+        st = L.clref_init(os.path.join(HERE, "_ref").encode(), variant.encode())
+        if st != 0:
+            raise RuntimeError(f"clref_init({variant}) = {st}: {L.clref_error().decode()}")
+        _clref = L
+    return _clref
+
+
+class CLRefScene:
+    """A scene on the reference OpenCL pipeline; BVH nodes from the reference Bvh2 builder
+    (librrref.so) when available, else from the oracle's bit-identical restatement."""
+
+    def __init__(self, scene, variant="ieee", nodes=None):
+        self.L = clref(variant)
+        self.scene = scene
+        self._desc = scene.desc()
+        if nodes is None:
+            o = OracleScene(scene)
+            o.build()
+            nodes = o.nodes()
+        self.nodes = np.ascontiguousarray(nodes)
+        self.h = self.L.clref_scene_create(ctypes.byref(self._desc), _p(self.nodes), len(self.nodes))
+        if not self.h:
+            raise RuntimeError(self.L.clref_error().decode())
+
+    def render(self, cam, frame=0, max_depth=2):
+        W, H = int(cam["width"][0]), int(cam["height"][0])
+        out = np.zeros((H, W, 4), np.float32)
+        st = self.L.clref_render(self.h, _p(cam), frame, max_depth, _p(out), None)
+        if st != 0:
+            raise RuntimeError(f"clref_render {st}: {self.L.clref_error().decode()}")
+        return out
+
+    def accumulate(self, frame, filt, H, W):
+        img = np.zeros((H, W, 4), np.float32)
+        st = self.L.clref_accumulate(self.h, frame, _p(filt), _p(img))
+        if st != 0:
+            raise RuntimeError(f"clref_accumulate {st}: {self.L.clref_error().decode()}")
+        return img
+
+    def trace(self, rays, any_hit=False, init=-7):
+        from mcrt.types import ISECT_DTYPE
+        if any_hit:
+            out = np.full(len(rays), init, np.int32)
+        else:
+            out = np.zeros(len(rays), ISECT_DTYPE)
+            out["shapeid"] = init
+            out["primid"] = init
+        st = self.L.clref_trace(self.h, _p(rays), len(rays), _p(out), 1 if any_hit else 0)
+        if st != 0:
+            raise RuntimeError(f"clref_trace {st}: {self.L.clref_error().decode()}")
+        return out

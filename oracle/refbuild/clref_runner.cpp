@@ -1,0 +1,334 @@
+// TEST INFRASTRUCTURE ONLY -- runs the REFERENCE's own OpenCL kernels on the GPU box.
+//
+// The code objects in oracle/_ref/clref_*.hsaco are the reference's assets/kernels/PathTracing.cl,
+// reconstruction.cl and RadeonRays' intersect_bvh2_lds.cl, compiled here for gfx950 by ROCm clang
+// against ROCm's OpenCL device libraries (oracle/refbuild/Makefile).  This host driver (ours)
+// loads them through the ROCm OpenCL runtime (clCreateProgramWithBinary) and replays the
+// reference's host launch sequence:
+//   RTPrimaryRaysPass::update   (RTPrimaryRaysPass.cpp:32-67): GeneratePerspectiveRays, intersect_main
+//   RTPathTracingPass::update   (RTPathTracingPass.cpp:40-114): per bounce PathTracing, occluded_main,
+//                                ShadowPass, intersect_main
+//   RTReconstructionPass        (RTReconstructionPass.cpp:71-123): ReconstructionPass
+// with 8x8 work-groups for application kernels and 64-wide groups for RadeonRays
+// (IntersectorLDS::Intersect, intersector_lds.cpp:266-295).  The BVH node array is the
+// reference builder's (oracle/_ref/librrref.so = RadeonRays bvh2.cpp).
+#define CL_TARGET_OPENCL_VERSION 120
+#include <CL/cl.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "../../include/mcrt_capi.h"
+
+namespace {
+std::string g_err;
+
+bool ok(cl_int e, const char* what) {
+    if (e != CL_SUCCESS) {
+        g_err = std::string(what) + " failed: " + std::to_string(e);
+        return false;
+    }
+    return true;
+}
+
+std::vector<unsigned char> readFile(const std::string& p) {
+    std::ifstream f(p, std::ios::binary);
+    return std::vector<unsigned char>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+struct Runtime {
+    cl_platform_id plat = nullptr;
+    cl_device_id dev = nullptr;
+    cl_context ctx = nullptr;
+    cl_command_queue q = nullptr;
+    cl_program pt = nullptr, rr = nullptr, recon = nullptr;
+    cl_kernel kGen = nullptr, kPT = nullptr, kShadow = nullptr, kIsect = nullptr, kOccl = nullptr, kRecon = nullptr;
+    std::string deviceName;
+} R;
+
+cl_program loadProgram(const std::string& path) {
+    auto bin = readFile(path);
+    if (bin.empty()) { g_err = "cannot read " + path; return nullptr; }
+    size_t len = bin.size();
+    const unsigned char* p = bin.data();
+    cl_int st = 0, e = 0;
+    cl_program prog = clCreateProgramWithBinary(R.ctx, 1, &R.dev, &len, &p, &st, &e);
+    if (!ok(e, "clCreateProgramWithBinary") || !ok(st, "binary status")) return nullptr;
+    e = clBuildProgram(prog, 1, &R.dev, "", nullptr, nullptr);
+    if (e != CL_SUCCESS) {
+        size_t n = 0;
+        clGetProgramBuildInfo(prog, R.dev, CL_PROGRAM_BUILD_LOG, 0, nullptr, &n);
+        std::string log(n, '\0');
+        clGetProgramBuildInfo(prog, R.dev, CL_PROGRAM_BUILD_LOG, n, &log[0], nullptr);
+        g_err = "clBuildProgram(" + path + "): " + std::to_string(e) + " " + log;
+        return nullptr;
+    }
+    return prog;
+}
+
+cl_mem buf(size_t bytes, const void* host) {
+    cl_int e = 0;
+    if (bytes == 0) bytes = 16;
+    cl_mem m = clCreateBuffer(R.ctx, CL_MEM_READ_WRITE | (host ? CL_MEM_COPY_HOST_PTR : 0), bytes, (void*)host, &e);
+    if (!ok(e, "clCreateBuffer")) return nullptr;
+    if (!host) {
+        std::vector<unsigned char> z(bytes, 0);
+        clEnqueueWriteBuffer(R.q, m, CL_TRUE, 0, bytes, z.data(), 0, nullptr, nullptr);
+    }
+    return m;
+}
+
+struct Scene {
+    cl_mem shapes, indices, positions, uvs, normals, tangents, binormals, colors, textures, texData, sobol, lights,
+        materials, camera, nodes;
+    int numLights;
+    // per-resolution buffers
+    int W = 0, H = 0;
+    cl_mem rays = nullptr, rayDiff = nullptr, isect = nullptr, shadowRays = nullptr, occl = nullptr, thr = nullptr,
+           temp = nullptr, radiance = nullptr, stack = nullptr, count = nullptr, wsum = nullptr, wts = nullptr,
+           filter = nullptr, image = nullptr;
+};
+
+template <class T>
+cl_int arg(cl_kernel k, int i, const T& v) { return clSetKernelArg(k, i, sizeof(T), &v); }
+
+bool launch2D(cl_kernel k, int W, int H) {
+    size_t gs[2] = {(size_t)(W + 7) / 8 * 8, (size_t)(H + 7) / 8 * 8}, ls[2] = {8, 8};
+    return ok(clEnqueueNDRangeKernel(R.q, k, 2, nullptr, gs, ls, 0, nullptr, nullptr), "launch2D") &&
+           ok(clFinish(R.q), "clFinish");
+}
+bool launchRR(cl_kernel k, Scene* s, cl_mem rays, cl_mem out, int n) {
+    cl_int e = 0;
+    e |= arg(k, 0, s->nodes);
+    e |= arg(k, 1, rays);
+    e |= arg(k, 2, s->count);
+    e |= arg(k, 3, s->stack);
+    e |= arg(k, 4, out);
+    if (!ok(e, "set RR args")) return false;
+    size_t gs = (size_t)(n + 63) / 64 * 64, ls = 64;
+    return ok(clEnqueueNDRangeKernel(R.q, k, 1, nullptr, &gs, &ls, 0, nullptr, nullptr), "launchRR") &&
+           ok(clFinish(R.q), "clFinish");
+}
+bool ensureBuffers(Scene* s, int W, int H) {
+    if (s->W == W && s->H == H) return true;
+    cl_mem* old[] = {&s->rays, &s->rayDiff, &s->isect, &s->shadowRays, &s->occl, &s->thr, &s->temp, &s->radiance,
+                     &s->stack, &s->count, &s->wsum, &s->wts, &s->filter};
+    for (auto* m : old)
+        if (*m) clReleaseMemObject(*m), *m = nullptr;
+    if (s->image) clReleaseMemObject(s->image), s->image = nullptr;
+    size_t N = (size_t)W * H;
+    s->rays = buf(48 * N, nullptr);
+    s->rayDiff = buf(64 * N, nullptr);
+    s->isect = buf(32 * N, nullptr);
+    s->shadowRays = buf(48 * N, nullptr);
+    s->occl = buf(4 * N, nullptr);
+    s->thr = buf(32 * N, nullptr);
+    s->temp = buf(16 * N, nullptr);
+    s->radiance = buf(16 * N, nullptr);
+    s->stack = buf(4 * N * 64, nullptr);
+    int n = (int)N;
+    s->count = buf(4, &n);
+    s->wsum = buf(16 * N, nullptr);
+    s->wts = buf(4 * N, nullptr);
+    s->filter = buf(sizeof(mcrt_filter), nullptr);
+    cl_image_format fmt = {CL_RGBA, CL_FLOAT};
+    cl_int e = 0;
+    s->image = clCreateImage2D(R.ctx, CL_MEM_READ_WRITE, &fmt, W, H, 0, nullptr, &e);
+    if (!ok(e, "clCreateImage2D")) return false;
+    s->W = W;
+    s->H = H;
+    return s->rays && s->stack;
+}
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) const char* clref_error() { return g_err.c_str(); }
+
+__attribute__((visibility("default"))) const char* clref_device() { return R.deviceName.c_str(); }
+
+// variant: "fast" = the reference's build options (-cl-mad-enable -cl-fast-relaxed-math), "ieee" = none
+__attribute__((visibility("default"))) int clref_init(const char* dir, const char* variant) {
+    cl_uint np = 0;
+    if (!ok(clGetPlatformIDs(0, nullptr, &np), "clGetPlatformIDs") || np == 0) { g_err = "no OpenCL platform"; return -1; }
+    std::vector<cl_platform_id> ps(np);
+    clGetPlatformIDs(np, ps.data(), nullptr);
+    for (auto p : ps) {
+        cl_uint nd = 0;
+        if (clGetDeviceIDs(p, CL_DEVICE_TYPE_GPU, 0, nullptr, &nd) == CL_SUCCESS && nd > 0) {
+            R.plat = p;
+            clGetDeviceIDs(p, CL_DEVICE_TYPE_GPU, 1, &R.dev, nullptr);
+            break;
+        }
+    }
+    if (!R.dev) { g_err = "no OpenCL GPU device"; return -2; }
+    char name[256] = {0};
+    clGetDeviceInfo(R.dev, CL_DEVICE_NAME, sizeof(name), name, nullptr);
+    R.deviceName = name;
+    cl_int e = 0;
+    R.ctx = clCreateContext(nullptr, 1, &R.dev, nullptr, nullptr, &e);
+    if (!ok(e, "clCreateContext")) return -3;
+    R.q = clCreateCommandQueue(R.ctx, R.dev, 0, &e);
+    if (!ok(e, "clCreateCommandQueue")) return -4;
+    std::string d(dir);
+    R.pt = loadProgram(d + "/clref_pt_" + variant + ".hsaco");
+    R.rr = loadProgram(d + "/clref_rr.hsaco");
+    R.recon = loadProgram(d + "/clref_recon.hsaco");
+    if (!R.pt || !R.rr || !R.recon) return -5;
+    R.kGen = clCreateKernel(R.pt, "GeneratePerspectiveRays", &e);
+    if (!ok(e, "kernel GeneratePerspectiveRays")) return -6;
+    R.kPT = clCreateKernel(R.pt, "PathTracing", &e);
+    if (!ok(e, "kernel PathTracing")) return -6;
+    R.kShadow = clCreateKernel(R.pt, "ShadowPass", &e);
+    if (!ok(e, "kernel ShadowPass")) return -6;
+    R.kIsect = clCreateKernel(R.rr, "intersect_main", &e);
+    if (!ok(e, "kernel intersect_main")) return -6;
+    R.kOccl = clCreateKernel(R.rr, "occluded_main", &e);
+    if (!ok(e, "kernel occluded_main")) return -6;
+    R.kRecon = clCreateKernel(R.recon, "ReconstructionPass", &e);
+    if (!ok(e, "kernel ReconstructionPass")) return -6;
+    return 0;
+}
+
+// nodes: RadeonRays Bvh2 node array (64 B each) from the reference builder
+__attribute__((visibility("default"))) void* clref_scene_create(const mcrt_scene_desc* d, const void* nodes,
+                                                                int64_t num_nodes) {
+    auto* s = new Scene();
+    s->shapes = buf(sizeof(mcrt_shape) * d->num_shapes, d->shapes);
+    s->indices = buf(4ull * d->num_indices, d->indices);
+    s->positions = buf(16ull * d->num_vertices, d->positions);
+    s->uvs = buf(8ull * d->num_vertices, d->uvs);
+    s->normals = buf(16ull * d->num_vertices, d->normals);
+    s->tangents = buf(16ull * d->num_vertices, d->tangents);
+    s->binormals = buf(16ull * d->num_vertices, d->binormals);
+    s->colors = d->colors ? buf(16ull * d->num_vertices, d->colors) : buf(16, nullptr);
+    s->textures = d->num_textures ? buf(16ull * d->num_textures, d->textures) : buf(16, nullptr);
+    s->texData = d->tex_data_bytes ? buf(d->tex_data_bytes, d->tex_data) : buf(16, nullptr);
+    s->sobol = d->sobol_matrices ? buf(4ull * d->num_sobol_words, d->sobol_matrices) : buf(16, nullptr);
+    s->lights = d->num_lights ? buf(sizeof(mcrt_light) * d->num_lights, d->lights) : buf(16, nullptr);
+    s->materials = d->num_materials ? buf(sizeof(mcrt_material) * d->num_materials, d->materials) : buf(16, nullptr);
+    s->camera = buf(sizeof(mcrt_camera), nullptr);
+    s->nodes = buf(64ull * num_nodes, nodes);
+    s->numLights = (int)d->num_lights;
+    if (!s->shapes || !s->nodes) { delete s; return nullptr; }
+    return s;
+}
+
+static bool setSceneArgs(cl_kernel k, Scene* s, int& a) {   // RTScene::setSceneArgs, RTScene.cpp:178-197
+    cl_int e = 0;
+    e |= arg(k, a++, s->shapes);
+    e |= arg(k, a++, s->indices);
+    e |= arg(k, a++, s->positions);
+    e |= arg(k, a++, s->uvs);
+    e |= arg(k, a++, s->normals);
+    e |= arg(k, a++, s->tangents);
+    e |= arg(k, a++, s->binormals);
+    e |= arg(k, a++, s->colors);
+    e |= arg(k, a++, s->textures);
+    e |= arg(k, a++, s->texData);
+    e |= arg(k, a++, s->sobol);
+    e |= arg(k, a++, s->lights);
+    e |= arg(k, a++, s->numLights);
+    e |= arg(k, a++, s->materials);
+    e |= arg(k, a++, s->camera);
+    return ok(e, "scene args");
+}
+
+// One frame (RTPrimaryRaysPass + RTPathTracingPass); radiance_out: W*H float4 ("RadianceBufferCL").
+__attribute__((visibility("default"))) int clref_render(void* sp, const mcrt_camera* cam, int frame, int maxDepth,
+                                                        float* radiance_out, double* ms_out) {
+    Scene* s = (Scene*)sp;
+    const int W = (int)cam->width, H = (int)cam->height;
+    if (!ensureBuffers(s, W, H)) return -1;
+    if (!ok(clEnqueueWriteBuffer(R.q, s->camera, CL_TRUE, 0, sizeof(mcrt_camera), cam, 0, nullptr, nullptr), "camera"))
+        return -1;
+    cl_int e = 0;
+    e |= arg(R.kGen, 0, s->rays);
+    e |= arg(R.kGen, 1, s->rayDiff);
+    e |= arg(R.kGen, 2, s->camera);
+    if (!ok(e, "gen args") || !launch2D(R.kGen, W, H)) return -2;
+    if (!launchRR(R.kIsect, s, s->rays, s->isect, W * H)) return -3;
+    for (int b = 0; b < maxDepth; ++b) {
+        int a = 0;
+        if (!setSceneArgs(R.kPT, s, a)) return -4;
+        e = 0;
+        e |= arg(R.kPT, a++, W);
+        e |= arg(R.kPT, a++, H);
+        e |= arg(R.kPT, a++, s->shadowRays);
+        e |= arg(R.kPT, a++, s->rays);
+        e |= arg(R.kPT, a++, s->isect);
+        e |= arg(R.kPT, a++, frame);
+        e |= arg(R.kPT, a++, maxDepth);
+        e |= arg(R.kPT, a++, b);
+        e |= arg(R.kPT, a++, s->temp);
+        e |= arg(R.kPT, a++, s->thr);
+        if (!ok(e, "PT args") || !launch2D(R.kPT, W, H)) return -5;
+        if (!launchRR(R.kOccl, s, s->shadowRays, s->occl, W * H)) return -6;
+        e = 0;
+        e |= arg(R.kShadow, 0, s->shadowRays);
+        e |= arg(R.kShadow, 1, s->occl);
+        e |= arg(R.kShadow, 2, W);
+        e |= arg(R.kShadow, 3, H);
+        e |= arg(R.kShadow, 4, b);
+        e |= arg(R.kShadow, 5, s->thr);
+        e |= arg(R.kShadow, 6, s->temp);
+        e |= arg(R.kShadow, 7, s->radiance);
+        if (!ok(e, "shadow args") || !launch2D(R.kShadow, W, H)) return -7;
+        if (b + 1 < maxDepth && !launchRR(R.kIsect, s, s->rays, s->isect, W * H)) return -8;
+    }
+    clFinish(R.q);
+    (void)ms_out;
+    if (radiance_out &&
+        !ok(clEnqueueReadBuffer(R.q, s->radiance, CL_TRUE, 0, 16ull * W * H, radiance_out, 0, nullptr, nullptr), "read"))
+        return -9;
+    return 0;
+}
+
+// ReconstructionPass (reconstruction.cl:6-60); image_out: W*H float4
+__attribute__((visibility("default"))) int clref_accumulate(void* sp, int frame, const mcrt_filter* f, float* image_out) {
+    Scene* s = (Scene*)sp;
+    if (!ok(clEnqueueWriteBuffer(R.q, s->filter, CL_TRUE, 0, sizeof(mcrt_filter), f, 0, nullptr, nullptr), "filter"))
+        return -1;
+    cl_int e = 0;
+    e |= arg(R.kRecon, 0, s->W);
+    e |= arg(R.kRecon, 1, s->H);
+    e |= arg(R.kRecon, 2, frame);
+    e |= arg(R.kRecon, 3, s->filter);
+    e |= arg(R.kRecon, 4, s->radiance);
+    e |= arg(R.kRecon, 5, s->wsum);
+    e |= arg(R.kRecon, 6, s->wts);
+    e |= arg(R.kRecon, 7, s->image);
+    if (!ok(e, "recon args") || !launch2D(R.kRecon, s->W, s->H)) return -2;
+    size_t origin[3] = {0, 0, 0}, region[3] = {(size_t)s->W, (size_t)s->H, 1};
+    if (image_out &&
+        !ok(clEnqueueReadImage(R.q, s->image, CL_TRUE, origin, region, 0, 0, image_out, 0, nullptr, nullptr), "read image"))
+        return -3;
+    return 0;
+}
+
+// RadeonRays QueryIntersection / QueryOcclusion on host rays (48 B) -> host hits (32 B / int)
+__attribute__((visibility("default"))) int clref_trace(void* sp, const void* rays, int n, void* out, int any) {
+    Scene* s = (Scene*)sp;
+    cl_mem r = buf(48ull * n, rays);
+    cl_mem o = buf((any ? 4ull : 32ull) * n, out);   // pre-filled: inactive rays stay untouched
+    cl_mem st = buf(4ull * n * 64, nullptr);
+    cl_mem cnt = buf(4, &n);
+    cl_mem saveStack = s->stack, saveCount = s->count;
+    s->stack = st;
+    s->count = cnt;
+    bool good = launchRR(any ? R.kOccl : R.kIsect, s, r, o, n);
+    s->stack = saveStack;
+    s->count = saveCount;
+    if (good) good = ok(clEnqueueReadBuffer(R.q, o, CL_TRUE, 0, (any ? 4ull : 32ull) * n, out, 0, nullptr, nullptr), "read");
+    clReleaseMemObject(r);
+    clReleaseMemObject(o);
+    clReleaseMemObject(st);
+    clReleaseMemObject(cnt);
+    return good ? 0 : -1;
+}
+
+}  // extern "C"
