@@ -289,6 +289,13 @@ MCRT_API mcrt_status mcrt_framebuffer_device_ptrs(mcrt_framebuffer fb, void** ra
                                                   void** weight_sum, void** image);
 /* Copies device -> host (RGBA32F, W*H*4 floats).  which: 0 radiance, 1 weighted sum, 2 image. */
 MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float* host_rgba);
+/* Device-to-device copy of one frame-buffer array into caller memory (e.g. a torch/RCCL
+ * buffer for the multi-GPU reduce): which 0 radiance (float4), 1 weighted sum (float4),
+ * 2 image (float4), 3 weight sum (float).  Enqueued on the context stream. */
+MCRT_API mcrt_status mcrt_framebuffer_copy_device(mcrt_framebuffer fb, int which, void* d_dst);
+/* Inverse for multi-GPU: overwrite the weighted sums (float4) and weights (float) from device
+ * memory (after a reduce) and recompute the image = sum / weight on the device. */
+MCRT_API mcrt_status mcrt_framebuffer_set_accumulation(mcrt_framebuffer fb, const void* d_wsum, const void* d_wts);
 /* Per-frame path statistics of the last render (paths, closest rays, any rays, ...). */
 MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closest_rays, int64_t* any_rays,
                                             int64_t* shaded_paths);

@@ -736,6 +736,27 @@ MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float
     return MCRT_OK;
 }
 
+MCRT_API mcrt_status mcrt_framebuffer_copy_device(mcrt_framebuffer fb, int which, void* d_dst) {
+    if (!fb || !d_dst || which < 0 || which > 3) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    const void* src = which == 0 ? (const void*)fb->radiance : which == 1 ? (const void*)fb->wsum
+                      : which == 2 ? (const void*)fb->image : (const void*)fb->wts;
+    HIPCHK(ctx, hipMemcpyAsync(d_dst, src, (which == 3 ? 4 : 16) * fb->N, hipMemcpyDeviceToDevice, ctx->stream));
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_set_accumulation(mcrt_framebuffer fb, const void* d_wsum, const void* d_wts) {
+    if (!fb || !d_wsum || !d_wts) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipMemcpyAsync(fb->wsum, d_wsum, 16 * fb->N, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(fb->wts, d_wts, 4 * fb->N, hipMemcpyDeviceToDevice, ctx->stream));
+    mcrt::launch_resolve(fb->W, fb->H, fb->wsum, fb->wts, fb->image, ctx->stream);
+    HIPCHK(ctx, hipGetLastError());
+    return MCRT_OK;
+}
+
 MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closest_rays, int64_t* any_rays,
                                             int64_t* shaded_paths) {
     if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");

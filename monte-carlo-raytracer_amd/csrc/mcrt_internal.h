@@ -62,6 +62,7 @@ void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int
                    int maxCount, hipStream_t st);
 void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st);
+void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st);
 }  // namespace mcrt
 
 // Host BVH builder (mcrt_bvh.cpp)

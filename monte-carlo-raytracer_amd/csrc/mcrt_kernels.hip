@@ -680,6 +680,16 @@ __global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, floa
     image[pix] = make_float4(s.x / ws, s.y / ws, s.z / ws, s.w / ws);
 }
 
+// image = sum / weight after a multi-GPU reduce of the accumulators
+__global__ __launch_bounds__(256) void k_resolve(int n, const float4* __restrict__ wsum, const float* __restrict__ wts,
+                                                 float4* __restrict__ image) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 s = wsum[i];
+    const float w = wts[i];
+    image[i] = make_float4(s.x / w, s.y / w, s.z / w, s.w / w);
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
@@ -720,6 +730,11 @@ void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* rad
                        float4* image, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + 255) / 256;
     hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(256), 0, st, f, frame, w, radiance, wsum, wts, image);
+}
+
+void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st) {
+    const int n = (int)(W * H);
+    hipLaunchKernelGGL(k_resolve, dim3((n + 255) / 256), dim3(256), 0, st, n, wsum, wts, image);
 }
 
 }  // namespace mcrt

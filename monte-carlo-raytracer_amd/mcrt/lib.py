@@ -46,6 +46,8 @@ SIGNATURES = {
     "mcrt_framebuffer_device_ptrs": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_framebuffer_read": (_c.c_int, [_vp, _c.c_int, _vp]),
     "mcrt_framebuffer_stats": (_c.c_int, [_vp, _vp, _vp, _vp]),
+    "mcrt_framebuffer_copy_device": (_c.c_int, [_vp, _c.c_int, _vp]),
+    "mcrt_framebuffer_set_accumulation": (_c.c_int, [_vp, _vp, _vp]),
     "mcrt_make_pinhole_camera": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _c.c_float, _c.c_float, _c.c_uint32,
                                             _c.c_uint32, _vp, _vp]),
 }
@@ -197,6 +199,12 @@ class FrameBuffer:
         _check(lib().mcrt_framebuffer_device_ptrs(self.h, _c.byref(r), _c.byref(s), _c.byref(w), _c.byref(i)),
                self.ctx.h)
         return r.value, s.value, w.value, i.value
+
+    def copy_device(self, which, dst_ptr):
+        _check(lib().mcrt_framebuffer_copy_device(self.h, which, dst_ptr), self.ctx.h)
+
+    def set_accumulation(self, wsum_ptr, wts_ptr):
+        _check(lib().mcrt_framebuffer_set_accumulation(self.h, wsum_ptr, wts_ptr), self.ctx.h)
 
     def stats(self):
         a, b, c = _c.c_int64(), _c.c_int64(), _c.c_int64()

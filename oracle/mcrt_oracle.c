@@ -1464,7 +1464,7 @@ typedef struct {
     int frame, maxDepth, sampler, W, H;
     float* radiance;
     const int32_t* rows;
-    atomic_llong stats[4];
+    atomic_llong stats[6];
 } RenderCtx;
 
 static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
@@ -1484,10 +1484,10 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
     v3 radianceAcc = V3(0, 0, 0);
     mcrt_intersection isect;
     int nv = 0;
-    int64_t nclosest = 0, nany = 0, vclosest = 0, vany = 0;
+    int64_t nprim = 0, vprim = 0, nclosest = 0, nany = 0, vclosest = 0, vany = 0;
     /* RTPrimaryRaysPass: first closest hit */
     traceClosest(s, &ray, &isect, stack, &nv);
-    nclosest++; vclosest += nv;
+    nprim++; vprim += nv;
     for (int b = 0; b < rc->maxDepth; ++b) {
         v3 temp = V3(0, 0, 0);
         int ignoreOcclusion = 0;
@@ -1581,10 +1581,12 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
     }
     float* out = &rc->radiance[4 * (size_t)bufferIdx];
     out[0] = radianceAcc.x; out[1] = radianceAcc.y; out[2] = radianceAcc.z; out[3] = 0.0f;
-    atomic_fetch_add(&rc->stats[0], nclosest);
-    atomic_fetch_add(&rc->stats[1], nany);
-    atomic_fetch_add(&rc->stats[2], vclosest);
-    atomic_fetch_add(&rc->stats[3], vany);
+    atomic_fetch_add(&rc->stats[0], nprim);
+    atomic_fetch_add(&rc->stats[1], vprim);
+    atomic_fetch_add(&rc->stats[2], nclosest);
+    atomic_fetch_add(&rc->stats[3], vclosest);
+    atomic_fetch_add(&rc->stats[4], nany);
+    atomic_fetch_add(&rc->stats[5], vany);
 }
 
 static void render_row(void* c, int64_t i, uint32_t* stack) {
@@ -1598,7 +1600,7 @@ static void render_common(orc_scene* s, const mcrt_camera* cam, int frame, int m
     RenderCtx rc;
     rc.s = s; rc.cam = cam; rc.frame = frame; rc.maxDepth = max_depth; rc.sampler = sampler;
     rc.W = (int)cam->width; rc.H = (int)cam->height; rc.radiance = radiance;
-    for (int k = 0; k < 4; ++k) atomic_init(&rc.stats[k], 0);
+    for (int k = 0; k < 6; ++k) atomic_init(&rc.stats[k], 0);
     if (rows) {
         rc.rows = rows;
         parallel_for(nrows, threads, 1, render_row, &rc);
@@ -1609,13 +1611,13 @@ static void render_common(orc_scene* s, const mcrt_camera* cam, int frame, int m
         parallel_for(nrows, threads, 1, render_row, &rc);
         free(r);
     }
-    if (stats) for (int k = 0; k < 4; ++k) stats[k] = atomic_load(&rc.stats[k]);
+    if (stats) for (int k = 0; k < 6; ++k) stats[k] = atomic_load(&rc.stats[k]);
 }
 
 void orc_render_frame(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,
                       int y0, int y1, int threads, float* radiance, int64_t* stats) {
     if (!s->nodes || s->d.num_lights == 0) {   /* RTPathTracingPass.cpp:42: no lights -> pass skipped */
-        if (stats) memset(stats, 0, sizeof(int64_t) * 4);
+        if (stats) memset(stats, 0, sizeof(int64_t) * 6);
         if (s->d.num_lights == 0) {
             for (int y = y0; y < y1; ++y)
                 for (uint32_t x = 0; x < cam->width; ++x)

@@ -137,8 +137,10 @@ bool ensureBuffers(Scene* s, int W, int H) {
     s->filter = buf(sizeof(mcrt_filter), nullptr);
     cl_image_format fmt = {CL_RGBA, CL_FLOAT};
     cl_int e = 0;
+    // CDNA devices report no image support: ReconstructionPass then cannot run (its
+    // output is a write_only image2d_t); the frame pipeline does not need it.
     s->image = clCreateImage2D(R.ctx, CL_MEM_READ_WRITE, &fmt, W, H, 0, nullptr, &e);
-    if (!ok(e, "clCreateImage2D")) return false;
+    if (e != CL_SUCCESS) s->image = nullptr;
     s->W = W;
     s->H = H;
     return s->rays && s->stack;
@@ -291,6 +293,7 @@ __attribute__((visibility("default"))) int clref_render(void* sp, const mcrt_cam
 // ReconstructionPass (reconstruction.cl:6-60); image_out: W*H float4
 __attribute__((visibility("default"))) int clref_accumulate(void* sp, int frame, const mcrt_filter* f, float* image_out) {
     Scene* s = (Scene*)sp;
+    if (!s->image) { g_err = "device has no OpenCL image support (ReconstructionPass writes an image2d_t)"; return -10; }
     if (!ok(clEnqueueWriteBuffer(R.q, s->filter, CL_TRUE, 0, sizeof(mcrt_filter), f, 0, nullptr, nullptr), "filter"))
         return -1;
     cl_int e = 0;

@@ -60,10 +60,13 @@ def main():
     cs = cache["mixed"]
     cam = scene_camera("mixed", 64, 48)
     filt = T.make_filter(T.BOX)
-    for f in range(8):
-        cs.render(cam, frame=f, max_depth=2)
-        img = cs.accumulate(f, filt, 48, 64)
-    res["mixed_accum8_64x48"] = img
+    try:
+        for f in range(8):
+            cs.render(cam, frame=f, max_depth=2)
+            img = cs.accumulate(f, filt, 48, 64)
+        res["mixed_accum8_64x48"] = img
+    except RuntimeError as e:   # no OpenCL image support on CDNA
+        print("ReconstructionPass skipped:", e)
     # RadeonRays queries: conformance rays on orig.objm, random rays on bunny / mixed
     sc, z = rr_cornell_scene()
     rc = po.CLRefScene(sc, variant)
