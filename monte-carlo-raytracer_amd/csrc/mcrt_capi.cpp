@@ -776,6 +776,31 @@ MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closes
     return MCRT_OK;
 }
 
+MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which, void* host_dst,
+                                                 int64_t max_records, int32_t* count) {
+    if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
+    mcrt_ctx ctx = fb->ctx;
+    if (which != 0 && which != 1) return fail(ctx, MCRT_ERROR_INVALID_ARG, "which must be 0 (shadow) or 1 (extension)");
+    if (max_records < 0 || (max_records > 0 && !host_dst)) return fail(ctx, MCRT_ERROR_INVALID_ARG, "bad destination");
+    if (fb->lastMaxDepth <= 0) return fail(ctx, MCRT_ERROR_INVALID_ARG, "nothing rendered yet");
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    int c[64];
+    HIPCHK(ctx, hipMemcpy(c, fb->counters, sizeof(c), hipMemcpyDeviceToHost));
+    const int b = fb->lastMaxDepth - 1;
+    const int n = which == 0 ? c[b] : c[32 + b];
+    if (count) *count = n;
+    const int64_t m = std::min<int64_t>(n, max_records);
+    if (m == 0) return MCRT_OK;
+    const float4* src[3];
+    if (which == 0) { src[0] = fb->sO; src[1] = fb->sD; src[2] = fb->sL; }
+    else { src[0] = fb->eO[b & 1]; src[1] = fb->eD[b & 1]; src[2] = fb->eT[b & 1]; }
+    for (int k = 0; k < 3; ++k)
+        HIPCHK(ctx, hipMemcpy(static_cast<char*>(host_dst) + (size_t)k * 16 * max_records, src[k], 16 * (size_t)m,
+                              hipMemcpyDeviceToHost));
+    return MCRT_OK;
+}
+
 // ---------------------------------------------------------------------------
 // host camera helper (RTPrimaryRaysPass::generatePrimaryRays + RTUtil::screenToRay)
 // ---------------------------------------------------------------------------

@@ -1,8 +1,15 @@
-// mcrt_device.h -- device-side building blocks of the MI355X path-tracing core.
+// mcrt_device.h -- device-side math of the MI355X path-tracing core.
 //
-// Semantics follow the reference OpenCL kernels (paths: KRN = assets/kernels,
-// RR = third_party/RadeonRays/RadeonRays); the data layout and control flow are
-// our own (SoA path queues, wave64 compaction, 64-B BVH nodes).
+// Numerics policy (DESIGN.md "Numerics"): the reference's GPU build is OpenCL C compiled by
+// ROCm clang with OpenCL-default floating point: contraction only inside one expression
+// (FP_CONTRACT ON), 2.5-ulp division, 3-ulp sqrt, and the ROCm device-library builtins
+// (dot = fma chain, cross = fma with a negated product, mix = fma, normalize = x * rsqrt with
+// range scaling, clamp = med3).  This file reproduces exactly those operation sequences with
+// clang ext_vector types (so expressions contract as in OpenCL) and is compiled with
+// -ffp-contract=on -fno-hip-fp32-correctly-rounded-divide-sqrt; the HIP path therefore
+// computes the same fp32 results as the reference kernels on the same hardware for
+// identical inputs (and uses the cheaper division / sqrt sequences).
+// Paths: KRN = assets/kernels, RR = third_party/RadeonRays/RadeonRays.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -11,69 +18,115 @@
 
 #define MCRT_DEV __device__ __forceinline__
 
-// ---------------------------------------------------------------------------
-// small vector type (OpenCL float3 semantics)
-// ---------------------------------------------------------------------------
-struct v3 {
-    float x, y, z;
-};
-MCRT_DEV v3 mk3(float x, float y, float z) { return v3{x, y, z}; }
-MCRT_DEV v3 operator+(v3 a, v3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
-MCRT_DEV v3 operator-(v3 a, v3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
-MCRT_DEV v3 operator*(v3 a, v3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
-MCRT_DEV v3 operator*(v3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
-MCRT_DEV v3 operator*(float s, v3 a) { return mk3(s * a.x, s * a.y, s * a.z); }
-MCRT_DEV v3 operator/(v3 a, float s) { return mk3(a.x / s, a.y / s, a.z / s); }
-MCRT_DEV v3 operator-(v3 a) { return mk3(-a.x, -a.y, -a.z); }
-MCRT_DEV float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-MCRT_DEV v3 cross(v3 a, v3 b) { return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
-MCRT_DEV v3 normalize(v3 p) {
-    float l2 = dot(p, p);
-    if (l2 < 1.17549435e-38f) { p = p * 0x1.0p+86f; l2 = dot(p, p); }
-    else if (__builtin_isinf(l2)) { p = p * 0x1.0p-65f; l2 = dot(p, p); }
-    if (l2 == 0.0f) return p;
-    return p * (1.0f / sqrtf(l2));
-}
-MCRT_DEV float length(v3 p) { return sqrtf(dot(p, p)); }
-MCRT_DEV v3 mix(v3 a, v3 b, float t) { return a + (b - a) * t; }
-MCRT_DEV float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
-MCRT_DEV float signf(float x) {
-    if (x > 0.0f) return 1.0f;
-    if (x < 0.0f) return -1.0f;
-    if (x == 0.0f) return x;
-    return 0.0f;
-}
-MCRT_DEV v3 ld3(const mcrt_float4& p) { return mk3(p.x, p.y, p.z); }
-MCRT_DEV v3 ld3(const float4& p) { return mk3(p.x, p.y, p.z); }
-MCRT_DEV float absDot(v3 a, v3 b) { return fabsf(dot(a, b)); }
-MCRT_DEV bool isNearZero(float v) { return fabsf(v) < 1e-8f; }
-MCRT_DEV bool isNotNearZero(float v) { return fabsf(v) > 1e-8f; }
+typedef float f3 __attribute__((ext_vector_type(3)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 
-#define PI_F 3.14159265359f   // KRN/math.cl:8
+MCRT_DEV f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+MCRT_DEV f3 splat3(float x) { return f3{x, x, x}; }
+MCRT_DEV f3 ld3(const mcrt_float4& p) { return f3{p.x, p.y, p.z}; }
+MCRT_DEV f3 ld3(const float4& p) { return f3{p.x, p.y, p.z}; }
+
+// ---- OpenCL builtins as implemented by the ROCm device libraries (opencl.bc / ocml.bc) ----
+MCRT_DEV float cl_dot(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+MCRT_DEV f3 cl_cross(f3 a, f3 b) {
+    return f3{fmaf(a.y, b.z, b.y * -a.z), fmaf(a.z, b.x, b.z * -a.x), fmaf(a.x, b.y, b.x * -a.y)};
+}
+MCRT_DEV f3 cl_mix(f3 a, f3 b, float t) {
+    const f3 d = b - a;
+    return f3{fmaf(d.x, t, a.x), fmaf(d.y, t, a.y), fmaf(d.z, t, a.z)};
+}
+MCRT_DEV float cl_mixf(float a, float b, float t) { return fmaf(b - a, t, a); }
+// fp32 division and sqrt exactly as the AMDGPU backend lowers the reference's OpenCL `/`
+// (2.5 ulp: frexp / v_rcp / ldexp) and `sqrt` (3 ulp: v_sqrt with range scaling) with fp32
+// denormals enabled.  Spelled out with target builtins because compiler transforms (LICM,
+// branch merging) may drop the accuracy metadata of a plain `/` and silently switch to the
+// correctly rounded sequence -- in the product and in the reference alike, at different sites.
+MCRT_DEV float cl_div(float a, float b) {
+    const float r = __builtin_amdgcn_rcpf(__builtin_amdgcn_frexp_mantf(b));
+    return __builtin_ldexpf(__builtin_amdgcn_frexp_mantf(a) * r,
+                            __builtin_amdgcn_frexp_expf(a) - __builtin_amdgcn_frexp_expf(b));
+}
+MCRT_DEV f2 cl_div(f2 a, float b) { return f2{cl_div(a.x, b), cl_div(a.y, b)}; }
+MCRT_DEV f3 cl_div(f3 a, float b) { return f3{cl_div(a.x, b), cl_div(a.y, b), cl_div(a.z, b)}; }
+MCRT_DEV f4 cl_div(f4 a, float b) { return f4{cl_div(a.x, b), cl_div(a.y, b), cl_div(a.z, b), cl_div(a.w, b)}; }
+MCRT_DEV float cl_sqrt(float x) {
+    const bool tiny = x < 0x1.0p-126f;
+    return __builtin_ldexpf(__builtin_amdgcn_sqrtf(__builtin_ldexpf(x, tiny ? 32 : 0)), tiny ? -16 : 0);
+}
+// Correctly rounded division (f32 operands, f64 quotient: exact rounding).  Only where the
+// reference's own compiled kernel ends up with a precise fdiv (see evaluateUberBSDF).
+MCRT_DEV float cr_div(float a, float b) { return (float)((double)a / (double)b); }
+MCRT_DEV f3 cl_normalize(f3 p) {
+    if (p.x == 0.0f && p.y == 0.0f && p.z == 0.0f) return p;
+    float l2 = cl_dot(p, p);
+    if (l2 < 0x1.0p-126f) {
+        p = p * 0x1.0p+86f;
+        l2 = cl_dot(p, p);
+    } else if (l2 == __builtin_inff()) {
+        p = p * 0x1.0p-66f;
+        l2 = cl_dot(p, p);
+        if (l2 == __builtin_inff()) {
+            p = f3{__builtin_copysignf(__builtin_isinf(p.x) ? 1.0f : 0.0f, p.x),
+                   __builtin_copysignf(__builtin_isinf(p.y) ? 1.0f : 0.0f, p.y),
+                   __builtin_copysignf(__builtin_isinf(p.z) ? 1.0f : 0.0f, p.z)};
+            l2 = cl_dot(p, p);
+        }
+    }
+    return p * rsqrtf(l2);
+}
+MCRT_DEV float cl_length(f3 p) {
+    const float l2 = cl_dot(p, p);
+    if (l2 < 0x1.0p-126f) return cl_sqrt(cl_dot(p * 0x1.0p+86f, p * 0x1.0p+86f)) * 0x1.0p-86f;
+    if (l2 == __builtin_inff()) return cl_sqrt(cl_dot(p * 0x1.0p-66f, p * 0x1.0p-66f)) * 0x1.0p+66f;
+    return cl_sqrt(l2);
+}
+MCRT_DEV float cl_distance(f3 a, f3 b) { return cl_length(a - b); }
+MCRT_DEV float cl_clamp(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
+MCRT_DEV float cl_sign(float x) {
+    return __builtin_copysignf((__builtin_isnan(x) || x == 0.0f) ? 0.0f : 1.0f, x);
+}
+
+// ---- KRN/math.cl, KRN/matrix.cl ----
+#define PI_F 3.14159265359f
 #define PI_INV_F 0.31830988618f
+#define PI2_F 6.28318530718f
 #define PI_DIV_4_F 0.78539816339f
 #define PI_DIV_2_F 1.57079632679f
 #define RT_TRACE_OFFSET_F 0.00001f
 #define RT_MAX_TRACE_F 1000.0f
 
-// KRN/math.cl:53-66
-MCRT_DEV v3 orthogonalVector(v3 n) {
+MCRT_DEV f3 computeOrthogonalVector(f3 n) {   // math.cl:53-66
     if (fabsf(n.z) > 0.0f) {
-        float d = sqrtf(n.z * n.z + n.x * n.x);
-        return mk3(-n.z / d, 0.0f, n.x / d);
+        float d = cl_sqrt(n.z * n.z + n.x * n.x);
+        return f3{cl_div(-n.z, d), 0.0f, cl_div(n.x, d)};
     }
-    float d = sqrtf(n.y * n.y + n.x * n.x);
-    return mk3(n.y / d, -n.x / d, 0.0f);
+    float d = cl_sqrt(n.y * n.y + n.x * n.x);
+    return f3{cl_div(n.y, d), cl_div(-n.x, d), 0.0f};
 }
-// KRN/matrix.cl:44-60 (row-major mat4)
-MCRT_DEV v3 xformVec(const mcrt_mat4& m, v3 v) { return mk3(dot(ld3(m.m0), v), dot(ld3(m.m1), v), dot(ld3(m.m2), v)); }
-MCRT_DEV v3 xformPt(const mcrt_mat4& m, v3 v) {
-    return mk3(dot(ld3(m.m0), v) + m.m0.w, dot(ld3(m.m1), v) + m.m1.w, dot(ld3(m.m2), v) + m.m2.w);
+MCRT_DEV float absDot(f3 a, f3 b) { return fabsf(cl_dot(a, b)); }
+MCRT_DEV bool isNearZero(float v) { return fabsf(v) < 1e-8f; }
+MCRT_DEV bool isNotNearZero(float v) { return fabsf(v) > 1e-8f; }
+MCRT_DEV float distanceSquared(f3 p0, f3 p1) { return cl_dot(p0 - p1, p0 - p1); }
+MCRT_DEV f3 lerpDirection(f3 d0, f3 d1, f3 d2, f3 d3, float t0, float t1) {   // math.cl:88-91
+    return cl_normalize(cl_mix(cl_mix(d0, d1, t0), cl_mix(d3, d2, t0), t1));
+}
+MCRT_DEV f3 transformVector3(const mcrt_mat4& m, f3 v) {   // matrix.cl:44-51
+    f3 r;
+    r.x = cl_dot(ld3(m.m0), v);
+    r.y = cl_dot(ld3(m.m1), v);
+    r.z = cl_dot(ld3(m.m2), v);
+    return r;
+}
+MCRT_DEV f3 transformPoint3(const mcrt_mat4& m, f3 v) {   // matrix.cl:53-60
+    f3 r;
+    r.x = cl_dot(ld3(m.m0), v) + m.m0.w;
+    r.y = cl_dot(ld3(m.m1), v) + m.m1.w;
+    r.z = cl_dot(ld3(m.m2), v) + m.m2.w;
+    return r;
 }
 
-// ---------------------------------------------------------------------------
-// RNG + samplers (KRN/rng.cl:48-107, KRN/samplers.cl:64-122)
-// ---------------------------------------------------------------------------
+// ---- RNG + samplers: KRN/rng.cl:48-107, KRN/samplers.cl:64-122 ----
 MCRT_DEV uint32_t wangHash(uint32_t s) {
     s = (s ^ 61u) ^ (s >> 16);
     s *= 9u;
@@ -108,7 +161,7 @@ MCRT_DEV Sampler makeSampler(int kind, uint32_t pix, int frame, int bounce, uint
     }
     return s;
 }
-MCRT_DEV float sample1D(Sampler& s) {
+MCRT_DEV float getSample1D(Sampler& s) {
     if (s.mats) {
         uint32_t v = s.scramble;
         uint32_t idx = s.idx;
@@ -118,284 +171,328 @@ MCRT_DEV float sample1D(Sampler& s) {
         s.dim++;
         return (float)v * 0x1p-32f;
     }
-    return (float)xorshift(s.idx) * 0x1p-32f;   // rng.cl:104-107 (/0xffffffff == /2^32 in float)
+    return (float)xorshift(s.idx) * 0x1p-32f;   // (float)x / 0xffffffff == x * 2^-32 exactly
 }
-struct v2 {
-    float x, y;
-};
-MCRT_DEV v2 sample2D(Sampler& s) {
-    v2 u;
-    u.x = sample1D(s);
-    u.y = sample1D(s);
+MCRT_DEV f2 getSample2D(Sampler& s) {
+    f2 u;
+    u.x = getSample1D(s);
+    u.y = getSample1D(s);
     return u;
 }
 
-// KRN/samplers.cl:169-198
-MCRT_DEV v2 concentricDisc(v2 u) {
-    float ox = 2.0f * u.x - 1.0f, oy = 2.0f * u.y - 1.0f;
-    if (u.x < 1e-8f && u.y < 1e-8f) return v2{0.0f, 0.0f};
+MCRT_DEV f2 concentricSampleDisc(f2 u) {   // samplers.cl:169-191
+    f2 uOffset = 2.0f * u - f2{1.0f, 1.0f};
+    if (u.x < 1e-8f && u.y < 1e-8f) return f2{0.0f, 0.0f};
     float theta, r;
-    if (fabsf(ox) > fabsf(oy)) { r = ox; theta = PI_DIV_4_F * (oy / ox); }
-    else { r = oy; theta = PI_DIV_2_F - PI_DIV_4_F * (ox / oy); }
-    float s, c;
-    sincosf(theta, &s, &c);
-    return v2{r * c, r * s};
+    if (fabsf(uOffset.x) > fabsf(uOffset.y)) {
+        r = uOffset.x;
+        theta = PI_DIV_4_F * cl_div(uOffset.y, uOffset.x);
+    } else {
+        r = uOffset.y;
+        theta = PI_DIV_2_F - PI_DIV_4_F * cl_div(uOffset.x, uOffset.y);
+    }
+    return r * f2{cosf(theta), sinf(theta)};
 }
-MCRT_DEV v3 cosineHemisphere(v2 u) {
-    v2 d = concentricDisc(u);
-    float y = sqrtf(fmaxf(0.0f, 1.0f - d.x * d.x - d.y * d.y));
-    return mk3(d.x, y, d.y);
+MCRT_DEV f3 cosineSampleHemisphere(f2 u) {   // samplers.cl:193-198
+    f2 d = concentricSampleDisc(u);
+    float y = cl_sqrt(fmaxf(0.0f, 1.0f - d.x * d.x - d.y * d.y));
+    return f3{d.x, y, d.y};
 }
 
-// ---------------------------------------------------------------------------
-// Uber BSDF (KRN/bxdfs.cl); shading frame: normal = y, tangent = x, binormal = z
-// ---------------------------------------------------------------------------
+// ---- Uber BSDF: KRN/bxdfs.cl (shading frame: normal = y, tangent = x, binormal = z) ----
 enum : int {
     BSDF_REFLECTION = 1, BSDF_TRANSMISSION = 2, BSDF_DIFFUSE = 4, BSDF_GLOSSY = 8, BSDF_SPECULAR = 16,
     BSDF_SPEC_REFL = 17, BSDF_SPEC_TRANS = 18, BSDF_LAMBERT = 5, BSDF_MF_REFL = 9, BSDF_MF_TRANS = 10,
 };
-MCRT_DEV float cosT(v3 w) { return w.y; }
-MCRT_DEV float cos2T(v3 w) { return w.y * w.y; }
-MCRT_DEV float absCosT(v3 w) { return fabsf(w.y); }
-MCRT_DEV float sin2T(v3 w) { return fmaxf(0.0f, 1.0f - cos2T(w)); }
-MCRT_DEV float sinT(v3 w) { return sqrtf(sin2T(w)); }
-MCRT_DEV float tanT(v3 w) { return sinT(w) / cosT(w); }
-MCRT_DEV float tan2T(v3 w) { return sin2T(w) / cos2T(w); }
-MCRT_DEV float cosP(v3 w) { float st = sinT(w); return st == 0 ? 1.0f : clampf(w.x / st, -1.0f, 1.0f); }
-MCRT_DEV float sinP(v3 w) { float st = sinT(w); return clampf(w.z / st, -1.0f, 1.0f); }   // bxdfs.cl:38 (always clamps)
-MCRT_DEV bool sameHemi(v3 a, v3 b) { return a.y * b.y > 0.0f; }
-MCRT_DEV bool isBlack(v3 c) { return c.x < 0.000001f && c.y < 0.000001f && c.z < 0.000001f; }
-MCRT_DEV bool notBlack(v3 c) { return c.x > 0.000001f || c.y > 0.000001f || c.z > 0.000001f; }
+MCRT_DEV float evalCosTheta(f3 w) { return w.y; }
+MCRT_DEV float evalCosSqTheta(f3 w) { return w.y * w.y; }
+MCRT_DEV float evalAbsCosTheta(f3 w) { return fabsf(w.y); }
+MCRT_DEV float evalSinSqTheta(f3 w) { return fmaxf(0.0f, 1.0f - evalCosSqTheta(w)); }
+MCRT_DEV float evalSinTheta(f3 w) { return cl_sqrt(evalSinSqTheta(w)); }
+MCRT_DEV float evalTanTheta(f3 w) { return cl_div(evalSinTheta(w), evalCosTheta(w)); }
+MCRT_DEV float evalTanSqTheta(f3 w) { return cl_div(evalSinSqTheta(w), evalCosSqTheta(w)); }
+MCRT_DEV float evalCosPhi(f3 w) {
+    float st = evalSinTheta(w);
+    return st == 0 ? 1.0f : cl_clamp(cl_div(w.x, st), -1.0f, 1.0f);
+}
+MCRT_DEV float evalSinPhi(f3 w) {   // bxdfs.cl:35-39: the `evalSinTheta == 0` test is always false
+    float st = evalSinTheta(w);
+    return cl_clamp(cl_div(w.z, st), -1.0f, 1.0f);
+}
+MCRT_DEV float evalCosSqPhi(f3 w) { return evalCosPhi(w) * evalCosPhi(w); }
+MCRT_DEV float evalSinSqPhi(f3 w) { return evalSinPhi(w) * evalSinPhi(w); }
+MCRT_DEV bool isSameHemisphere(f3 a, f3 b) { return a.y * b.y > 0.0f; }
+MCRT_DEV bool isBlack(f3 c) { return c.x < 0.000001f && c.y < 0.000001f && c.z < 0.000001f; }
+MCRT_DEV bool isNotBlack(f3 c) { return c.x > 0.000001f || c.y > 0.000001f || c.z > 0.000001f; }
 
-// bxdfs.cl:159-190
-MCRT_DEV float fresnelDielectric(float cosI, float etaI, float etaT) {
-    cosI = clampf(cosI, -1.0f, 1.0f);
-    if (cosI <= 0.0f) { float h = etaI; etaI = etaT; etaT = h; cosI = fabsf(cosI); }
-    float sinI = sqrtf(fmaxf(0.0f, 1.0f - cosI * cosI));
-    float sinT_ = etaI / etaT * sinI;
-    if (sinT_ >= 1.0f) return 1.0f;
-    float cosT_ = sqrtf(fmaxf(0.0f, 1.0f - sinT_ * sinT_));
-    float rparl = ((etaT * cosI) - (etaI * cosT_)) / ((etaT * cosI) + (etaI * cosT_));
-    float rperp = ((etaI * cosI) - (etaT * cosT_)) / ((etaI * cosI) + (etaT * cosT_));
+MCRT_DEV float evaluateFresnelDielectric(float cosThetaI, float etaI, float etaT) {   // bxdfs.cl:159-190
+    cosThetaI = cl_clamp(cosThetaI, -1.0f, 1.0f);
+    if (cosThetaI <= 0.0f) {
+        float h = etaI;
+        etaI = etaT;
+        etaT = h;
+        cosThetaI = fabsf(cosThetaI);
+    }
+    float sinThetaI = cl_sqrt(fmaxf(0.0f, 1.0f - cosThetaI * cosThetaI));
+    float sinThetaT = cl_div(etaI, etaT) * sinThetaI;
+    if (sinThetaT >= 1.0f) return 1.0f;
+    float cosThetaT = cl_sqrt(fmaxf(0.0f, 1.0f - sinThetaT * sinThetaT));
+    float rparl = cl_div(((etaT * cosThetaI) - (etaI * cosThetaT)), ((etaT * cosThetaI) + (etaI * cosThetaT)));
+    float rperp = cl_div(((etaI * cosThetaI) - (etaT * cosThetaT)), ((etaI * cosThetaI) + (etaT * cosThetaT)));
     return (rparl * rparl + rperp * rperp) * 0.5f;
 }
-MCRT_DEV bool refractDir(v3 wi, v3 n, float eta, v3& wt) {   // bxdfs.cl:233-245
-    float cI = dot(n, wi);
-    float s2I = fmaxf(0.0f, 1.0f - cI * cI);
-    float s2T = eta * eta * s2I;
-    if (s2T >= 1.0f) return false;
-    float cT = sqrtf(1.0f - s2T);
-    wt = (-eta) * wi + (eta * cI - cT) * n;
+MCRT_DEV f3 reflect(f3 wo, f3 n) { return -wo + 2.0f * cl_dot(n, wo) * n; }   // bxdfs.cl:228-231
+MCRT_DEV bool refract(f3 wi, f3 n, float eta, f3* wt) {   // bxdfs.cl:233-245
+    float cosThetaI = cl_dot(n, wi);
+    float sin2ThetaI = fmaxf(0.0f, 1.0f - cosThetaI * cosThetaI);
+    float sin2ThetaT = eta * eta * sin2ThetaI;
+    if (sin2ThetaT >= 1.0f) return false;
+    float cosThetaT = cl_sqrt(1.0f - sin2ThetaT);
+    *wt = -eta * wi + (eta * cosThetaI - cosThetaT) * n;
     return true;
 }
-MCRT_DEV float roughnessToAlpha(float r) {   // bxdfs.cl:385-390
-    r = fmaxf(r, 1e-3f);
-    float x = logf(r);
+// bxdfs.cl:330-347.  Kept as calls: in the reference these terms enter `f +=` through a
+// function call, so they must not contract into the accumulation.
+MCRT_DEV f3 evaluateLambertianReflection(f3 R) { return R * PI_INV_F; }
+MCRT_DEV float evaluateLambertianReflectionPdf(f3 wo, f3 wi) {
+    return isSameHemisphere(wo, wi) ? evalAbsCosTheta(wi) * PI_INV_F : 0.0f;
+}
+MCRT_DEV f3 sampleSpecularReflection_Dielectric(f3 R, float etaI, float etaT, f3 wo, f3* wi, float* pdf) {
+    *wi = f3{-wo.x, wo.y, -wo.z};   // bxdfs.cl:259-268
+    *pdf = 1.0f;
+    float F = evaluateFresnelDielectric(evalCosTheta(*wi), etaI, etaT);
+    return cl_div(F * R, evalAbsCosTheta(*wi));
+}
+MCRT_DEV f3 sampleSpecularTransmission(f3 T, float etaA, float etaB, f3 wo, f3* wi, float* pdf) {   // :288-307
+    bool isEntering = evalCosTheta(wo) > 0.0f;
+    float etaI = isEntering ? etaA : etaB;
+    float etaT = isEntering ? etaB : etaA;
+    f3 n = f3{0.0f, 1.0f, 0.0f} * cl_sign(wo.y);
+    if (!refract(wo, n, cl_div(etaI, etaT), wi)) return f3{0.0f, 0.0f, 0.0f};
+    *pdf = 1.0f;
+    f3 ft = T * (1.0f - evaluateFresnelDielectric(evalCosTheta(*wi), etaA, etaB));
+    ft *= cl_div((etaI * etaI), (etaT * etaT));   // TRANSPORT_MODE_RADIANCE
+    return cl_div(ft, evalAbsCosTheta(*wi));
+}
+MCRT_DEV float roughnessToAlpha(float roughness) {   // bxdfs.cl:385-390
+    roughness = fmaxf(roughness, 1e-3f);
+    float x = logf(roughness);
     return 1.62142f + 0.819955f * x + 0.1734f * x * x + 0.0171201f * x * x * x + 0.000640711f * x * x * x * x;
 }
-MCRT_DEV float trD(v3 wh, v2 a) {   // bxdfs.cl:406-415
-    float t2 = tan2T(wh);
-    if (__builtin_isinf(t2)) return 0.0f;
-    float c4 = cos2T(wh) * cos2T(wh);
-    float cp = cosP(wh), sp = sinP(wh);
-    float e = (cp * cp / (a.x * a.x) + sp * sp / (a.y * a.y)) * t2;
-    return 1.0f / (PI_F * a.x * a.y * c4 * (1.0f + e) * (1.0f + e));
+MCRT_DEV float computeTrowbridgeReitzDistribution(f3 wh, f2 alpha) {   // :406-415
+    float tan2Theta = evalTanSqTheta(wh);
+    if (__builtin_isinf(tan2Theta)) return 0.0f;
+    const float cos4Theta = evalCosSqTheta(wh) * evalCosSqTheta(wh);
+    float e = (cl_div(evalCosSqPhi(wh), (alpha.x * alpha.x)) + cl_div(evalSinSqPhi(wh), (alpha.y * alpha.y))) * tan2Theta;
+    return cl_div(1.0f, (PI_F * alpha.x * alpha.y * cos4Theta * (1.0f + e) * (1.0f + e)));
 }
-MCRT_DEV float trLambda(v3 w, v2 a) {   // bxdfs.cl:435-445
-    float at = fabsf(tanT(w));
-    if (__builtin_isinf(at)) return 0.0f;
-    float cp = cosP(w), sp = sinP(w);
-    float aw = sqrtf(cp * cp * a.x * a.x + sp * sp * a.y * a.y);
-    float x = (aw * at) * (aw * at);
-    return (-1.0f + sqrtf(1.f + x)) / 2.0f;
+MCRT_DEV float computeTrowbridgeReitzDistributionLambda(f3 w, f2 alpha) {   // :435-445
+    float absTanTheta = fabsf(evalTanTheta(w));
+    if (__builtin_isinf(absTanTheta)) return 0.0f;
+    float alphaW = cl_sqrt(evalCosSqPhi(w) * alpha.x * alpha.x + evalSinSqPhi(w) * alpha.y * alpha.y);
+    float alpha2Tan2Theta = (alphaW * absTanTheta) * (alphaW * absTanTheta);
+    return (-1.0f + cl_sqrt(1.f + alpha2Tan2Theta)) * 0.5f;   // x / 2.0f folds to x * 0.5f
 }
-MCRT_DEV float trG(v3 wo, v3 wi, v2 a) { return 1.0f / (1.0f + trLambda(wo, a) + trLambda(wi, a)); }
-// bxdfs.cl:481-500
-MCRT_DEV v3 mfReflEval(v3 R, v2 a, float etaI, float etaT, v3 wo, v3 wi) {
-    float cO = absCosT(wo), cI = absCosT(wi);
-    v3 wh = wi + wo;
-    if (cI == 0.0f || cO == 0.0f) return mk3(0, 0, 0);
-    if (wh.x == 0.0f && wh.y == 0.0f && wh.z == 0.0f) return mk3(0, 0, 0);
-    wh = normalize(wh);
-    float F = fresnelDielectric(dot(wi, wh), etaI, etaT);
-    return R * trD(wh, a) * trG(wo, wi, a) * F / (4.0f * cI * cO);
+MCRT_DEV float computeTrowbridgeReitzDistributionG(f3 wo, f3 wi, f2 alpha) {   // :461-474
+    return cl_div(1.0f, (1.0f + computeTrowbridgeReitzDistributionLambda(wo, alpha) + computeTrowbridgeReitzDistributionLambda(wi, alpha)));
 }
-// bxdfs.cl:563-588
-MCRT_DEV v3 mfTransEval(v3 T, v2 a, float etaI, float etaT, v3 wo, v3 wi) {
-    if (sameHemi(wo, wi)) return mk3(0, 0, 0);
-    float cO = cosT(wo), cI = cosT(wi);
-    if (cI == 0.0f || cO == 0.0f) return mk3(0, 0, 0);
-    float eta = cosT(wo) > 0.0f ? (etaT / etaI) : (etaI / etaT);
-    v3 wh = normalize(wo + wi * eta);
-    if (wh.z < 0) wh = -wh;
-    float F = fresnelDielectric(dot(wo, wh), etaI, etaT);
-    float sd = dot(wo, wh) + eta * dot(wi, wh);
-    float factor = 1.0f / eta;   // TRANSPORT_MODE_RADIANCE
-    float s = fabsf(trD(wh, a) * trG(wo, wi, a) * eta * eta * absDot(wi, wh) * absDot(wo, wh) * factor * factor /
-                    (cI * cO * sd * sd));
-    return (mk3(1.0f - F, 1.0f - F, 1.0f - F) * T) * s;
+MCRT_DEV f3 evaluateMicrofacetReflection(f3 R, f2 alpha, float etaI, float etaT, f3 wo, f3 wi) {   // :481-500
+    float cosThetaO = evalAbsCosTheta(wo);
+    float cosThetaI = evalAbsCosTheta(wi);
+    f3 wh = wi + wo;
+    if (cosThetaI == 0.0f || cosThetaO == 0.0f) return f3{0.0f, 0.0f, 0.0f};
+    if (wh.x == 0.0f && wh.y == 0.0f && wh.z == 0.0f) return f3{0.0f, 0.0f, 0.0f};
+    wh = cl_normalize(wh);
+    float F = evaluateFresnelDielectric(cl_dot(wi, wh), etaI, etaT);
+    return cl_div(R * computeTrowbridgeReitzDistribution(wh, alpha) * computeTrowbridgeReitzDistributionG(wo, wi, alpha) * F,
+                  (4.0f * cosThetaI * cosThetaO));
 }
-// bxdfs.cl:647-675
-MCRT_DEV v3 trSampleWh(v2 u, v3 wo, v2 a) {
-    float cosTh;
+// The reciprocals of eta in the microfacet-transmission functions are correctly rounded:
+// the reference's compiler hoists `etaI / etaT` (etaI = 1) out of the eta selects, which drops
+// its 2.5-ulp accuracy metadata, in the NEE evaluation and in the sampling path alike
+// (the sampled, evaluated and pdf etas are one CSE'd value there).
+MCRT_DEV f3 evaluateMicrofacetTransmission(f3 T, f2 alpha, float etaI, float etaT, f3 wo, f3 wi) {   // :563-588
+    if (isSameHemisphere(wo, wi)) return f3{0.0f, 0.0f, 0.0f};
+    float cosThetaO = evalCosTheta(wo);
+    float cosThetaI = evalCosTheta(wi);
+    if (cosThetaI == 0.0f || cosThetaO == 0.0f) return f3{0.0f, 0.0f, 0.0f};
+    float eta = evalCosTheta(wo) > 0.0f ? cr_div(etaT, etaI) : cr_div(etaI, etaT);
+    f3 wh = cl_normalize(wo + wi * eta);
+    if (wh.z < 0) wh = -wh;   // bxdfs.cl:577 (z, not y: SURVEY App. A Q4)
+    float F = evaluateFresnelDielectric(cl_dot(wo, wh), etaI, etaT);
+    float sqrtDenom = cl_dot(wo, wh) + eta * cl_dot(wi, wh);
+    float factor = cr_div(1.0f, eta);   // TRANSPORT_MODE_RADIANCE
+    return (f3{1.0f, 1.0f, 1.0f} - F) * T *
+           fabsf(cl_div(computeTrowbridgeReitzDistribution(wh, alpha) * computeTrowbridgeReitzDistributionG(wo, wi, alpha) *
+                            eta * eta * absDot(wi, wh) * absDot(wo, wh) * factor * factor,
+                        (cosThetaI * cosThetaO * sqrtDenom * sqrtDenom)));
+}
+MCRT_DEV f3 sampleTrowbridgeReitzDistribution_wh(f2 u, f3 wo, f2 alpha) {   // :647-675
+    // cosTheta = 1 / sqrt(.) is correctly rounded: the reference's compiler merges the two
+    // branches' divisions after the if/else and drops their accuracy metadata.
+    float cosTheta = 0.0f;
     float phi = (2.0f * PI_F) * u.y;
-    if (a.x == a.y) {
-        float t2 = a.x * a.x * u.x / (1.0f - u.x);
-        cosTh = 1.0f / sqrtf(1.0f + t2);
+    if (alpha.x == alpha.y) {
+        float tanTheta2 = cl_div(alpha.x * alpha.x * u.x, (1.0f - u.x));
+        cosTheta = cr_div(1.0f, cl_sqrt(1.0f + tanTheta2));
     } else {
-        phi = atanf(a.y / a.x * tanf(2.0f * PI_F * u.y + 0.5f * PI_F));
+        phi = atanf(cl_div(alpha.y, alpha.x) * tanf(2.0f * PI_F * u.y + 0.5f * PI_F));
         if (u.y > .5f) phi += PI_F;
-        float sp, cp;
-        sincosf(phi, &sp, &cp);
-        float a2 = 1.0f / (cp * cp / (a.x * a.x) + sp * sp / (a.y * a.y));
-        float t2 = a2 * u.x / (1.0f - u.x);
-        cosTh = 1.0f / sqrtf(1.0f + t2);
+        float sinPhi = sinf(phi);
+        float cosPhi = cosf(phi);
+        const float alphax2 = alpha.x * alpha.x, alphay2 = alpha.y * alpha.y;
+        const float alpha2 = cl_div(1.0f, (cl_div(cosPhi * cosPhi, alphax2) + cl_div(sinPhi * sinPhi, alphay2)));
+        float tanTheta2 = cl_div(alpha2 * u.x, (1.0f - u.x));
+        cosTheta = cr_div(1.0f, cl_sqrt(1.0f + tanTheta2));
     }
-    float sinTh = sqrtf(fmaxf(0.0f, 1.0f - cosTh * cosTh));
-    float sp, cp;
-    sincosf(phi, &sp, &cp);
-    v3 wh = mk3(sinTh * cp, cosTh, sinTh * sp);
-    if (!sameHemi(wo, wh)) wh = -wh;
+    float sinTheta = cl_sqrt(fmaxf(0.0f, 1.0f - cosTheta * cosTheta));
+    f3 wh = f3{sinTheta * cosf(phi), cosTheta, sinTheta * sinf(phi)};   // math.cl:18-23
+    if (!isSameHemisphere(wo, wh)) wh = -wh;
     return wh;
 }
-MCRT_DEV float mfReflPdf(v3 wo, v3 wi, v3 wh, v2 a) {   // bxdfs.cl:695-701
-    if (!sameHemi(wo, wi)) return 0.0f;
-    return trD(wh, a) * absCosT(wh) / (4.0f * dot(wo, wh));
+MCRT_DEV float evalTrowbridgeReitzPdf_wh(f3 wo, f3 wh, f2 alpha) {
+    return computeTrowbridgeReitzDistribution(wh, alpha) * evalAbsCosTheta(wh);
 }
-MCRT_DEV float mfTransPdf(v3 wo, v3 wi, v2 a, float etaA, float etaB) {   // bxdfs.cl:717-729
-    if (sameHemi(wo, wi)) return 0.0f;
-    float eta = cosT(wo) > 0.0f ? (etaB / etaA) : (etaA / etaB);
-    v3 wh = normalize(wo + wi * eta);
-    float sd = dot(wo, wh) + eta * dot(wi, wh);
-    float dwh = fabsf((eta * eta * dot(wi, wh)) / (sd * sd));
-    return trD(wh, a) * absCosT(wh) * dwh;
+MCRT_DEV float evalMicrofacetReflectionPdf(f3 wo, f3 wi, f3 wh, f2 alpha) {   // :695-701
+    if (!isSameHemisphere(wo, wi)) return 0.0f;
+    return cl_div(evalTrowbridgeReitzPdf_wh(wo, wh, alpha), (4.0f * cl_dot(wo, wh)));
+}
+MCRT_DEV float evalMicrofacetTransmissionPdf(f3 wo, f3 wi, f2 alpha, float etaA, float etaB) {   // :717-729
+    if (isSameHemisphere(wo, wi)) return 0.0f;
+    float eta = evalCosTheta(wo) > 0.0f ? cr_div(etaB, etaA) : cr_div(etaA, etaB);
+    f3 wh = cl_normalize(wo + wi * eta);
+    float sqrtDenom = cl_dot(wo, wh) + eta * cl_dot(wi, wh);
+    float dwh_dwi = fabsf(cl_div((eta * eta * cl_dot(wi, wh)), (sqrtDenom * sqrtDenom)));
+    return evalTrowbridgeReitzPdf_wh(wo, wh, alpha) * dwh_dwi;
+}
+MCRT_DEV f3 sampleMicrofacetReflection(f2 u, f3 R, f2 alpha, float etaI, float etaT, f3 wo, f3* wi, float* pdf) {
+    f3 wh = sampleTrowbridgeReitzDistribution_wh(u, wo, alpha);   // :731-749
+    *wi = reflect(wo, wh);
+    if (!isSameHemisphere(wo, *wi)) return f3{0.0f, 0.0f, 0.0f};
+    *pdf = evalMicrofacetReflectionPdf(wo, *wi, wh, alpha);
+    return evaluateMicrofacetReflection(R, alpha, etaI, etaT, wo, *wi);
+}
+MCRT_DEV f3 sampleMicrofacetTransmission(f2 u, f3 T, f2 alpha, float etaA, float etaB, f3 wo, f3* wi, float* pdf) {
+    f3 wh = sampleTrowbridgeReitzDistribution_wh(u, wo, alpha);   // :751-762
+    float eta = evalCosTheta(wo) > 0.0f ? cr_div(etaA, etaB) : cr_div(etaB, etaA);
+    if (!refract(wo, wh, eta, wi)) return f3{0.0f, 0.0f, 0.0f};
+    *pdf = evalMicrofacetTransmissionPdf(wo, *wi, alpha, etaA, etaB);
+    return evaluateMicrofacetTransmission(T, alpha, etaA, etaB, wo, *wi);
 }
 
 struct Frame {   // the RTInteraction fields the shading uses
-    v3 p, gn, sn, t, b;   // t = sdpdu, b = sdpdv
-    v2 uv;
+    f3 p, gn, sn, sdpdu, sdpdv;
+    f2 uv;
 };
-MCRT_DEV v3 toLocal(v3 v, const Frame& f) { return mk3(dot(f.t, v), dot(f.sn, v), dot(f.b, v)); }
-MCRT_DEV v3 toWorld(v3 w, const Frame& f) {
-    return mk3(f.t.x * w.x + f.sn.x * w.y + f.b.x * w.z, f.t.y * w.x + f.sn.y * w.y + f.b.y * w.z,
-               f.t.z * w.x + f.sn.z * w.y + f.b.z * w.z);
+MCRT_DEV f3 dirToShadingSpace(f3 w, const Frame& si) {   // bxdfs.cl:81-107
+    return f3{cl_dot(si.sdpdu, w), cl_dot(si.sn, w), cl_dot(si.sdpdv, w)};
+}
+MCRT_DEV f3 dirFromShadingToWorld(f3 w, const Frame& si) {   // bxdfs.cl:94-112
+    const f3 t = si.sdpdu, n = si.sn, bn = si.sdpdv;
+    return f3{t.x * w.x + n.x * w.y + bn.x * w.z, t.y * w.x + n.y * w.y + bn.y * w.z, t.z * w.x + n.z * w.y + bn.z * w.z};
+}
+MCRT_DEV bool isReflection(f3 woWorld, f3 wiWorld, const Frame& si) {
+    return cl_dot(si.gn, woWorld) * cl_dot(si.gn, wiWorld) > 0.0f;
 }
 
 struct Uber {   // RTUberMaterialProperties (materials.cl:67-74)
-    v3 kd, ks, kr, kt, op;
-    float ktw;
-    v2 a;
+    f3 Kd, Ks, Kr, opacity;
+    f4 Kt;
+    f2 roughness;
     float eta;
 };
 
 // bxdfs.cl:804-827
-MCRT_DEV v3 uberEval(const Uber& m, const Frame& f, v3 woW, v3 wiW) {
-    if (!(dot(f.gn, woW) * dot(f.gn, wiW) > 0.0f)) {
-        if (m.ktw < 0.5f) return mk3(0, 0, 0);
-        return mfTransEval(m.kt * m.op, m.a, 1.0f, m.eta, toLocal(woW, f), toLocal(wiW, f));
+MCRT_DEV f3 evaluateUberBSDF(const Uber& m, const Frame& si, f3 woWorld, f3 wiWorld) {
+    if (!isReflection(woWorld, wiWorld, si)) {
+        bool isPerfectSpecularTransmission = m.Kt.w < 0.5f;
+        if (isPerfectSpecularTransmission) return f3{0.0f, 0.0f, 0.0f};
+        f3 wo = dirToShadingSpace(woWorld, si);
+        f3 wi = dirToShadingSpace(wiWorld, si);
+        f3 kt = m.Kt.xyz * m.opacity;
+        return evaluateMicrofacetTransmission(kt, m.roughness, 1.0f, m.eta, wo, wi);
     }
-    v3 wo = toLocal(woW, f), wi = toLocal(wiW, f);
-    return mfReflEval(m.ks * m.op, m.a, 1.0f, m.eta, wo, wi) + (m.kd * m.op) * PI_INV_F;
+    f3 wo = dirToShadingSpace(woWorld, si);
+    f3 wi = dirToShadingSpace(wiWorld, si);
+    f3 kd = m.Kd * m.opacity;
+    f3 ks = m.Ks * m.opacity;
+    return evaluateMicrofacetReflection(ks, m.roughness, 1.0f, m.eta, wo, wi) + evaluateLambertianReflection(kd);
 }
 
-// bxdfs.cl:892-1053 (wi zero-initialised: SURVEY.md App. A Q3)
-MCRT_DEV v3 uberSample(const Uber& m, const Frame& f, v2 u, v3 woW, v3& wiW, float& pdf, int& sampledType) {
-    v3 t = mk3(1.0f - m.op.x, 1.0f - m.op.y, 1.0f - m.op.z);
-    v3 kd = m.kd * m.op, ks = m.ks * m.op, kt = m.kt * m.op, kr = m.kr * m.op;
-    v3 wo = toLocal(woW, f);
-    v3 wi = mk3(0, 0, 0);
-    bool perfT = m.ktw < 0.5f;
-    bool hasT = notBlack(t), hasKd = notBlack(kd), hasKs = notBlack(ks), hasKr = notBlack(kr), hasKt = notBlack(kt);
-    sampledType = 0;
-    int n = (int)hasT + (int)hasKd + (int)hasKs + (int)hasKr + (int)hasKt;   // hasKt counts as spec or glossy
-    if (n == 0) return mk3(0, 0, 0);
-    int chosen = min((int)floorf(u.x * n), n - 1);
-    u.x = u.x * n - chosen;
-    v3 fr = mk3(0, 0, 0);
-    pdf = 0.0f;
-    bool spec = false;
+// bxdfs.cl:892-1053, type = BSDF_ALL, radiance transport; `wi` zero-initialised
+MCRT_DEV f3 sampleUberBSDF(const Uber& m, const Frame& si, f2 u, f3 woWorld, f3* wiWorld, float* pdf, int* sampledType) {
+    f3 t = f3{1.0f, 1.0f, 1.0f} - m.opacity;
+    int numBxDFs = 0;
+    f3 kd = m.Kd * m.opacity;
+    f3 ks = m.Ks * m.opacity;
+    f3 kt = m.Kt.xyz * m.opacity;
+    f3 kr = m.Kr * m.opacity;
+    f3 wo = dirToShadingSpace(woWorld, si);
+    f3 wi = f3{0.0f, 0.0f, 0.0f};
+    bool isPerfectSpecularTransmission = m.Kt.w < 0.5f;
+    *sampledType = 0;
+    const bool hasT = isNotBlack(t), hasKd = isNotBlack(kd), hasKs = isNotBlack(ks), hasKr = isNotBlack(kr),
+               hasKt = isNotBlack(kt);
+    numBxDFs = (int)hasT + (int)hasKd + (int)hasKs + (int)hasKr + (int)hasKt;
+    if (numBxDFs == 0) return f3{0.0f, 0.0f, 0.0f};
+    int chosenBxDFIdx = min((int)floorf(u.x * numBxDFs), numBxDFs - 1);
+    u.x = u.x * numBxDFs - chosenBxDFIdx;
+    f3 f = f3{0.0f, 0.0f, 0.0f};
+    *pdf = 0.0f;
+    bool isSamplingSpecular = false;
     if (hasT) {
-        if (chosen-- == 0) {   // specular transmission of the transparency (eta 1 / 1)
-            // sampleSpecularTransmission(t, 1, 1): etaI == etaT => refract never fails
-            float sg = signf(wo.y);
-            v3 nn = mk3(0.0f, 1.0f, 0.0f) * sg;
-            if (refractDir(wo, nn, 1.0f, wi)) {
-                pdf = 1.0f;
-                v3 ft = t * (1.0f - fresnelDielectric(cosT(wi), 1.0f, 1.0f));
-                ft = ft * ((1.0f * 1.0f) / (1.0f * 1.0f));
-                fr = fr + ft / absCosT(wi);
-            }
-            sampledType |= BSDF_SPEC_TRANS;
-            spec = true;
+        if (chosenBxDFIdx-- == 0) {
+            f += sampleSpecularTransmission(t, 1.0f, 1.0f, wo, &wi, pdf);
+            *sampledType |= BSDF_SPEC_TRANS;
+            isSamplingSpecular = true;
         }
     }
-    if (perfT && hasKt) {
-        if (chosen-- == 0) {   // sampleSpecularTransmission(kt, 1, eta), bxdfs.cl:288-307
-            bool entering = cosT(wo) > 0.0f;
-            float etaI = entering ? 1.0f : m.eta, etaT = entering ? m.eta : 1.0f;
-            v3 nn = mk3(0.0f, 1.0f, 0.0f) * signf(wo.y);
-            if (refractDir(wo, nn, etaI / etaT, wi)) {
-                pdf = 1.0f;
-                v3 ft = kt * (1.0f - fresnelDielectric(cosT(wi), 1.0f, m.eta));
-                ft = ft * ((etaI * etaI) / (etaT * etaT));
-                fr = fr + ft / absCosT(wi);
-            }
-            sampledType |= BSDF_SPEC_TRANS;
-            spec = true;
+    if (isPerfectSpecularTransmission && hasKt) {
+        if (chosenBxDFIdx-- == 0) {
+            f += sampleSpecularTransmission(kt, 1.0f, m.eta, wo, &wi, pdf);
+            *sampledType |= BSDF_SPEC_TRANS;
+            isSamplingSpecular = true;
         }
     }
     if (hasKr) {
-        if (chosen-- == 0) {   // bxdfs.cl:259-268
-            wi = mk3(-wo.x, wo.y, -wo.z);
-            pdf = 1.0f;
-            float F = fresnelDielectric(cosT(wi), 1.0f, m.eta);
-            fr = fr + (F * kr) / absCosT(wi);
-            sampledType |= BSDF_SPEC_REFL;
-            spec = true;
+        if (chosenBxDFIdx-- == 0) {
+            f += sampleSpecularReflection_Dielectric(kr, 1.0f, m.eta, wo, &wi, pdf);
+            *sampledType |= BSDF_SPEC_REFL;
+            isSamplingSpecular = true;
         }
     }
-    if (hasKt) {   // bxdfs.cl:1004: tested regardless of Kt.w (Q2)
-        if (chosen-- == 0) {   // bxdfs.cl:751-762
-            v3 wh = trSampleWh(u, wo, m.a);
-            float eta = cosT(wo) > 0.0f ? (1.0f / m.eta) : (m.eta / 1.0f);
-            if (refractDir(wo, wh, eta, wi)) {
-                pdf = mfTransPdf(wo, wi, m.a, 1.0f, m.eta);
-                fr = fr + mfTransEval(kt, m.a, 1.0f, m.eta, wo, wi);
-            }
-            sampledType |= BSDF_MF_TRANS;
+    if (hasKt) {   // bxdfs.cl:1004, independent of Kt.w
+        if (chosenBxDFIdx-- == 0) {
+            f += sampleMicrofacetTransmission(u, kt, m.roughness, 1.0f, m.eta, wo, &wi, pdf);
+            *sampledType |= BSDF_MF_TRANS;
         }
     }
-    bool lambertEval = false;
+    bool isLambertianEvaluationRequested = false;
     if (hasKd) {
-        if (chosen-- == 0) {   // bxdfs.cl:317-347
-            wi = cosineHemisphere(u);
+        if (chosenBxDFIdx-- == 0) {
+            wi = cosineSampleHemisphere(u);   // sampleCosineHemisphere, bxdfs.cl:317-328
             if (wo.y < 0.0f) wi.y *= -1.0f;
-            pdf = absCosT(wi) * PI_INV_F;
-            fr = fr + kd * PI_INV_F;
-            sampledType |= BSDF_LAMBERT;
-        } else if (!spec && sameHemi(wi, wo)) {
-            lambertEval = true;
+            *pdf = evalAbsCosTheta(wi) * PI_INV_F;
+            f += evaluateLambertianReflection(kd);
+            *sampledType |= BSDF_LAMBERT;
+        } else if (!isSamplingSpecular && isSameHemisphere(wi, wo)) {
+            isLambertianEvaluationRequested = true;
         }
     }
     if (hasKs) {
-        if (chosen-- == 0) {   // bxdfs.cl:731-749
-            v3 wh = trSampleWh(u, wo, m.a);
-            wi = -wo + (2.0f * dot(wh, wo)) * wh;
-            if (sameHemi(wo, wi)) {
-                pdf = mfReflPdf(wo, wi, wh, m.a);
-                fr = fr + mfReflEval(ks, m.a, 1.0f, m.eta, wo, wi);
-            }
-            sampledType |= BSDF_MF_REFL;
-        } else if (!spec && sameHemi(wi, wo)) {
-            fr = fr + mfReflEval(ks, m.a, 1.0f, m.eta, wo, wi);
-            pdf += mfReflPdf(wo, wi, normalize(wo + wi), m.a);
+        if (chosenBxDFIdx-- == 0) {
+            f += sampleMicrofacetReflection(u, ks, m.roughness, 1.0f, m.eta, wo, &wi, pdf);
+            *sampledType |= BSDF_MF_REFL;
+        } else if (!isSamplingSpecular && isSameHemisphere(wi, wo)) {
+            f += evaluateMicrofacetReflection(ks, m.roughness, 1.0f, m.eta, wo, wi);
+            *pdf += evalMicrofacetReflectionPdf(wo, wi, cl_normalize(wo + wi), m.roughness);
         }
     }
-    if (lambertEval) {
-        fr = fr + kd * PI_INV_F;
-        pdf += sameHemi(wo, wi) ? absCosT(wi) * PI_INV_F : 0.0f;
+    if (isLambertianEvaluationRequested) {
+        f += evaluateLambertianReflection(kd);
+        *pdf += evaluateLambertianReflectionPdf(wo, wi);
     }
-    pdf /= (float)n;
-    wiW = toWorld(wi, f);
-    return fr;
+    *pdf = cl_div(*pdf, (float)numBxDFs);
+    *wiWorld = dirFromShadingToWorld(wi, si);
+    return f;
 }

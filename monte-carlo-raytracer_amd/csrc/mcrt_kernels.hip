@@ -22,32 +22,35 @@
 #define TRACE_BLOCK 256
 
 struct TraceRay {
-    v3 o, d;
+    f3 o, d;
     float tmax;
     int mask;
 };
 
 // RR common.cl:220-232
-MCRT_DEV v3 safeInvDir(v3 d) {
-    const float eps = 1e-8f;
-    return mk3(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)), 1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
-               1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
+MCRT_DEV f3 safeInvDir(f3 d) {
+    const float ooeps = 1e-8f;
+    f3 inv;
+    inv.x = cl_div(1.0f, (fabsf(d.x) > ooeps ? d.x : copysignf(ooeps, d.x)));
+    inv.y = cl_div(1.0f, (fabsf(d.y) > ooeps ? d.y : copysignf(ooeps, d.y)));
+    inv.z = cl_div(1.0f, (fabsf(d.z) > ooeps ? d.z : copysignf(ooeps, d.z)));
+    return inv;
 }
 
-// RR common.cl:177-218; 1/denom as v_rcp_f32 (what native_recip lowers to on AMD).
+// RR common.cl:177-218; native_recip lowers to v_rcp_f32 on AMD.
 MCRT_DEV float triHit(const TraceRay& r, float4 A, float4 E1, float4 E2, float tmax) {
-    v3 e1 = ld3(E1), e2 = ld3(E2), a = ld3(A);
-    v3 s1 = cross(r.d, e2);
-    float denom = dot(s1, e1);
+    const f3 e1 = ld3(E1), e2 = ld3(E2);
+    const f3 s1 = cl_cross(r.d, e2);
+    const float denom = cl_dot(s1, e1);
     if (denom == 0.f) return tmax;
-    float invd = __builtin_amdgcn_rcpf(denom);
-    v3 dd = r.o - a;
-    float b1 = dot(dd, s1) * invd;
-    v3 s2 = cross(dd, e1);
-    float b2 = dot(r.d, s2) * invd;
-    float t = dot(e2, s2) * invd;
-    if (b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || t < 0.f || t > tmax) return tmax;
-    return t;
+    const float invd = __builtin_amdgcn_rcpf(denom);
+    const f3 d = r.o - ld3(A);
+    const float b1 = cl_dot(d, s1) * invd;
+    const f3 s2 = cl_cross(d, e1);
+    const float b2 = cl_dot(r.d, s2) * invd;
+    const float temp = cl_dot(e2, s2) * invd;
+    if (b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || temp < 0.f || temp > tmax) return tmax;
+    return temp;
 }
 
 // Closest (ANY = false) or any (ANY = true) hit.  Returns the triangle index or -1 and
@@ -55,8 +58,8 @@ MCRT_DEV float triHit(const TraceRay& r, float4 A, float4 E1, float4 E2, float t
 template <bool ANY>
 MCRT_DEV int traverse(const float4* __restrict__ nodes, const float4* __restrict__ tris, const TraceRay& r,
                       uint32_t* stk, uint32_t* spill, int spillCap, int* overflowFlag, float& tHit) {
-    const v3 inv = safeInvDir(r.d);
-    const v3 oxi = mk3(-r.o.x * inv.x, -r.o.y * inv.y, -r.o.z * inv.z);
+    const f3 inv = safeInvDir(r.d);
+    const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
     float t = r.tmax;
     int hitTri = -1;
     int node = 0;
@@ -140,15 +143,30 @@ MCRT_DEV int traverse(const float4* __restrict__ nodes, const float4* __restrict
     return hitTri;
 }
 
-// RR common.cl:249-277
-MCRT_DEV void triBary(v3 p, float4 A, float4 E1, float4 E2, float& u, float& v) {
-    v3 e1 = ld3(E1), e2 = ld3(E2), e = p - ld3(A);
-    float d00 = dot(e1, e1), d01 = dot(e1, e2), d11 = dot(e2, e2), d20 = dot(e, e1), d21 = dot(e, e2);
-    float den = d00 * d11 - d01 * d01;
-    if (den == 0.f) { u = 0.f; v = 0.f; return; }
-    float inv = __builtin_amdgcn_rcpf(den);
-    u = (d11 * d20 - d01 * d21) * inv;
-    v = (d00 * d21 - d01 * d20) * inv;
+// RR common.cl:249-277 (triangle_calculate_barycentrics)
+MCRT_DEV f2 triBary(f3 p, float4 A, float4 E1, float4 E2) {
+    const f3 e1 = ld3(E1), e2 = ld3(E2);
+    const f3 e = p - ld3(A);
+    const float d00 = cl_dot(e1, e1);
+    const float d01 = cl_dot(e1, e2);
+    const float d11 = cl_dot(e2, e2);
+    const float d20 = cl_dot(e, e1);
+    const float d21 = cl_dot(e, e2);
+    float denom = (d00 * d11 - d01 * d01);
+    if (denom == 0.f) return f2{0.f, 0.f};
+    const float invdenom = __builtin_amdgcn_rcpf(denom);
+    const float b1 = (d11 * d20 - d01 * d21) * invdenom;
+    const float b2 = (d00 * d21 - d01 * d20) * invdenom;
+    return f2{b1, b2};
+}
+
+// hit record of the closest-hit kernels: (u, v, t, triangle) -- intersect_bvh2_lds.cl:200-215
+MCRT_DEV float4 closestRecord(const float4* __restrict__ tris, const TraceRay& r, int tri, float t) {
+    if (tri < 0) return make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+    const float4 A = tris[3 * tri], E1 = tris[3 * tri + 1], E2 = tris[3 * tri + 2];
+    const f3 p = r.o + t * r.d;
+    const f2 uv = triBary(p, A, E1, E2);
+    return make_float4(uv.x, uv.y, t, __int_as_float(tri));
 }
 
 // Wave-uniform chunk fetch for persistent waves.
@@ -183,8 +201,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(TraceCtx c, const mc
         const mcrt_ray rr = rays[i];
         if (rr.extra[1] == 0) continue;   // inactive: output untouched (intersect_bvh2_lds.cl:88)
         TraceRay r;
-        r.o = mk3(rr.o.x, rr.o.y, rr.o.z);
-        r.d = mk3(rr.d.x, rr.d.y, rr.d.z);
+        r.o = ld3(rr.o);
+        r.d = ld3(rr.d);
         r.tmax = rr.o.w;
         r.mask = rr.extra[0];
         float t;
@@ -192,14 +210,12 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(TraceCtx c, const mc
         if (ANY) {
             occl[i] = tri >= 0 ? 1 : -1;
         } else if (tri >= 0) {
-            const float4 A = c.tris[3 * tri], E1 = c.tris[3 * tri + 1], E2 = c.tris[3 * tri + 2];
-            float u, v;
-            triBary(r.o + t * r.d, A, E1, E2, u, v);
+            const float4 h4 = closestRecord(c.tris, r, tri, t);
             mcrt_intersection h;
-            h.shapeid = __float_as_int(A.w);
-            h.primid = __float_as_int(E1.w);
+            h.shapeid = __float_as_int(c.tris[3 * tri].w);
+            h.primid = __float_as_int(c.tris[3 * tri + 1].w);
             h.padding[0] = h.padding[1] = 0;
-            h.uvwt.x = u; h.uvwt.y = v; h.uvwt.z = 0.0f; h.uvwt.w = t;
+            h.uvwt.x = h4.x; h.uvwt.y = h4.y; h.uvwt.z = 0.0f; h.uvwt.w = t;
             hits[i] = h;
         } else {
             hits[i].shapeid = -1;
@@ -220,10 +236,10 @@ MCRT_DEV bool tilePixel(const FrameArgs& f, int tile, int lane, int& x, int& y) 
     return x < (int)f.W && y < (int)f.H;
 }
 
-MCRT_DEV v3 cameraDir(const mcrt_camera& cam, int x, int y) {   // PathTracing.cl:13-35
-    const float rx = 1.0f / (float)cam.width, ry = 1.0f / (float)cam.height;
-    const float u = (float)x * rx, v = (float)y * ry;
-    return normalize(mix(mix(ld3(cam.r00), ld3(cam.r10), u), mix(ld3(cam.r01), ld3(cam.r11), u), v));
+MCRT_DEV f3 cameraDir(const mcrt_camera& cam, int x, int y) {   // PathTracing.cl:13-27
+    const f2 r = f2{cl_div(1.0f, (float)cam.width), cl_div(1.0f, (float)cam.height)};
+    const f2 uv = f2{(float)x * r.x, (float)y * r.y};
+    return lerpDirection(ld3(cam.r00), ld3(cam.r10), ld3(cam.r11), ld3(cam.r01), uv.x, uv.y);
 }
 
 // Camera ray generation fused with the first closest-hit query (RTPrimaryRaysPass).
@@ -249,14 +265,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_primary(TraceCtx c, FrameArgs f
         r.mask = -1;
         float t;
         int tri = traverse<false>(c.nodes, c.tris, r, stk, spill, c.spillCap, c.overflow, t);
-        float4 h = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-        if (tri >= 0) {
-            const float4 A = c.tris[3 * tri], E1 = c.tris[3 * tri + 1], E2 = c.tris[3 * tri + 2];
-            float u, v;
-            triBary(r.o + t * r.d, A, E1, E2, u, v);
-            h = make_float4(u, v, t, __int_as_float(tri));
-        }
-        hitOut[(size_t)y * f.W + x] = h;
+        hitOut[(size_t)y * f.W + x] = closestRecord(c.tris, r, tri, t);
     }
 }
 
@@ -282,14 +291,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_extend(TraceCtx c, const int* _
         r.mask = -1;
         float t;
         int tri = traverse<false>(c.nodes, c.tris, r, stk, spill, c.spillCap, c.overflow, t);
-        float4 h = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-        if (tri >= 0) {
-            const float4 A = c.tris[3 * tri], E1 = c.tris[3 * tri + 1], E2 = c.tris[3 * tri + 2];
-            float u, v;
-            triBary(r.o + t * r.d, A, E1, E2, u, v);
-            h = make_float4(u, v, t, __int_as_float(tri));
-        }
-        hitOut[i] = h;
+        hitOut[i] = closestRecord(c.tris, r, tri, t);
     }
 }
 
@@ -329,64 +331,67 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(TraceCtx c, const int* _
 // ---------------------------------------------------------------------------
 // shading
 // ---------------------------------------------------------------------------
-// KRN/textures.cl:70-125 (bilinear RGBA8, wrap modes)
-MCRT_DEV float4 readTex(const SceneArgs& s, int texId, v2 uv) {
-    const mcrt_texture_desc td = s.textures[texId];
-    const int w = td.width, h = td.height;
-    uv.x -= 1.0f / (float)w * 0.5f;
-    uv.y -= 1.0f / (float)h * 0.5f;
-    switch (td.wrap) {
-    case 0: uv.x -= floorf(uv.x); uv.y -= floorf(uv.y); break;
+// KRN/textures.cl:70-125 (readTexture2Df_linear: bilinear RGBA8, wrap modes)
+MCRT_DEV f4 readTex(const SceneArgs& s, int texId, f2 uv) {
+    const mcrt_texture_desc tex = s.textures[texId];
+    const int w = tex.width, h = tex.height;
+    // The reference's compiled kernel folds `-(1/w)` into `-1/w` and so loses the 2.5-ulp
+    // metadata: these two reciprocals are correctly rounded there (and here).
+    uv.x -= cr_div(1.0f, (float)w) * 0.5f;
+    uv.y -= cr_div(1.0f, (float)h) * 0.5f;
+    switch (tex.wrap) {
+    case 0: uv -= f2{floorf(uv.x), floorf(uv.y)}; break;
     case 1:
         if (uv.x > 1.0f || uv.x < 0.0f) uv.x = 1.0f - (uv.x - floorf(uv.x));
         if (uv.y > 1.0f || uv.y < 0.0f) uv.y = 1.0f - (uv.y - floorf(uv.y));
         break;
-    case 2: uv.x = clampf(uv.x, 0.0f, 1.0f); uv.y = clampf(uv.y, 0.0f, 1.0f); break;
+    case 2: uv = f2{cl_clamp(uv.x, 0.0f, 1.0f), cl_clamp(uv.y, 0.0f, 1.0f)}; break;
     case 3:
-        if (uv.x > 1.0f || uv.x < 0.0f || uv.y > 1.0f || uv.y < 0.0f) return make_float4(0.f, 0.f, 0.f, 0.f);
+        if (uv.x > 1.0f || uv.x < 0.0f || uv.y > 1.0f || uv.y < 0.0f) return f4{0.0f, 0.0f, 0.0f, 0.0f};
         break;
     }
-    int x0 = ((int)floorf(uv.x * (float)w)) % w;
-    int y0 = ((int)floorf(uv.y * (float)h)) % h;
-    int x1 = (x0 + 1) % w, y1 = (y0 + 1) % h;
-    x0 = min(max(x0, 0), w - 1); y0 = min(max(y0, 0), h - 1);
-    x1 = min(max(x1, 0), w - 1); y1 = min(max(y1, 0), h - 1);
-    const float tx = uv.x * (float)w - floorf(uv.x * (float)w);
-    const float ty = uv.y * (float)h - floorf(uv.y * (float)h);
-    const uchar4* base = reinterpret_cast<const uchar4*>(s.texData + td.memOffset);
-    const uchar4 p00 = base[x0 + y0 * w], p10 = base[x1 + y0 * w], p01 = base[x0 + y1 * w], p11 = base[x1 + y1 * w];
-    auto lerp = [&](float a, float b, float c, float d) {
-        float m0 = a + (b - a) * tx, m1 = c + (d - c) * tx;
-        return (m0 + (m1 - m0) * ty) * (1.0f / 255.0f);
-    };
-    return make_float4(lerp(p00.x, p10.x, p01.x, p11.x), lerp(p00.y, p10.y, p01.y, p11.y),
-                       lerp(p00.z, p10.z, p01.z, p11.z), lerp(p00.w, p10.w, p01.w, p11.w));
+    int x0 = ((int)floorf(uv.x * w)) % w;
+    int y0 = ((int)floorf(uv.y * h)) % h;
+    int x1 = (x0 + 1) % w;
+    int y1 = (y0 + 1) % h;
+    x0 = min(max(x0, 0), w - 1);
+    y0 = min(max(y0, 0), h - 1);
+    x1 = min(max(x1, 0), w - 1);
+    y1 = min(max(y1, 0), h - 1);
+    const f2 t = f2{uv.x * w - floorf(uv.x * w), uv.y * h - floorf(uv.y * h)};
+    const uchar4* texD = reinterpret_cast<const uchar4*>(s.texData + tex.memOffset);
+    const uchar4 c00 = texD[x0 + y0 * w], c10 = texD[x1 + y0 * w], c01 = texD[x0 + y1 * w], c11 = texD[x1 + y1 * w];
+    const f4 v00 = f4{(float)c00.x, (float)c00.y, (float)c00.z, (float)c00.w};
+    const f4 v10 = f4{(float)c10.x, (float)c10.y, (float)c10.z, (float)c10.w};
+    const f4 v01 = f4{(float)c01.x, (float)c01.y, (float)c01.z, (float)c01.w};
+    const f4 v11 = f4{(float)c11.x, (float)c11.y, (float)c11.z, (float)c11.w};
+    // mix(a, b, t) = fma(b - a, t, a) per component (device-library mix)
+    const f4 m0 = f4{fmaf(v10.x - v00.x, t.x, v00.x), fmaf(v10.y - v00.y, t.x, v00.y), fmaf(v10.z - v00.z, t.x, v00.z),
+                     fmaf(v10.w - v00.w, t.x, v00.w)};
+    const f4 m1 = f4{fmaf(v11.x - v01.x, t.x, v01.x), fmaf(v11.y - v01.y, t.x, v01.y), fmaf(v11.z - v01.z, t.x, v01.z),
+                     fmaf(v11.w - v01.w, t.x, v01.w)};
+    const f4 m = f4{fmaf(m1.x - m0.x, t.y, m0.x), fmaf(m1.y - m0.y, t.y, m0.y), fmaf(m1.z - m0.z, t.y, m0.z),
+                    fmaf(m1.w - m0.w, t.y, m0.w)};
+    return m * (1.0f / 255.0f);
 }
 
-// KRN/materials.cl:76-91
-MCRT_DEV Uber uberProps(const SceneArgs& s, const mcrt_material& m, v2 uv) {
+// KRN/materials.cl:76-91 (getUberMaterialProperties)
+MCRT_DEV Uber uberProps(const SceneArgs& s, const mcrt_material& material, f2 uv) {
     Uber u;
-    float4 kdo = make_float4(1.f, 1.f, 1.f, 1.f);
-    if (m.uber_diffuseTexId != -1) kdo = readTex(s, m.uber_diffuseTexId, uv);
-    u.kd = mk3(kdo.x, kdo.y, kdo.z) * ld3(m.uber_kd);
-    v3 t3 = mk3(1, 1, 1);
-    if (m.uber_glossyTexId != -1) { float4 t = readTex(s, m.uber_glossyTexId, uv); t3 = mk3(t.x, t.y, t.z); }
-    u.ks = t3 * ld3(m.uber_ks);
-    t3 = mk3(1, 1, 1);
-    if (m.uber_specReflectionTexId != -1) { float4 t = readTex(s, m.uber_specReflectionTexId, uv); t3 = mk3(t.x, t.y, t.z); }
-    u.kr = t3 * ld3(m.uber_kr);
-    t3 = mk3(1, 1, 1);
-    if (m.uber_transmissionTexId != -1) { float4 t = readTex(s, m.uber_transmissionTexId, uv); t3 = mk3(t.x, t.y, t.z); }
-    u.kt = t3 * ld3(m.uber_kt);
-    u.ktw = m.uber_kt.w;
-    t3 = mk3(1, 1, 1);
-    if (m.uber_opacityTexId != -1) { float4 t = readTex(s, m.uber_opacityTexId, uv); t3 = mk3(t.x, t.y, t.z); }
-    u.op = (t3 * ld3(m.uber_opacity)) * kdo.w;
-    v2 r = v2{m.uber_roughness.x, m.uber_roughness.y};
-    if (m.uber_roughnessTexId != -1) { float4 t = readTex(s, m.uber_roughnessTexId, uv); r = v2{t.x, t.y}; }
-    u.eta = m.uber_eta;
-    if (m.uber_iorTexId != -1) u.eta = readTex(s, m.uber_iorTexId, uv).x;
-    u.a = v2{roughnessToAlpha(r.x), roughnessToAlpha(r.y)};
+    const f4 Kd_opacity = material.uber_diffuseTexId != -1 ? readTex(s, material.uber_diffuseTexId, uv) : f4{1.0f, 1.0f, 1.0f, 1.0f};
+    u.Kd = Kd_opacity.xyz * ld3(material.uber_kd);
+    u.Ks = (material.uber_glossyTexId != -1 ? readTex(s, material.uber_glossyTexId, uv).xyz : splat3(1.0f)) * ld3(material.uber_ks);
+    u.Kr = (material.uber_specReflectionTexId != -1 ? readTex(s, material.uber_specReflectionTexId, uv).xyz : splat3(1.0f)) *
+           ld3(material.uber_kr);
+    u.Kt.xyz = (material.uber_transmissionTexId != -1 ? readTex(s, material.uber_transmissionTexId, uv).xyz : splat3(1.0f)) *
+               ld3(material.uber_kt);
+    u.Kt.w = material.uber_kt.w;
+    u.opacity = (material.uber_opacityTexId != -1 ? readTex(s, material.uber_opacityTexId, uv).xyz : splat3(1.0f)) *
+                ld3(material.uber_opacity) * Kd_opacity.w;
+    u.roughness = material.uber_roughnessTexId != -1 ? readTex(s, material.uber_roughnessTexId, uv).xy
+                                                      : f2{material.uber_roughness.x, material.uber_roughness.y};
+    u.eta = material.uber_iorTexId != -1 ? readTex(s, material.uber_iorTexId, uv).x : material.uber_eta;
+    u.roughness = f2{roughnessToAlpha(u.roughness.x), roughnessToAlpha(u.roughness.y)};
     return u;
 }
 
@@ -410,191 +415,244 @@ struct ShadeOut {
     float4 eO, eD, eT;   // extension ray + throughput
 };
 
+// KRN/geometry.cl:9-28
+MCRT_DEV void computeTrianglePartialDerivates(f2 uv0, f2 uv1, f2 uv2, f3 p0, f3 p1, f3 p2, f3 normal, f3* dpdu, f3* dpdv) {
+    f2 duv02 = uv0 - uv2;
+    f2 duv12 = uv1 - uv2;
+    f3 dp02 = p0 - p2;
+    f3 dp12 = p1 - p2;
+    float det = duv02.x * duv12.y - duv02.y * duv12.x;
+    if (isNotNearZero(det)) {
+        float invdet = cl_div(1.0f, det);
+        *dpdu = (duv12.y * dp02 - duv02.y * dp12) * invdet;
+        *dpdv = -(-duv12.x * dp02 + duv02.x * dp12) * invdet;
+    } else {
+        *dpdu = cl_normalize(computeOrthogonalVector(normal));
+        *dpdv = cl_normalize(cl_cross(normal, *dpdu));
+    }
+}
+
+// KRN/samplers.cl:259-269 (sampleDisk); returns the sampled point, *pdf = 1 / area
+MCRT_DEV f3 sampleDisk(f3 p, f3 n, float radius, f2 u, float* pdf) {
+    f2 p2d = concentricSampleDisc(u);
+    f3 t = computeOrthogonalVector(n);
+    f3 b = cl_normalize(cl_cross(n, t));
+    f3 itp = p + t * p2d.x * radius + b * p2d.y * radius;
+    *pdf = cl_div(1.0f, (PI_F * radius * radius));
+    return itp;
+}
+
+// KRN/samplers.cl:275-285 (sampleTriangle)
+MCRT_DEV f3 sampleTriangle(f3 p0, f3 p1, f3 p2, f2 u, f3* gn) {
+    const float su0 = cl_sqrt(u.x);
+    f2 b = f2{1.0f - su0, u.y * su0};
+    f3 itp = b.x * p0 + b.y * p1 + (1 - b.x - b.y) * p2;
+    f3 c = cl_cross(p1 - p0, p2 - p0);
+    *gn = cl_normalize(c);
+    return itp;
+}
+
+// computeSurfaceInteraction (geometry.cl:177-215)
+MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, int shapeIdx, int primIdx, f2 barycentrics) {
+    Frame si;
+    const mcrt_shape& shape = s.shapes[shapeIdx];
+    const uint32_t i0 = s.indices[shape.startIdx + 3 * primIdx];
+    const uint32_t i1 = s.indices[shape.startIdx + 3 * primIdx + 1];
+    const uint32_t i2 = s.indices[shape.startIdx + 3 * primIdx + 2];
+    const f3 p0 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i0]));
+    const f3 p1 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i1]));
+    const f3 p2 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i2]));
+    const float2 t0 = s.uvs[shape.startVertex + i0], t1 = s.uvs[shape.startVertex + i1], t2 = s.uvs[shape.startVertex + i2];
+    const f2 uv0 = f2{t0.x, t0.y}, uv1 = f2{t1.x, t1.y}, uv2 = f2{t2.x, t2.y};
+    const f3 n0 = transformVector3(shape.toWorldInverseTranspose, ld3(s.normals[shape.startVertex + i0]));
+    const f3 n1 = transformVector3(shape.toWorldInverseTranspose, ld3(s.normals[shape.startVertex + i1]));
+    const f3 n2 = transformVector3(shape.toWorldInverseTranspose, ld3(s.normals[shape.startVertex + i2]));
+    si.p = p0 * (1.0f - barycentrics.x - barycentrics.y) + p1 * barycentrics.x + p2 * barycentrics.y;
+    si.uv = uv0 * (1.0f - barycentrics.x - barycentrics.y) + uv1 * barycentrics.x + uv2 * barycentrics.y;
+    si.gn = cl_normalize(cl_cross(p0 - p2, p1 - p2));
+    si.sn = cl_normalize(n0 * (1.0f - barycentrics.x - barycentrics.y) + n1 * barycentrics.x + n2 * barycentrics.y);
+    f3 dpdu, dpdv;
+    computeTrianglePartialDerivates(uv0, uv1, uv2, p0, p1, p2, si.sn, &dpdu, &dpdv);
+    si.sdpdu = cl_normalize(dpdu - cl_dot(si.sn, dpdu) * si.sn);
+    si.sdpdv = cl_normalize(dpdv - cl_dot(si.sn, dpdv) * si.sn - cl_dot(si.sdpdu, dpdv) * si.sdpdu);
+    return si;
+}
+
+// applyNormalMapping_internal (materials.cl:11-19)
+MCRT_DEV void applyNormalMapping(const SceneArgs& s, int texId, Frame& si) {
+    const f3 nm = 2.0f * readTex(s, texId, si.uv).xyz - 1.0f;
+    si.sn = cl_normalize(si.sdpdu * nm.x + si.sdpdv * nm.y + si.sn * nm.z);
+    si.sdpdu = cl_normalize(cl_cross(si.sn, si.sdpdv));
+    si.sdpdv = cl_normalize(cl_cross(si.sdpdu, si.sn));
+}
+
+struct LightSample {
+    f3 Li, wi;
+    float pdf;
+    bool shadowSet;   // setRay() was called on the shadow ray
+    f3 shadowO;
+    float shadowT;
+};
+
+// sampleLightLi (lights.cl:45-146)
+MCRT_DEV LightSample sampleLightLi(const SceneArgs& s, const mcrt_light& light, const Frame& si, float traceErrorOffset,
+                                   f2 u) {
+    LightSample r;
+    r.Li = splat3(0.0f);
+    r.wi = splat3(0.0f);
+    r.pdf = 0.0f;
+    r.shadowSet = false;
+    r.shadowO = splat3(0.0f);
+    r.shadowT = 0.0f;
+    if (light.type == MCRT_DIRECTIONAL_LIGHT) {
+        r.wi = -ld3(light.d);
+        r.pdf = 1.0f;
+        r.shadowO = si.p + si.gn * traceErrorOffset;
+        r.shadowT = 1000.0f;
+        r.shadowSet = true;
+        r.Li = ld3(light.intensity);
+    } else if (light.type == MCRT_POINT_LIGHT) {
+        f3 wi = ld3(light.p) - si.p;
+        float distSq = cl_dot(wi, wi);
+        if (!isNearZero(distSq)) {
+            float dist = cl_sqrt(distSq);
+            wi = cl_div(wi, dist);
+            r.wi = wi;
+            r.pdf = 1.0f;
+            r.shadowO = si.p + si.gn * traceErrorOffset;
+            r.shadowT = dist;
+            r.shadowSet = true;
+            r.Li = cl_div(ld3(light.intensity), distSq);
+        } else {
+            r.wi = wi;
+        }
+    } else if (light.type == MCRT_DISK_AREA_LIGHT || light.type == MCRT_TRIANGLE_MESH_AREA_LIGHT) {
+        f3 lp, lgn;
+        if (light.type == MCRT_DISK_AREA_LIGHT) {
+            lp = sampleDisk(ld3(light.p), ld3(light.d), light.radius, u, &r.pdf);
+            lgn = ld3(light.d);
+        } else {
+            const mcrt_shape shape = s.shapes[light.shapeId];
+            int triangleIdx = (int)((uint32_t)((int)floorf(u.x * shape.numTriangles)) % shape.numTriangles);
+            u.x = u.x * shape.numTriangles - triangleIdx;
+            const uint32_t i0 = s.indices[shape.startIdx + 3 * triangleIdx];
+            const uint32_t i1 = s.indices[shape.startIdx + 3 * triangleIdx + 1];
+            const uint32_t i2 = s.indices[shape.startIdx + 3 * triangleIdx + 2];
+            const f3 p0 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i0]));
+            const f3 p1 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i1]));
+            const f3 p2 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i2]));
+            lp = sampleTriangle(p0, p1, p2, u, &lgn);
+            r.pdf = cl_div(1.0f, light.area);
+        }
+        const f3 rayOrigin = si.p + si.gn * traceErrorOffset;
+        const f3 rayTarget = lp + lgn * RT_TRACE_OFFSET_F;
+        r.wi = light.type == MCRT_DISK_AREA_LIGHT ? cl_normalize(rayTarget - rayOrigin) : cl_normalize(lp - si.p);
+        const float distSq = distanceSquared(lp, si.p);
+        const float c = absDot(lgn, -r.wi);
+        if (isNearZero(c)) {
+            r.pdf = 0.0f;
+        } else {
+            r.pdf *= cl_div(distSq, c);
+            r.shadowO = rayOrigin;
+            r.shadowT = cl_distance(rayOrigin, rayTarget);
+            r.shadowSet = true;
+            r.Li = cl_dot(lgn, -r.wi) > 0.0f ? ld3(light.intensity) : splat3(0.0f);
+        }
+    }
+    return r;
+}
+
 // PathTracing kernel body (PathTracing.cl:52-184) for one path.
 // Returns the radiance term added at this vertex by emission (or by a NaN NEE term
 // with no shadow ray).  NEE terms go to the shadow queue.
-MCRT_DEV v3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pix, float4 hit, v3 dir, v3 throughput,
+MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pix, float4 hit, f3 dir, f3 throughput,
                       int prevFlags, ShadeOut& o) {
     o.pushS = false;
     o.pushE = false;
-    v3 add = mk3(0, 0, 0);
+    f3 add = splat3(0.0f);
     const int tri = __float_as_int(hit.w);
     if (tri < 0 || s.numLights <= 0) return add;
     const float4 A = s.tris[3 * tri], E1 = s.tris[3 * tri + 1];
-    const int shapeId = __float_as_int(A.w), primIdx = __float_as_int(E1.w);
-    const mcrt_shape& sh = s.shapes[shapeId];
-    // computeSurfaceInteraction, geometry.cl:177-215
-    const uint32_t ib = sh.startIdx + 3u * (uint32_t)primIdx;
-    const uint32_t i0 = s.indices[ib] + sh.startVertex, i1 = s.indices[ib + 1] + sh.startVertex,
-                   i2 = s.indices[ib + 2] + sh.startVertex;
-    const v3 p0 = xformPt(sh.toWorldTransform, ld3(s.positions[i0]));
-    const v3 p1 = xformPt(sh.toWorldTransform, ld3(s.positions[i1]));
-    const v3 p2 = xformPt(sh.toWorldTransform, ld3(s.positions[i2]));
-    const float2 uv0 = s.uvs[i0], uv1 = s.uvs[i1], uv2 = s.uvs[i2];
-    const v3 nn0 = xformVec(sh.toWorldInverseTranspose, ld3(s.normals[i0]));
-    const v3 nn1 = xformVec(sh.toWorldInverseTranspose, ld3(s.normals[i1]));
-    const v3 nn2 = xformVec(sh.toWorldInverseTranspose, ld3(s.normals[i2]));
-    const float bu = hit.x, bv = hit.y, w0 = 1.0f - bu - bv;
-    Frame fr;
-    fr.p = p0 * w0 + p1 * bu + p2 * bv;
-    fr.uv = v2{uv0.x * w0 + uv1.x * bu + uv2.x * bv, uv0.y * w0 + uv1.y * bu + uv2.y * bv};
-    fr.gn = normalize(cross(p0 - p2, p1 - p2));
-    fr.sn = normalize(nn0 * w0 + nn1 * bu + nn2 * bv);
-    v3 dpdu, dpdv;
-    {   // geometry.cl:9-28
-        const float du02x = uv0.x - uv2.x, du02y = uv0.y - uv2.y, du12x = uv1.x - uv2.x, du12y = uv1.y - uv2.y;
-        const v3 dp02 = p0 - p2, dp12 = p1 - p2;
-        const float det = du02x * du12y - du02y * du12x;
-        if (isNotNearZero(det)) {
-            const float invdet = 1.0f / det;
-            dpdu = (du12y * dp02 - du02y * dp12) * invdet;
-            dpdv = (-((-du12x) * dp02 + du02x * dp12)) * invdet;
-        } else {
-            dpdu = normalize(orthogonalVector(fr.sn));
-            dpdv = normalize(cross(fr.sn, dpdu));
-        }
-    }
-    fr.t = normalize(dpdu - dot(fr.sn, dpdu) * fr.sn);
-    fr.b = normalize(dpdv - dot(fr.sn, dpdv) * fr.sn - dot(fr.t, dpdv) * fr.t);
-    const v3 wo = -dir;
-    float offset = dot(fr.gn, wo) < 0.0f ? -RT_TRACE_OFFSET_F : RT_TRACE_OFFSET_F;
-    const int matId = sh.materialId;
+    const int shapeIdx = __float_as_int(A.w), primIdx = __float_as_int(E1.w);
+    const mcrt_shape& shape = s.shapes[shapeIdx];
+    Frame si = computeSurfaceInteraction(s, shapeIdx, primIdx, f2{hit.x, hit.y});
+    const f3 wo = -dir;
+    const bool isBackfacing = cl_dot(si.gn, wo) < 0.0f;
+    const float traceErrorOffset = isBackfacing ? -RT_TRACE_OFFSET_F : RT_TRACE_OFFSET_F;
+    const int materialId = shape.materialId;
     mcrt_material mat;
-    if (matId != -1) {
-        mat = s.materials[matId];
-        if (mat.uber_normalMapId != -1) {   // materials.cl:14-30
-            const float4 tn = readTex(s, mat.uber_normalMapId, fr.uv);
-            const v3 nm = mk3(2.0f * tn.x - 1.0f, 2.0f * tn.y - 1.0f, 2.0f * tn.z - 1.0f);
-            fr.sn = normalize(fr.t * nm.x + fr.b * nm.y + fr.sn * nm.z);
-            fr.t = normalize(cross(fr.sn, fr.b));
-            fr.b = normalize(cross(fr.t, fr.sn));
-        }
+    if (materialId != -1) {
+        mat = s.materials[materialId];
+        if (mat.uber_normalMapId != -1) applyNormalMapping(s, mat.uber_normalMapId, si);
     }
-    if (bounce == 0) throughput = mk3(1.0f, 1.0f, 1.0f);
-    // emission (PathTracing.cl:86-101)
-    if (sh.lightID != -1 && (bounce == 0 || (prevFlags & BSDF_SPECULAR) == BSDF_SPECULAR)) {
-        const mcrt_light& L = s.lights[sh.lightID];
-        v3 Le = mk3(0, 0, 0);
-        if ((L.type == MCRT_DISK_AREA_LIGHT || L.type == MCRT_TRIANGLE_MESH_AREA_LIGHT) && dot(fr.gn, wo) > 0.0f)
+    if (bounce == 0) throughput = splat3(1.0f);
+    // emission (PathTracing.cl:82-101)
+    if (shape.lightID != -1 && (bounce == 0 || (prevFlags & BSDF_SPECULAR) == BSDF_SPECULAR)) {
+        const mcrt_light& L = s.lights[shape.lightID];
+        f3 Le = splat3(0.0f);
+        if ((L.type == MCRT_DISK_AREA_LIGHT || L.type == MCRT_TRIANGLE_MESH_AREA_LIGHT) && cl_dot(si.gn, wo) > 0.0f)
             Le = ld3(L.intensity);
         return throughput * Le;
     }
-    Sampler smp = makeSampler(f.sampler, (uint32_t)pix, f.frame, bounce, f.W, f.H, s.sobol);
-    // next-event estimation: one light (PathTracing.cl:107-136, lights.cl:45-146)
+    Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, bounce, f.W, f.H, s.sobol);
+    const bool isUber = materialId != -1 && mat.type == 0;   // materials.cl:130-142: other types evaluate to 0
+    Uber um;
+    if (isUber) um = uberProps(s, mat, si.uv);
+    // next-event estimation, one light (PathTracing.cl:107-136)
     {
-        uint32_t li = (uint32_t)floorf(sample1D(smp) * (float)s.numLights);
-        li %= (uint32_t)s.numLights;
-        const v2 u = sample2D(smp);
-        const mcrt_light L = s.lights[li];
-        v3 wi = mk3(0, 0, 0), Li = mk3(0, 0, 0);
-        float pdf = 0.0f;
-        bool shadowSet = false;
-        v3 so = mk3(0, 0, 0);
-        float stmax = 0.0f;
-        const v3 ro = fr.p + fr.gn * offset;
-        if (L.type == MCRT_DIRECTIONAL_LIGHT) {
-            wi = -ld3(L.d);
-            pdf = 1.0f;
-            so = ro; stmax = 1000.0f; shadowSet = true;
-            Li = ld3(L.intensity);
-        } else if (L.type == MCRT_POINT_LIGHT) {
-            v3 w = ld3(L.p) - fr.p;
-            const float d2 = dot(w, w);
-            if (!isNearZero(d2)) {
-                const float dist = sqrtf(d2);
-                wi = w / dist;
-                pdf = 1.0f;
-                so = ro; stmax = dist; shadowSet = true;
-                Li = ld3(L.intensity) / d2;
-            }
-        } else if (L.type == MCRT_DISK_AREA_LIGHT || L.type == MCRT_TRIANGLE_MESH_AREA_LIGHT) {
-            v3 lp, lg;
-            if (L.type == MCRT_DISK_AREA_LIGHT) {   // samplers.cl:259-269
-                const v2 d2 = concentricDisc(u);
-                const v3 n = ld3(L.d);
-                const v3 t = orthogonalVector(n);
-                const v3 b = normalize(cross(n, t));
-                lp = ld3(L.p) + t * d2.x * L.radius + b * d2.y * L.radius;
-                lg = n;
-                pdf = 1.0f / (PI_F * L.radius * L.radius);
-            } else {   // lights.cl:102-141, samplers.cl:227-231,275-285
-                const mcrt_shape& ls = s.shapes[L.shapeId];
-                const int nt = (int)ls.numTriangles;
-                const int k = (int)((uint32_t)((int)floorf(u.x * (float)ls.numTriangles)) % ls.numTriangles);
-                v2 uu = v2{u.x * (float)nt - (float)k, u.y};
-                const uint32_t lb = ls.startIdx + 3u * (uint32_t)k;
-                const v3 q0 = xformPt(ls.toWorldTransform, ld3(s.positions[ls.startVertex + s.indices[lb]]));
-                const v3 q1 = xformPt(ls.toWorldTransform, ld3(s.positions[ls.startVertex + s.indices[lb + 1]]));
-                const v3 q2 = xformPt(ls.toWorldTransform, ld3(s.positions[ls.startVertex + s.indices[lb + 2]]));
-                const float su0 = sqrtf(uu.x);
-                const float bx = 1.0f - su0, by = uu.y * su0;
-                lp = bx * q0 + by * q1 + (1.0f - bx - by) * q2;
-                lg = normalize(cross(q1 - q0, q2 - q0));
-                pdf = 1.0f / L.area;
-            }
-            const v3 rt = lp + lg * RT_TRACE_OFFSET_F;
-            wi = (L.type == MCRT_DISK_AREA_LIGHT) ? normalize(rt - ro) : normalize(lp - fr.p);
-            const v3 dd = lp - fr.p;
-            const float dist2 = dot(dd, dd);
-            const float cth = absDot(lg, -wi);
-            if (isNearZero(cth)) {
-                pdf = 0.0f;
-            } else {
-                pdf *= dist2 / cth;
-                so = ro;
-                stmax = length(ro - rt);
-                shadowSet = true;
-                Li = dot(lg, -wi) > 0.0f ? ld3(L.intensity) : mk3(0, 0, 0);
-            }
+        uint32_t lightIdx = (uint32_t)floorf(getSample1D(sampler) * s.numLights);
+        lightIdx %= (uint32_t)s.numLights;
+        const f2 u = getSample2D(sampler);
+        const mcrt_light light = s.lights[lightIdx];
+        const LightSample ls = sampleLightLi(s, light, si, traceErrorOffset, u);
+        float lightPdf = ls.pdf * light.choicePdf;
+        f3 L = splat3(0.0f);
+        if (materialId != -1) {
+            f3 bsdf = isUber ? evaluateUberBSDF(um, si, wo, ls.wi) : splat3(0.0f);
+            bsdf *= absDot(ls.wi, si.sn);
+            if (!isNearZero(lightPdf)) L = cl_div(ls.Li * bsdf, lightPdf);
         }
-        pdf *= L.choicePdf;
-        v3 Lo = mk3(0, 0, 0);
-        Uber um;
-        if (matId != -1) {
-            um = uberProps(s, mat, fr.uv);
-            v3 bsdf = uberEval(um, fr, wo, wi);
-            bsdf = bsdf * absDot(wi, fr.sn);
-            if (!isNearZero(pdf)) Lo = (Li * bsdf) / pdf;
-        }
-        const v3 term = throughput * Lo;
+        const f3 term = throughput * L;
         if (term.x != 0.0f || term.y != 0.0f || term.z != 0.0f) {
-            if (shadowSet) {
+            if (ls.shadowSet) {
                 o.pushS = true;
-                o.sO = make_float4(so.x, so.y, so.z, stmax);
-                o.sD = make_float4(wi.x, wi.y, wi.z, __int_as_float(pix));
+                o.sO = make_float4(ls.shadowO.x, ls.shadowO.y, ls.shadowO.z, ls.shadowT);
+                o.sD = make_float4(ls.wi.x, ls.wi.y, ls.wi.z, __int_as_float(pix));
                 o.sL = make_float4(term.x, term.y, term.z, 0.0f);
             } else {
-                add = term * 0.0f;   // V = 0 (NaN stays NaN, ShadowPass semantics)
+                add = term * 0.0f;   // no shadow ray: V = 0 (a NaN term stays NaN, ShadowPass semantics)
             }
         }
-        // extension (PathTracing.cl:138-175)
-        if (bounce + 1 < f.maxDepth) {
-            const v2 bs = sample2D(smp);
-            if (matId != -1) {
-                v3 wn;
-                float bpdf;
-                int st;
-                const v3 fb = uberSample(um, fr, bs, wo, wn, bpdf, st);
-                if (!(isNearZero(bpdf) || isBlack(fb))) {
-                    const v3 tp = (fb / bpdf) * absDot(wn, fr.sn);
-                    const v3 nt = throughput * tp;
-                    float off = offset;
-                    if ((st & BSDF_TRANSMISSION) != 0 && dot(fr.gn, wn) * signf(off) < 0.0f) off *= -1.0f;
-                    const v3 no = fr.p + fr.gn * off;
-                    bool alive = true;
-                    if (f.russianRoulette && bounce + 1 >= f.rrStartDepth) {   // perf mode only
-                        const float q = fmaxf(0.05f, 1.0f - fmaxf(nt.x, fmaxf(nt.y, nt.z)));
-                        const float ur = (float)wangHash((uint32_t)pix * 9781u + (uint32_t)f.frame * 6271u + (uint32_t)bounce) * 0x1p-32f;
-                        alive = ur >= q;
-                        o.eT = make_float4(nt.x / (1.0f - q), nt.y / (1.0f - q), nt.z / (1.0f - q), 0.0f);
-                    } else {
-                        o.eT = make_float4(nt.x, nt.y, nt.z, 0.0f);
-                    }
-                    if (alive) {
-                        o.pushE = true;
-                        o.eO = make_float4(no.x, no.y, no.z, __int_as_float(pix));
-                        o.eD = make_float4(wn.x, wn.y, wn.z, __int_as_float(st));
-                    }
+    }
+    // extension (PathTracing.cl:138-175)
+    if (bounce + 1 < f.maxDepth) {
+        const f2 bsdfSample = getSample2D(sampler);
+        if (isUber) {
+            f3 wi;
+            float pdf;
+            int sampledType;
+            f3 bsdfBounce = sampleUberBSDF(um, si, bsdfSample, wo, &wi, &pdf, &sampledType);
+            if (!(isNearZero(pdf) || isBlack(bsdfBounce))) {
+                bsdfBounce = cl_div(bsdfBounce, pdf);
+                const f3 tp = bsdfBounce * absDot(wi, si.sn);
+                const f3 nt = throughput * tp;
+                float off = traceErrorOffset;
+                if ((sampledType & BSDF_TRANSMISSION) != 0 && cl_dot(si.gn, wi) * cl_sign(off) < 0.0f) off *= -1.0f;
+                const f3 no = si.p + si.gn * off;
+                bool alive = true;
+                if (f.russianRoulette && bounce + 1 >= f.rrStartDepth) {   // opt-in perf mode
+                    const float q = fmaxf(0.05f, 1.0f - fmaxf(nt.x, fmaxf(nt.y, nt.z)));
+                    const float ur = (float)wangHash((uint32_t)pix * 9781u + (uint32_t)f.frame * 6271u + (uint32_t)bounce) * 0x1p-32f;
+                    alive = ur >= q;
+                    const f3 ntq = cl_div(nt, (1.0f - q));
+                    o.eT = make_float4(ntq.x, ntq.y, ntq.z, 0.0f);
+                } else {
+                    o.eT = make_float4(nt.x, nt.y, nt.z, 0.0f);
+                }
+                if (alive) {
+                    o.pushE = true;
+                    o.eO = make_float4(no.x, no.y, no.z, __int_as_float(pix));
+                    o.eD = make_float4(wi.x, wi.y, wi.z, __int_as_float(sampledType));
                 }
             }
         }
@@ -615,8 +673,8 @@ __global__ __launch_bounds__(256) void k_shade0(SceneArgs s, FrameArgs f, const 
     if (valid) {
         const mcrt_camera& cam = *camp;
         const int pix = y * (int)f.W + x;
-        const v3 dir = cameraDir(cam, x, y);
-        const v3 add = shadePath(s, f, 0, pix, hits[pix], dir, mk3(1, 1, 1), 0, o);
+        const f3 dir = cameraDir(cam, x, y);
+        const f3 add = shadePath(s, f, 0, pix, hits[pix], dir, splat3(1.0f), 0, o);
         radiance[pix] = make_float4(add.x, add.y, add.z, 0.0f);
     }
     const int ss = waveAppend(q.shadowCount, o.pushS);
@@ -637,7 +695,7 @@ __global__ __launch_bounds__(256) void k_shadeN(SceneArgs s, FrameArgs f, int bo
     if (i < n) {
         const float4 O = qO[i], D = qD[i], Tp = qT[i];
         const int pix = __float_as_int(O.w);
-        const v3 add = shadePath(s, f, bounce, pix, hits[i], ld3(D), ld3(Tp), __float_as_int(D.w), o);
+        const f3 add = shadePath(s, f, bounce, pix, hits[i], ld3(D), ld3(Tp), __float_as_int(D.w), o);
         if (add.x != 0.0f || add.y != 0.0f || add.z != 0.0f || add.x != add.x) {
             float4 r = radiance[pix];
             r.x += add.x; r.y += add.y; r.z += add.z;
@@ -662,22 +720,24 @@ __global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, floa
     int x, y;
     if (tile >= f.numTiles || !tilePixel(f, tile, lane, x, y)) return;
     const int pix = y * (int)f.W + x;
-    const float4 r = radiance[pix];
-    const float4 c = make_float4(clampf(r.x, 0.0f, 1000.0f), clampf(r.y, 0.0f, 1000.0f), clampf(r.z, 0.0f, 1000.0f),
-                                 clampf(r.w, 0.0f, 1000.0f));
-    float4 s;
+    const float4 r4 = radiance[pix];
+    const f4 radiance4 = f4{cl_clamp(r4.x, 0.0f, 1000.0f), cl_clamp(r4.y, 0.0f, 1000.0f), cl_clamp(r4.z, 0.0f, 1000.0f),
+                            cl_clamp(r4.w, 0.0f, 1000.0f)};
+    f4 s;
     float ws;
     if (frame == 0) {
-        s = make_float4(c.x * w, c.y * w, c.z * w, c.w * w);
+        s = radiance4 * w;
         ws = w;
     } else {
-        s = wsum[pix];
-        s.x += c.x * w; s.y += c.y * w; s.z += c.z * w; s.w += c.w * w;
+        const float4 o = wsum[pix];
+        s = f4{o.x, o.y, o.z, o.w};
+        s += radiance4 * w;
         ws = wts[pix] + w;
     }
-    wsum[pix] = s;
+    wsum[pix] = make_float4(s.x, s.y, s.z, s.w);
     wts[pix] = ws;
-    image[pix] = make_float4(s.x / ws, s.y / ws, s.z / ws, s.w / ws);
+    const f4 fin = cl_div(s, ws);
+    image[pix] = make_float4(fin.x, fin.y, fin.z, fin.w);
 }
 
 // image = sum / weight after a multi-GPU reduce of the accumulators
@@ -687,7 +747,7 @@ __global__ __launch_bounds__(256) void k_resolve(int n, const float4* __restrict
     if (i >= n) return;
     const float4 s = wsum[i];
     const float w = wts[i];
-    image[i] = make_float4(s.x / w, s.y / w, s.z / w, s.w / w);
+    image[i] = make_float4(cl_div(s.x, w), cl_div(s.y, w), cl_div(s.z, w), cl_div(s.w, w));
 }
 
 // ---------------------------------------------------------------------------

@@ -48,6 +48,7 @@ SIGNATURES = {
     "mcrt_framebuffer_stats": (_c.c_int, [_vp, _vp, _vp, _vp]),
     "mcrt_framebuffer_copy_device": (_c.c_int, [_vp, _c.c_int, _vp]),
     "mcrt_framebuffer_set_accumulation": (_c.c_int, [_vp, _vp, _vp]),
+    "mcrt_framebuffer_read_queue": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int32)]),
     "mcrt_make_pinhole_camera": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _c.c_float, _c.c_float, _c.c_uint32,
                                             _c.c_uint32, _vp, _vp]),
 }
@@ -210,6 +211,15 @@ class FrameBuffer:
         a, b, c = _c.c_int64(), _c.c_int64(), _c.c_int64()
         _check(lib().mcrt_framebuffer_stats(self.h, _c.byref(a), _c.byref(b), _c.byref(c)), self.ctx.h)
         return {"closest_rays": a.value, "any_rays": b.value, "shaded_paths": c.value}
+
+    def read_queue(self, which):
+        """(a, b, c) float4 arrays of the last bounce's shadow (0) / extension (1) queue."""
+        cnt = _c.c_int32()
+        _check(lib().mcrt_framebuffer_read_queue(self.h, which, None, 0, _c.byref(cnt)), self.ctx.h)
+        n = cnt.value
+        out = np.zeros((3, max(n, 1), 4), np.float32)
+        _check(lib().mcrt_framebuffer_read_queue(self.h, which, _p(out), max(n, 1), _c.byref(cnt)), self.ctx.h)
+        return out[0, :n], out[1, :n], out[2, :n]
 
     def close(self):
         if self.h:

@@ -284,6 +284,7 @@ def clref(variant="ieee"):
         L.clref_render.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _vp, _vp]
         L.clref_accumulate.argtypes = [_vp, _c.c_int, _vp, _vp]
         L.clref_trace.argtypes = [_vp, _vp, _c.c_int, _vp, _c.c_int]
+        L.clref_read.argtypes = [_vp, _c.c_int, _vp]
         st = L.clref_init(os.path.join(HERE, "_ref").encode(), variant.encode())
         if st != 0:
             raise RuntimeError(f"clref_init({variant}) = {st}: {L.clref_error().decode()}")
@@ -322,6 +323,18 @@ class CLRefScene:
         if st != 0:
             raise RuntimeError(f"clref_accumulate {st}: {self.L.clref_error().decode()}")
         return img
+
+    READ = {"rays": (0, 48), "isect": (1, 32), "shadow_rays": (2, 48), "temp": (3, 16), "throughput": (4, 32),
+            "occlusion": (5, 4), "radiance": (6, 16)}
+
+    def read(self, which, W, H):
+        """Raw bytes of an intermediate buffer of the last frame (diagnostics)."""
+        idx, sz = self.READ[which]
+        out = np.zeros(W * H * sz, np.uint8)
+        st = self.L.clref_read(self.h, idx, _p(out))
+        if st != 0:
+            raise RuntimeError(f"clref_read {st}: {self.L.clref_error().decode()}")
+        return out
 
     def trace(self, rays, any_hit=False, init=-7):
         from mcrt.types import ISECT_DTYPE

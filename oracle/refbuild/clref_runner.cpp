@@ -334,4 +334,55 @@ __attribute__((visibility("default"))) int clref_trace(void* sp, const void* ray
     return good ? 0 : -1;
 }
 
+// Debug read-back of the last frame's intermediate buffers (stage-level parity diagnostics):
+// which 0 rays (48 B), 1 isect (32 B), 2 shadow rays (48 B), 3 temp radiance (16 B),
+// 4 throughput records (32 B), 5 occlusion (4 B), 6 radiance (16 B); per pixel.
+__attribute__((visibility("default"))) int clref_read(void* sp, int which, void* out) {
+    Scene* s = (Scene*)sp;
+    const size_t n = (size_t)s->W * s->H;
+    cl_mem m[7] = {s->rays, s->isect, s->shadowRays, s->temp, s->thr, s->occl, s->radiance};
+    size_t sz[7] = {48, 32, 48, 16, 32, 4, 16};
+    if (which < 0 || which > 6 || !m[which]) { g_err = "clref_read: bad buffer"; return -1; }
+    return ok(clEnqueueReadBuffer(R.q, m[which], CL_TRUE, 0, sz[which] * n, out, 0, nullptr, nullptr), "read") ? 0 : -2;
+}
+
+// Stage probe (clprobe.cl, test infrastructure): per-pixel intermediates of the reference's
+// PathTracing functions for given intersections / incoming directions; out: 20 float4 / pixel.
+__attribute__((visibility("default"))) int clref_probe(void* sp, const char* hsaco, const void* isects,
+                                                       const float* dirs, int W, int H, int frame, float* out) {
+    Scene* s = (Scene*)sp;
+    static cl_program prog = nullptr;
+    static cl_kernel k = nullptr;
+    cl_int e = 0;
+    if (!k) {
+        prog = loadProgram(hsaco);
+        if (!prog) return -1;
+        k = clCreateKernel(prog, "ProbeShade", &e);
+        if (!ok(e, "kernel ProbeShade")) return -2;
+    }
+    const size_t n = (size_t)W * H;
+    cl_mem bi = buf(32 * n, isects), bd = buf(16 * n, dirs), bs = buf(48 * n, nullptr);
+    std::vector<float> zero(80 * n, 0.0f);
+    cl_mem bo = buf(80 * 4 * n, zero.data());
+    int a = 0;
+    if (!setSceneArgs(k, s, a)) return -3;
+    e = 0;
+    e |= arg(k, a++, W);
+    e |= arg(k, a++, H);
+    e |= arg(k, a++, frame);
+    e |= arg(k, a++, bi);
+    e |= arg(k, a++, bd);
+    e |= arg(k, a++, bs);
+    e |= arg(k, a++, bo);
+    if (!ok(e, "probe args")) return -4;
+    size_t gs = (n + 63) / 64 * 64, ls = 64;
+    bool good = ok(clEnqueueNDRangeKernel(R.q, k, 1, nullptr, &gs, &ls, 0, nullptr, nullptr), "probe launch") &&
+                ok(clEnqueueReadBuffer(R.q, bo, CL_TRUE, 0, 80 * 4 * n, out, 0, nullptr, nullptr), "probe read");
+    clReleaseMemObject(bi);
+    clReleaseMemObject(bd);
+    clReleaseMemObject(bs);
+    clReleaseMemObject(bo);
+    return good ? 0 : -5;
+}
+
 }  // extern "C"

@@ -40,9 +40,19 @@ def build_scene(name):
     raise KeyError(name)
 
 
+def sm_job(out_path, variant, W, H, tris):
+    """Two depth-2 frames of the San-Miguel proxy (test_san_miguel_proxy_bit_exact_vs_reference)."""
+    cs = po.CLRefScene(scenes.san_miguel_proxy(tris=tris), variant)
+    cam = scene_camera("san_miguel_proxy", W, H)
+    np.savez_compressed(out_path, **{f"f{f}": cs.render(cam, frame=f, max_depth=2) for f in (0, 1)})
+
+
 def main():
     out_path = sys.argv[1]
     variant = sys.argv[2] if len(sys.argv) > 2 else "ieee"
+    if len(sys.argv) > 3 and sys.argv[3] == "sm":
+        sm_job(out_path, variant, int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6]))
+        return
     res = {}
     t0 = time.time()
     po.clref(variant)

@@ -1,0 +1,79 @@
+"""Diagnostic / comparison job (GPU box): renders frame(s) of a scene with the product and with
+the reference's own OpenCL kernels (child process), saves both, and times the reference pipeline.
+
+usage: python tools/sm_diag.py OUT_PREFIX [scene] [W] [H] [tris] [frames]
+  product -> OUT_PREFIX_product.npz ; reference -> OUT_PREFIX_clref_{ieee,fast}.npz
+"""
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "monte-carlo-raytracer_amd"))
+sys.path.insert(0, ROOT)
+
+
+def make(scene_name, tris):
+    from mcrt import scenes
+    return scenes.san_miguel_proxy(tris=tris) if scene_name == "san_miguel_proxy" else scenes.dragon_proxy(tris=tris)
+
+
+def product(prefix, scene_name, W, H, tris, frames):
+    from mcrt import lib
+    from mcrt.camera import scene_camera
+    sc = make(scene_name, tris)
+    cam = scene_camera(scene_name, W, H)
+    ctx = lib.Context(0)
+    ds = lib.DeviceScene(ctx, sc)
+    fb = lib.FrameBuffer(ctx, W, H)
+    out = {}
+    for f in range(frames):
+        fb.render(ds, cam, frame=f, max_depth=2)
+        out[f"f{f}"] = fb.read(0)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for f in range(frames):
+        fb.render(ds, cam, frame=f, max_depth=2)
+    ctx.sync()
+    out["ms_per_frame"] = np.array((time.perf_counter() - t0) / frames * 1e3)
+    np.savez_compressed(prefix + "_product.npz", **out)
+    print("product ms/frame", float(out["ms_per_frame"]))
+
+
+def reference(prefix, scene_name, W, H, tris, frames, variant):
+    from mcrt.camera import scene_camera
+    from oracle import pyoracle as po
+    sc = make(scene_name, tris)
+    cam = scene_camera(scene_name, W, H)
+    nodes = None
+    cs = po.CLRefScene(sc, variant, nodes=nodes)
+    out = {}
+    for f in range(frames):
+        out[f"f{f}"] = cs.render(cam, frame=f, max_depth=2)
+    t0 = time.perf_counter()
+    for f in range(frames):
+        cs.render(cam, frame=f, max_depth=2)
+    out["ms_per_frame"] = np.array((time.perf_counter() - t0) / frames * 1e3)
+    np.savez_compressed(prefix + f"_clref_{variant}.npz", **out)
+    print(f"reference OpenCL ({variant}) ms/frame", float(out["ms_per_frame"]))
+
+
+if __name__ == "__main__":
+    prefix = sys.argv[1]
+    scene_name = sys.argv[2] if len(sys.argv) > 2 else "san_miguel_proxy"
+    W = int(sys.argv[3]) if len(sys.argv) > 3 else 1920
+    H = int(sys.argv[4]) if len(sys.argv) > 4 else 1080
+    tris = int(sys.argv[5]) if len(sys.argv) > 5 else 10_000_000
+    frames = int(sys.argv[6]) if len(sys.argv) > 6 else 2
+    if len(sys.argv) > 7:   # child: reference variant
+        reference(prefix, scene_name, W, H, tris, frames, sys.argv[7])
+        sys.exit(0)
+    product(prefix, scene_name, W, H, tris, frames)
+    for v in ("ieee", "fast"):
+        r = subprocess.run([sys.executable, __file__, prefix, scene_name, str(W), str(H), str(tris), str(frames), v],
+                           timeout=900)
+        if r.returncode != 0:
+            sys.exit(r.returncode)

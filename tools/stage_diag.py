@@ -1,0 +1,116 @@
+"""Stage-level bit parity of the product against the reference OpenCL kernels (GPU box).
+Child process (clref): renders frame 0 at max_depth 1 and 2 and dumps the intermediate
+buffers.  Parent (product): replays the reference's own primary rays / shadow rays through
+mcrt_trace_closest / mcrt_trace_any and renders the same frames; prints exact-match rates.
+usage: python tools/stage_diag.py OUT_DIR"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "monte-carlo-raytracer_amd"))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from clref_job import build_scene  # noqa: E402
+
+CASES = [("cornell", 64, 64), ("mixed", 96, 64)]
+
+
+def cam_of(name, W, H):
+    from mcrt.camera import scene_camera
+    return scene_camera("dragon_proxy" if name == "dragon_small" else name, W, H)
+
+
+def child(out_dir):
+    from oracle import pyoracle as po
+    for name, W, H in CASES:
+        cs = po.CLRefScene(build_scene(name), "ieee")
+        cam = cam_of(name, W, H)
+        res = {}
+        for D in (1, 2):
+            res[f"rad_d{D}"] = cs.render(cam, frame=0, max_depth=D)
+            if D == 1:
+                for b in ("rays", "isect", "shadow_rays", "temp", "occlusion"):
+                    res[f"{b}_d1"] = cs.read(b, W, H)
+        np.savez_compressed(os.path.join(out_dir, f"stage_{name}.npz"), **res)
+
+
+def bits_equal(a, b):
+    return np.ascontiguousarray(a).view(np.uint32) == np.ascontiguousarray(b).view(np.uint32)
+
+
+def parent(out_dir):
+    import torch
+    from mcrt import lib
+    from mcrt import types as T
+    r = subprocess.run([sys.executable, __file__, out_dir, "child"], timeout=300)
+    if r.returncode != 0:
+        sys.exit(r.returncode)
+    ctx = lib.Context(0)
+    for name, W, H in CASES:
+        z = np.load(os.path.join(out_dir, f"stage_{name}.npz"))
+        sc = build_scene(name)
+        ds = lib.DeviceScene(ctx, sc)
+        fb = lib.FrameBuffer(ctx, W, H)
+        cam = cam_of(name, W, H)
+        n = W * H
+        # 1. primary hits on the reference's own primary rays
+        rays = z["rays_d1"].view(T.RAY_DTYPE)
+        rt = torch.from_numpy(z["rays_d1"].copy()).cuda()
+        ht = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+        ds.trace_closest(rt.data_ptr(), n, ht.data_ptr())
+        ctx.sync()
+        hp = ht.cpu().numpy().view(T.ISECT_DTYPE)
+        hr = z["isect_d1"].view(T.ISECT_DTYPE)
+        act = rays["extra"][:, 1] != 0
+        # after PathTracing(D=1) the primary rays of hit pixels are still active (no extension)
+        same_id = (hp["shapeid"] == hr["shapeid"]) & (hp["primid"] == hr["primid"])
+        uvwt_eq = bits_equal(hp["uvwt"][:, [0, 1, 3]], hr["uvwt"][:, [0, 1, 3]]).all(-1)
+        hit = hr["shapeid"] >= 0
+        print(f"[{name}] primary: active {act.mean():.3f} same prim {same_id[act].mean():.5f} "
+              f"uv,t bit-exact (hits) {uvwt_eq[act & hit].mean():.5f}")
+        # 2. shadow rays of bounce 0 through the product's any-hit
+        srays = z["shadow_rays_d1"].view(T.RAY_DTYPE)
+        st = torch.from_numpy(z["shadow_rays_d1"].copy()).cuda()
+        ot = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+        ds.trace_any(st.data_ptr(), n, ot.data_ptr())
+        ctx.sync()
+        op = ot.cpu().numpy()
+        orf = z["occlusion_d1"].view(np.int32)
+        sact = srays["extra"][:, 1] != 0
+        print(f"[{name}] shadow: active {sact.mean():.3f} occlusion equal {(op == orf)[sact].mean():.5f}")
+        # 3. frames
+        for D in (1, 2):
+            fb.render(ds, cam, frame=0, max_depth=D)
+            g = fb.read(0)
+            ref = z[f"rad_d{D}"]
+            eq = bits_equal(g[..., :3], ref[..., :3]).all(-1)
+            nz = (ref[..., :3] != 0).any(-1)
+            print(f"[{name}] D={D}: bit-exact px {eq.mean():.5f}, among lit {eq[nz].mean():.5f}")
+            if D == 1:
+                np.save(os.path.join(out_dir, f"prod_{name}_d1.npy"), g)
+                qa, qb, qc = fb.read_queue(0)
+                np.savez(os.path.join(out_dir, f"prodq_{name}_d1.npz"), a=qa, b=qb, c=qc)
+                pix = qb[:, 3].view(np.int32)
+                rs = srays[pix]
+                temp = z["temp_d1"].view(np.float32).reshape(n, 4)[pix]
+                o_eq = bits_equal(qa[:, :3], rs["o"][:, :3]).all(-1)
+                t_eq = bits_equal(qa[:, 3], rs["o"][:, 3])
+                d_eq = bits_equal(qb[:, :3], rs["d"][:, :3]).all(-1)
+                l_eq = bits_equal(qc[:, :3], temp[:, :3]).all(-1)
+                print(f"[{name}] shadow queue {len(pix)}: origin {o_eq.mean():.5f} tmax {t_eq.mean():.5f} "
+                      f"dir {d_eq.mean():.5f} L {l_eq.mean():.5f}")
+        fb.close()
+        ds.close()
+
+
+if __name__ == "__main__":
+    out = sys.argv[1]
+    os.makedirs(out, exist_ok=True)
+    if len(sys.argv) > 2:
+        child(out)
+    else:
+        parent(out)
