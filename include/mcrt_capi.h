@@ -299,10 +299,10 @@ MCRT_API mcrt_status mcrt_framebuffer_set_accumulation(mcrt_framebuffer fb, cons
 /* Per-frame path statistics of the last render (paths, closest rays, any rays, ...). */
 MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closest_rays, int64_t* any_rays,
                                             int64_t* shaded_paths);
-/* Host copy of a ray queue written by the LAST bounce of the last render (the state the
- * reference keeps in its per-pixel trace_shadowRays / trace_rays / throughput buffers):
- *   which 0: shadow queue    -- origin.xyz|tmax, dir.xyz|pixel(int bits), throughput*L
- *   which 1: extension queue -- origin.xyz|pixel(int bits), dir.xyz|bsdf flags, throughput
+/* Host copy of a ray queue of the last render (the state the reference keeps in its
+ * per-pixel trace_shadowRays / trace_rays / throughput buffers):
+ *   which 0: shadow queue of the last bounce    -- origin.xyz|tmax, dir.xyz|pixel(int bits), throughput*L
+ *   which 1: last extension queue (bounce D-2)  -- origin.xyz|pixel(int bits), dir.xyz|bsdf flags, throughput
  * Writes min(count, max_records) records as three float4 arrays back to back
  * (dst = [a0..a(n-1) | b0.. | c0..], 48 * max_records bytes) and the full count. */
 MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which, void* host_dst,

@@ -8,12 +8,14 @@
 // reference (_mm_rcp_ps / _mm_dp_ps) is kept so the tree -- and with it the node-visit
 // counts the roofline is priced on -- matches the reference on the same host.
 //
-// GPU layout (ours): only internal nodes are stored, 64 B each, holding both child boxes:
-//   float4 (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
-//   float4 (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
-//   float4 (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
-//   int4   (child0, child1, 0, 0)   child >= 0: node index, child < 0: ~triangle index
-// Triangles (48 B): (v0, shapeId), (v1 - v0, primId), (v2 - v0, 0), numbered in DFS leaf order.
+// GPU layout (ours): one 64-B record per node of the RR tree, in its DFS numbering, so every
+// traversal step is one uniform 64-B fetch whatever the node type:
+//   internal: float4 (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)   (child boxes, x/y slab pairs)
+//             float4 (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+//             float4 (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
+//             int4   (child0, child1, 0, 0)                 (child indices >= 1)
+//   leaf:     float4 (v0, shapeId bits), float4 (v1 - v0, primId bits), float4 (v2 - v0, 0),
+//             int4   (-1, -1, 0, 0)
 #include <immintrin.h>
 
 #include <atomic>
@@ -288,15 +290,13 @@ bool build_bvh(const float* tri, const int32_t* shapeOf, const int32_t* primOf, 
         for (int t = 0; t < threads; ++t) th.emplace_back(worker);
         for (auto& x : th) x.join();
     }
-    // convert to the GPU layout
-    std::vector<int32_t> gpuIndex(count, 0);
-    std::size_t nInternal = 0, nLeaves = 0;
-    for (std::size_t i = 0; i < count; ++i) gpuIndex[i] = b.isInternal[i] ? (int32_t)nInternal++ : ~(int32_t)nLeaves++;
-    const bool singleLeaf = (nInternal == 0);
-    out.numNodes = singleLeaf ? 1 : nInternal;
-    out.numTris = nLeaves;
+    // convert to the GPU layout: one 64-B record per RR node, same DFS numbering
+    // (left child = i + 1, right child = i + 1 + size(left)), leaves hold their triangle.
+    out.numNodes = count;
+    out.numTris = 0;
+    for (std::size_t i = 0; i < count; ++i) out.numTris += b.isInternal[i] ? 0 : 1;
     out.nodes = (float*)std::malloc(sizeof(float) * 16 * out.numNodes);
-    out.tris = (float*)std::malloc(sizeof(float) * 12 * out.numTris);
+    out.tris = nullptr;
     out.depth = b.maxDepth.load();
     auto leafBox = [&](uint32_t ref, float* bx) {
         const float* p = &tri[9 * (std::size_t)ref];
@@ -307,47 +307,11 @@ bool build_bvh(const float* tri, const int32_t* shapeOf, const int32_t* primOf, 
             bx[3 + c] = (a < mx) ? mx : a;
         }
     };
-    for (std::size_t i = 0; i < count; ++i) {
-        if (b.isInternal[i]) continue;
-        const uint32_t ref = b.leafRef[i];
-        const int32_t t = ~gpuIndex[i];
-        const float* p = &tri[9 * (std::size_t)ref];
-        float* o = &out.tris[12 * (std::size_t)t];
-        o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
-        std::memcpy(&o[3], &shapeOf[ref], 4);
-        o[4] = p[3] - p[0]; o[5] = p[4] - p[1]; o[6] = p[5] - p[2];
-        std::memcpy(&o[7], &primOf[ref], 4);
-        o[8] = p[6] - p[0]; o[9] = p[7] - p[1]; o[10] = p[8] - p[2];
-        o[11] = 0.0f;
-    }
     auto childBox = [&](std::size_t c, float* bx) {
         if (b.isInternal[c]) std::memcpy(bx, &b.box[6 * c], sizeof(float) * 6);
         else leafBox(b.leafRef[c], bx);
     };
-    if (singleLeaf) {
-        float bx[6];
-        leafBox(b.leafRef[0], bx);
-        float* o = out.nodes;
-        o[0] = bx[0]; o[1] = bx[3]; o[2] = bx[1]; o[3] = bx[4];
-        o[4] = INFINITY; o[5] = -INFINITY; o[6] = INFINITY; o[7] = -INFINITY;   // empty second child
-        o[8] = bx[2]; o[9] = bx[5]; o[10] = INFINITY; o[11] = -INFINITY;
-        int32_t ch[4] = {~0, ~0, 0, 0};
-        std::memcpy(&o[12], ch, 16);
-        return true;
-    }
-    for (std::size_t i = 0; i < count; ++i) {   // left child = i + 1
-        if (!b.isInternal[i]) continue;
-        const std::size_t l = i + 1;
-        float* o = &out.nodes[16 * (std::size_t)gpuIndex[i]];
-        float b0[6];
-        childBox(l, b0);
-        o[0] = b0[0]; o[1] = b0[3]; o[2] = b0[1]; o[3] = b0[4];
-        o[8] = b0[2]; o[9] = b0[5];
-        const int32_t ch0 = gpuIndex[l];
-        std::memcpy(&o[12], &ch0, 4);
-    }
-    // right children: subtree sizes via a reverse scan (size(i) = 1 for leaves,
-    // 1 + size(i+1) + size(right) for internal nodes, right = i + 1 + size(i+1)).
+    // subtree sizes via a reverse scan (size(i) = 1 for leaves, 1 + size(l) + size(r) otherwise)
     std::vector<uint32_t> sz(count, 1);
     for (std::size_t ii = count; ii-- > 0;) {
         if (!b.isInternal[ii]) continue;
@@ -356,15 +320,29 @@ bool build_bvh(const float* tri, const int32_t* shapeOf, const int32_t* primOf, 
         sz[ii] = 1 + sz[l] + sz[r];
     }
     for (std::size_t i = 0; i < count; ++i) {
-        if (!b.isInternal[i]) continue;
-        const std::size_t r = i + 1 + sz[i + 1];
-        float* o = &out.nodes[16 * (std::size_t)gpuIndex[i]];
-        float b1[6];
+        float* o = &out.nodes[16 * i];
+        if (!b.isInternal[i]) {
+            const uint32_t ref = b.leafRef[i];
+            const float* p = &tri[9 * (std::size_t)ref];
+            o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
+            std::memcpy(&o[3], &shapeOf[ref], 4);
+            o[4] = p[3] - p[0]; o[5] = p[4] - p[1]; o[6] = p[5] - p[2];
+            std::memcpy(&o[7], &primOf[ref], 4);
+            o[8] = p[6] - p[0]; o[9] = p[7] - p[1]; o[10] = p[8] - p[2];
+            o[11] = 0.0f;
+            const int32_t mark[4] = {-1, -1, 0, 0};
+            std::memcpy(&o[12], mark, 16);
+            continue;
+        }
+        const std::size_t l = i + 1, r = i + 1 + sz[i + 1];
+        float b0[6], b1[6];
+        childBox(l, b0);
         childBox(r, b1);
+        o[0] = b0[0]; o[1] = b0[3]; o[2] = b0[1]; o[3] = b0[4];
         o[4] = b1[0]; o[5] = b1[3]; o[6] = b1[1]; o[7] = b1[4];
-        o[10] = b1[2]; o[11] = b1[5];
-        int32_t ch[3] = {gpuIndex[r], 0, 0};
-        std::memcpy(&o[13], ch, 12);
+        o[8] = b0[2]; o[9] = b0[5]; o[10] = b1[2]; o[11] = b1[5];
+        const int32_t ch[4] = {(int32_t)l, (int32_t)r, 0, 0};
+        std::memcpy(&o[12], ch, 16);
     }
     return true;
 }

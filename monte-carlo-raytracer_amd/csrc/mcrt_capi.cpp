@@ -79,7 +79,7 @@ struct mcrt_scene_s {
     // traversal scratch
     uint32_t* dSpill = nullptr;
     int spillCap = 0;
-    int traceGrid = 0;
+    size_t spillRays = 0;           // rays the spill buffer covers (spillCap words each)
     int* dScratch = nullptr;   // [0] overflow flag, [1..] work counters for API queries
 };
 
@@ -209,10 +209,22 @@ static float filter_weight(const mcrt_filter& f) {
     }
 }
 
+// Per-ray spill columns for `rays` rays (rounded up to whole waves); grown on demand.
+static bool ensure_spill(mcrt_scene s, size_t rays) {
+    rays = (rays + 63) / 64 * 64;
+    if (rays <= s->spillRays && s->dSpill) return true;
+    hipStreamSynchronize(s->ctx->stream);   // the old buffer may still be in use
+    if (s->dSpill) hipFree(s->dSpill);
+    s->dSpill = nullptr;
+    s->spillRays = 0;
+    if (hipMalloc(&s->dSpill, rays * (size_t)s->spillCap * sizeof(uint32_t)) != hipSuccess) return false;
+    s->spillRays = rays;
+    return true;
+}
+
 static TraceCtx trace_ctx(mcrt_scene s) {
     TraceCtx c;
     c.nodes = (const float4*)s->dNodes;
-    c.tris = (const float4*)s->dTris;
     c.spill = s->dSpill;
     c.spillCap = s->spillCap;
     c.overflow = s->dScratch;
@@ -231,7 +243,7 @@ static SceneArgs scene_args(mcrt_scene s) {
     a.sobol = (const uint32_t*)s->dSobol;
     a.lights = (const mcrt_light*)s->dLights;
     a.materials = (const mcrt_material*)s->dMaterials;
-    a.tris = (const float4*)s->dTris;
+    a.nodes = (const float4*)s->dNodes;
     a.numLights = (int)s->numLights;
     return a;
 }
@@ -330,6 +342,7 @@ static void scene_free_device(mcrt_scene s) {
     if (s->dSpill) hipFree(s->dSpill);
     if (s->dScratch) hipFree(s->dScratch);
     s->dSpill = nullptr;
+    s->spillRays = 0;
     s->dScratch = nullptr;
 }
 
@@ -479,23 +492,22 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     if (s->dTris) hipFree(s->dTris);
     s->dNodes = s->dTris = nullptr;
     hipError_t e = hipMalloc(&s->dNodes, 64 * bvh.numNodes);
-    if (e == hipSuccess) e = hipMalloc(&s->dTris, 48 * bvh.numTris);
     if (e == hipSuccess) e = hipMemcpy(s->dNodes, bvh.nodes, 64 * bvh.numNodes, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(s->dTris, bvh.tris, 48 * bvh.numTris, hipMemcpyHostToDevice);
     s->numNodes = bvh.numNodes;
     s->numTris = (uint32_t)bvh.numTris;
     s->bvhDepth = bvh.depth;
     mcrt::free_bvh(bvh);
     if (e != hipSuccess) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, std::string("BVH upload: ") + hipGetErrorString(e));
-    // traversal scratch: persistent grid = CUs x 8 blocks of 256 threads; spill deep enough for the tree
+    // traversal scratch: overflow flag; per-ray spill columns deep enough for the tree
+    // (allocated by ensure_spill for the largest launch)
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
-    s->traceGrid = ctx->numCUs * 8;
-    const int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;
-    if (needCap > s->spillCap) {
+    const int needCap = ((s->bvhDepth + 2 + 14) / 15) * 15;
+    if (needCap != s->spillCap) {
         if (s->dSpill) hipFree(s->dSpill);
-        s->spillCap = std::max(needCap, 32);
-        HIPCHK(ctx, hipMalloc(&s->dSpill, (size_t)s->traceGrid * 256 * s->spillCap * sizeof(uint32_t)));
+        s->dSpill = nullptr;
+        s->spillRays = 0;
+        s->spillCap = needCap;
     }
     s->buildMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MCRT_OK;
@@ -505,7 +517,7 @@ MCRT_API mcrt_status mcrt_accel_info(mcrt_scene s, uint64_t* num_nodes, uint64_t
                                      uint32_t* num_triangles) {
     if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
     if (num_nodes) *num_nodes = s->numNodes;
-    if (device_bytes) *device_bytes = 64ull * s->numNodes + 48ull * s->numTris;
+    if (device_bytes) *device_bytes = 64ull * s->numNodes;
     if (build_ms) *build_ms = s->buildMs;
     if (num_triangles) *num_triangles = s->numTris;
     return MCRT_OK;
@@ -523,12 +535,10 @@ static mcrt_status trace_common(mcrt_scene s, const mcrt_ray* rays, int32_t n, m
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "invalid ray query arguments");
     if (n == 0) return MCRT_OK;
     hipSetDevice(ctx->device);
-    int* work = s->dScratch + (any ? 2 : 1);
-    HIPCHK(ctx, hipMemsetAsync(work, 0, sizeof(int), ctx->stream));
+    if (!ensure_spill(s, (size_t)n)) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
     {
         Timed t(ctx, any ? K_TRACE_ANY : K_TRACE_CLOSEST, nullptr, n);
-        int grid = std::min(s->traceGrid, (n + 255) / 256);
-        mcrt::launch_trace_rays(any, trace_ctx(s), rays, n, work, hits, occl, std::max(grid, 1), ctx->stream);
+        mcrt::launch_trace_rays(any, trace_ctx(s), rays, n, hits, occl, ctx->stream);
     }
     HIPCHK(ctx, hipGetLastError());
     return MCRT_OK;
@@ -654,17 +664,17 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
     HIPCHK(ctx, hipMemsetAsync(fb->counters, 0, 128 * sizeof(int), st));
     int* shadowCnt = fb->counters;          // [b]
     int* extCnt = fb->counters + 32;        // [b]
-    int* work = fb->counters + 64;          // [0] primary, [1+2b] shadow, [2+2b] extend
-    const TraceCtx tc = trace_ctx(s);
     const SceneArgs sa = scene_args(s);
     if (s->numLights == 0) {   // RTPathTracingPass.cpp:42: no lights -> pass skipped; radiance = 0 here
         HIPCHK(ctx, hipMemsetAsync(fb->radiance, 0, 16 * fb->N, st));
         return MCRT_OK;
     }
-    const int grid = s->traceGrid;
+    if (!ensure_spill(s, std::max((size_t)f.numTiles * 64, fb->N)))
+        return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
+    const TraceCtx tcs = trace_ctx(s);   // after ensure_spill (the buffer may have moved)
     {
         Timed t(ctx, K_PRIMARY, nullptr, (int64_t)f.numTiles * 64);
-        mcrt::launch_primary(tc, f, dCam, work + 0, fb->hitsP, grid, st);
+        mcrt::launch_primary(tcs, f, dCam, fb->hitsP, st);
     }
     for (int b = 0; b < p->max_depth; ++b) {
         QueueArgs q;
@@ -678,8 +688,8 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
         } else {
             {
                 Timed t(ctx, K_EXTEND, extCnt + b - 1, 0);
-                mcrt::launch_extend(tc, extCnt + b - 1, work + 2 + 2 * b, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1],
-                                    fb->hitsE, grid, st);
+                mcrt::launch_extend(tcs, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1], fb->hitsE,
+                                    (int)fb->N, st);
             }
             Timed t(ctx, K_SHADEN, extCnt + b - 1, 0);
             mcrt::launch_shadeN(sa, f, b, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1],
@@ -687,7 +697,7 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
         }
         {
             Timed t(ctx, K_SHADOW, shadowCnt + b, 0);
-            mcrt::launch_shadow(tc, shadowCnt + b, work + 1 + 2 * b, fb->sO, fb->sD, fb->sL, fb->radiance, grid, st);
+            mcrt::launch_shadow(tcs, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, (int)fb->N, st);
         }
     }
     HIPCHK(ctx, hipGetLastError());
@@ -787,14 +797,14 @@ MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which,
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     int c[64];
     HIPCHK(ctx, hipMemcpy(c, fb->counters, sizeof(c), hipMemcpyDeviceToHost));
-    const int b = fb->lastMaxDepth - 1;
-    const int n = which == 0 ? c[b] : c[32 + b];
+    const int b = which == 0 ? fb->lastMaxDepth - 1 : fb->lastMaxDepth - 2;   // last shadow / last extension queue
+    const int n = b < 0 ? 0 : (which == 0 ? c[b] : c[32 + b]);
     if (count) *count = n;
     const int64_t m = std::min<int64_t>(n, max_records);
     if (m == 0) return MCRT_OK;
     const float4* src[3];
     if (which == 0) { src[0] = fb->sO; src[1] = fb->sD; src[2] = fb->sL; }
-    else { src[0] = fb->eO[b & 1]; src[1] = fb->eD[b & 1]; src[2] = fb->eT[b & 1]; }
+    else { src[0] = fb->eO[b & 1]; src[1] = fb->eD[b & 1]; src[2] = fb->eT[b & 1]; }   // b >= 0 here
     for (int k = 0; k < 3; ++k)
         HIPCHK(ctx, hipMemcpy(static_cast<char*>(host_dst) + (size_t)k * 16 * max_records, src[k], 16 * (size_t)m,
                               hipMemcpyDeviceToHost));

@@ -19,7 +19,7 @@ struct SceneArgs {
     const uint32_t* sobol;
     const mcrt_light* lights;
     const mcrt_material* materials;
-    const float4* tris;   // 3 float4 per triangle: (v0, shape), (e1, prim), (e2, -)
+    const float4* nodes;  // unified BVH (mcrt_bvh.cpp): leaf k = (v0, shape), (e1, prim), (e2, -), marker
     int numLights;
 };
 
@@ -39,22 +39,20 @@ struct QueueArgs {
 };
 
 struct TraceCtx {
-    const float4* nodes;   // 4 float4 per node: x-slabs c0, x/y c1, z c0|c1, children
-    const float4* tris;
+    const float4* nodes;   // 4 float4 per node (mcrt_bvh.cpp): internal = child boxes + indices, leaf = triangle
     uint32_t* spill;
-    int spillCap;           // spill entries per lane
+    int spillCap;           // spill entries per ray (multiple of STACK_LDS - 1)
     int* overflow;
 };
 
 namespace mcrt {
-void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, int* work, mcrt_intersection* hits,
-                       int* occl, int grid, hipStream_t st);
-void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, int* work, float4* hits, int grid,
-                    hipStream_t st);
-void launch_extend(const TraceCtx& c, const int* count, int* work, const float4* qO, const float4* qD, float4* hits,
-                   int grid, hipStream_t st);
-void launch_shadow(const TraceCtx& c, const int* count, int* work, const float4* sO, const float4* sD,
-                   const float4* sL, float4* radiance, int grid, hipStream_t st);
+void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, mcrt_intersection* hits, int* occl,
+                       hipStream_t st);
+void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st);
+void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
+                   hipStream_t st);
+void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
+                   float4* radiance, int maxCount, hipStream_t st);
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st);
 void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,
@@ -72,7 +70,7 @@ struct BvhOut {
     std::size_t numNodes = 0;
     std::size_t numTris = 0;
     float* nodes = nullptr;   // 16 floats per node
-    float* tris = nullptr;    // 12 floats per triangle
+    float* tris = nullptr;    // unused (leaves live in `nodes`)
     int depth = 0;
 };
 // world-space triangles (9 floats each), shape id / prim id per triangle

@@ -8,10 +8,10 @@
 //     k_shadow           any-hit over the shadow queue; radiance += L * V (ShadowPass)
 //     k_extend           closest hit over the extension queue (if b + 1 < D)
 //   k_accumulate         ReconstructionPass (clamp, weighted running mean)
-// Traversal: 64-B two-child nodes (both child boxes in the parent), leaves referenced by
-// index into a 48-B triangle array (v0, e1, e2; w = shape id / prim id), per-lane LDS short
-// stack (16 entries, [entry][lane] layout -> conflict free) with global spill, persistent
-// waves pulling 64-ray chunks from an atomic counter.
+// Traversal: the RadeonRays Bvh2 as one array of 64-B records (internal nodes hold both child
+// boxes, leaves their triangle), one flat loop per ray with a per-lane LDS short stack
+// (16 entries, [entry][lane] layout -> conflict free) spilling to a per-ray global column;
+// one wave per workgroup, the hardware dispatcher schedules the waves.
 #include "mcrt_device.h"
 #include "mcrt_internal.h"
 
@@ -19,7 +19,6 @@
 // traversal
 // ---------------------------------------------------------------------------
 #define STACK_LDS 16
-#define TRACE_BLOCK 256
 
 struct TraceRay {
     f3 o, d;
@@ -53,94 +52,86 @@ MCRT_DEV float triHit(const TraceRay& r, float4 A, float4 E1, float4 E2, float t
     return temp;
 }
 
-// Closest (ANY = false) or any (ANY = true) hit.  Returns the triangle index or -1 and
-// leaves the hit distance in tHit.  stk: this lane's LDS stack column; spill: global.
+// Closest (ANY = false) or any (ANY = true) hit over the unified node array (mcrt_bvh.cpp):
+// the RadeonRays intersect_bvh2_lds.cl:107-178 loop -- one uniform 64-B fetch per step, an
+// internal node tests both child boxes (nearer child first, far child to the stack), a leaf
+// tests its triangle.  Returns the hit leaf's node index or -1; tHit = hit distance.
+// stk: this lane's LDS stack column ([entry][lane], conflict free); spill: global overflow.
 template <bool ANY>
-MCRT_DEV int traverse(const float4* __restrict__ nodes, const float4* __restrict__ tris, const TraceRay& r,
-                      uint32_t* stk, uint32_t* spill, int spillCap, int* overflowFlag, float& tHit) {
+MCRT_DEV int traverse(const float4* __restrict__ nodes, const TraceRay& r, uint32_t* stk, uint32_t* spill, int spillCap,
+                      int* overflowFlag, float& tHit) {
+    // One flat loop with a single exit (node == DONE): stack entry 0 is a DONE sentinel, so a
+    // pop is one LDS read and no lane idles at a nested loop boundary waiting for the others.
+    constexpr int DONE = -1, POP = -2;
     const f3 inv = safeInvDir(r.d);
     const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
     float t = r.tmax;
-    int hitTri = -1;
+    int hit = -1;
     int node = 0;
-    int sp = 0, spillTop = 0;
-    for (;;) {
+    stk[0] = (uint32_t)DONE;
+    int sp = 1, spillTop = 0;
+    while (node != DONE) {
         const float4 n0 = nodes[4 * node + 0];
         const float4 n1 = nodes[4 * node + 1];
         const float4 n2 = nodes[4 * node + 2];
         const int4 n3 = *reinterpret_cast<const int4*>(&nodes[4 * node + 3]);
-        // slab tests of both children (RR intersect_bvh2_lds.cl:54-63, mad -> fma)
-        float ax0 = fmaf(n0.x, inv.x, oxi.x), ax1 = fmaf(n0.y, inv.x, oxi.x);
-        float ay0 = fmaf(n0.z, inv.y, oxi.y), ay1 = fmaf(n0.w, inv.y, oxi.y);
-        float az0 = fmaf(n2.x, inv.z, oxi.z), az1 = fmaf(n2.y, inv.z, oxi.z);
-        float bx0 = fmaf(n1.x, inv.x, oxi.x), bx1 = fmaf(n1.y, inv.x, oxi.x);
-        float by0 = fmaf(n1.z, inv.y, oxi.y), by1 = fmaf(n1.w, inv.y, oxi.y);
-        float bz0 = fmaf(n2.z, inv.z, oxi.z), bz1 = fmaf(n2.w, inv.z, oxi.z);
-        float a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
-        float a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), t);
-        float b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
-        float b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), t);
-        bool h0 = a0 <= a1, h1 = b0 <= b1;
-        bool swap = h1 && (a0 > b0);   // nearer child first (intersect_bvh2_lds.cl:128-141)
-        int cf = swap ? n3.y : n3.x, cs = swap ? n3.x : n3.y;
-        bool hf = swap ? h1 : h0, hs = swap ? h0 : h1;
-        // leaf children are intersected immediately, near first
-        if (hf && cf < 0) {
-            const int ti = ~cf;
-            const float4 A = tris[3 * ti], E1 = tris[3 * ti + 1], E2 = tris[3 * ti + 2];
-            if (r.mask != __float_as_int(A.w)) {   // RR_RAY_MASK
-                float th = triHit(r, A, E1, E2, t);
-                if (th < t) {
-                    t = th;
-                    hitTri = ti;
-                    if (ANY) break;
-                }
-            }
-            hf = false;
-        }
-        if (hs && cs < 0) {
-            const int ti = ~cs;
-            const float4 A = tris[3 * ti], E1 = tris[3 * ti + 1], E2 = tris[3 * ti + 2];
-            if (r.mask != __float_as_int(A.w)) {
-                float th = triHit(r, A, E1, E2, t);
-                if (th < t) {
-                    t = th;
-                    hitTri = ti;
-                    if (ANY) break;
-                }
-            }
-            hs = false;
-        }
-        if (hf) {
-            if (hs) {   // push the far child
-                if (sp == STACK_LDS) {
-                    if (spillTop + STACK_LDS <= spillCap) {
-                        for (int k = 0; k < STACK_LDS; ++k) spill[(size_t)(spillTop + k) * 64] = stk[k * 64];
-                        spillTop += STACK_LDS;
+        // keep the whole 64-B record in one round trip: without this the compiler defers the
+        // two words only internal nodes use into a second, dependent load after the branch
+        asm volatile("" ::"v"(n1.w), "v"(n2.w));
+        int next;
+        if (n3.x >= 0) {
+            // slab tests of both children (RR intersect_bvh2_lds.cl:54-63, mad -> fma)
+            const float ax0 = fmaf(n0.x, inv.x, oxi.x), ax1 = fmaf(n0.y, inv.x, oxi.x);
+            const float ay0 = fmaf(n0.z, inv.y, oxi.y), ay1 = fmaf(n0.w, inv.y, oxi.y);
+            const float az0 = fmaf(n2.x, inv.z, oxi.z), az1 = fmaf(n2.y, inv.z, oxi.z);
+            const float bx0 = fmaf(n1.x, inv.x, oxi.x), bx1 = fmaf(n1.y, inv.x, oxi.x);
+            const float by0 = fmaf(n1.z, inv.y, oxi.y), by1 = fmaf(n1.w, inv.y, oxi.y);
+            const float bz0 = fmaf(n2.z, inv.z, oxi.z), bz1 = fmaf(n2.w, inv.z, oxi.z);
+            const float a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
+            const float a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), t);
+            const float b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
+            const float b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), t);
+            const bool h0 = a0 <= a1, h1 = b0 <= b1;
+            const bool c1first = h1 && (a0 > b0);   // intersect_bvh2_lds.cl:128-141
+            if (h0 && h1) {   // defer the far child
+                if (sp == STACK_LDS) {   // spill entries 1..15 (RR: intersect_bvh2_lds.cl:146-155)
+                    if (spillTop + STACK_LDS - 1 <= spillCap) {
+                        for (int k = 1; k < STACK_LDS; ++k) spill[(size_t)(spillTop + k - 1) * 64] = stk[k * 64];
+                        spillTop += STACK_LDS - 1;
                     } else {
                         *overflowFlag = 1;   // depth beyond capacity: drop (reported by the host)
                     }
-                    sp = 0;
+                    sp = 1;
                 }
-                stk[sp * 64] = (uint32_t)cs;
+                stk[sp * 64] = (uint32_t)(c1first ? n3.x : n3.y);
                 ++sp;
             }
-            node = cf;
-        } else if (hs) {
-            node = cs;
+            next = (h0 || h1) ? ((c1first || !h0) ? n3.y : n3.x) : POP;
         } else {
-            if (sp == 0) {
-                if (spillTop == 0) break;
-                spillTop -= STACK_LDS;
-                for (int k = 0; k < STACK_LDS; ++k) stk[k * 64] = spill[(size_t)(spillTop + k) * 64];
-                sp = STACK_LDS;
+            next = POP;
+            if (r.mask != __float_as_int(n0.w)) {   // RR_RAY_MASK
+                const float th = triHit(r, n0, n1, n2, t);
+                if (th < t) {
+                    t = th;
+                    hit = node;
+                    if (ANY) next = DONE;
+                }
             }
-            --sp;
-            node = (int)stk[sp * 64];
         }
+        if (next == POP) {
+            --sp;
+            next = (int)stk[sp * 64];
+            if (next == DONE && spillTop > 0) {   // refill (intersect_bvh2_lds.cl:182-191)
+                spillTop -= STACK_LDS - 1;
+                for (int k = 1; k < STACK_LDS; ++k) stk[k * 64] = spill[(size_t)(spillTop + k - 1) * 64];
+                sp = STACK_LDS - 1;
+                next = (int)stk[sp * 64];
+            }
+        }
+        node = next;
     }
     tHit = t;
-    return hitTri;
+    return hit;
 }
 
 // RR common.cl:249-277 (triangle_calculate_barycentrics)
@@ -161,66 +152,55 @@ MCRT_DEV f2 triBary(f3 p, float4 A, float4 E1, float4 E2) {
 }
 
 // hit record of the closest-hit kernels: (u, v, t, triangle) -- intersect_bvh2_lds.cl:200-215
-MCRT_DEV float4 closestRecord(const float4* __restrict__ tris, const TraceRay& r, int tri, float t) {
+MCRT_DEV float4 closestRecord(const float4* __restrict__ nodes, const TraceRay& r, int tri, float t) {
     if (tri < 0) return make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-    const float4 A = tris[3 * tri], E1 = tris[3 * tri + 1], E2 = tris[3 * tri + 2];
+    const float4 A = nodes[4 * tri], E1 = nodes[4 * tri + 1], E2 = nodes[4 * tri + 2];
     const f3 p = r.o + t * r.d;
     const f2 uv = triBary(p, A, E1, E2);
     return make_float4(uv.x, uv.y, t, __int_as_float(tri));
 }
 
-// Wave-uniform chunk fetch for persistent waves.
-MCRT_DEV int nextChunk(int* counter, int lane) {
-    int base = 0;
-    if (lane == 0) base = atomicAdd(counter, 64);
-    return __shfl(base, 0);
-}
-
-MCRT_DEV uint32_t* laneSpill(const TraceCtx& c) {
-    const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int wave = gtid >> 6, lane = gtid & 63;
+// Per-ray spill column: rays are grouped 64 to a wave; lane l of wave w owns entries
+// spill[(w * spillCap + k) * 64 + l], k < spillCap (coalesced across the wave).
+MCRT_DEV uint32_t* raySpill(const TraceCtx& c, int wave, int lane) {
     return c.spill + (size_t)wave * 64 * c.spillCap + lane;
 }
 
 // ---------------------------------------------------------------------------
-// RadeonRays-compatible queries on AoS rays (mcrt_trace_closest / mcrt_trace_any)
+// RadeonRays-compatible queries on AoS rays (mcrt_trace_closest / mcrt_trace_any).
+// One ray per lane, one wave per workgroup (LDS stack 4 KB): the hardware dispatcher keeps
+// 8 waves per SIMD resident and refills them as they finish -- measured faster on MI355X
+// than a persistent grid pulling work from an atomic queue.
 // ---------------------------------------------------------------------------
 template <bool ANY>
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(TraceCtx c, const mcrt_ray* __restrict__ rays, int n,
-                                                            int* work, mcrt_intersection* __restrict__ hits,
-                                                            int* __restrict__ occl) {
-    __shared__ uint32_t lds[STACK_LDS * TRACE_BLOCK];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t* stk = lds + wv * 64 * STACK_LDS + lane;
-    uint32_t* spill = laneSpill(c);
-    for (;;) {
-        const int base = nextChunk(work, lane);
-        if (base >= n) break;
-        const int i = base + lane;
-        if (i >= n) continue;
-        const mcrt_ray rr = rays[i];
-        if (rr.extra[1] == 0) continue;   // inactive: output untouched (intersect_bvh2_lds.cl:88)
-        TraceRay r;
-        r.o = ld3(rr.o);
-        r.d = ld3(rr.d);
-        r.tmax = rr.o.w;
-        r.mask = rr.extra[0];
-        float t;
-        int tri = traverse<ANY>(c.nodes, c.tris, r, stk, spill, c.spillCap, c.overflow, t);
-        if (ANY) {
-            occl[i] = tri >= 0 ? 1 : -1;
-        } else if (tri >= 0) {
-            const float4 h4 = closestRecord(c.tris, r, tri, t);
-            mcrt_intersection h;
-            h.shapeid = __float_as_int(c.tris[3 * tri].w);
-            h.primid = __float_as_int(c.tris[3 * tri + 1].w);
-            h.padding[0] = h.padding[1] = 0;
-            h.uvwt.x = h4.x; h.uvwt.y = h4.y; h.uvwt.z = 0.0f; h.uvwt.w = t;
-            hits[i] = h;
-        } else {
-            hits[i].shapeid = -1;
-            hits[i].primid = -1;
-        }
+__global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* __restrict__ rays, int n,
+                                                   mcrt_intersection* __restrict__ hits, int* __restrict__ occl) {
+    __shared__ uint32_t lds[STACK_LDS * 64];
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * 64 + lane;
+    if (i >= n) return;
+    const mcrt_ray rr = rays[i];
+    if (rr.extra[1] == 0) return;   // inactive: output untouched (intersect_bvh2_lds.cl:88)
+    TraceRay r;
+    r.o = ld3(rr.o);
+    r.d = ld3(rr.d);
+    r.tmax = rr.o.w;
+    r.mask = rr.extra[0];
+    float t;
+    const int tri = traverse<ANY>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+    if (ANY) {
+        occl[i] = tri >= 0 ? 1 : -1;
+    } else if (tri >= 0) {
+        const float4 h4 = closestRecord(c.nodes, r, tri, t);
+        mcrt_intersection h;
+        h.shapeid = __float_as_int(c.nodes[4 * tri].w);
+        h.primid = __float_as_int(c.nodes[4 * tri + 1].w);
+        h.padding[0] = h.padding[1] = 0;
+        h.uvwt.x = h4.x; h.uvwt.y = h4.y; h.uvwt.z = 0.0f; h.uvwt.w = t;
+        hits[i] = h;
+    } else {
+        hits[i].shapeid = -1;
+        hits[i].primid = -1;
     }
 }
 
@@ -242,90 +222,73 @@ MCRT_DEV f3 cameraDir(const mcrt_camera& cam, int x, int y) {   // PathTracing.c
     return lerpDirection(ld3(cam.r00), ld3(cam.r10), ld3(cam.r11), ld3(cam.r01), uv.x, uv.y);
 }
 
-// Camera ray generation fused with the first closest-hit query (RTPrimaryRaysPass).
-__global__ __launch_bounds__(TRACE_BLOCK) void k_primary(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
-                                                         int* work, float4* __restrict__ hitOut) {
-    __shared__ uint32_t lds[STACK_LDS * TRACE_BLOCK];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t* stk = lds + wv * 64 * STACK_LDS + lane;
-    uint32_t* spill = laneSpill(c);
-    const mcrt_camera cam = *camp;
-    const int ntiles = f.numTiles;
-    for (;;) {
-        int tile = 0;
-        if (lane == 0) tile = atomicAdd(work, 1);
-        tile = __shfl(tile, 0);
-        if (tile >= ntiles) break;
-        int x, y;
-        if (!tilePixel(f, tile, lane, x, y)) continue;
-        TraceRay r;
-        r.o = ld3(cam.pos);
-        r.d = cameraDir(cam, x, y);
-        r.tmax = 1000.0f;
-        r.mask = -1;
-        float t;
-        int tri = traverse<false>(c.nodes, c.tris, r, stk, spill, c.spillCap, c.overflow, t);
-        hitOut[(size_t)y * f.W + x] = closestRecord(c.tris, r, tri, t);
-    }
+// Camera ray generation fused with the first closest-hit query (RTPrimaryRaysPass):
+// one workgroup = one wave = one 8x8 pixel tile of the rank's bands.
+__global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
+                                                float4* __restrict__ hitOut) {
+    __shared__ uint32_t lds[STACK_LDS * 64];
+    const int lane = threadIdx.x;
+    const int tile = blockIdx.x;
+    int x, y;
+    if (!tilePixel(f, tile, lane, x, y)) return;
+    const mcrt_camera& cam = *camp;
+    TraceRay r;
+    r.o = ld3(cam.pos);
+    r.d = cameraDir(cam, x, y);
+    r.tmax = 1000.0f;
+    r.mask = -1;
+    float t;
+    const int tri = traverse<false>(c.nodes, r, lds + lane, raySpill(c, tile, lane), c.spillCap, c.overflow, t);
+    hitOut[(size_t)y * f.W + x] = closestRecord(c.nodes, r, tri, t);
 }
 
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
-__global__ __launch_bounds__(TRACE_BLOCK) void k_extend(TraceCtx c, const int* __restrict__ count, int* work,
-                                                        const float4* __restrict__ qO, const float4* __restrict__ qD,
-                                                        float4* __restrict__ hitOut) {
-    __shared__ uint32_t lds[STACK_LDS * TRACE_BLOCK];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t* stk = lds + wv * 64 * STACK_LDS + lane;
-    uint32_t* spill = laneSpill(c);
+// The grid covers the queue's capacity; workgroups past the device-side count exit at once.
+__global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ qO,
+                                               const float4* __restrict__ qD, float4* __restrict__ hitOut) {
+    __shared__ uint32_t lds[STACK_LDS * 64];
     const int n = *count;
-    for (;;) {
-        const int base = nextChunk(work, lane);
-        if (base >= n) break;
-        const int i = base + lane;
-        if (i >= n) continue;
-        const float4 o = qO[i], d = qD[i];
-        TraceRay r;
-        r.o = ld3(o);
-        r.d = ld3(d);
-        r.tmax = RT_MAX_TRACE_F;
-        r.mask = -1;
-        float t;
-        int tri = traverse<false>(c.nodes, c.tris, r, stk, spill, c.spillCap, c.overflow, t);
-        hitOut[i] = closestRecord(c.tris, r, tri, t);
-    }
+    if ((int)blockIdx.x * 64 >= n) return;
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * 64 + lane;
+    if (i >= n) return;
+    const float4 o = qO[i], d = qD[i];
+    TraceRay r;
+    r.o = ld3(o);
+    r.d = ld3(d);
+    r.tmax = RT_MAX_TRACE_F;
+    r.mask = -1;
+    float t;
+    const int tri = traverse<false>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+    hitOut[i] = closestRecord(c.nodes, r, tri, t);
 }
 
 // Any hit over the shadow queue + ShadowPass (PathTracing.cl:186-217):
 // sO = (o.xyz, tmax), sD = (d.xyz, pix), sL = throughput * L; radiance[pix] += L * V.
-__global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(TraceCtx c, const int* __restrict__ count, int* work,
-                                                        const float4* __restrict__ sO, const float4* __restrict__ sD,
-                                                        const float4* __restrict__ sL, float4* __restrict__ radiance) {
-    __shared__ uint32_t lds[STACK_LDS * TRACE_BLOCK];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t* stk = lds + wv * 64 * STACK_LDS + lane;
-    uint32_t* spill = laneSpill(c);
+__global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ sO,
+                                               const float4* __restrict__ sD, const float4* __restrict__ sL,
+                                               float4* __restrict__ radiance) {
+    __shared__ uint32_t lds[STACK_LDS * 64];
     const int n = *count;
-    for (;;) {
-        const int base = nextChunk(work, lane);
-        if (base >= n) break;
-        const int i = base + lane;
-        if (i >= n) continue;
-        const float4 o = sO[i], d = sD[i], L = sL[i];
-        TraceRay r;
-        r.o = ld3(o);
-        r.d = ld3(d);
-        r.tmax = o.w;
-        r.mask = -1;
-        float t;
-        int tri = traverse<true>(c.nodes, c.tris, r, stk, spill, c.spillCap, c.overflow, t);
-        const float V = tri >= 0 ? 0.0f : 1.0f;
-        const int pix = __float_as_int(d.w);
-        float4 acc = radiance[pix];
-        acc.x += L.x * V;
-        acc.y += L.y * V;
-        acc.z += L.z * V;
-        radiance[pix] = acc;
-    }
+    if ((int)blockIdx.x * 64 >= n) return;
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * 64 + lane;
+    if (i >= n) return;
+    const float4 o = sO[i], d = sD[i], L = sL[i];
+    TraceRay r;
+    r.o = ld3(o);
+    r.d = ld3(d);
+    r.tmax = o.w;
+    r.mask = -1;
+    float t;
+    const int tri = traverse<true>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+    const float V = tri >= 0 ? 0.0f : 1.0f;
+    const int pix = __float_as_int(d.w);
+    float4 acc = radiance[pix];
+    acc.x += L.x * V;
+    acc.y += L.y * V;
+    acc.z += L.z * V;
+    radiance[pix] = acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -572,7 +535,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
     f3 add = splat3(0.0f);
     const int tri = __float_as_int(hit.w);
     if (tri < 0 || s.numLights <= 0) return add;
-    const float4 A = s.tris[3 * tri], E1 = s.tris[3 * tri + 1];
+    const float4 A = s.nodes[4 * tri], E1 = s.nodes[4 * tri + 1];
     const int shapeIdx = __float_as_int(A.w), primIdx = __float_as_int(E1.w);
     const mcrt_shape& shape = s.shapes[shapeIdx];
     Frame si = computeSurfaceInteraction(s, shapeIdx, primIdx, f2{hit.x, hit.y});
@@ -755,24 +718,22 @@ __global__ __launch_bounds__(256) void k_resolve(int n, const float4* __restrict
 // ---------------------------------------------------------------------------
 namespace mcrt {
 
-void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, int* work, mcrt_intersection* hits,
-                       int* occl, int grid, hipStream_t st) {
-    if (any)
-        hipLaunchKernelGGL(k_trace_rays<true>, dim3(grid), dim3(TRACE_BLOCK), 0, st, c, rays, n, work, hits, occl);
-    else
-        hipLaunchKernelGGL(k_trace_rays<false>, dim3(grid), dim3(TRACE_BLOCK), 0, st, c, rays, n, work, hits, occl);
+void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, mcrt_intersection* hits, int* occl,
+                       hipStream_t st) {
+    const dim3 g((n + 63) / 64), b(64);
+    if (any) hipLaunchKernelGGL(k_trace_rays<true>, g, b, 0, st, c, rays, n, hits, occl);
+    else hipLaunchKernelGGL(k_trace_rays<false>, g, b, 0, st, c, rays, n, hits, occl);
 }
-void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, int* work, float4* hits, int grid,
-                    hipStream_t st) {
-    hipLaunchKernelGGL(k_primary, dim3(grid), dim3(TRACE_BLOCK), 0, st, c, f, cam, work, hits);
+void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st) {
+    hipLaunchKernelGGL(k_primary, dim3(f.numTiles), dim3(64), 0, st, c, f, cam, hits);
 }
-void launch_extend(const TraceCtx& c, const int* count, int* work, const float4* qO, const float4* qD, float4* hits,
-                   int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_extend, dim3(grid), dim3(TRACE_BLOCK), 0, st, c, count, work, qO, qD, hits);
+void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
+                   hipStream_t st) {
+    hipLaunchKernelGGL(k_extend, dim3((maxCount + 63) / 64), dim3(64), 0, st, c, count, qO, qD, hits);
 }
-void launch_shadow(const TraceCtx& c, const int* count, int* work, const float4* sO, const float4* sD,
-                   const float4* sL, float4* radiance, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_shadow, dim3(grid), dim3(TRACE_BLOCK), 0, st, c, count, work, sO, sD, sL, radiance);
+void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
+                   float4* radiance, int maxCount, hipStream_t st) {
+    hipLaunchKernelGGL(k_shadow, dim3((maxCount + 63) / 64), dim3(64), 0, st, c, count, sO, sD, sL, radiance);
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {
