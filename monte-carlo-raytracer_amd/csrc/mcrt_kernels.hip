@@ -15,6 +15,20 @@
 #include "mcrt_device.h"
 #include "mcrt_internal.h"
 
+// Shading workgroup size (threads; one queue atomic per workgroup and queue).
+#ifndef SHADE_BLOCK
+#define SHADE_BLOCK 256
+#endif
+// Occupancy target of the shading kernels (waves per SIMD); 0 = compiler's choice.
+#ifndef MCRT_SHADE_WAVES
+#define MCRT_SHADE_WAVES 0
+#endif
+#if MCRT_SHADE_WAVES > 0
+#define MCRT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(MCRT_SHADE_WAVES, MCRT_SHADE_WAVES)))
+#else
+#define MCRT_SHADE_ATTR
+#endif
+
 // ---------------------------------------------------------------------------
 // traversal
 // ---------------------------------------------------------------------------
@@ -359,6 +373,33 @@ MCRT_DEV Uber uberProps(const SceneArgs& s, const mcrt_material& material, f2 uv
 }
 
 // Wave-aggregated queue append: returns this lane's slot (valid where pred).
+// Block-aggregated queue append: ONE global atomic per workgroup instead of one per wave.
+// Device-scope atomics on one address serialise across the 8 XCDs (~10+ ns each), which made
+// per-wave appends the bottleneck of the shading kernels.  Every thread of the block must call.
+template <int NW>
+MCRT_DEV int blockAppend(int* counter, bool pred, int* ldsWave /* NW + 1 ints */) {
+    const unsigned long long m = __ballot(pred);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) ldsWave[wv] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int sum = 0;
+        for (int w = 0; w < NW; ++w) {
+            const int c = ldsWave[w];
+            ldsWave[w] = sum;
+            sum += c;
+        }
+        ldsWave[NW] = sum ? atomicAdd(counter, sum) : 0;
+    }
+    __syncthreads();
+    const unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
+    const int prefix = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+    const int slot = ldsWave[NW] + ldsWave[wv] + prefix;
+    __syncthreads();   // ldsWave is reused by the next append
+    return slot;
+}
+
+// May be called under divergent control flow: only active lanes take part.
 MCRT_DEV int waveAppend(int* counter, bool pred) {
     const unsigned long long m = __ballot(pred);
     if (m == 0) return 0;
@@ -372,11 +413,6 @@ MCRT_DEV int waveAppend(int* counter, bool pred) {
     return base + prefix;
 }
 
-struct ShadeOut {
-    bool pushS, pushE;
-    float4 sO, sD, sL;   // shadow ray
-    float4 eO, eD, eT;   // extension ray + throughput
-};
 
 // KRN/geometry.cl:9-28
 MCRT_DEV void computeTrianglePartialDerivates(f2 uv0, f2 uv1, f2 uv2, f3 p0, f3 p1, f3 p2, f3 normal, f3* dpdu, f3* dpdv) {
@@ -528,10 +564,14 @@ MCRT_DEV LightSample sampleLightLi(const SceneArgs& s, const mcrt_light& light, 
 // PathTracing kernel body (PathTracing.cl:52-184) for one path.
 // Returns the radiance term added at this vertex by emission (or by a NaN NEE term
 // with no shadow ray).  NEE terms go to the shadow queue.
+struct ShadeOut {
+    bool pushS, pushE;
+    float4 sO, sD, sL;   // shadow ray
+    float4 eO, eD, eT;   // extension ray + throughput
+};
+
 MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pix, float4 hit, f3 dir, f3 throughput,
                       int prevFlags, ShadeOut& o) {
-    o.pushS = false;
-    o.pushE = false;
     f3 add = splat3(0.0f);
     const int tri = __float_as_int(hit.w);
     if (tri < 0 || s.numLights <= 0) return add;
@@ -603,19 +643,18 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
                 if ((sampledType & BSDF_TRANSMISSION) != 0 && cl_dot(si.gn, wi) * cl_sign(off) < 0.0f) off *= -1.0f;
                 const f3 no = si.p + si.gn * off;
                 bool alive = true;
+                f3 tp1 = nt;
                 if (f.russianRoulette && bounce + 1 >= f.rrStartDepth) {   // opt-in perf mode
-                    const float q = fmaxf(0.05f, 1.0f - fmaxf(nt.x, fmaxf(nt.y, nt.z)));
+                    const float qr = fmaxf(0.05f, 1.0f - fmaxf(nt.x, fmaxf(nt.y, nt.z)));
                     const float ur = (float)wangHash((uint32_t)pix * 9781u + (uint32_t)f.frame * 6271u + (uint32_t)bounce) * 0x1p-32f;
-                    alive = ur >= q;
-                    const f3 ntq = cl_div(nt, (1.0f - q));
-                    o.eT = make_float4(ntq.x, ntq.y, ntq.z, 0.0f);
-                } else {
-                    o.eT = make_float4(nt.x, nt.y, nt.z, 0.0f);
+                    alive = ur >= qr;
+                    tp1 = cl_div(nt, (1.0f - qr));
                 }
                 if (alive) {
                     o.pushE = true;
                     o.eO = make_float4(no.x, no.y, no.z, __int_as_float(pix));
                     o.eD = make_float4(wi.x, wi.y, wi.z, __int_as_float(sampledType));
+                    o.eT = make_float4(tp1.x, tp1.y, tp1.z, 0.0f);
                 }
             }
         }
@@ -624,13 +663,14 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
 }
 
 // Bounce 0: every pixel of the band (tile order); writes radiance[pix] (= `=` of ShadowPass).
-__global__ __launch_bounds__(256) void k_shade0(SceneArgs s, FrameArgs f, const mcrt_camera* __restrict__ camp,
+__global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArgs s, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 const float4* __restrict__ hits, float4* __restrict__ radiance,
                                                 QueueArgs q) {
     const int lane = threadIdx.x & 63;
     const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     int x = 0, y = 0;
     bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y);
+    __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
     ShadeOut o;
     o.pushS = o.pushE = false;
     if (valid) {
@@ -640,19 +680,21 @@ __global__ __launch_bounds__(256) void k_shade0(SceneArgs s, FrameArgs f, const 
         const f3 add = shadePath(s, f, 0, pix, hits[pix], dir, splat3(1.0f), 0, o);
         radiance[pix] = make_float4(add.x, add.y, add.z, 0.0f);
     }
-    const int ss = waveAppend(q.shadowCount, o.pushS);
+    const int ss = blockAppend<SHADE_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
-    const int es = waveAppend(q.extCountOut, o.pushE);
+    const int es = blockAppend<SHADE_BLOCK / 64>(q.extCountOut, o.pushE, ldsWave);
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 
 // Bounce >= 1: the compacted extension queue of the previous bounce.
-__global__ __launch_bounds__(256) void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
+__global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
                                                 const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                 const float4* __restrict__ qT, const float4* __restrict__ hits,
                                                 float4* __restrict__ radiance, QueueArgs q) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = *countIn;
+    __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
+    if ((int)blockIdx.x * SHADE_BLOCK >= n) return;   // whole block past the queue: uniform exit
     ShadeOut o;
     o.pushS = o.pushE = false;
     if (i < n) {
@@ -665,9 +707,9 @@ __global__ __launch_bounds__(256) void k_shadeN(SceneArgs s, FrameArgs f, int bo
             radiance[pix] = r;
         }
     }
-    const int ss = waveAppend(q.shadowCount, o.pushS);
+    const int ss = blockAppend<SHADE_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
-    const int es = waveAppend(q.extCountOut, o.pushE);
+    const int es = blockAppend<SHADE_BLOCK / 64>(q.extCountOut, o.pushE, ldsWave);
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 
@@ -737,15 +779,15 @@ void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const 
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {
-    const int blocks = (f.numTiles * 64 + 255) / 256;
-    hipLaunchKernelGGL(k_shade0, dim3(blocks), dim3(256), 0, st, s, f, cam, hits, radiance, q);
+    const int blocks = (f.numTiles * 64 + SHADE_BLOCK - 1) / SHADE_BLOCK;
+    hipLaunchKernelGGL(k_shade0, dim3(blocks), dim3(SHADE_BLOCK), 0, st, s, f, cam, hits, radiance, q);
 }
 void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,
                    const float4* qD, const float4* qT, const float4* hits, float4* radiance, const QueueArgs& q,
                    int maxCount, hipStream_t st) {
-    const int blocks = (maxCount + 255) / 256;
-    hipLaunchKernelGGL(k_shadeN, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, s, f, bounce, countIn, qO, qD, qT,
-                       hits, radiance, q);
+    const int blocks = (maxCount + SHADE_BLOCK - 1) / SHADE_BLOCK;
+    hipLaunchKernelGGL(k_shadeN, dim3(blocks > 0 ? blocks : 1), dim3(SHADE_BLOCK), 0, st, s, f, bounce, countIn, qO, qD,
+                       qT, hits, radiance, q);
 }
 void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st) {

@@ -12,7 +12,8 @@ import numpy as np
 from . import PKG_DIR
 from . import types as T
 
-LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libmcrt.so")
+# MCRT_LIB_PATH: an alternative in-tree build of the same library (kernel tuning experiments)
+LIB_PATH = os.environ.get("MCRT_LIB_PATH") or os.path.join(os.path.dirname(PKG_DIR), "libmcrt.so")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), "include", "mcrt_capi.h")
 
 _c = ctypes
