@@ -118,6 +118,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    from mcrt import dist as mdist
     from mcrt import lib, scenes
     from mcrt import types as T
     from mcrt.camera import scene_camera
@@ -170,8 +171,7 @@ def main():
         fb.copy_device(1, acc_s.data_ptr())
         fb.copy_device(3, acc_w.data_ptr())
         ctx.sync()
-        dist.reduce(acc_s, dst=0, op=dist.ReduceOp.SUM)
-        dist.reduce(acc_w, dst=0, op=dist.ReduceOp.SUM)
+        mdist.reduce_accumulators(acc_s, acc_w, dst=0)
         if rank == 0:
             torch.cuda.synchronize()
             fb.set_accumulation(acc_s.data_ptr(), acc_w.data_ptr())

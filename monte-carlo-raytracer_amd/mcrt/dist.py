@@ -1,0 +1,52 @@
+"""Multi-GPU image partition and reduction, one process per GPU.
+
+Tile split: the image is cut into 8-row blocks; bands of `band_rows` rows (a multiple of 8)
+are dealt round-robin to the ranks (interleaved for balance against sky/foliage skew).  The
+kernels enumerate a rank's pixels with the same formula (mcrt_kernels.hip tilePixel), every
+rank keeps full-frame accumulators that are zero outside its rows, and ONE sum-reduce of the
+accumulators to rank 0 (RCCL over xGMI on the GPU, gloo in the CPU tests) ends the job --
+paths are independent and the RNG is keyed by the global pixel index, so the reduced image
+equals the single-GPU image bit for bit (each pixel has exactly one non-zero contribution).
+"""
+import numpy as np
+
+
+def band_blocks(height, band_rows, num_bands, band_index):
+    """Global 8-row block indices owned by `band_index` (tilePixel's gb for tb = 0, 1, ...)."""
+    if band_rows % 8 or band_rows <= 0:
+        raise ValueError("band_rows must be a positive multiple of 8")
+    if not 0 <= band_index < num_bands:
+        raise ValueError("band_index out of range")
+    bpb = band_rows // 8
+    nblocks = (height + 7) // 8
+    out = []
+    tb = 0
+    while True:
+        gb = (tb // bpb) * bpb * num_bands + band_index * bpb + (tb % bpb)
+        if gb >= nblocks:
+            # later local blocks can only map further down the image
+            if tb % bpb == 0:
+                break
+            tb += 1
+            continue
+        out.append(gb)
+        tb += 1
+    return np.asarray(out, np.int64)
+
+
+def band_rows_of(height, band_rows, num_bands, band_index):
+    """Image rows owned by `band_index`."""
+    rows = (band_blocks(height, band_rows, num_bands, band_index)[:, None] * 8 + np.arange(8)[None, :]).ravel()
+    return rows[rows < height]
+
+
+def reduce_accumulators(wsum, wts, dst=0, group=None):
+    """Sum the per-rank accumulators into rank `dst` (torch tensors, in place on dst)."""
+    import torch.distributed as dist
+    dist.reduce(wsum, dst=dst, op=dist.ReduceOp.SUM, group=group)
+    dist.reduce(wts, dst=dst, op=dist.ReduceOp.SUM, group=group)
+
+
+def resolve(wsum, wts):
+    """image = sum(w * L) / sum(w) (k_resolve); numpy or torch."""
+    return wsum / wts[..., None]
