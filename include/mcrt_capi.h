@@ -195,6 +195,10 @@ typedef struct {
 #define MCRT_SAMPLER_SOBOL  0   /* KRN/samplers.cl:16 */
 #define MCRT_SAMPLER_RANDOM 1   /* KRN/samplers.cl:17 (reference default) */
 
+/* Integrators: RTPathTracingPass (KRN/PathTracing.cl) and RTBDPTPass (KRN/BDPT.cl). */
+#define MCRT_INTEGRATOR_PT   0
+#define MCRT_INTEGRATOR_BDPT 1
+
 /* One frame = one sample per pixel (RTPathTracingPass::update, APP/.../RTPathTracingPass.cpp:40-114). */
 typedef struct {
     int32_t frame_index;        /* integrator_frameNum */
@@ -207,6 +211,10 @@ typedef struct {
     int32_t band_rows;
     int32_t num_bands;
     int32_t band_index;
+    /* MCRT_INTEGRATOR_PT (0, default) or MCRT_INTEGRATOR_BDPT.  BDPT (RTBDPTPass::update,
+     * APP/.../RTBDPTPass.cpp:67-128) needs the whole image in one band (num_bands = 1): its
+     * light-tracing strategies splat into any pixel.  Multi-GPU BDPT splits frames instead. */
+    int32_t integrator;
 } mcrt_frame_params;
 
 typedef struct mcrt_ctx_s*         mcrt_ctx;
@@ -307,6 +315,15 @@ MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closes
  * (dst = [a0..a(n-1) | b0.. | c0..], 48 * max_records bytes) and the full count. */
 MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which, void* host_dst,
                                                  int64_t max_records, int32_t* count);
+/* Host copy of the BDPT state of the last BDPT frame (the reference keeps it in RTBDPTPass's
+ * m_cameraVertices / m_lightVertices / vertex-count buffers, RTBDPTPass.cpp:456-470):
+ *   which 0: camera vertices, (D+2) depths x 8 planes of float4 x W*H (layout: mcrt_bdpt.hip)
+ *         1: light vertices, (D+1) depths x 8 planes     2/3: camera / light vertex counts (int32 x W*H)
+ *         4: own-strategy contributions ((C-D) planes)   5: persistent s=1 sampled light vertices (D planes)
+ *         6: light-tracing (t=1) splat sums of the frame (float4 x W*H)
+ * Copies min(bytes, size) bytes; *needed = the array's size (host_dst may be NULL to query it). */
+MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, void* host_dst, uint64_t bytes,
+                                                uint64_t* needed);
 
 /* ------------------------------------------------------------------------ */
 /* Host helpers                                                              */

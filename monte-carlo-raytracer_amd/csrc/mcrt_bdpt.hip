@@ -1,0 +1,859 @@
+// mcrt_bdpt.hip -- bidirectional path tracing (KRN/BDPT.cl, host pass RTBDPTPass.cpp:67-488) on gfx950.
+//
+// One frame (1 sample per pixel, maxDepth D) is, per rank band:
+//   k_bdpt_start          camera vertex 0 + light vertex 0 of every pixel (GenerateStartVertices,
+//                         BDPT.cl:240-312); both first rays go to one compacted ray queue
+//   for d in 1..D+1:
+//     k_extend            closest hit over the queue (camera and light rays together)
+//     k_bdpt_vertex       GenerateSecondaryVertices (BDPT.cl:317-458) for every queued ray: the
+//                         surface vertex at depth d and, unless the subpath is done, its next ray
+//   k_bdpt_connect        PrepareConnections (BDPT.cl:460-646) fused with the visibility-independent
+//                         part of ConnectVertices (BDPT.cl:671-913): every (t, s) strategy's
+//                         unweighted contribution AND its MIS weight, so only strategies with a
+//                         non-zero weighted contribution emit a connection ray (compacted queue)
+//   k_bdpt_vis            any hit over the connection queue: an occluded own strategy is zeroed
+//                         in its slot; an unoccluded t = 1 strategy (light tracing) is splatted
+//                         with a float atomic into the splat buffer of the pixel it projects to
+//   k_bdpt_gather         radiance = (own strategies summed in the reference's (t, s) order) + splats
+//
+// HBM layout (N = W*H pixels; all planes are float4 x N, so every access is coalesced):
+//   camera vertices  (D+2) depths x 8 planes, light vertices (D+1) x 8 planes:
+//     0 p.xyz|traceErrorOffset  1 gn.xyz|pdfFwd  2 sn.xyz|pdfRev  3 wo.xyz|pdfPos
+//     4 sdpdu.xyz|uv.x  5 sdpdv.xyz|uv.y  6 throughput.xyz|-  7 int4(type, flags, lightIdx, materialIdx)
+//   (the reference's 240-B RTBDPTVertex holds the same fields plus unused differentials).
+//   vertex counts: int x N per subpath.  sampled light vertex of the s = 1 strategy, persistent across
+//   frames (the reference reads it before overwriting it, BDPT.cl:585-586): D planes of float4
+//   (p.xyz | flags<<16 | lightIdx).  own-strategy slots: (C - D) planes of float4 (C = maxConnections).
+//   splat buffer: float4 x N (zero between frames).
+//
+// Arithmetic mirrors the reference expressions (mcrt_device.h conventions: cl_div = the 2.5-ulp
+// OpenCL division, contraction as ROCm clang does at -O3 with FP_CONTRACT ON).
+#include "mcrt_device.h"
+#include "mcrt_internal.h"
+#include "mcrt_traverse.h"
+#include "mcrt_shading.h"
+
+#ifndef BDPT_BLOCK
+#define BDPT_BLOCK 256
+#endif
+
+// RTBDPTVertexType / RTBDPTVertexFlag (kernel_data.h:202-218)
+enum { RT_BDPT_CAMERA_VERTEX = 0, RT_BDPT_LIGHT_VERTEX = 1, RT_BDPT_SURFACE_VERTEX = 2 };
+enum {
+    VF_CONNECTIBLE = 1,
+    VF_DELTA_LIGHT = 1 << 1,
+    VF_DELTA = 1 << 2,
+    VF_INFINITE_LIGHT = 1 << 3,
+};
+#define MCRT_LIGHT_FLAG_DELTA_LIGHT (MCRT_LIGHT_FLAG_DELTA_POSITION | MCRT_LIGHT_FLAG_DELTA_DIRECTION)
+
+struct BVertex {
+    Frame fr;   // p, gn, sn, sdpdu, sdpdv, uv
+    f3 wo, throughput;
+    float traceErrorOffset, pdfFwd, pdfRev, pdfPos;
+    int type, flags, lightIdx, materialIdx;
+};
+
+// --- plane addressing ---------------------------------------------------------------------
+MCRT_DEV float4* vplane(float4* base, int depth, int k, int N) { return base + (size_t)(depth * 8 + k) * N; }
+MCRT_DEV const float4* vplane(const float4* base, int depth, int k, int N) {
+    return base + (size_t)(depth * 8 + k) * N;
+}
+
+MCRT_DEV BVertex loadVertex(const float4* base, int depth, int pix, int N) {
+    BVertex v;
+    const float4 a = vplane(base, depth, 0, N)[pix], b = vplane(base, depth, 1, N)[pix];
+    const float4 c = vplane(base, depth, 2, N)[pix], d = vplane(base, depth, 3, N)[pix];
+    const float4 e = vplane(base, depth, 4, N)[pix], f = vplane(base, depth, 5, N)[pix];
+    const float4 g = vplane(base, depth, 6, N)[pix];
+    const int4 h = *reinterpret_cast<const int4*>(&vplane(base, depth, 7, N)[pix]);
+    v.fr.p = ld3(a);
+    v.traceErrorOffset = a.w;
+    v.fr.gn = ld3(b);
+    v.pdfFwd = b.w;
+    v.fr.sn = ld3(c);
+    v.pdfRev = c.w;
+    v.wo = ld3(d);
+    v.pdfPos = d.w;
+    v.fr.sdpdu = ld3(e);
+    v.fr.sdpdv = ld3(f);
+    v.fr.uv = f2{e.w, f.w};
+    v.throughput = ld3(g);
+    v.type = h.x;
+    v.flags = h.y;
+    v.lightIdx = h.z;
+    v.materialIdx = h.w;
+    return v;
+}
+// Position / geometric normal / flags only (the "next" or "prev" vertex of a pdf evaluation)
+struct BVertexPos {
+    f3 p, gn;
+    int flags;
+};
+MCRT_DEV BVertexPos loadVertexPos(const float4* base, int depth, int pix, int N) {
+    BVertexPos v;
+    v.p = ld3(vplane(base, depth, 0, N)[pix]);
+    v.gn = ld3(vplane(base, depth, 1, N)[pix]);
+    v.flags = reinterpret_cast<const int4*>(&vplane(base, depth, 7, N)[pix])->y;
+    return v;
+}
+MCRT_DEV BVertexPos posOf(const BVertex& v) { return BVertexPos{v.fr.p, v.fr.gn, v.flags}; }
+
+MCRT_DEV void storeVertex(float4* base, int depth, int pix, int N, const BVertex& v) {
+    vplane(base, depth, 0, N)[pix] = make_float4(v.fr.p.x, v.fr.p.y, v.fr.p.z, v.traceErrorOffset);
+    vplane(base, depth, 1, N)[pix] = make_float4(v.fr.gn.x, v.fr.gn.y, v.fr.gn.z, v.pdfFwd);
+    vplane(base, depth, 2, N)[pix] = make_float4(v.fr.sn.x, v.fr.sn.y, v.fr.sn.z, v.pdfRev);
+    vplane(base, depth, 3, N)[pix] = make_float4(v.wo.x, v.wo.y, v.wo.z, v.pdfPos);
+    vplane(base, depth, 4, N)[pix] = make_float4(v.fr.sdpdu.x, v.fr.sdpdu.y, v.fr.sdpdu.z, v.fr.uv.x);
+    vplane(base, depth, 5, N)[pix] = make_float4(v.fr.sdpdv.x, v.fr.sdpdv.y, v.fr.sdpdv.z, v.fr.uv.y);
+    vplane(base, depth, 6, N)[pix] = make_float4(v.throughput.x, v.throughput.y, v.throughput.z, 0.0f);
+    *reinterpret_cast<int4*>(&vplane(base, depth, 7, N)[pix]) = make_int4(v.type, v.flags, v.lightIdx, v.materialIdx);
+}
+MCRT_DEV void storePdfFwd(float4* base, int depth, int pix, int N, float x) {
+    reinterpret_cast<float*>(&vplane(base, depth, 1, N)[pix])[3] = x;
+}
+MCRT_DEV void storePdfRev(float4* base, int depth, int pix, int N, float x) {
+    reinterpret_cast<float*>(&vplane(base, depth, 2, N)[pix])[3] = x;
+}
+
+// --- kernel_data.h:447-474 vertex predicates ----------------------------------------------
+MCRT_DEV bool isVertexOnSurface(f3 gn) {   // BDPT.cl:39-42
+    return isNotNearZero(gn.x) || isNotNearZero(gn.y) || isNotNearZero(gn.z);
+}
+MCRT_DEV bool isInfinite(int flags) { return (flags & VF_INFINITE_LIGHT) != 0; }
+MCRT_DEV bool isDeltaV(int flags) { return (flags & VF_DELTA) != 0; }
+MCRT_DEV bool isConnectible(int flags) { return (flags & VF_CONNECTIBLE) != 0; }
+MCRT_DEV bool isDeltaLightV(int flags) { return (flags & VF_DELTA_LIGHT) != 0; }
+MCRT_DEV float remap0(float f) { return f == 0.0f ? 1.0f : f; }   // BDPT.cl:649-652
+
+MCRT_DEV float dot4(float4 a, float4 b) {   // OpenCL dot(float4): fma chain
+    return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+}
+MCRT_DEV float4 transformVector4(const mcrt_mat4& m, float4 v) {   // matrix.cl:62-70
+    const float4 m0 = make_float4(m.m0.x, m.m0.y, m.m0.z, m.m0.w), m1 = make_float4(m.m1.x, m.m1.y, m.m1.z, m.m1.w);
+    const float4 m2 = make_float4(m.m2.x, m.m2.y, m.m2.z, m.m2.w), m3 = make_float4(m.m3.x, m.m3.y, m.m3.z, m.m3.w);
+    return make_float4(dot4(m0, v), dot4(m1, v), dot4(m2, v), dot4(m3, v));
+}
+
+// --- cameras.cl ------------------------------------------------------------------------
+// evalPinholeCameraPdfWe (cameras.cl:34-59): returns pdfDir (pdfPos is 1 or 0 alongside it)
+MCRT_DEV float evalPinholeCameraPdfWe(const mcrt_camera& cam, f3 o, f3 d) {
+    const float cosTheta = cl_dot(d, ld3(cam.direction));
+    if (cosTheta <= 0.0f) return 0.0f;
+    const float r = cl_div(1.0f, cosTheta);
+    const f3 pf = o + d * r;
+    const float4 img = transformVector4(cam.worldToClip, make_float4(pf.x, pf.y, pf.z, 1.0f));
+    if (img.x < -img.w || img.x > img.w || img.y < -img.w || img.y > img.w) return 0.0f;
+    return cl_div(1.0f, (cam.area * cosTheta * cosTheta * cosTheta));
+}
+// evalPinholeCameraWe (cameras.cl:8-32); *nip written only when inside the image.
+// `rayDirection / cosTheta` is correctly rounded in the reference's PrepareConnections.
+MCRT_DEV float evalPinholeCameraWe(const mcrt_camera& cam, f3 o, f3 d, f2* nip) {
+    const float cosTheta = cl_dot(d, ld3(cam.direction));
+    if (cosTheta <= 0.0f) return 0.0f;
+    const f3 q = f3{cr_div(d.x, cosTheta), cr_div(d.y, cosTheta), cr_div(d.z, cosTheta)};
+    const f3 pf = o + q;
+    const float4 img = transformVector4(cam.worldToClip, make_float4(pf.x, pf.y, pf.z, 1.0f));
+    if (img.x < -img.w || img.x > img.w || img.y < -img.w || img.y > img.w) return 0.0f;
+    const f2 ndc = f2{cl_div(img.x, img.w), cl_div(img.y, img.w)};
+    *nip = (ndc + f2{1.0f, 1.0f}) * 0.5f;
+    return cl_div(1.0f, (cam.area * cosTheta * cosTheta * cosTheta));
+}
+
+// --- lights.cl -------------------------------------------------------------------------
+// evalLightPdfLe (lights.cl:227-252)
+MCRT_DEV void evalLightPdfLe(const mcrt_light& light, f3 rayDirection, f3 lightNormal, float* pdfPos, float* pdfDir) {
+    if (light.type == MCRT_DIRECTIONAL_LIGHT) {
+        *pdfPos = cl_div(1.0f, light.area);
+        *pdfDir = 0.0f;
+    } else if (light.type == MCRT_POINT_LIGHT) {
+        *pdfPos = 0.0f;
+        *pdfDir = 0.07957747154f;   // PI4_INV
+    } else {
+        *pdfPos = cl_div(1.0f, light.area);
+        *pdfDir = cl_dot(lightNormal, rayDirection) * PI_INV_F;   // cosineHemispherePdf
+    }
+}
+// evalLightLe (lights.cl:26-35)
+MCRT_DEV f3 evalLightLe(const mcrt_light& light, f3 gn, f3 w) {
+    if (light.type == MCRT_DISK_AREA_LIGHT || light.type == MCRT_TRIANGLE_MESH_AREA_LIGHT)
+        return cl_dot(gn, w) > 0.0f ? ld3(light.intensity) : splat3(0.0f);
+    return splat3(0.0f);
+}
+// sampleLightLe (lights.cl:148-225)
+struct LightLe {
+    f3 Le, origin, dir, normal;
+    float pdfPos, pdfDir;
+};
+MCRT_DEV LightLe sampleLightLe(const SceneArgs& s, const mcrt_light& light, f2 u1, f2 u2) {
+    LightLe r;
+    r.Le = splat3(0.0f);
+    r.origin = r.dir = r.normal = splat3(0.0f);
+    r.pdfPos = r.pdfDir = 0.0f;
+    if (light.type == MCRT_DIRECTIONAL_LIGHT) {
+        r.origin = sampleDisk(ld3(light.p), ld3(light.d), light.radius, u1, &r.pdfPos);
+        r.normal = ld3(light.d);
+        r.pdfDir = 1.0f;
+        r.dir = ld3(light.d);
+        r.Le = ld3(light.intensity);
+    } else if (light.type == MCRT_POINT_LIGHT) {
+        const float y = 1.0f - 2.0f * u1.x;   // uniformSampleSphere (samplers.cl:143-149)
+        const float rr = cl_sqrt(fmaxf(0.0f, 1.0f - y * y));
+        const float phi = 2.0f * PI_F * u1.y;
+        r.dir = f3{rr * cosf(phi), y, rr * sinf(phi)};
+        r.origin = ld3(light.p);
+        r.normal = r.dir;
+        r.pdfPos = 1.0f;
+        r.pdfDir = 0.07957747154f;
+        r.Le = ld3(light.intensity);
+    } else if (light.type == MCRT_DISK_AREA_LIGHT || light.type == MCRT_TRIANGLE_MESH_AREA_LIGHT) {
+        f3 sp, gn;
+        if (light.type == MCRT_DISK_AREA_LIGHT) {
+            sp = sampleDisk(ld3(light.p), ld3(light.d), light.radius, u1, &r.pdfPos);
+            gn = ld3(light.d);
+        } else {
+            const mcrt_shape shape = s.shapes[light.shapeId];
+            const int triangleIdx = ((int)floorf(u1.x * shape.numTriangles)) % (int)shape.numTriangles;
+            u1.x = u1.x * shape.numTriangles - triangleIdx;
+            const uint32_t i0 = s.indices[shape.startIdx + 3 * triangleIdx];
+            const uint32_t i1 = s.indices[shape.startIdx + 3 * triangleIdx + 1];
+            const uint32_t i2 = s.indices[shape.startIdx + 3 * triangleIdx + 2];
+            const f3 p0 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i0]));
+            const f3 p1 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i1]));
+            const f3 p2 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i2]));
+            sp = sampleTriangle(p0, p1, p2, u1, &gn);
+            r.pdfPos = cl_div(1.0f, light.area);
+        }
+        r.normal = gn;
+        const f3 w = cosineSampleHemisphere(u2);
+        r.pdfDir = w.y * PI_INV_F;
+        const f3 v0 = computeOrthogonalVector(gn);
+        const f3 v1 = cl_cross(v0, gn);
+        r.dir = w.x * v0 + w.y * gn + w.z * v1;
+        r.origin = sp + gn * RT_TRACE_OFFSET_F;
+        r.Le = ld3(light.intensity);
+    }
+    return r;
+}
+
+// --- materials.cl with transport modes ----------------------------------------------------
+MCRT_DEV f3 evaluateMaterial(const SceneArgs& s, int materialIdx, f3 wo, f3 wi, const Frame& si, int mode) {
+    const mcrt_material mat = s.materials[materialIdx];
+    if (mat.type != 0) return splat3(0.0f);   // materials.cl:131-142: only RT_UBER_MATERIAL
+    const Uber um = uberProps(s, mat, si.uv);
+    return evaluateUberBSDF(um, si, wo, wi, mode);
+}
+MCRT_DEV float evaluateMaterialPdf(const SceneArgs& s, int materialIdx, f3 wo, f3 wi, const Frame& si) {
+    const mcrt_material mat = s.materials[materialIdx];
+    if (mat.type != 0) return 0.0f;
+    const Uber um = uberProps(s, mat, si.uv);
+    return evaluateUberBSDF_Pdf(um, si, wo, wi);
+}
+// hasMaterialNonDeltaComponents (materials.cl:163-183)
+MCRT_DEV bool hasMaterialNonDeltaComponents(const SceneArgs& s, int materialIdx, const Frame& si) {
+    const mcrt_material mat = s.materials[materialIdx];
+    if (mat.type != 0) return false;
+    const f3 Kd = mat.uber_diffuseTexId != -1 ? readTex(s, mat.uber_diffuseTexId, si.uv).xyz : ld3(mat.uber_kd);
+    const f3 Ks = mat.uber_glossyTexId != -1 ? readTex(s, mat.uber_glossyTexId, si.uv).xyz : ld3(mat.uber_ks);
+    const f3 op = mat.uber_opacityTexId != -1 ? readTex(s, mat.uber_opacityTexId, si.uv).xyz : ld3(mat.uber_opacity);
+    const f3 kd = Kd * op, ks = Ks * op;
+    return !isBlack(kd) || !isBlack(ks);
+}
+
+// computeShadingNormalCorrection (BDPT.cl:23-36).  The reference's compiled kernels evaluate
+// this division correctly rounded (its accuracy metadata is dropped when the select of the
+// three return values is folded), in GenerateSecondaryVertices and PrepareConnections alike.
+MCRT_DEV float shadingNormalCorrection(const Frame& si, f3 wo, f3 wi, int mode) {
+    if (mode == TRANSPORT_MODE_IMPORTANCE) {
+        const float denom = absDot(wo, si.gn) * absDot(wi, si.sn);
+        if (isNearZero(denom)) return 0.0f;
+        return cr_div((absDot(wo, si.sn) * absDot(wi, si.gn)), denom);
+    }
+    return 1.0f;
+}
+
+// --- vertex densities (BDPT.cl:44-154) -------------------------------------------------------
+// convertVertexDensity(pdf, this, next)
+MCRT_DEV float convertVertexDensity(float pdf, f3 thisP, const BVertexPos& next) {
+    if (isInfinite(next.flags)) return pdf;
+    const f3 w = next.p - thisP;
+    const float lenSq = cl_dot(w, w);
+    if (isNearZero(lenSq)) return 0.0f;
+    const float invDistSq = cl_div(1.0f, lenSq);
+    if (isVertexOnSurface(next.gn)) pdf *= absDot(next.gn, w * cl_sqrt(invDistSq));
+    return pdf * invDistSq;
+}
+// evalVertexPdfLight(this = light-like vertex, v)
+MCRT_DEV float evalVertexPdfLight(const SceneArgs& s, f3 thisP, f3 thisGn, int thisFlags, int thisLight,
+                                  const BVertexPos& v) {
+    f3 w = v.p - thisP;
+    const float lenSq = cl_dot(w, w);
+    if (isNearZero(lenSq)) return 0.0f;
+    const float invDistSq = cl_div(1.0f, lenSq);
+    w *= cl_sqrt(invDistSq);
+    float pdf;
+    if (isInfinite(thisFlags)) {
+        const float radius = s.lights[thisLight].radius;
+        pdf = cl_div(1.0f, (PI_F * radius * radius));
+    } else {
+        float pdfPos, pdfDir;
+        evalLightPdfLe(s.lights[thisLight], w, thisGn, &pdfPos, &pdfDir);
+        pdf = pdfDir * invDistSq;
+    }
+    if (isVertexOnSurface(v.gn)) pdf *= absDot(v.gn, w);
+    return pdf;
+}
+// evalVertexPdfLightOrigin(this, nextVertexPos)
+MCRT_DEV float evalVertexPdfLightOrigin(const SceneArgs& s, f3 thisP, f3 thisGn, int thisFlags, int thisLight, f3 nextP) {
+    f3 w = nextP - thisP;
+    const float lenSq = cl_dot(w, w);
+    if (isNearZero(lenSq)) return 0.0f;
+    w *= cl_sqrt(cl_div(1.0f, lenSq));
+    if (isInfinite(thisFlags)) return 0.0f;
+    float pdfPos, pdfDir;
+    const mcrt_light light = s.lights[thisLight];
+    evalLightPdfLe(light, w, thisGn, &pdfPos, &pdfDir);
+    return pdfPos * light.choicePdf;
+}
+// evalVertexPdf(this, prev (may be null), next)
+MCRT_DEV float evalVertexPdf(const SceneArgs& s, const mcrt_camera& cam, const BVertex& v, bool hasPrev, f3 prevP,
+                             const BVertexPos& next) {
+    if (v.type == RT_BDPT_LIGHT_VERTEX) return evalVertexPdfLight(s, v.fr.p, v.fr.gn, v.flags, v.lightIdx, next);
+    f3 wn = next.p - v.fr.p;
+    float lenSq = cl_dot(wn, wn);
+    if (isNearZero(lenSq)) return 0.0f;
+    wn = cl_div(wn, cl_sqrt(lenSq));
+    float pdf = 0.0f;
+    if (v.type == RT_BDPT_CAMERA_VERTEX) {
+        pdf = evalPinholeCameraPdfWe(cam, v.fr.p, wn);
+    } else if (v.type == RT_BDPT_SURFACE_VERTEX) {
+        f3 wp = splat3(0.0f);
+        if (hasPrev) {
+            wp = prevP - v.fr.p;
+            lenSq = cl_dot(wp, wp);
+            if (isNearZero(lenSq)) return 0.0f;
+            wp = cl_div(wp, cl_sqrt(lenSq));
+        }
+        pdf = evaluateMaterialPdf(s, v.materialIdx, wp, wn, v.fr);
+    }
+    return convertVertexDensity(pdf, v.fr.p, next);
+}
+// evalVertex_f(this, next, mode) (BDPT.cl:215-235)
+MCRT_DEV f3 evalVertex_f(const SceneArgs& s, const BVertex& v, f3 nextP, int mode) {
+    f3 wi = nextP - v.fr.p;
+    const float lenSq = cl_dot(wi, wi);
+    if (isNearZero(lenSq)) return splat3(0.0f);
+    wi = cl_div(wi, cl_sqrt(lenSq));
+    if (v.type == RT_BDPT_SURFACE_VERTEX) {
+        const f3 f = evaluateMaterial(s, v.materialIdx, v.wo, wi, v.fr, mode);
+        return f * shadingNormalCorrection(v.fr, v.wo, wi, mode);
+    }
+    return f3{1.0f, 0.0784f, 0.5765f};
+}
+
+MCRT_DEV BVertex createCameraVertex(f3 p, f3 throughput) {   // BDPT.cl:159-174
+    BVertex v;
+    v.fr.p = p;
+    v.fr.gn = v.fr.sn = v.fr.sdpdu = v.fr.sdpdv = splat3(0.0f);
+    v.fr.uv = f2{0.0f, 0.0f};
+    v.wo = splat3(0.0f);
+    v.throughput = throughput;
+    v.traceErrorOffset = 0.0f;
+    v.type = RT_BDPT_CAMERA_VERTEX;
+    v.flags = VF_CONNECTIBLE;
+    v.lightIdx = -1;
+    v.materialIdx = -1;
+    v.pdfRev = v.pdfFwd = v.pdfPos = 0.0f;
+    return v;
+}
+MCRT_DEV BVertex createLightVertex(int lightIdx, f3 p, f3 n, f3 throughput, float pdfFwd, int lightFlags) {
+    BVertex v;   // BDPT.cl:176-202
+    v.fr.p = p;
+    v.fr.gn = n;
+    v.fr.sn = n;
+    v.fr.sdpdu = v.fr.sdpdv = splat3(0.0f);
+    v.fr.uv = f2{0.0f, 0.0f};
+    v.wo = splat3(0.0f);
+    v.throughput = throughput;
+    v.traceErrorOffset = RT_TRACE_OFFSET_F;
+    v.type = RT_BDPT_LIGHT_VERTEX;
+    v.lightIdx = lightIdx;
+    v.materialIdx = -1;
+    v.pdfRev = 0.0f;
+    v.pdfFwd = pdfFwd;
+    v.pdfPos = 0.0f;
+    if ((lightFlags & MCRT_LIGHT_FLAG_DELTA_DIRECTION) != 0) {
+        v.flags = VF_DELTA_LIGHT | VF_INFINITE_LIGHT;
+    } else {
+        v.flags = VF_CONNECTIBLE;
+        if ((lightFlags & MCRT_LIGHT_FLAG_DELTA_POSITION) != 0) v.flags |= VF_DELTA_LIGHT;
+    }
+    return v;
+}
+
+// --- kernels --------------------------------------------------------------------------------
+// Ray-queue record (3 float4): (o.xyz, tag = 2*pix + isLight), (d.xyz, fwdPdf), (throughput.xyz, 0)
+MCRT_DEV void pushRay(const BdptQueue& q, int slot, f3 o, int tag, f3 d, float fwdPdf, f3 tp) {
+    q.o[slot] = make_float4(o.x, o.y, o.z, __int_as_float(tag));
+    q.d[slot] = make_float4(d.x, d.y, d.z, fwdPdf);
+    q.t[slot] = make_float4(tp.x, tp.y, tp.z, 0.0f);
+}
+
+// GenerateStartVertices (BDPT.cl:240-312) over the rank's 8x8 tiles; both first rays queued.
+__global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArgs f, BdptArgs b,
+                                                           const mcrt_camera* __restrict__ camp, BdptQueue qOut) {
+    const int lane = threadIdx.x & 63;
+    const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int x = 0, y = 0;
+    const bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y) && s.numLights > 0;
+    __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
+    const int N = (int)(f.W * f.H);
+    const int pix = y * (int)f.W + x;
+    f3 camDir = splat3(0.0f), camPos = splat3(0.0f), lo = splat3(0.0f), ld = splat3(0.0f), lt = splat3(0.0f);
+    float camPdf = 0.0f, lightPdfDir = 0.0f;
+    if (valid) {
+        const mcrt_camera& cam = *camp;
+        b.splat[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        b.camCount[pix] = 1;
+        b.lightCount[pix] = 1;
+        // camera (BDPT.cl:280-292)
+        const f2 r = f2{cl_div(1.0f, (float)f.W), cl_div(1.0f, (float)f.H)};
+        const f2 uv = f2{(float)x * r.x, (float)y * r.y};
+        camDir = lerpDirection(ld3(cam.r00), ld3(cam.r10), ld3(cam.r11), ld3(cam.r01), uv.x, uv.y);
+        camPos = ld3(cam.pos);
+        storeVertex(b.camV, 0, pix, N, createCameraVertex(camPos, splat3(1.0f)));
+        camPdf = evalPinholeCameraPdfWe(cam, camPos, camDir);
+        // light (BDPT.cl:294-311)
+        Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, 0, f.W, f.H, s.sobol);
+        const int chosen = (int)(((uint32_t)floorf(getSample1D(sampler) * s.numLights)) % (uint32_t)s.numLights);
+        const mcrt_light light = s.lights[chosen];
+        const float lightPdf = light.choicePdf;
+        const f2 u1 = getSample2D(sampler);
+        const f2 u2 = getSample2D(sampler);
+        const LightLe le = sampleLightLe(s, light, u1, u2);
+        BVertex lv = createLightVertex(chosen, le.origin, le.normal, le.Le, le.pdfPos * lightPdf, light.flags);
+        lv.pdfPos = le.pdfPos;
+        storeVertex(b.lightV, 0, pix, N, lv);
+        lo = le.origin;
+        ld = le.dir;
+        lt = cl_div(le.Le * absDot(le.normal, le.dir), (lightPdf * le.pdfPos * le.pdfDir));
+        lightPdfDir = le.pdfDir;
+    }
+    const int cs = blockAppend<BDPT_BLOCK / 64>(qOut.count, valid, ldsWave);
+    if (valid) pushRay(qOut, cs, camPos, 2 * pix, camDir, camPdf, splat3(1.0f));
+    const int ls = blockAppend<BDPT_BLOCK / 64>(qOut.count, valid, ldsWave);
+    if (valid) pushRay(qOut, ls, lo, 2 * pix + 1, ld, lightPdfDir, lt);
+}
+
+// GenerateSecondaryVertices (BDPT.cl:317-458) for every queued subpath ray at depth d.
+__global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameArgs f, BdptArgs b, int depth,
+                                                            BdptQueue qIn, const float4* __restrict__ hits,
+                                                            BdptQueue qOut) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = *qIn.count;
+    __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
+    if ((int)blockIdx.x * BDPT_BLOCK >= n) return;
+    const int N = (int)(f.W * f.H);
+    const int D = f.maxDepth;
+    bool push = false;
+    f3 no = splat3(0.0f), nd = splat3(0.0f), ntp = splat3(0.0f);
+    float nPdf = 0.0f;
+    int tag = 0;
+    if (i < n) {
+        const float4 O = qIn.o[i], Dd = qIn.d[i], Tp = qIn.t[i];
+        tag = __float_as_int(O.w);
+        const int pix = tag >> 1;
+        const bool isCamera = (tag & 1) == 0;
+        float4* V = isCamera ? b.camV : b.lightV;
+        const float4 hit = hits[i];
+        const int tri = __float_as_int(hit.w);
+        int shapeIdx = -1, primIdx = -1;
+        if (tri >= 0) {
+            shapeIdx = __float_as_int(s.nodes[4 * tri].w);
+            primIdx = __float_as_int(s.nodes[4 * tri + 1].w);
+        }
+        const mcrt_shape* shape = tri >= 0 ? &s.shapes[shapeIdx] : nullptr;
+        if (shape && shape->materialId != -1) {
+            (isCamera ? b.camCount : b.lightCount)[pix] = depth + 1;
+            const f3 rayD = ld3(Dd);
+            BVertex cur;
+            cur.fr = computeSurfaceInteraction(s, shapeIdx, primIdx, f2{hit.x, hit.y});
+            cur.wo = -rayD;
+            const bool isBackfacing = cl_dot(cur.fr.gn, cur.wo) < 0.0f;
+            cur.traceErrorOffset = isBackfacing ? -RT_TRACE_OFFSET_F : RT_TRACE_OFFSET_F;
+            const int materialIdx = shape->materialId;
+            const mcrt_material mat = s.materials[materialIdx];
+            if (mat.uber_normalMapId != -1) applyNormalMapping(s, mat.uber_normalMapId, cur.fr);
+            const int mode = isCamera ? TRANSPORT_MODE_RADIANCE : TRANSPORT_MODE_IMPORTANCE;
+            const BVertexPos prev = loadVertexPos(V, depth - 1, pix, N);
+            float pdfFwd = Dd.w;
+            f3 throughput = ld3(Tp);
+            // setSurfaceVertex (BDPT.cl:204-213)
+            cur.throughput = throughput;
+            cur.type = RT_BDPT_SURFACE_VERTEX;
+            cur.materialIdx = materialIdx;
+            cur.flags = 0;
+            cur.pdfRev = 0.0f;
+            cur.pdfPos = 0.0f;
+            cur.pdfFwd = convertVertexDensity(pdfFwd, prev.p, posOf(cur));
+            cur.lightIdx = shape->lightID;
+            // infinite-light correction of the first light-subpath vertex (BDPT.cl:383-393)
+            if (!isCamera && depth == 1 && isInfinite(prev.flags)) {
+                const float prevPdfPos = vplane(V, 0, 3, N)[pix].w;
+                cur.pdfFwd = prevPdfPos;
+                if (isVertexOnSurface(cur.fr.gn)) cur.pdfFwd *= absDot(rayD, cur.fr.gn);
+                storePdfFwd(V, 0, pix, N, 0.0f);
+            }
+            if (depth == D + (isCamera ? 1 : 0)) {   // subpath complete (BDPT.cl:395-403)
+                if (hasMaterialNonDeltaComponents(s, materialIdx, cur.fr)) cur.flags |= VF_CONNECTIBLE;
+                storeVertex(V, depth, pix, N, cur);
+            } else {
+                Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, depth + (D + 1) * (isCamera ? 1 : 0),
+                                              f.W, f.H, s.sobol);
+                const f3 wo = cur.wo;
+                const f2 bsdfSample = getSample2D(sampler);
+                f3 wi = splat3(0.0f), fv = splat3(0.0f);
+                int sampledType = 0, numNonDelta = 0;
+                if (mat.type == 0) {
+                    const Uber um = uberProps(s, mat, cur.fr.uv);
+                    fv = sampleUberBSDF(um, cur.fr, bsdfSample, wo, &wi, &pdfFwd, &sampledType, mode, &numNonDelta);
+                }
+                if (numNonDelta > 0) cur.flags |= VF_CONNECTIBLE;
+                if (isBlack(fv) || isNearZero(pdfFwd)) {
+                    storeVertex(V, depth, pix, N, cur);
+                } else {
+                    throughput = throughput * cl_div(fv * absDot(wi, cur.fr.sn), pdfFwd);
+                    float pdfRev;
+                    if ((sampledType & BSDF_SPECULAR) != 0) {
+                        cur.flags |= VF_DELTA;
+                        pdfFwd = 0.0f;
+                        pdfRev = 0.0f;
+                    } else {
+                        pdfRev = evaluateMaterialPdf(s, materialIdx, wi, wo, cur.fr);
+                    }
+                    float off = cur.traceErrorOffset;
+                    if ((sampledType & BSDF_TRANSMISSION) != 0 && cl_dot(cur.fr.gn, wi) * cl_sign(off) < 0.0f) off *= -1.0f;
+                    no = cur.fr.p + cur.fr.gn * off;
+                    nd = wi;
+                    throughput *= shadingNormalCorrection(cur.fr, wo, wi, mode);
+                    storePdfRev(V, depth - 1, pix, N, convertVertexDensity(pdfRev, cur.fr.p, prev));
+                    storeVertex(V, depth, pix, N, cur);
+                    ntp = throughput;
+                    nPdf = pdfFwd;
+                    push = true;
+                }
+            }
+        }
+    }
+    const int slot = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
+    if (push) pushRay(qOut, slot, no, tag, nd, nPdf, ntp);
+}
+
+// Connection-ray record (3 float4): (o.xyz, tmax), (d.xyz, code), (c.xyz, 0) where code >= 0 is an
+// own-strategy slot index (slot * N + pix) and code < 0 a splat target pixel (~code).
+MCRT_DEV void pushConn(const BdptQueue& q, int slot, f3 o, float tmax, f3 d, int code, f3 c) {
+    q.o[slot] = make_float4(o.x, o.y, o.z, tmax);
+    q.d[slot] = make_float4(d.x, d.y, d.z, __int_as_float(code));
+    q.t[slot] = make_float4(c.x, c.y, c.z, 0.0f);
+}
+
+// PrepareConnections (BDPT.cl:460-646) + the MIS weights of ConnectVertices (BDPT.cl:739-876).
+// Per pixel, one thread walks the strategies in the reference's (t, s) order.  Own strategies
+// (t >= 2) get a slot, written here (zero when they need no connection or contribute nothing);
+// strategies with a non-zero weighted contribution that need visibility are queued.
+__global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameArgs f, BdptArgs b,
+                                                             const mcrt_camera* __restrict__ camp, BdptQueue qOut) {
+    const int lane = threadIdx.x & 63;
+    const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int x = 0, y = 0;
+    const bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y) && s.numLights > 0;
+    __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
+    const int N = (int)(f.W * f.H);
+    const int D = f.maxDepth;
+    const int pix = y * (int)f.W + x;
+    const mcrt_camera& cam = *camp;
+    const int camCount = valid ? b.camCount[pix] : 0;
+    const int lightCount = valid ? b.lightCount[pix] : 0;
+    Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, (D + 1) + (D + 2), f.W, f.H, s.sobol);
+    int ownSlot = 0;
+    // Every thread of the block runs the same number of append rounds (block-wide barrier).
+    for (int t = 1; t <= D + 2; ++t) {
+        for (int sI = 0; sI <= D + 1; ++sI) {
+            const int curDepth = t + sI - 2;
+            if ((t == 1 && sI == 1) || curDepth < 0 || curDepth > D) continue;   // uniform skip
+            const bool live = t <= camCount && sI <= lightCount;
+            bool push = false, needRay = false;
+            f3 L = splat3(0.0f), rayO = splat3(0.0f), rayD = splat3(0.0f);
+            float rayT = 0.0f;
+            int code = 0;
+            if (live) {
+                const BVertex cv = loadVertex(b.camV, t - 1, pix, N);
+                // sampled vertices of the t = 1 / s = 1 strategies (replace pt / qs in the MIS)
+                BVertex samp;
+                if (sI == 0) {
+                    // ConnectVertices (BDPT.cl:723-731): emission of a camera vertex that is a light
+                    if (cv.type == RT_BDPT_LIGHT_VERTEX || cv.lightIdx != -1) {
+                        const f3 Le = evalLightLe(s.lights[cv.lightIdx], cv.fr.gn, cv.wo);
+                        L = Le * cv.throughput;
+                    }
+                } else if (t == 1) {
+                    const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
+                    if (isConnectible(lv.flags)) {
+                        // samplePinholeCameraWi (cameras.cl:61-69)
+                        f3 wi = ld3(cam.pos) - lv.fr.p;
+                        const float dist = cl_length(wi);
+                        wi = cl_div(wi, dist);
+                        const float pdf = cl_div((dist * dist), absDot(ld3(cam.direction), wi));
+                        f2 nip = f2{cl_div((float)x, (float)f.W), cl_div((float)y, (float)f.H)};
+                        const float imp = evalPinholeCameraWe(cam, ld3(cam.pos), -wi, &nip);
+                        const f3 importance = splat3(imp);
+                        if (pdf > 0.0f && isNotBlack(importance)) {
+                            samp = createCameraVertex(ld3(cam.pos), cl_div(importance, pdf));
+                            int ix = (int)floorf(nip.x * f.W + 0.5f), iy = (int)floorf(nip.y * f.H + 0.5f);
+                            ix = min(max(ix, 0), (int)f.W - 1);
+                            iy = min(max(iy, 0), (int)f.H - 1);
+                            code = ~(ix + iy * (int)f.W);
+                            L = lv.throughput * samp.throughput * evalVertex_f(s, lv, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                            if (isVertexOnSurface(lv.fr.gn)) L *= absDot(wi, lv.fr.sn);
+                            rayO = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
+                            rayT = cl_distance(rayO, ld3(cam.pos));
+                            rayD = cl_div(ld3(cam.pos) - rayO, rayT);
+                            needRay = true;
+                        }
+                    }
+                } else if (sI == 1) {
+                    if (isConnectible(cv.flags)) {
+                        const int chosen = min((int)floorf(getSample1D(sampler) * s.numLights), s.numLights - 1);
+                        const mcrt_light light = s.lights[chosen];
+                        const float lightPdf = light.choicePdf;
+                        const f2 u = getSample2D(sampler);
+                        const LightSample ls = sampleLightLi(s, light, cv.fr, cv.traceErrorOffset, u);
+                        if (isNotNearZero(ls.pdf) && isNotBlack(ls.Li)) {
+                            // the reference evaluates pdfFwd on the PREVIOUS content of the sampled
+                            // vertex slot before overwriting it (BDPT.cl:585-586)
+                            float4* stale = b.sampLight + (size_t)(t - 2) * N + pix;
+                            const float4 st = *stale;
+                            const int stBits = __float_as_int(st.w);
+                            const int stFlags = stBits >> 16, stLight = (int)(short)(stBits & 0xffff);
+                            const float pdfFwdS = evalVertexPdfLightOrigin(s, ld3(st), splat3(0.0f), stFlags, stLight,
+                                                                          cv.fr.p);
+                            samp = createLightVertex(chosen, ls.lightPos, ls.lightNormal, cl_div(ls.Li, (lightPdf * ls.pdf)),
+                                                     pdfFwdS, light.flags);
+                            *stale = make_float4(samp.fr.p.x, samp.fr.p.y, samp.fr.p.z,
+                                                 __int_as_float((samp.flags << 16) | (chosen & 0xffff)));
+                            const f3 fm = evaluateMaterial(s, cv.materialIdx, cv.wo, ls.wi, cv.fr, TRANSPORT_MODE_RADIANCE);
+                            L = cv.throughput * samp.throughput * fm;
+                            if (isVertexOnSurface(cv.fr.gn)) L *= absDot(ls.wi, cv.fr.sn);
+                            if (ls.shadowSet) {
+                                rayO = ls.shadowO;
+                                rayT = ls.shadowT;
+                                rayD = ls.wi;
+                                needRay = true;
+                            }
+                        }
+                    }
+                } else {
+                    const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
+                    if (isConnectible(cv.flags) && isConnectible(lv.flags)) {
+                        const f3 lvf = evalVertex_f(s, lv, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                        const f3 cvf = evalVertex_f(s, cv, lv.fr.p, TRANSPORT_MODE_RADIANCE);
+                        const f3 lp = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
+                        const f3 cp = cv.fr.p + cv.fr.gn * cv.traceErrorOffset;
+                        f3 w = cp - lp;
+                        const float sqDist = cl_dot(w, w);
+                        const float dist = cl_sqrt(sqDist);
+                        w = cl_div(w, dist);
+                        if (isNotNearZero(sqDist)) {
+                            const float g = cl_div(absDot(cv.fr.sn, w) * absDot(lv.fr.sn, w), sqDist);
+                            L = lv.throughput * cv.throughput * lvf * cvf * g;
+                        }
+                        if (isNotBlack(L)) {
+                            rayO = lp;
+                            rayT = dist;
+                            rayD = w;
+                            needRay = true;
+                        }
+                    }
+                }
+                // MIS weight (BDPT.cl:739-876), independent of visibility
+                float misWeight = 1.0f;
+                if (isBlack(L)) {
+                    misWeight = 0.0f;
+                } else if (sI + t != 2) {
+                    // pt = camera vertex t-1 (or the sampled camera vertex), qs = light vertex s-1 (or the
+                    // sampled light vertex), with their delta flags cleared and pdfRev re-evaluated
+                    BVertex pt = t == 1 ? samp : cv;
+                    BVertex qs;
+                    if (sI == 1) qs = samp;
+                    else if (sI > 1) qs = loadVertex(b.lightV, sI - 1, pix, N);
+                    BVertexPos ptPrev, qsPrev;
+                    if (t > 1) ptPrev = loadVertexPos(b.camV, t - 2, pix, N);
+                    if (sI > 1) qsPrev = loadVertexPos(b.lightV, sI - 2, pix, N);
+                    pt.flags &= ~VF_DELTA;
+                    if (sI > 0) qs.flags &= ~VF_DELTA;
+                    const float ptRev = sI > 0 ? evalVertexPdf(s, cam, qs, sI > 1, qsPrev.p, posOf(pt))
+                                               : evalVertexPdfLightOrigin(s, pt.fr.p, pt.fr.gn, pt.flags, pt.lightIdx, ptPrev.p);
+                    float ptPrevRev = 0.0f, qsRev = 0.0f, qsPrevRev = 0.0f;
+                    if (t > 1)
+                        ptPrevRev = sI > 0 ? evalVertexPdf(s, cam, pt, true, qs.fr.p, ptPrev)
+                                           : evalVertexPdfLight(s, pt.fr.p, pt.fr.gn, pt.flags, pt.lightIdx, ptPrev);
+                    if (sI > 0) qsRev = evalVertexPdf(s, cam, pt, t > 1, ptPrev.p, posOf(qs));
+                    if (sI > 1) qsPrevRev = evalVertexPdf(s, cam, qs, true, pt.fr.p, qsPrev);
+                    float sumRi = 0.0f;
+                    // camera subpath (BDPT.cl:819-827)
+                    float ri = 1.0f;
+                    int flagsHi = pt.flags;   // flags of vertex i (walking down from t-1)
+                    for (int i = t - 1; i > 0; --i) {
+                        float rev, fwd;
+                        int fl, flLo;
+                        if (i == t - 1) {
+                            rev = ptRev;
+                            fwd = pt.pdfFwd;
+                            fl = pt.flags;
+                        } else {
+                            const float4 pb = vplane(b.camV, i, 1, N)[pix];
+                            const float4 pc = vplane(b.camV, i, 2, N)[pix];
+                            fwd = pb.w;
+                            rev = (i == t - 2) ? ptPrevRev : pc.w;
+                            fl = flagsHi;
+                        }
+                        flLo = reinterpret_cast<const int4*>(&vplane(b.camV, i - 1, 7, N)[pix])->y;
+                        ri *= cl_div(remap0(rev), remap0(fwd));
+                        if (!isDeltaV(fl) && !isDeltaV(flLo)) sumRi += ri;
+                        flagsHi = flLo;
+                    }
+                    // light subpath (BDPT.cl:829-838)
+                    ri = 1.0f;
+                    for (int i = sI - 1; i >= 0; --i) {
+                        float rev, fwd;
+                        int fl;
+                        if (i == sI - 1) {
+                            rev = qsRev;
+                            fwd = qs.pdfFwd;
+                            fl = qs.flags;
+                        } else {
+                            const float4 pb = vplane(b.lightV, i, 1, N)[pix];
+                            const float4 pc = vplane(b.lightV, i, 2, N)[pix];
+                            fwd = pb.w;
+                            rev = (i == sI - 2) ? qsPrevRev : pc.w;
+                            fl = reinterpret_cast<const int4*>(&vplane(b.lightV, i, 7, N)[pix])->y;
+                        }
+                        ri *= cl_div(remap0(rev), remap0(fwd));
+                        bool deltaLightVertex;
+                        if (i > 0) {
+                            deltaLightVertex = isDeltaV(reinterpret_cast<const int4*>(&vplane(b.lightV, i - 1, 7, N)[pix])->y);
+                        } else {
+                            const int f0 = (sI == 1) ? qs.flags
+                                                     : reinterpret_cast<const int4*>(&vplane(b.lightV, 0, 7, N)[pix])->y;
+                            deltaLightVertex = isDeltaLightV(f0);
+                        }
+                        if (!isDeltaV(fl) && !deltaLightVertex) sumRi += ri;
+                    }
+                    misWeight = cl_div(1.0f, (1.0f + sumRi));
+                }
+                const f3 c = L * misWeight;
+                const bool nonzero = c.x != 0.0f || c.y != 0.0f || c.z != 0.0f;
+                if (sI > 0 && nonzero) push = needRay;   // no connection ray = not visible (contributes 0)
+                if (t >= 2) {
+                    const f3 own = (sI == 0 || push) ? c : splat3(0.0f);
+                    b.slots[(size_t)ownSlot * N + pix] = make_float4(own.x, own.y, own.z, 0.0f);
+                    if (push) code = ownSlot * N + pix;
+                }
+                L = c;
+            } else if (valid && t >= 2) {
+                b.slots[(size_t)ownSlot * N + pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // strategy absent
+            }
+            if (t >= 2) ++ownSlot;
+            const int qs = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
+            if (push) pushConn(qOut, qs, rayO, rayT, rayD, code, L);
+        }
+    }
+}
+
+// Any hit over the connection queue (RR occluded_main semantics): occluded own strategies are
+// zeroed in their slot, unoccluded light-tracing strategies splatted (BDPT.cl:888-899).
+__global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const int* __restrict__ count,
+                                                 const float4* __restrict__ sO, const float4* __restrict__ sD,
+                                                 const float4* __restrict__ sL) {
+    __shared__ uint32_t lds[STACK_LDS * 64];
+    const int n = *count;
+    if ((int)blockIdx.x * 64 >= n) return;
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * 64 + lane;
+    if (i >= n) return;
+    const float4 o = sO[i], d = sD[i];
+    TraceRay r;
+    r.o = ld3(o);
+    r.d = ld3(d);
+    r.tmax = o.w;
+    r.mask = -1;
+    float t;
+    const int tri = traverse<true>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+    const int code = __float_as_int(d.w);
+    if (code >= 0) {
+        if (tri >= 0) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    } else if (tri < 0) {
+        const float4 L = sL[i];
+        float* dst = reinterpret_cast<float*>(&b.splat[~code]);
+        atomicAdd(dst + 0, L.x);
+        atomicAdd(dst + 1, L.y);
+        atomicAdd(dst + 2, L.z);
+    }
+}
+
+// Own strategies summed in (t, s) order (the reference's per-thread atomicAdd_f order), then the
+// splats; radiance = float4(sum, 0) as CopyBuffer (BDPT.cl:916-932).  Clears the splat buffer.
+__global__ __launch_bounds__(256) void k_bdpt_gather(FrameArgs f, BdptArgs b, float4* __restrict__ radiance) {
+    const int lane = threadIdx.x & 63;
+    const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int x, y;
+    if (tile >= f.numTiles || !tilePixel(f, tile, lane, x, y)) return;
+    const int N = (int)(f.W * f.H);
+    const int pix = y * (int)f.W + x;
+    float rx = 0.0f, ry = 0.0f, rz = 0.0f;
+    for (int k = 0; k < b.ownSlots; ++k) {
+        const float4 c = b.slots[(size_t)k * N + pix];
+        rx += c.x;
+        ry += c.y;
+        rz += c.z;
+    }
+    const float4 sp = b.splat[pix];
+    radiance[pix] = make_float4(rx + sp.x, ry + sp.y, rz + sp.z, 0.0f);
+}
+
+// Splats that land outside the rank's bands (multi-GPU band split): added by the rank that owns
+// the pixel after the all-reduce of the splat buffers (mcrt_capi.cpp).
+__global__ __launch_bounds__(256) void k_bdpt_clear_splat(int n, float4* __restrict__ splat) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) splat[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+namespace mcrt {
+void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
+                       const BdptQueue& q, hipStream_t st) {
+    const int blocks = (f.numTiles * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK;
+    hipLaunchKernelGGL(k_bdpt_start, dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, q);
+}
+void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
+                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st) {
+    const int blocks = (maxCount + BDPT_BLOCK - 1) / BDPT_BLOCK;
+    hipLaunchKernelGGL(k_bdpt_vertex, dim3(blocks > 0 ? blocks : 1), dim3(BDPT_BLOCK), 0, st, s, f, b, depth, qIn, hits,
+                       qOut);
+}
+void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
+                         const BdptQueue& q, hipStream_t st) {
+    const int blocks = (f.numTiles * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK;
+    hipLaunchKernelGGL(k_bdpt_connect, dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, q);
+}
+void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st) {
+    hipLaunchKernelGGL(k_bdpt_vis, dim3((maxCount + 63) / 64 > 0 ? (maxCount + 63) / 64 : 1), dim3(64), 0, st, c, b,
+                       q.count, q.o, q.d, q.t);
+}
+void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, hipStream_t st) {
+    const int blocks = (f.numTiles * 64 + 255) / 256;
+    hipLaunchKernelGGL(k_bdpt_gather, dim3(blocks), dim3(256), 0, st, f, b, radiance);
+}
+void launch_bdpt_clear_splat(int n, float4* splat, hipStream_t st) {
+    hipLaunchKernelGGL(k_bdpt_clear_splat, dim3((n + 255) / 256), dim3(256), 0, st, n, splat);
+}
+}  // namespace mcrt

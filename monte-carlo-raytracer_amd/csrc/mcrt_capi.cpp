@@ -25,9 +25,13 @@ thread_local std::string g_lastError;
 
 #define MCRT_MAX_BOUNCES 32
 
-enum KernelId { K_PRIMARY, K_SHADE0, K_SHADEN, K_SHADOW, K_EXTEND, K_ACCUM, K_TRACE_CLOSEST, K_TRACE_ANY, K_COUNT };
-const char* kKernelNames[K_COUNT] = {"k_primary", "k_shade0", "k_shadeN", "k_shadow",
-                                     "k_extend",  "k_accumulate", "k_trace_closest", "k_trace_any"};
+enum KernelId {
+    K_PRIMARY, K_SHADE0, K_SHADEN, K_SHADOW, K_EXTEND, K_ACCUM, K_TRACE_CLOSEST, K_TRACE_ANY,
+    K_BDPT_START, K_BDPT_VERTEX, K_BDPT_CONNECT, K_BDPT_VIS, K_BDPT_GATHER, K_COUNT
+};
+const char* kKernelNames[K_COUNT] = {"k_primary",    "k_shade0",      "k_shadeN",       "k_shadow",   "k_extend",
+                                     "k_accumulate", "k_trace_closest", "k_trace_any",  "k_bdpt_start",
+                                     "k_bdpt_vertex", "k_bdpt_connect", "k_bdpt_vis",   "k_bdpt_gather"};
 
 }  // namespace
 
@@ -102,7 +106,16 @@ struct mcrt_framebuffer_s {
     int64_t lastPixels = 0;
     FrameArgs bands{};      // band layout of the last mcrt_render_frame (used by mcrt_accumulate)
     bool haveBands = false;
+    // BDPT state (allocated on the first BDPT frame for a max depth; mcrt_bdpt.hip has the layout)
+    int bdptDepth = 0;
+    float4 *camV = nullptr, *lightV = nullptr, *sampLight = nullptr, *slots = nullptr, *splat = nullptr;
+    int *camCount = nullptr, *lightCount = nullptr, *bdptCounters = nullptr;
+    float4 *bqO[2] = {}, *bqD[2] = {}, *bqT[2] = {}, *bHits = nullptr;
+    float4 *cO = nullptr, *cD = nullptr, *cL = nullptr;   // connection queue
+    int lastIntegrator = MCRT_INTEGRATOR_PT;
 };
+
+static int bdpt_max_connections(int D) { const int t = D + 2; return t * (t + 1) / 2 - 2; }   // RTBDPTPass.cpp:404-408
 
 // ---------------------------------------------------------------------------
 // helpers
@@ -555,11 +568,58 @@ MCRT_API mcrt_status mcrt_trace_any(mcrt_scene s, const mcrt_ray* d_rays, int32_
 // ---------------------------------------------------------------------------
 // frame buffer + integrator
 // ---------------------------------------------------------------------------
+static void fb_free_bdpt(mcrt_framebuffer fb) {
+    void* ptrs[] = {fb->camV,   fb->lightV, fb->sampLight, fb->slots,  fb->splat,  fb->camCount, fb->lightCount,
+                    fb->bdptCounters, fb->bqO[0], fb->bqO[1], fb->bqD[0], fb->bqD[1], fb->bqT[0], fb->bqT[1],
+                    fb->bHits,  fb->cO,     fb->cD,        fb->cL};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    fb->camV = fb->lightV = fb->sampLight = fb->slots = fb->splat = fb->bHits = fb->cO = fb->cD = fb->cL = nullptr;
+    fb->camCount = fb->lightCount = fb->bdptCounters = nullptr;
+    for (int i = 0; i < 2; ++i) fb->bqO[i] = fb->bqD[i] = fb->bqT[i] = nullptr;
+    fb->bdptDepth = 0;
+}
+
 static void fb_free(mcrt_framebuffer fb) {
     void* ptrs[] = {fb->radiance, fb->wsum, fb->wts, fb->image, fb->hitsP, fb->hitsE, fb->eO[0], fb->eO[1],
                     fb->eD[0],    fb->eD[1], fb->eT[0], fb->eT[1], fb->sO,   fb->sD,   fb->sL,    fb->counters};
     for (void* p : ptrs)
         if (p) hipFree(p);
+    fb_free_bdpt(fb);
+}
+
+// RTBDPTPass::createBuffers (RTBDPTPass.cpp:442-479), sized for max depth D.  The persistent
+// sampled-light-vertex planes start zeroed (the reference's buffer starts with whatever the
+// allocation holds; its clref runner zero-fills it too).
+static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D) {
+    if (fb->bdptDepth == D) return hipSuccess;
+    hipStreamSynchronize(fb->ctx->stream);
+    fb_free_bdpt(fb);
+    const size_t N = fb->N, C = (size_t)bdpt_max_connections(D);
+    hipError_t e = hipSuccess;
+    auto A = [&](auto** p, size_t bytes) {
+        if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
+    };
+    A(&fb->camV, 16 * N * 8 * (D + 2));
+    A(&fb->lightV, 16 * N * 8 * (D + 1));
+    A(&fb->sampLight, 16 * N * D);
+    A(&fb->slots, 16 * N * (C - D));
+    A(&fb->splat, 16 * N);
+    A(&fb->camCount, 4 * N);
+    A(&fb->lightCount, 4 * N);
+    A(&fb->bdptCounters, 64 * sizeof(int));
+    for (int i = 0; i < 2; ++i) { A(&fb->bqO[i], 32 * N); A(&fb->bqD[i], 32 * N); A(&fb->bqT[i], 32 * N); }
+    A(&fb->bHits, 32 * N);
+    A(&fb->cO, 16 * N * C);
+    A(&fb->cD, 16 * N * C);
+    A(&fb->cL, 16 * N * C);
+    if (e == hipSuccess) e = hipMemset(fb->sampLight, 0, 16 * N * D);
+    if (e == hipSuccess) e = hipMemset(fb->splat, 0, 16 * N);
+    if (e == hipSuccess) e = hipMemset(fb->camV, 0, 16 * N * 8 * (D + 2));
+    if (e == hipSuccess) e = hipMemset(fb->lightV, 0, 16 * N * 8 * (D + 1));
+    if (e != hipSuccess) { fb_free_bdpt(fb); return e; }
+    fb->bdptDepth = D;
+    return hipSuccess;
 }
 
 MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint32_t height, mcrt_framebuffer* out) {
@@ -636,6 +696,83 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
     return true;
 }
 
+// RTBDPTPass::update (RTBDPTPass.cpp:67-128): start vertices, D+1 rounds of (trace, vertex),
+// connections + MIS, visibility, gather.  Rays of both subpaths share one compacted queue.
+static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cam, const mcrt_frame_params* p,
+                               const FrameArgs& f) {
+    mcrt_ctx ctx = s->ctx;
+    hipStream_t st = ctx->stream;
+    const int D = p->max_depth;
+    HIPCHK(ctx, fb_ensure_bdpt(fb, D));
+    fb->lastMaxDepth = D;
+    fb->lastPixels = 0;
+    fb->bands = f;
+    fb->haveBands = true;
+    fb->lastIntegrator = MCRT_INTEGRATOR_BDPT;
+    mcrt_camera* dCam = reinterpret_cast<mcrt_camera*>(fb->counters + 128);
+    HIPCHK(ctx, hipMemcpyAsync(dCam, cam, sizeof(mcrt_camera), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemsetAsync(fb->bdptCounters, 0, 64 * sizeof(int), st));
+    if (s->numLights == 0) {   // RTBDPTPass.cpp:69: no lights -> pass skipped
+        HIPCHK(ctx, hipMemsetAsync(fb->radiance, 0, 16 * fb->N, st));
+        return MCRT_OK;
+    }
+    const size_t N = fb->N, C = (size_t)bdpt_max_connections(D);
+    if (!ensure_spill(s, std::max(2 * N, C * N))) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
+    const TraceCtx tcs = trace_ctx(s);
+    const SceneArgs sa = scene_args(s);
+    BdptArgs b;
+    b.camV = fb->camV;
+    b.lightV = fb->lightV;
+    b.camCount = fb->camCount;
+    b.lightCount = fb->lightCount;
+    b.sampLight = fb->sampLight;
+    b.slots = fb->slots;
+    b.splat = fb->splat;
+    b.ownSlots = (int)C - D;
+    int* cnt = fb->bdptCounters;   // [d] ray queue of depth d, [32] connection queue
+    auto queue = [&](int d) {
+        BdptQueue q;
+        q.count = cnt + d;
+        q.o = fb->bqO[d & 1];
+        q.d = fb->bqD[d & 1];
+        q.t = fb->bqT[d & 1];
+        return q;
+    };
+    {
+        Timed t(ctx, K_BDPT_START, nullptr, (int64_t)f.numTiles * 64);
+        mcrt::launch_bdpt_start(sa, f, b, dCam, queue(0), st);
+    }
+    for (int d = 1; d <= D + 1; ++d) {
+        const BdptQueue qIn = queue(d - 1), qOut = queue(d);
+        {
+            Timed t(ctx, K_EXTEND, qIn.count, 0);
+            mcrt::launch_extend(tcs, qIn.count, qIn.o, qIn.d, fb->bHits, (int)(2 * N), st);
+        }
+        Timed t(ctx, K_BDPT_VERTEX, qIn.count, 0);
+        mcrt::launch_bdpt_vertex(sa, f, b, d, qIn, fb->bHits, qOut, (int)(2 * N), st);
+    }
+    BdptQueue cq;
+    cq.count = cnt + 32;
+    cq.o = fb->cO;
+    cq.d = fb->cD;
+    cq.t = fb->cL;
+    {
+        Timed t(ctx, K_BDPT_CONNECT, nullptr, (int64_t)f.numTiles * 64);
+        mcrt::launch_bdpt_connect(sa, f, b, dCam, cq, st);
+    }
+    {
+        Timed t(ctx, K_BDPT_VIS, cq.count, 0);
+        mcrt::launch_bdpt_vis(tcs, b, cq, (int)(C * N), st);
+    }
+    {
+        Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)f.numTiles * 64);
+        mcrt::launch_bdpt_gather(f, b, fb->radiance, st);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    fb->lastPixels = (int64_t)f.numTiles * 64;
+    return MCRT_OK;
+}
+
 MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cam,
                                        const mcrt_frame_params* p) {
     if (!s || !fb || !cam || !p) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
@@ -649,10 +786,15 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "unknown sampler");
     if (p->sampler == MCRT_SAMPLER_SOBOL && !s->hasSobol)
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "Sobol sampler requires the 1024x52 Sobol matrices in the scene");
+    if (p->integrator != MCRT_INTEGRATOR_PT && p->integrator != MCRT_INTEGRATOR_BDPT)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "unknown integrator");
+    if (p->integrator == MCRT_INTEGRATOR_BDPT && p->num_bands > 1)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "BDPT renders whole frames (num_bands must be 1)");
     FrameArgs f;
     std::string err;
     if (!frame_args(fb, p, f, err)) return fail(ctx, MCRT_ERROR_INVALID_ARG, err);
     hipSetDevice(ctx->device);
+    if (p->integrator == MCRT_INTEGRATOR_BDPT) return render_bdpt(s, fb, cam, p, f);
     hipStream_t st = ctx->stream;
     fb->lastMaxDepth = p->max_depth;
     fb->lastPixels = 0;
@@ -672,6 +814,7 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
     if (!ensure_spill(s, std::max((size_t)f.numTiles * 64, fb->N)))
         return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
     const TraceCtx tcs = trace_ctx(s);   // after ensure_spill (the buffer may have moved)
+    fb->lastIntegrator = MCRT_INTEGRATOR_PT;
     {
         Timed t(ctx, K_PRIMARY, nullptr, (int64_t)f.numTiles * 64);
         mcrt::launch_primary(tcs, f, dCam, fb->hitsP, st);
@@ -774,6 +917,15 @@ MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closes
     hipSetDevice(ctx->device);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     int c[64];
+    if (fb->lastIntegrator == MCRT_INTEGRATOR_BDPT) {   // closest: all subpath rays; any: connection rays
+        HIPCHK(ctx, hipMemcpy(c, fb->bdptCounters, sizeof(c), hipMemcpyDeviceToHost));
+        int64_t cl = 0;
+        for (int d = 0; d <= fb->lastMaxDepth; ++d) cl += c[d];
+        if (closest_rays) *closest_rays = cl;
+        if (any_rays) *any_rays = c[32];
+        if (shaded_paths) *shaded_paths = cl;
+        return MCRT_OK;
+    }
     HIPCHK(ctx, hipMemcpy(c, fb->counters, sizeof(c), hipMemcpyDeviceToHost));
     int64_t cl = fb->lastPixels, an = 0, sh = fb->lastPixels;
     for (int b = 0; b < fb->lastMaxDepth; ++b) {
@@ -808,6 +960,32 @@ MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which,
     for (int k = 0; k < 3; ++k)
         HIPCHK(ctx, hipMemcpy(static_cast<char*>(host_dst) + (size_t)k * 16 * max_records, src[k], 16 * (size_t)m,
                               hipMemcpyDeviceToHost));
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, void* host_dst, uint64_t bytes,
+                                                uint64_t* needed) {
+    if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
+    mcrt_ctx ctx = fb->ctx;
+    if (fb->bdptDepth <= 0) return fail(ctx, MCRT_ERROR_INVALID_ARG, "no BDPT frame rendered yet");
+    const size_t N = fb->N, D = (size_t)fb->bdptDepth, C = (size_t)bdpt_max_connections(fb->bdptDepth);
+    const void* src = nullptr;
+    size_t sz = 0;
+    switch (which) {
+    case 0: src = fb->camV; sz = 16 * N * 8 * (D + 2); break;
+    case 1: src = fb->lightV; sz = 16 * N * 8 * (D + 1); break;
+    case 2: src = fb->camCount; sz = 4 * N; break;
+    case 3: src = fb->lightCount; sz = 4 * N; break;
+    case 4: src = fb->slots; sz = 16 * N * (C - D); break;
+    case 5: src = fb->sampLight; sz = 16 * N * D; break;
+    case 6: src = fb->splat; sz = 16 * N; break;
+    default: return fail(ctx, MCRT_ERROR_INVALID_ARG, "which must be 0..6");
+    }
+    if (needed) *needed = sz;
+    if (!host_dst || bytes == 0) return MCRT_OK;
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpy(host_dst, src, std::min<size_t>(sz, bytes), hipMemcpyDeviceToHost));
     return MCRT_OK;
 }
 

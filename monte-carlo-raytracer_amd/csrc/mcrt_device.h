@@ -263,7 +263,12 @@ MCRT_DEV f3 sampleSpecularReflection_Dielectric(f3 R, float etaI, float etaT, f3
     float F = evaluateFresnelDielectric(evalCosTheta(*wi), etaI, etaT);
     return cl_div(F * R, evalAbsCosTheta(*wi));
 }
-MCRT_DEV f3 sampleSpecularTransmission(f3 T, float etaA, float etaB, f3 wo, f3* wi, float* pdf) {   // :288-307
+// TransportMode (bxdfs.cl:143-147): the path tracer is radiance transport; BDPT light
+// subpaths are importance transport.
+enum { TRANSPORT_MODE_RADIANCE = 0, TRANSPORT_MODE_IMPORTANCE = 1 };
+
+MCRT_DEV f3 sampleSpecularTransmission(f3 T, float etaA, float etaB, f3 wo, f3* wi, float* pdf,
+                                       int mode = TRANSPORT_MODE_RADIANCE) {   // :288-307
     bool isEntering = evalCosTheta(wo) > 0.0f;
     float etaI = isEntering ? etaA : etaB;
     float etaT = isEntering ? etaB : etaA;
@@ -271,7 +276,7 @@ MCRT_DEV f3 sampleSpecularTransmission(f3 T, float etaA, float etaB, f3 wo, f3* 
     if (!refract(wo, n, cl_div(etaI, etaT), wi)) return f3{0.0f, 0.0f, 0.0f};
     *pdf = 1.0f;
     f3 ft = T * (1.0f - evaluateFresnelDielectric(evalCosTheta(*wi), etaA, etaB));
-    ft *= cl_div((etaI * etaI), (etaT * etaT));   // TRANSPORT_MODE_RADIANCE
+    if (mode == TRANSPORT_MODE_RADIANCE) ft *= cl_div((etaI * etaI), (etaT * etaT));
     return cl_div(ft, evalAbsCosTheta(*wi));
 }
 MCRT_DEV float roughnessToAlpha(float roughness) {   // bxdfs.cl:385-390
@@ -311,7 +316,8 @@ MCRT_DEV f3 evaluateMicrofacetReflection(f3 R, f2 alpha, float etaI, float etaT,
 // the reference's compiler hoists `etaI / etaT` (etaI = 1) out of the eta selects, which drops
 // its 2.5-ulp accuracy metadata, in the NEE evaluation and in the sampling path alike
 // (the sampled, evaluated and pdf etas are one CSE'd value there).
-MCRT_DEV f3 evaluateMicrofacetTransmission(f3 T, f2 alpha, float etaI, float etaT, f3 wo, f3 wi) {   // :563-588
+MCRT_DEV f3 evaluateMicrofacetTransmission(f3 T, f2 alpha, float etaI, float etaT, f3 wo, f3 wi,
+                                          int mode = TRANSPORT_MODE_RADIANCE) {   // :563-588
     if (isSameHemisphere(wo, wi)) return f3{0.0f, 0.0f, 0.0f};
     float cosThetaO = evalCosTheta(wo);
     float cosThetaI = evalCosTheta(wi);
@@ -321,7 +327,7 @@ MCRT_DEV f3 evaluateMicrofacetTransmission(f3 T, f2 alpha, float etaI, float eta
     if (wh.z < 0) wh = -wh;   // bxdfs.cl:577 (z, not y: SURVEY App. A Q4)
     float F = evaluateFresnelDielectric(cl_dot(wo, wh), etaI, etaT);
     float sqrtDenom = cl_dot(wo, wh) + eta * cl_dot(wi, wh);
-    float factor = cr_div(1.0f, eta);   // TRANSPORT_MODE_RADIANCE
+    float factor = (mode == TRANSPORT_MODE_RADIANCE) ? cr_div(1.0f, eta) : 1.0f;
     return (f3{1.0f, 1.0f, 1.0f} - F) * T *
            fabsf(cl_div(computeTrowbridgeReitzDistribution(wh, alpha) * computeTrowbridgeReitzDistributionG(wo, wi, alpha) *
                             eta * eta * absDot(wi, wh) * absDot(wo, wh) * factor * factor,
@@ -372,12 +378,13 @@ MCRT_DEV f3 sampleMicrofacetReflection(f2 u, f3 R, f2 alpha, float etaI, float e
     *pdf = evalMicrofacetReflectionPdf(wo, *wi, wh, alpha);
     return evaluateMicrofacetReflection(R, alpha, etaI, etaT, wo, *wi);
 }
-MCRT_DEV f3 sampleMicrofacetTransmission(f2 u, f3 T, f2 alpha, float etaA, float etaB, f3 wo, f3* wi, float* pdf) {
+MCRT_DEV f3 sampleMicrofacetTransmission(f2 u, f3 T, f2 alpha, float etaA, float etaB, f3 wo, f3* wi, float* pdf,
+                                         int mode = TRANSPORT_MODE_RADIANCE) {
     f3 wh = sampleTrowbridgeReitzDistribution_wh(u, wo, alpha);   // :751-762
     float eta = evalCosTheta(wo) > 0.0f ? cr_div(etaA, etaB) : cr_div(etaB, etaA);
     if (!refract(wo, wh, eta, wi)) return f3{0.0f, 0.0f, 0.0f};
     *pdf = evalMicrofacetTransmissionPdf(wo, *wi, alpha, etaA, etaB);
-    return evaluateMicrofacetTransmission(T, alpha, etaA, etaB, wo, *wi);
+    return evaluateMicrofacetTransmission(T, alpha, etaA, etaB, wo, *wi, mode);
 }
 
 struct Frame {   // the RTInteraction fields the shading uses
@@ -403,14 +410,14 @@ struct Uber {   // RTUberMaterialProperties (materials.cl:67-74)
 };
 
 // bxdfs.cl:804-827
-MCRT_DEV f3 evaluateUberBSDF(const Uber& m, const Frame& si, f3 woWorld, f3 wiWorld) {
+MCRT_DEV f3 evaluateUberBSDF(const Uber& m, const Frame& si, f3 woWorld, f3 wiWorld, int mode = TRANSPORT_MODE_RADIANCE) {
     if (!isReflection(woWorld, wiWorld, si)) {
         bool isPerfectSpecularTransmission = m.Kt.w < 0.5f;
         if (isPerfectSpecularTransmission) return f3{0.0f, 0.0f, 0.0f};
         f3 wo = dirToShadingSpace(woWorld, si);
         f3 wi = dirToShadingSpace(wiWorld, si);
         f3 kt = m.Kt.xyz * m.opacity;
-        return evaluateMicrofacetTransmission(kt, m.roughness, 1.0f, m.eta, wo, wi);
+        return evaluateMicrofacetTransmission(kt, m.roughness, 1.0f, m.eta, wo, wi, mode);
     }
     f3 wo = dirToShadingSpace(woWorld, si);
     f3 wi = dirToShadingSpace(wiWorld, si);
@@ -419,8 +426,10 @@ MCRT_DEV f3 evaluateUberBSDF(const Uber& m, const Frame& si, f3 woWorld, f3 wiWo
     return evaluateMicrofacetReflection(ks, m.roughness, 1.0f, m.eta, wo, wi) + evaluateLambertianReflection(kd);
 }
 
-// bxdfs.cl:892-1053, type = BSDF_ALL, radiance transport; `wi` zero-initialised
-MCRT_DEV f3 sampleUberBSDF(const Uber& m, const Frame& si, f2 u, f3 woWorld, f3* wiWorld, float* pdf, int* sampledType) {
+// bxdfs.cl:892-1053, type = BSDF_ALL; `wi` zero-initialised.
+// numNonDeltaTypes (optional) counts the matching non-specular lobes (BDPT connectibility).
+MCRT_DEV f3 sampleUberBSDF(const Uber& m, const Frame& si, f2 u, f3 woWorld, f3* wiWorld, float* pdf, int* sampledType,
+                           int mode = TRANSPORT_MODE_RADIANCE, int* numNonDeltaTypes = nullptr) {
     f3 t = f3{1.0f, 1.0f, 1.0f} - m.opacity;
     int numBxDFs = 0;
     f3 kd = m.Kd * m.opacity;
@@ -434,6 +443,7 @@ MCRT_DEV f3 sampleUberBSDF(const Uber& m, const Frame& si, f2 u, f3 woWorld, f3*
     const bool hasT = isNotBlack(t), hasKd = isNotBlack(kd), hasKs = isNotBlack(ks), hasKr = isNotBlack(kr),
                hasKt = isNotBlack(kt);
     numBxDFs = (int)hasT + (int)hasKd + (int)hasKs + (int)hasKr + (int)hasKt;
+    if (numNonDeltaTypes) *numNonDeltaTypes = (int)hasKd + (int)hasKs + (int)(hasKt && !isPerfectSpecularTransmission);
     if (numBxDFs == 0) return f3{0.0f, 0.0f, 0.0f};
     int chosenBxDFIdx = min((int)floorf(u.x * numBxDFs), numBxDFs - 1);
     u.x = u.x * numBxDFs - chosenBxDFIdx;
@@ -442,14 +452,14 @@ MCRT_DEV f3 sampleUberBSDF(const Uber& m, const Frame& si, f2 u, f3 woWorld, f3*
     bool isSamplingSpecular = false;
     if (hasT) {
         if (chosenBxDFIdx-- == 0) {
-            f += sampleSpecularTransmission(t, 1.0f, 1.0f, wo, &wi, pdf);
+            f += sampleSpecularTransmission(t, 1.0f, 1.0f, wo, &wi, pdf, mode);
             *sampledType |= BSDF_SPEC_TRANS;
             isSamplingSpecular = true;
         }
     }
     if (isPerfectSpecularTransmission && hasKt) {
         if (chosenBxDFIdx-- == 0) {
-            f += sampleSpecularTransmission(kt, 1.0f, m.eta, wo, &wi, pdf);
+            f += sampleSpecularTransmission(kt, 1.0f, m.eta, wo, &wi, pdf, mode);
             *sampledType |= BSDF_SPEC_TRANS;
             isSamplingSpecular = true;
         }
@@ -463,7 +473,7 @@ MCRT_DEV f3 sampleUberBSDF(const Uber& m, const Frame& si, f2 u, f3 woWorld, f3*
     }
     if (hasKt) {   // bxdfs.cl:1004, independent of Kt.w
         if (chosenBxDFIdx-- == 0) {
-            f += sampleMicrofacetTransmission(u, kt, m.roughness, 1.0f, m.eta, wo, &wi, pdf);
+            f += sampleMicrofacetTransmission(u, kt, m.roughness, 1.0f, m.eta, wo, &wi, pdf, mode);
             *sampledType |= BSDF_MF_TRANS;
         }
     }
@@ -495,4 +505,38 @@ MCRT_DEV f3 sampleUberBSDF(const Uber& m, const Frame& si, f2 u, f3 woWorld, f3*
     *pdf = cl_div(*pdf, (float)numBxDFs);
     *wiWorld = dirFromShadingToWorld(wi, si);
     return f;
+}
+
+// bxdfs.cl:829-880 (evaluateUberBSDF_Pdf), type = BSDF_ALL
+MCRT_DEV float evaluateUberBSDF_Pdf(const Uber& m, const Frame& si, f3 woWorld, f3 wiWorld) {
+    f3 wo = dirToShadingSpace(woWorld, si);
+    f3 wi = dirToShadingSpace(wiWorld, si);
+    if (isNearZero(wo.y)) return 0.0f;
+    f3 t = f3{1.0f, 1.0f, 1.0f} - m.opacity;
+    int numBxDFs = 0;
+    f3 kd = m.Kd * m.opacity;
+    f3 ks = m.Ks * m.opacity;
+    f3 kt = m.Kt.xyz * m.opacity;
+    f3 kr = m.Kr * m.opacity;
+    float pdf = 0.0f;
+    if (isNotBlack(t)) ++numBxDFs;
+    if (isNotBlack(kr)) ++numBxDFs;
+    if (isNotBlack(kt)) {
+        if (m.Kt.w < 0.5f) {
+            ++numBxDFs;
+        } else {
+            pdf += evalMicrofacetTransmissionPdf(wo, wi, m.roughness, 1.0f, m.eta);
+            ++numBxDFs;
+        }
+    }
+    if (isNotBlack(kd)) {
+        pdf += evaluateLambertianReflectionPdf(wo, wi);
+        ++numBxDFs;
+    }
+    if (isNotBlack(ks)) {
+        pdf += evalMicrofacetReflectionPdf(wo, wi, cl_normalize(wo + wi), m.roughness);
+        ++numBxDFs;
+    }
+    if (numBxDFs > 1) pdf = cl_div(pdf, (float)numBxDFs);
+    return pdf;
 }

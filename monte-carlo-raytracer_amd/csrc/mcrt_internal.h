@@ -38,6 +38,22 @@ struct QueueArgs {
     float4 *eOout, *eDout, *eTout;
 };
 
+// BDPT per-frame state (mcrt_bdpt.hip header comment has the layout)
+struct BdptArgs {
+    float4* camV;        // (D+2) x 8 planes x N
+    float4* lightV;      // (D+1) x 8 planes x N
+    int* camCount;       // N
+    int* lightCount;     // N
+    float4* sampLight;   // D planes x N, persistent across frames
+    float4* slots;       // ownSlots planes x N
+    float4* splat;       // N
+    int ownSlots;        // strategies with t >= 2 = maxConnections - D
+};
+struct BdptQueue {
+    int* count;
+    float4 *o, *d, *t;
+};
+
 struct TraceCtx {
     const float4* nodes;   // 4 float4 per node (mcrt_bvh.cpp): internal = child boxes + indices, leaf = triangle
     uint32_t* spill;
@@ -61,6 +77,15 @@ void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int
 void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st);
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st);
+void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
+                       const BdptQueue& q, hipStream_t st);
+void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
+                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st);
+void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
+                         const BdptQueue& q, hipStream_t st);
+void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st);
+void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, hipStream_t st);
+void launch_bdpt_clear_splat(int n, float4* splat, hipStream_t st);
 }  // namespace mcrt
 
 // Host BVH builder (mcrt_bvh.cpp)

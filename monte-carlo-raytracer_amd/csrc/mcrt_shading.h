@@ -1,0 +1,288 @@
+// mcrt_shading.h -- surface interaction, textures, materials, light sampling and queue
+// helpers shared by the path-tracing (mcrt_kernels.hip) and BDPT (mcrt_bdpt.hip) kernels.
+#pragma once
+#include "mcrt_device.h"
+#include "mcrt_internal.h"
+
+// ---------------------------------------------------------------------------
+// pixel <-> band tile mapping (8x8 pixel tiles per wave; 8-row blocks dealt to bands)
+// ---------------------------------------------------------------------------
+MCRT_DEV bool tilePixel(const FrameArgs& f, int tile, int lane, int& x, int& y) {
+    const int tb = tile / f.tilesX, tx = tile - tb * f.tilesX;
+    const int bpb = f.bandRows >> 3;   // 8-row blocks per band
+    const int gb = (tb / bpb) * bpb * f.numBands + f.bandIndex * bpb + (tb % bpb);
+    x = tx * 8 + (lane & 7);
+    y = gb * 8 + (lane >> 3);
+    return x < (int)f.W && y < (int)f.H;
+}
+
+MCRT_DEV f3 cameraDir(const mcrt_camera& cam, int x, int y) {   // PathTracing.cl:13-27
+    const f2 r = f2{cl_div(1.0f, (float)cam.width), cl_div(1.0f, (float)cam.height)};
+    const f2 uv = f2{(float)x * r.x, (float)y * r.y};
+    return lerpDirection(ld3(cam.r00), ld3(cam.r10), ld3(cam.r11), ld3(cam.r01), uv.x, uv.y);
+}
+
+
+// ---------------------------------------------------------------------------
+// shading
+// ---------------------------------------------------------------------------
+// KRN/textures.cl:70-125 (readTexture2Df_linear: bilinear RGBA8, wrap modes)
+MCRT_DEV f4 readTex(const SceneArgs& s, int texId, f2 uv) {
+    const mcrt_texture_desc tex = s.textures[texId];
+    const int w = tex.width, h = tex.height;
+    // The reference's compiled kernel folds `-(1/w)` into `-1/w` and so loses the 2.5-ulp
+    // metadata: these two reciprocals are correctly rounded there (and here).
+    uv.x -= cr_div(1.0f, (float)w) * 0.5f;
+    uv.y -= cr_div(1.0f, (float)h) * 0.5f;
+    switch (tex.wrap) {
+    case 0: uv -= f2{floorf(uv.x), floorf(uv.y)}; break;
+    case 1:
+        if (uv.x > 1.0f || uv.x < 0.0f) uv.x = 1.0f - (uv.x - floorf(uv.x));
+        if (uv.y > 1.0f || uv.y < 0.0f) uv.y = 1.0f - (uv.y - floorf(uv.y));
+        break;
+    case 2: uv = f2{cl_clamp(uv.x, 0.0f, 1.0f), cl_clamp(uv.y, 0.0f, 1.0f)}; break;
+    case 3:
+        if (uv.x > 1.0f || uv.x < 0.0f || uv.y > 1.0f || uv.y < 0.0f) return f4{0.0f, 0.0f, 0.0f, 0.0f};
+        break;
+    }
+    int x0 = ((int)floorf(uv.x * w)) % w;
+    int y0 = ((int)floorf(uv.y * h)) % h;
+    int x1 = (x0 + 1) % w;
+    int y1 = (y0 + 1) % h;
+    x0 = min(max(x0, 0), w - 1);
+    y0 = min(max(y0, 0), h - 1);
+    x1 = min(max(x1, 0), w - 1);
+    y1 = min(max(y1, 0), h - 1);
+    const f2 t = f2{uv.x * w - floorf(uv.x * w), uv.y * h - floorf(uv.y * h)};
+    const uchar4* texD = reinterpret_cast<const uchar4*>(s.texData + tex.memOffset);
+    const uchar4 c00 = texD[x0 + y0 * w], c10 = texD[x1 + y0 * w], c01 = texD[x0 + y1 * w], c11 = texD[x1 + y1 * w];
+    const f4 v00 = f4{(float)c00.x, (float)c00.y, (float)c00.z, (float)c00.w};
+    const f4 v10 = f4{(float)c10.x, (float)c10.y, (float)c10.z, (float)c10.w};
+    const f4 v01 = f4{(float)c01.x, (float)c01.y, (float)c01.z, (float)c01.w};
+    const f4 v11 = f4{(float)c11.x, (float)c11.y, (float)c11.z, (float)c11.w};
+    // mix(a, b, t) = fma(b - a, t, a) per component (device-library mix)
+    const f4 m0 = f4{fmaf(v10.x - v00.x, t.x, v00.x), fmaf(v10.y - v00.y, t.x, v00.y), fmaf(v10.z - v00.z, t.x, v00.z),
+                     fmaf(v10.w - v00.w, t.x, v00.w)};
+    const f4 m1 = f4{fmaf(v11.x - v01.x, t.x, v01.x), fmaf(v11.y - v01.y, t.x, v01.y), fmaf(v11.z - v01.z, t.x, v01.z),
+                     fmaf(v11.w - v01.w, t.x, v01.w)};
+    const f4 m = f4{fmaf(m1.x - m0.x, t.y, m0.x), fmaf(m1.y - m0.y, t.y, m0.y), fmaf(m1.z - m0.z, t.y, m0.z),
+                    fmaf(m1.w - m0.w, t.y, m0.w)};
+    return m * (1.0f / 255.0f);
+}
+
+// KRN/materials.cl:76-91 (getUberMaterialProperties)
+MCRT_DEV Uber uberProps(const SceneArgs& s, const mcrt_material& material, f2 uv) {
+    Uber u;
+    const f4 Kd_opacity = material.uber_diffuseTexId != -1 ? readTex(s, material.uber_diffuseTexId, uv) : f4{1.0f, 1.0f, 1.0f, 1.0f};
+    u.Kd = Kd_opacity.xyz * ld3(material.uber_kd);
+    u.Ks = (material.uber_glossyTexId != -1 ? readTex(s, material.uber_glossyTexId, uv).xyz : splat3(1.0f)) * ld3(material.uber_ks);
+    u.Kr = (material.uber_specReflectionTexId != -1 ? readTex(s, material.uber_specReflectionTexId, uv).xyz : splat3(1.0f)) *
+           ld3(material.uber_kr);
+    u.Kt.xyz = (material.uber_transmissionTexId != -1 ? readTex(s, material.uber_transmissionTexId, uv).xyz : splat3(1.0f)) *
+               ld3(material.uber_kt);
+    u.Kt.w = material.uber_kt.w;
+    u.opacity = (material.uber_opacityTexId != -1 ? readTex(s, material.uber_opacityTexId, uv).xyz : splat3(1.0f)) *
+                ld3(material.uber_opacity) * Kd_opacity.w;
+    u.roughness = material.uber_roughnessTexId != -1 ? readTex(s, material.uber_roughnessTexId, uv).xy
+                                                      : f2{material.uber_roughness.x, material.uber_roughness.y};
+    u.eta = material.uber_iorTexId != -1 ? readTex(s, material.uber_iorTexId, uv).x : material.uber_eta;
+    u.roughness = f2{roughnessToAlpha(u.roughness.x), roughnessToAlpha(u.roughness.y)};
+    return u;
+}
+
+// Wave-aggregated queue append: returns this lane's slot (valid where pred).
+// Block-aggregated queue append: ONE global atomic per workgroup instead of one per wave.
+// Device-scope atomics on one address serialise across the 8 XCDs (~10+ ns each), which made
+// per-wave appends the bottleneck of the shading kernels.  Every thread of the block must call.
+template <int NW>
+MCRT_DEV int blockAppend(int* counter, bool pred, int* ldsWave /* NW + 1 ints */) {
+    const unsigned long long m = __ballot(pred);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) ldsWave[wv] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int sum = 0;
+        for (int w = 0; w < NW; ++w) {
+            const int c = ldsWave[w];
+            ldsWave[w] = sum;
+            sum += c;
+        }
+        ldsWave[NW] = sum ? atomicAdd(counter, sum) : 0;
+    }
+    __syncthreads();
+    const unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
+    const int prefix = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+    const int slot = ldsWave[NW] + ldsWave[wv] + prefix;
+    __syncthreads();   // ldsWave is reused by the next append
+    return slot;
+}
+
+// May be called under divergent control flow: only active lanes take part.
+MCRT_DEV int waveAppend(int* counter, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (m == 0) return 0;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, __popcll(m));
+    base = __shfl(base, leader);
+    const unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
+    const int prefix = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+    return base + prefix;
+}
+
+
+// KRN/geometry.cl:9-28
+MCRT_DEV void computeTrianglePartialDerivates(f2 uv0, f2 uv1, f2 uv2, f3 p0, f3 p1, f3 p2, f3 normal, f3* dpdu, f3* dpdv) {
+    f2 duv02 = uv0 - uv2;
+    f2 duv12 = uv1 - uv2;
+    f3 dp02 = p0 - p2;
+    f3 dp12 = p1 - p2;
+    float det = duv02.x * duv12.y - duv02.y * duv12.x;
+    if (isNotNearZero(det)) {
+        float invdet = cl_div(1.0f, det);
+        *dpdu = (duv12.y * dp02 - duv02.y * dp12) * invdet;
+        *dpdv = -(-duv12.x * dp02 + duv02.x * dp12) * invdet;
+    } else {
+        *dpdu = cl_normalize(computeOrthogonalVector(normal));
+        *dpdv = cl_normalize(cl_cross(normal, *dpdu));
+    }
+}
+
+// KRN/samplers.cl:259-269 (sampleDisk); returns the sampled point, *pdf = 1 / area
+MCRT_DEV f3 sampleDisk(f3 p, f3 n, float radius, f2 u, float* pdf) {
+    f2 p2d = concentricSampleDisc(u);
+    f3 t = computeOrthogonalVector(n);
+    f3 b = cl_normalize(cl_cross(n, t));
+    f3 itp = p + t * p2d.x * radius + b * p2d.y * radius;
+    *pdf = cl_div(1.0f, (PI_F * radius * radius));
+    return itp;
+}
+
+// KRN/samplers.cl:275-285 (sampleTriangle)
+MCRT_DEV f3 sampleTriangle(f3 p0, f3 p1, f3 p2, f2 u, f3* gn) {
+    const float su0 = cl_sqrt(u.x);
+    f2 b = f2{1.0f - su0, u.y * su0};
+    f3 itp = b.x * p0 + b.y * p1 + (1 - b.x - b.y) * p2;
+    f3 c = cl_cross(p1 - p0, p2 - p0);
+    *gn = cl_normalize(c);
+    return itp;
+}
+
+// computeSurfaceInteraction (geometry.cl:177-215)
+MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, int shapeIdx, int primIdx, f2 barycentrics) {
+    Frame si;
+    const mcrt_shape& shape = s.shapes[shapeIdx];
+    const uint32_t i0 = s.indices[shape.startIdx + 3 * primIdx];
+    const uint32_t i1 = s.indices[shape.startIdx + 3 * primIdx + 1];
+    const uint32_t i2 = s.indices[shape.startIdx + 3 * primIdx + 2];
+    const f3 p0 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i0]));
+    const f3 p1 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i1]));
+    const f3 p2 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i2]));
+    const float2 t0 = s.uvs[shape.startVertex + i0], t1 = s.uvs[shape.startVertex + i1], t2 = s.uvs[shape.startVertex + i2];
+    const f2 uv0 = f2{t0.x, t0.y}, uv1 = f2{t1.x, t1.y}, uv2 = f2{t2.x, t2.y};
+    const f3 n0 = transformVector3(shape.toWorldInverseTranspose, ld3(s.normals[shape.startVertex + i0]));
+    const f3 n1 = transformVector3(shape.toWorldInverseTranspose, ld3(s.normals[shape.startVertex + i1]));
+    const f3 n2 = transformVector3(shape.toWorldInverseTranspose, ld3(s.normals[shape.startVertex + i2]));
+    si.p = p0 * (1.0f - barycentrics.x - barycentrics.y) + p1 * barycentrics.x + p2 * barycentrics.y;
+    si.uv = uv0 * (1.0f - barycentrics.x - barycentrics.y) + uv1 * barycentrics.x + uv2 * barycentrics.y;
+    si.gn = cl_normalize(cl_cross(p0 - p2, p1 - p2));
+    si.sn = cl_normalize(n0 * (1.0f - barycentrics.x - barycentrics.y) + n1 * barycentrics.x + n2 * barycentrics.y);
+    f3 dpdu, dpdv;
+    computeTrianglePartialDerivates(uv0, uv1, uv2, p0, p1, p2, si.sn, &dpdu, &dpdv);
+    si.sdpdu = cl_normalize(dpdu - cl_dot(si.sn, dpdu) * si.sn);
+    si.sdpdv = cl_normalize(dpdv - cl_dot(si.sn, dpdv) * si.sn - cl_dot(si.sdpdu, dpdv) * si.sdpdu);
+    return si;
+}
+
+// applyNormalMapping_internal (materials.cl:11-19)
+MCRT_DEV void applyNormalMapping(const SceneArgs& s, int texId, Frame& si) {
+    const f3 nm = 2.0f * readTex(s, texId, si.uv).xyz - 1.0f;
+    si.sn = cl_normalize(si.sdpdu * nm.x + si.sdpdv * nm.y + si.sn * nm.z);
+    si.sdpdu = cl_normalize(cl_cross(si.sn, si.sdpdv));
+    si.sdpdv = cl_normalize(cl_cross(si.sdpdu, si.sn));
+}
+
+struct LightSample {
+    f3 Li, wi;
+    float pdf;
+    bool shadowSet;   // setRay() was called on the shadow ray
+    f3 shadowO;
+    float shadowT;
+    f3 lightPos, lightNormal;   // *lightPosition, *lightNormal (BDPT s = 1 strategy)
+};
+
+// sampleLightLi (lights.cl:45-146)
+MCRT_DEV LightSample sampleLightLi(const SceneArgs& s, const mcrt_light& light, const Frame& si, float traceErrorOffset,
+                                   f2 u) {
+    LightSample r;
+    r.Li = splat3(0.0f);
+    r.wi = splat3(0.0f);
+    r.pdf = 0.0f;
+    r.shadowSet = false;
+    r.shadowO = splat3(0.0f);
+    r.shadowT = 0.0f;
+    r.lightPos = splat3(0.0f);
+    r.lightNormal = splat3(0.0f);
+    if (light.type == MCRT_DIRECTIONAL_LIGHT) {
+        r.wi = -ld3(light.d);
+        r.lightPos = si.p + r.wi * light.radius * 2.0f;
+        r.pdf = 1.0f;
+        r.shadowO = si.p + si.gn * traceErrorOffset;
+        r.shadowT = 1000.0f;
+        r.shadowSet = true;
+        r.Li = ld3(light.intensity);
+    } else if (light.type == MCRT_POINT_LIGHT) {
+        f3 wi = ld3(light.p) - si.p;
+        float distSq = cl_dot(wi, wi);
+        if (!isNearZero(distSq)) {
+            float dist = cl_sqrt(distSq);
+            wi = cl_div(wi, dist);
+            r.wi = wi;
+            r.pdf = 1.0f;
+            r.lightPos = ld3(light.p);
+            r.shadowO = si.p + si.gn * traceErrorOffset;
+            r.shadowT = dist;
+            r.shadowSet = true;
+            r.Li = cl_div(ld3(light.intensity), distSq);
+        } else {
+            r.wi = wi;
+        }
+    } else if (light.type == MCRT_DISK_AREA_LIGHT || light.type == MCRT_TRIANGLE_MESH_AREA_LIGHT) {
+        f3 lp, lgn;
+        if (light.type == MCRT_DISK_AREA_LIGHT) {
+            lp = sampleDisk(ld3(light.p), ld3(light.d), light.radius, u, &r.pdf);
+            lgn = ld3(light.d);
+        } else {
+            const mcrt_shape shape = s.shapes[light.shapeId];
+            int triangleIdx = (int)((uint32_t)((int)floorf(u.x * shape.numTriangles)) % shape.numTriangles);
+            u.x = u.x * shape.numTriangles - triangleIdx;
+            const uint32_t i0 = s.indices[shape.startIdx + 3 * triangleIdx];
+            const uint32_t i1 = s.indices[shape.startIdx + 3 * triangleIdx + 1];
+            const uint32_t i2 = s.indices[shape.startIdx + 3 * triangleIdx + 2];
+            const f3 p0 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i0]));
+            const f3 p1 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i1]));
+            const f3 p2 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i2]));
+            lp = sampleTriangle(p0, p1, p2, u, &lgn);
+            r.pdf = cl_div(1.0f, light.area);
+        }
+        r.lightPos = lp;
+        r.lightNormal = lgn;
+        const f3 rayOrigin = si.p + si.gn * traceErrorOffset;
+        const f3 rayTarget = lp + lgn * RT_TRACE_OFFSET_F;
+        r.wi = light.type == MCRT_DISK_AREA_LIGHT ? cl_normalize(rayTarget - rayOrigin) : cl_normalize(lp - si.p);
+        const float distSq = distanceSquared(lp, si.p);
+        const float c = absDot(lgn, -r.wi);
+        if (isNearZero(c)) {
+            r.pdf = 0.0f;
+        } else {
+            r.pdf *= cl_div(distSq, c);
+            r.shadowO = rayOrigin;
+            r.shadowT = cl_distance(rayOrigin, rayTarget);
+            r.shadowSet = true;
+            r.Li = cl_dot(lgn, -r.wi) > 0.0f ? ld3(light.intensity) : splat3(0.0f);
+        }
+    }
+    return r;
+}
+

@@ -1,0 +1,157 @@
+// mcrt_traverse.h -- Bvh2 traversal shared by the path-tracing and BDPT kernels.
+// (Moved out of mcrt_kernels.hip; see there for the launch structure.)
+#pragma once
+#include "mcrt_device.h"
+#include "mcrt_internal.h"
+
+// ---------------------------------------------------------------------------
+// traversal
+// ---------------------------------------------------------------------------
+#define STACK_LDS 16
+
+struct TraceRay {
+    f3 o, d;
+    float tmax;
+    int mask;
+};
+
+// RR common.cl:220-232
+MCRT_DEV f3 safeInvDir(f3 d) {
+    const float ooeps = 1e-8f;
+    f3 inv;
+    inv.x = cl_div(1.0f, (fabsf(d.x) > ooeps ? d.x : copysignf(ooeps, d.x)));
+    inv.y = cl_div(1.0f, (fabsf(d.y) > ooeps ? d.y : copysignf(ooeps, d.y)));
+    inv.z = cl_div(1.0f, (fabsf(d.z) > ooeps ? d.z : copysignf(ooeps, d.z)));
+    return inv;
+}
+
+// RR common.cl:177-218; native_recip lowers to v_rcp_f32 on AMD.
+MCRT_DEV float triHit(const TraceRay& r, float4 A, float4 E1, float4 E2, float tmax) {
+    const f3 e1 = ld3(E1), e2 = ld3(E2);
+    const f3 s1 = cl_cross(r.d, e2);
+    const float denom = cl_dot(s1, e1);
+    if (denom == 0.f) return tmax;
+    const float invd = __builtin_amdgcn_rcpf(denom);
+    const f3 d = r.o - ld3(A);
+    const float b1 = cl_dot(d, s1) * invd;
+    const f3 s2 = cl_cross(d, e1);
+    const float b2 = cl_dot(r.d, s2) * invd;
+    const float temp = cl_dot(e2, s2) * invd;
+    if (b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || temp < 0.f || temp > tmax) return tmax;
+    return temp;
+}
+
+// Closest (ANY = false) or any (ANY = true) hit over the unified node array (mcrt_bvh.cpp):
+// the RadeonRays intersect_bvh2_lds.cl:107-178 loop -- one uniform 64-B fetch per step, an
+// internal node tests both child boxes (nearer child first, far child to the stack), a leaf
+// tests its triangle.  Returns the hit leaf's node index or -1; tHit = hit distance.
+// stk: this lane's LDS stack column ([entry][lane], conflict free); spill: global overflow.
+template <bool ANY>
+MCRT_DEV int traverse(const float4* __restrict__ nodes, const TraceRay& r, uint32_t* stk, uint32_t* spill, int spillCap,
+                      int* overflowFlag, float& tHit) {
+    // One flat loop with a single exit (node == DONE): stack entry 0 is a DONE sentinel, so a
+    // pop is one LDS read and no lane idles at a nested loop boundary waiting for the others.
+    constexpr int DONE = -1, POP = -2;
+    const f3 inv = safeInvDir(r.d);
+    const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
+    float t = r.tmax;
+    int hit = -1;
+    int node = 0;
+    stk[0] = (uint32_t)DONE;
+    int sp = 1, spillTop = 0;
+    while (node != DONE) {
+        const float4 n0 = nodes[4 * node + 0];
+        const float4 n1 = nodes[4 * node + 1];
+        const float4 n2 = nodes[4 * node + 2];
+        const int4 n3 = *reinterpret_cast<const int4*>(&nodes[4 * node + 3]);
+        // keep the whole 64-B record in one round trip: without this the compiler defers the
+        // two words only internal nodes use into a second, dependent load after the branch
+        asm volatile("" ::"v"(n1.w), "v"(n2.w));
+        int next;
+        if (n3.x >= 0) {
+            // slab tests of both children (RR intersect_bvh2_lds.cl:54-63, mad -> fma)
+            const float ax0 = fmaf(n0.x, inv.x, oxi.x), ax1 = fmaf(n0.y, inv.x, oxi.x);
+            const float ay0 = fmaf(n0.z, inv.y, oxi.y), ay1 = fmaf(n0.w, inv.y, oxi.y);
+            const float az0 = fmaf(n2.x, inv.z, oxi.z), az1 = fmaf(n2.y, inv.z, oxi.z);
+            const float bx0 = fmaf(n1.x, inv.x, oxi.x), bx1 = fmaf(n1.y, inv.x, oxi.x);
+            const float by0 = fmaf(n1.z, inv.y, oxi.y), by1 = fmaf(n1.w, inv.y, oxi.y);
+            const float bz0 = fmaf(n2.z, inv.z, oxi.z), bz1 = fmaf(n2.w, inv.z, oxi.z);
+            const float a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
+            const float a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), t);
+            const float b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
+            const float b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), t);
+            const bool h0 = a0 <= a1, h1 = b0 <= b1;
+            const bool c1first = h1 && (a0 > b0);   // intersect_bvh2_lds.cl:128-141
+            if (h0 && h1) {   // defer the far child
+                if (sp == STACK_LDS) {   // spill entries 1..15 (RR: intersect_bvh2_lds.cl:146-155)
+                    if (spillTop + STACK_LDS - 1 <= spillCap) {
+                        for (int k = 1; k < STACK_LDS; ++k) spill[(size_t)(spillTop + k - 1) * 64] = stk[k * 64];
+                        spillTop += STACK_LDS - 1;
+                    } else {
+                        *overflowFlag = 1;   // depth beyond capacity: drop (reported by the host)
+                    }
+                    sp = 1;
+                }
+                stk[sp * 64] = (uint32_t)(c1first ? n3.x : n3.y);
+                ++sp;
+            }
+            next = (h0 || h1) ? ((c1first || !h0) ? n3.y : n3.x) : POP;
+        } else {
+            next = POP;
+            if (r.mask != __float_as_int(n0.w)) {   // RR_RAY_MASK
+                const float th = triHit(r, n0, n1, n2, t);
+                if (th < t) {
+                    t = th;
+                    hit = node;
+                    if (ANY) next = DONE;
+                }
+            }
+        }
+        if (next == POP) {
+            --sp;
+            next = (int)stk[sp * 64];
+            if (next == DONE && spillTop > 0) {   // refill (intersect_bvh2_lds.cl:182-191)
+                spillTop -= STACK_LDS - 1;
+                for (int k = 1; k < STACK_LDS; ++k) stk[k * 64] = spill[(size_t)(spillTop + k - 1) * 64];
+                sp = STACK_LDS - 1;
+                next = (int)stk[sp * 64];
+            }
+        }
+        node = next;
+    }
+    tHit = t;
+    return hit;
+}
+
+// RR common.cl:249-277 (triangle_calculate_barycentrics)
+MCRT_DEV f2 triBary(f3 p, float4 A, float4 E1, float4 E2) {
+    const f3 e1 = ld3(E1), e2 = ld3(E2);
+    const f3 e = p - ld3(A);
+    const float d00 = cl_dot(e1, e1);
+    const float d01 = cl_dot(e1, e2);
+    const float d11 = cl_dot(e2, e2);
+    const float d20 = cl_dot(e, e1);
+    const float d21 = cl_dot(e, e2);
+    float denom = (d00 * d11 - d01 * d01);
+    if (denom == 0.f) return f2{0.f, 0.f};
+    const float invdenom = __builtin_amdgcn_rcpf(denom);
+    const float b1 = (d11 * d20 - d01 * d21) * invdenom;
+    const float b2 = (d00 * d21 - d01 * d20) * invdenom;
+    return f2{b1, b2};
+}
+
+// hit record of the closest-hit kernels: (u, v, t, triangle) -- intersect_bvh2_lds.cl:200-215
+MCRT_DEV float4 closestRecord(const float4* __restrict__ nodes, const TraceRay& r, int tri, float t) {
+    if (tri < 0) return make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+    const float4 A = nodes[4 * tri], E1 = nodes[4 * tri + 1], E2 = nodes[4 * tri + 2];
+    const f3 p = r.o + t * r.d;
+    const f2 uv = triBary(p, A, E1, E2);
+    return make_float4(uv.x, uv.y, t, __int_as_float(tri));
+}
+
+// Per-ray spill column: rays are grouped 64 to a wave; lane l of wave w owns entries
+// spill[(w * spillCap + k) * 64 + l], k < spillCap (coalesced across the wave).
+MCRT_DEV uint32_t* raySpill(const TraceCtx& c, int wave, int lane) {
+    return c.spill + (size_t)wave * 64 * c.spillCap + lane;
+}
+

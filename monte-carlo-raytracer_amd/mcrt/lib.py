@@ -5,6 +5,7 @@ the calls raise.  Device memory for ray queries comes from torch tensors on cuda
 (torch is plumbing here), everything else lives inside the library.
 """
 import ctypes
+import weakref
 import os
 
 import numpy as np
@@ -50,6 +51,7 @@ SIGNATURES = {
     "mcrt_framebuffer_copy_device": (_c.c_int, [_vp, _c.c_int, _vp]),
     "mcrt_framebuffer_set_accumulation": (_c.c_int, [_vp, _vp, _vp]),
     "mcrt_framebuffer_read_queue": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int32)]),
+    "mcrt_framebuffer_read_bdpt": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64)]),
     "mcrt_make_pinhole_camera": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _c.c_float, _c.c_float, _c.c_uint32,
                                             _c.c_uint32, _vp, _vp]),
 }
@@ -92,8 +94,16 @@ class Context:
         if profiling:
             self.set_profiling(True)
 
+    def _adopt(self, child):
+        """Scenes and frame buffers die with their context (closed first on ctx.close())."""
+        if not hasattr(self, "_children"):
+            self._children = weakref.WeakSet()
+        self._children.add(child)
+
     def close(self):
         if self.h:
+            for c in list(getattr(self, "_children", ())):
+                c.close()
             lib().mcrt_ctx_destroy(self.h)
             self.h = None
 
@@ -135,6 +145,7 @@ class DeviceScene:
         h = _vp()
         _check(lib().mcrt_scene_create(ctx.h, _c.byref(self._desc), _c.byref(h)), ctx.h)
         self.h = h
+        ctx._adopt(self)
         if build:
             self.build(cost, bins, sah)
 
@@ -180,10 +191,12 @@ class FrameBuffer:
         h = _vp()
         _check(lib().mcrt_framebuffer_create(ctx.h, width, height, _c.byref(h)), ctx.h)
         self.h = h
+        ctx._adopt(self)
 
     def render(self, dscene, cam, frame=0, max_depth=2, sampler=T.SAMPLER_RANDOM, rr=False, rr_start=3,
-               band_rows=8, num_bands=1, band_index=0):
-        p = T.FrameParams(frame, max_depth, sampler, 1 if rr else 0, rr_start, band_rows, num_bands, band_index)
+               band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_PT):
+        p = T.FrameParams(frame, max_depth, sampler, 1 if rr else 0, rr_start, band_rows, num_bands, band_index,
+                          integrator)
         cam = np.ascontiguousarray(cam)
         _check(lib().mcrt_render_frame(dscene.h, self.h, _p(cam), _c.byref(p)), self.ctx.h)
 
@@ -221,6 +234,18 @@ class FrameBuffer:
         out = np.zeros((3, max(n, 1), 4), np.float32)
         _check(lib().mcrt_framebuffer_read_queue(self.h, which, _p(out), max(n, 1), _c.byref(cnt)), self.ctx.h)
         return out[0, :n], out[1, :n], out[2, :n]
+
+    BDPT_READ = {"camera_vertices": 0, "light_vertices": 1, "camera_counts": 2, "light_counts": 3,
+                 "slots": 4, "sampled_light": 5, "splat": 6}
+
+    def read_bdpt(self, which):
+        """Raw bytes of a BDPT state array of the last BDPT frame (mcrt_framebuffer_read_bdpt)."""
+        need = _c.c_uint64()
+        idx = self.BDPT_READ[which]
+        _check(lib().mcrt_framebuffer_read_bdpt(self.h, idx, None, 0, _c.byref(need)), self.ctx.h)
+        out = np.zeros(need.value, np.uint8)
+        _check(lib().mcrt_framebuffer_read_bdpt(self.h, idx, _p(out), need.value, _c.byref(need)), self.ctx.h)
+        return out
 
     def close(self):
         if self.h:

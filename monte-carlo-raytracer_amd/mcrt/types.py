@@ -138,7 +138,12 @@ class FrameParams(ctypes.Structure):
         ("frame_index", ctypes.c_int32), ("max_depth", ctypes.c_int32), ("sampler", ctypes.c_int32),
         ("russian_roulette", ctypes.c_int32), ("rr_start_depth", ctypes.c_int32),
         ("band_rows", ctypes.c_int32), ("num_bands", ctypes.c_int32), ("band_index", ctypes.c_int32),
+        ("integrator", ctypes.c_int32),
     ]
+
+
+INTEGRATOR_PT = 0
+INTEGRATOR_BDPT = 1
 
 
 def ptr(a):

@@ -265,6 +265,15 @@ def ref_load_obj(path):
 # run through the ROCm OpenCL runtime by oracle/_ref/clref_runner.so.
 # --------------------------------------------------------------------------
 CLREF_LIB = os.path.join(HERE, "_ref", "clref_runner.so")
+
+# RTBDPTVertex (KRN/kernel_data.h:162-244): 240 B, RTInteraction at offset 16
+REF_VERTEX_DTYPE = np.dtype([
+    ("throughput", "<f4", 4), ("wo", "<f4", 4), ("p", "<f4", 4), ("uv", "<f4", 2), ("traceErrorOffset", "<f4"),
+    ("shapeIdx", "<i4"), ("gn", "<f4", 4), ("sn", "<f4", 4), ("dpdu", "<f4", 4), ("dpdv", "<f4", 4),
+    ("sdpdu", "<f4", 4), ("sdpdv", "<f4", 4), ("dpdx", "<f4", 4), ("dpdy", "<f4", 4), ("duvdx", "<f4", 2),
+    ("duvdy", "<f4", 2), ("type", "<i4"), ("flags", "<i4"), ("lightIdx", "<i4"), ("materialIdx", "<i4"),
+    ("pdfFwd", "<f4"), ("pdfRev", "<f4"), ("pdfPos", "<f4"), ("radianceBufferIdx", "<i4")])
+assert REF_VERTEX_DTYPE.itemsize == 240
 _clref = None
 
 
@@ -285,6 +294,9 @@ def clref(variant="ieee"):
         L.clref_accumulate.argtypes = [_vp, _c.c_int, _vp, _vp]
         L.clref_trace.argtypes = [_vp, _vp, _c.c_int, _vp, _c.c_int]
         L.clref_read.argtypes = [_vp, _c.c_int, _vp]
+        L.clref_bdpt_render.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _vp]
+        L.clref_bdpt_read.restype = _c.c_int64
+        L.clref_bdpt_read.argtypes = [_vp, _c.c_int, _vp]
         st = L.clref_init(os.path.join(HERE, "_ref").encode(), variant.encode())
         if st != 0:
             raise RuntimeError(f"clref_init({variant}) = {st}: {L.clref_error().decode()}")
@@ -334,6 +346,30 @@ class CLRefScene:
         st = self.L.clref_read(self.h, idx, _p(out))
         if st != 0:
             raise RuntimeError(f"clref_read {st}: {self.L.clref_error().decode()}")
+        return out
+
+    def render_bdpt(self, cam, frame=0, max_depth=2):
+        """One RTBDPTPass::update frame (BDPT.cl kernels); returns the W*H float4 radiance."""
+        W, H = int(cam["width"][0]), int(cam["height"][0])
+        out = np.zeros((H, W, 4), np.float32)
+        st = self.L.clref_bdpt_render(self.h, _p(cam), frame, max_depth, _p(out))
+        if st != 0:
+            raise RuntimeError(f"clref_bdpt_render {st}: {self.L.clref_error().decode()}")
+        return out
+
+    BDPT_READ = {"camera_vertices": 0, "light_vertices": 1, "camera_counts": 2, "light_counts": 3,
+                 "connection_rays": 4, "visibility": 5, "temp_radiance": 6, "sampled_light": 7, "sampled_camera": 8}
+
+    def read_bdpt(self, which):
+        """Raw bytes of a BDPT buffer of the last BDPT frame (RTBDPTPass's buffers)."""
+        idx = self.BDPT_READ[which]
+        n = self.L.clref_bdpt_read(self.h, idx, None)
+        if n < 0:
+            raise RuntimeError(f"clref_bdpt_read {n}: {self.L.clref_error().decode()}")
+        out = np.zeros(n, np.uint8)
+        st = self.L.clref_bdpt_read(self.h, idx, _p(out))
+        if st < 0:
+            raise RuntimeError(f"clref_bdpt_read {st}: {self.L.clref_error().decode()}")
         return out
 
     def trace(self, rays, any_hit=False, init=-7):

@@ -45,8 +45,9 @@ struct Runtime {
     cl_device_id dev = nullptr;
     cl_context ctx = nullptr;
     cl_command_queue q = nullptr;
-    cl_program pt = nullptr, rr = nullptr, recon = nullptr;
+    cl_program pt = nullptr, rr = nullptr, recon = nullptr, bdpt = nullptr;
     cl_kernel kGen = nullptr, kPT = nullptr, kShadow = nullptr, kIsect = nullptr, kOccl = nullptr, kRecon = nullptr;
+    cl_kernel kBStart = nullptr, kBSec = nullptr, kBPrep = nullptr, kBConn = nullptr, kBCopy = nullptr;
     std::string deviceName;
 } R;
 
@@ -91,6 +92,13 @@ struct Scene {
     cl_mem rays = nullptr, rayDiff = nullptr, isect = nullptr, shadowRays = nullptr, occl = nullptr, thr = nullptr,
            temp = nullptr, radiance = nullptr, stack = nullptr, count = nullptr, wsum = nullptr, wts = nullptr,
            filter = nullptr, image = nullptr;
+    // RTBDPTPass::createBuffers (RTBDPTPass.cpp:442-479)
+    int bW = 0, bH = 0, bD = 0;
+    cl_mem bFinal = nullptr, bRadiance = nullptr, camV = nullptr, lightV = nullptr, camRays = nullptr, camIsect = nullptr,
+           camThr = nullptr, camPdf = nullptr, camCnt = nullptr, lightRays = nullptr, lightIsect = nullptr,
+           lightThr = nullptr, lightPdf = nullptr, lightCnt = nullptr, connRays = nullptr, connVis = nullptr,
+           sampCamV = nullptr, sampLightV = nullptr, bTemp = nullptr, bStack = nullptr, bCount = nullptr,
+           bConnCount = nullptr;
 };
 
 template <class T>
@@ -193,6 +201,15 @@ __attribute__((visibility("default"))) int clref_init(const char* dir, const cha
     if (!ok(e, "kernel occluded_main")) return -6;
     R.kRecon = clCreateKernel(R.recon, "ReconstructionPass", &e);
     if (!ok(e, "kernel ReconstructionPass")) return -6;
+    R.bdpt = loadProgram(d + "/clref_bdpt_" + variant + ".hsaco");
+    if (!R.bdpt) return -5;
+    const char* bk[5] = {"GenerateStartVertices", "GenerateSecondaryVertices", "PrepareConnections", "ConnectVertices",
+                         "CopyBuffer"};
+    cl_kernel* bp[5] = {&R.kBStart, &R.kBSec, &R.kBPrep, &R.kBConn, &R.kBCopy};
+    for (int i = 0; i < 5; ++i) {
+        *bp[i] = clCreateKernel(R.bdpt, bk[i], &e);
+        if (!ok(e, bk[i])) return -6;
+    }
     return 0;
 }
 
@@ -383,6 +400,190 @@ __attribute__((visibility("default"))) int clref_probe(void* sp, const char* hsa
     clReleaseMemObject(bs);
     clReleaseMemObject(bo);
     return good ? 0 : -5;
+}
+
+// ---------------------------------------------------------------------------
+// BDPT (RTBDPTPass::update, RTBDPTPass.cpp:67-128; kernels BDPT.cl:240-932)
+// ---------------------------------------------------------------------------
+static const size_t kVertexBytes = 240;   // sizeof(RTBDPTVertex), kernel_data.h:220-244
+static int maxConnections(int D) { const int t = D + 2; return t * (t + 1) / 2 - 2; }   // RTBDPTPass.cpp:404-408
+
+static bool ensureBdptBuffers(Scene* s, int W, int H, int D) {
+    if (s->bW == W && s->bH == H && s->bD == D) return true;
+    cl_mem* old[] = {&s->bFinal, &s->bRadiance, &s->camV, &s->lightV, &s->camRays, &s->camIsect, &s->camThr,
+                     &s->camPdf, &s->camCnt, &s->lightRays, &s->lightIsect, &s->lightThr, &s->lightPdf, &s->lightCnt,
+                     &s->connRays, &s->connVis, &s->sampCamV, &s->sampLightV, &s->bTemp, &s->bStack, &s->bCount,
+                     &s->bConnCount};
+    for (auto* m : old)
+        if (*m) clReleaseMemObject(*m), *m = nullptr;
+    const size_t N = (size_t)W * H, C = (size_t)maxConnections(D);
+    // All buffers start zero-filled (buf()); the reference allocates them uninitialised.
+    s->bRadiance = buf(16 * N, nullptr);
+    s->bFinal = buf(12 * N, nullptr);
+    s->camV = buf(kVertexBytes * N * (D + 2), nullptr);
+    s->lightV = buf(kVertexBytes * N * (D + 1), nullptr);
+    s->camRays = buf(48 * N, nullptr);
+    s->camIsect = buf(32 * N, nullptr);
+    s->camThr = buf(16 * N, nullptr);
+    s->camPdf = buf(4 * N, nullptr);
+    s->camCnt = buf(4 * N, nullptr);
+    s->lightRays = buf(48 * N, nullptr);
+    s->lightIsect = buf(32 * N, nullptr);
+    s->lightThr = buf(16 * N, nullptr);
+    s->lightPdf = buf(4 * N, nullptr);
+    s->lightCnt = buf(4 * N, nullptr);
+    s->connRays = buf(48 * N * C, nullptr);
+    s->connVis = buf(4 * N * C, nullptr);
+    s->sampCamV = buf(kVertexBytes * N * D, nullptr);
+    s->sampLightV = buf(kVertexBytes * N * D, nullptr);
+    s->bTemp = buf(16 * N * C, nullptr);
+    s->bStack = buf(4 * N * C * 64, nullptr);
+    int n = (int)N, nc = (int)(N * C);
+    s->bCount = buf(4, &n);
+    s->bConnCount = buf(4, &nc);
+    s->bW = W;
+    s->bH = H;
+    s->bD = D;
+    return s->bStack && s->connRays && s->camV;
+}
+
+static bool launchRRn(cl_kernel k, Scene* s, cl_mem rays, cl_mem out, cl_mem count, int n) {
+    cl_int e = 0;
+    e |= arg(k, 0, s->nodes);
+    e |= arg(k, 1, rays);
+    e |= arg(k, 2, count);
+    e |= arg(k, 3, s->bStack);
+    e |= arg(k, 4, out);
+    if (!ok(e, "set RR args")) return false;
+    size_t gs = (size_t)(n + 63) / 64 * 64, ls = 64;
+    return ok(clEnqueueNDRangeKernel(R.q, k, 1, nullptr, &gs, &ls, 0, nullptr, nullptr), "launchRR") &&
+           ok(clFinish(R.q), "clFinish");
+}
+
+// One BDPT frame; radiance_out: W*H float4 (the pass's "RadianceBufferCL" after CopyBuffer).
+__attribute__((visibility("default"))) int clref_bdpt_render(void* sp, const mcrt_camera* cam, int frame, int maxDepth,
+                                                             float* radiance_out) {
+    Scene* s = (Scene*)sp;
+    const int W = (int)cam->width, H = (int)cam->height, N = W * H;
+    if (!ensureBdptBuffers(s, W, H, maxDepth)) return -1;
+    if (!ok(clEnqueueWriteBuffer(R.q, s->camera, CL_TRUE, 0, sizeof(mcrt_camera), cam, 0, nullptr, nullptr), "camera"))
+        return -1;
+    cl_int e = 0;
+    int a = 0;
+    // generateStartVertices (RTBDPTPass.cpp:130-221)
+    if (!setSceneArgs(R.kBStart, s, a)) return -2;
+    e |= arg(R.kBStart, a++, W);
+    e |= arg(R.kBStart, a++, H);
+    e |= arg(R.kBStart, a++, frame);
+    e |= arg(R.kBStart, a++, maxDepth);
+    e |= arg(R.kBStart, a++, s->camV);
+    e |= arg(R.kBStart, a++, s->camRays);
+    e |= arg(R.kBStart, a++, s->camThr);
+    e |= arg(R.kBStart, a++, s->camPdf);
+    e |= arg(R.kBStart, a++, s->camCnt);
+    e |= arg(R.kBStart, a++, s->lightV);
+    e |= arg(R.kBStart, a++, s->lightRays);
+    e |= arg(R.kBStart, a++, s->lightThr);
+    e |= arg(R.kBStart, a++, s->lightPdf);
+    e |= arg(R.kBStart, a++, s->lightCnt);
+    e |= arg(R.kBStart, a++, s->bFinal);
+    if (!ok(e, "start args") || !launch2D(R.kBStart, W, H)) return -2;
+    if (!launchRRn(R.kIsect, s, s->camRays, s->camIsect, s->bCount, N)) return -3;
+    if (!launchRRn(R.kIsect, s, s->lightRays, s->lightIsect, s->bCount, N)) return -3;
+    // generateSecondaryVertices (RTBDPTPass.cpp:223-307)
+    a = 0;
+    if (!setSceneArgs(R.kBSec, s, a)) return -4;
+    e = 0;
+    e |= arg(R.kBSec, a++, W);
+    e |= arg(R.kBSec, a++, H);
+    e |= arg(R.kBSec, a++, frame);
+    e |= arg(R.kBSec, a++, maxDepth);
+    const int pathArg = a;
+    if (!ok(e, "secondary args")) return -4;
+    for (int depth = 1; depth <= maxDepth + 1; ++depth) {
+        for (int isCam = 1; isCam >= 0; --isCam) {
+            if (!isCam && depth > maxDepth) continue;
+            a = pathArg;
+            e = 0;
+            e |= arg(R.kBSec, a++, isCam);
+            e |= arg(R.kBSec, a++, isCam ? s->camV : s->lightV);
+            e |= arg(R.kBSec, a++, isCam ? s->camRays : s->lightRays);
+            e |= arg(R.kBSec, a++, isCam ? s->camIsect : s->lightIsect);
+            e |= arg(R.kBSec, a++, isCam ? s->camThr : s->lightThr);
+            e |= arg(R.kBSec, a++, isCam ? s->camPdf : s->lightPdf);
+            e |= arg(R.kBSec, a++, isCam ? s->camCnt : s->lightCnt);
+            e |= arg(R.kBSec, a++, depth);
+            if (!ok(e, "secondary path args") || !launch2D(R.kBSec, W, H)) return -5;
+        }
+        if (!launchRRn(R.kIsect, s, s->camRays, s->camIsect, s->bCount, N)) return -6;
+        if (depth <= maxDepth && !launchRRn(R.kIsect, s, s->lightRays, s->lightIsect, s->bCount, N)) return -6;
+    }
+    // prepareVertexConnections (RTBDPTPass.cpp:309-359)
+    a = 0;
+    if (!setSceneArgs(R.kBPrep, s, a)) return -7;
+    e = 0;
+    e |= arg(R.kBPrep, a++, W);
+    e |= arg(R.kBPrep, a++, H);
+    e |= arg(R.kBPrep, a++, frame);
+    e |= arg(R.kBPrep, a++, maxDepth);
+    e |= arg(R.kBPrep, a++, s->camV);
+    e |= arg(R.kBPrep, a++, s->lightV);
+    e |= arg(R.kBPrep, a++, s->sampCamV);
+    e |= arg(R.kBPrep, a++, s->sampLightV);
+    e |= arg(R.kBPrep, a++, s->connRays);
+    e |= arg(R.kBPrep, a++, s->camCnt);
+    e |= arg(R.kBPrep, a++, s->lightCnt);
+    e |= arg(R.kBPrep, a++, s->bTemp);
+    if (!ok(e, "prepare args") || !launch2D(R.kBPrep, W, H)) return -7;
+    const int NC = N * maxConnections(maxDepth);
+    if (!launchRRn(R.kOccl, s, s->connRays, s->connVis, s->bConnCount, NC)) return -8;
+    // makeConnections (RTBDPTPass.cpp:361-402)
+    a = 0;
+    if (!setSceneArgs(R.kBConn, s, a)) return -9;
+    e = 0;
+    e |= arg(R.kBConn, a++, W);
+    e |= arg(R.kBConn, a++, H);
+    e |= arg(R.kBConn, a++, frame);
+    e |= arg(R.kBConn, a++, maxDepth);
+    e |= arg(R.kBConn, a++, s->camV);
+    e |= arg(R.kBConn, a++, s->lightV);
+    e |= arg(R.kBConn, a++, s->sampCamV);
+    e |= arg(R.kBConn, a++, s->sampLightV);
+    e |= arg(R.kBConn, a++, s->connRays);
+    e |= arg(R.kBConn, a++, s->connVis);
+    e |= arg(R.kBConn, a++, s->camCnt);
+    e |= arg(R.kBConn, a++, s->lightCnt);
+    e |= arg(R.kBConn, a++, s->bTemp);
+    e |= arg(R.kBConn, a++, s->bFinal);
+    if (!ok(e, "connect args") || !launch2D(R.kBConn, W, H)) return -9;
+    // copyRadianceBuffer (RTBDPTPass.cpp:410-440)
+    e = 0;
+    e |= arg(R.kBCopy, 0, W);
+    e |= arg(R.kBCopy, 1, H);
+    e |= arg(R.kBCopy, 2, s->bFinal);
+    e |= arg(R.kBCopy, 3, s->bRadiance);
+    if (!ok(e, "copy args") || !launch2D(R.kBCopy, W, H)) return -10;
+    if (radiance_out &&
+        !ok(clEnqueueReadBuffer(R.q, s->bRadiance, CL_TRUE, 0, 16ull * N, radiance_out, 0, nullptr, nullptr), "read"))
+        return -11;
+    return 0;
+}
+
+// Debug read-back of the last BDPT frame: which 0 camera vertices (240 B x (D+2) per pixel),
+// 1 light vertices (240 B x (D+1)), 2 camera vertex counts (int), 3 light vertex counts (int),
+// 4 connection rays (48 B x C per pixel), 5 connection visibilities (int x C), 6 temp radiance
+// (float4 x C), 7 sampled light vertices (240 B x D), 8 sampled camera vertices (240 B x D).
+__attribute__((visibility("default"))) int64_t clref_bdpt_read(void* sp, int which, void* out) {
+    Scene* s = (Scene*)sp;
+    const size_t N = (size_t)s->bW * s->bH, C = (size_t)maxConnections(s->bD), D = (size_t)s->bD;
+    cl_mem m[9] = {s->camV, s->lightV, s->camCnt, s->lightCnt, s->connRays, s->connVis, s->bTemp, s->sampLightV,
+                   s->sampCamV};
+    size_t sz[9] = {kVertexBytes * N * (D + 2), kVertexBytes * N * (D + 1), 4 * N, 4 * N, 48 * N * C, 4 * N * C,
+                    16 * N * C, kVertexBytes * N * D, kVertexBytes * N * D};
+    if (which < 0 || which > 8 || !m[which]) { g_err = "clref_bdpt_read: bad buffer"; return -1; }
+    if (!out) return (int64_t)sz[which];
+    return ok(clEnqueueReadBuffer(R.q, m[which], CL_TRUE, 0, sz[which], out, 0, nullptr, nullptr), "read")
+               ? (int64_t)sz[which] : -2;
 }
 
 }  // extern "C"

@@ -30,6 +30,35 @@ CASES = [  # (scene, W, H, frames, max_depth)
 ]
 
 
+BDPT_CASES = [  # (scene, W, H, frames rendered in order from fresh buffers, max_depth)
+    ("mixed", 96, 64, (0, 1, 2), 2),
+    ("cornell", 64, 64, (0, 1), 2),
+    ("mixed", 64, 48, (0, 1), 4),
+]
+
+
+def bdpt_key(case):
+    name, W, H, frames, D = case
+    return f"bdpt_{name}_{W}x{H}_d{D}"
+
+
+def bdpt_job(out_path, variant):
+    """RTBDPTPass frames (fresh buffers per case) + the last frame's vertex arrays and counts."""
+    res = {}
+    for case in BDPT_CASES:
+        name, W, H, frames, D = case
+        cs = po.CLRefScene(build_scene(name), variant)
+        cam = scene_camera(name, W, H)
+        key = bdpt_key(case)
+        for f in frames:
+            res[f"{key}_f{f}"] = cs.render_bdpt(cam, frame=f, max_depth=D)
+        for which in ("camera_vertices", "light_vertices", "camera_counts", "light_counts", "temp_radiance",
+                      "visibility", "connection_rays"):
+            res[f"{key}_{which}"] = cs.read_bdpt(which)
+    np.savez_compressed(out_path, **res)
+    print(f"clref bdpt job ({variant}): {len(res)} arrays -> {out_path}")
+
+
 def build_scene(name):
     if name == "mixed":
         return scenes.test_scene()
@@ -50,6 +79,9 @@ def sm_job(out_path, variant, W, H, tris):
 def main():
     out_path = sys.argv[1]
     variant = sys.argv[2] if len(sys.argv) > 2 else "ieee"
+    if len(sys.argv) > 3 and sys.argv[3] == "bdpt":
+        bdpt_job(out_path, variant)
+        return
     if len(sys.argv) > 3 and sys.argv[3] == "sm":
         sm_job(out_path, variant, int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6]))
         return

@@ -1,0 +1,134 @@
+"""GPU parity of the BDPT integrator (mcrt_bdpt.hip) against the REFERENCE's own BDPT.cl kernels
+run live on this MI355X through RTBDPTPass's launch sequence (tests/clref_job.py ... bdpt, in a
+child process).
+
+What is compared, per case (frames rendered in order from fresh buffers on both sides, since
+the reference's s = 1 strategy reads the previous frame's sampled light vertex, BDPT.cl:585):
+  * vertex counts of both subpaths: bit-exact;
+  * every defined field of every camera / light subpath vertex (position, normals, directions,
+    uv, throughput, pdfFwd, pdfRev, type, flags, light, material): bit-exact;
+  * the frame radiance: the reference sums each pixel's strategies with float atomics whose
+    order depends on thread scheduling (light-tracing splats from other pixels interleave,
+    BDPT.cl:888-907), so the image is compared with a relative tolerance of 4e-6 (a few ulp of
+    a sum of <= ~30 non-negative terms) and the bit-exact fraction is reported."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from clref_job import BDPT_CASES, bdpt_key, build_scene
+from mcrt import types as T
+from mcrt.camera import scene_camera
+from oracle import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+REL_TOL = 4e-6
+
+
+@pytest.fixture(scope="module")
+def clref_bdpt(tmp_path_factory):
+    if not po.clref_available():
+        pytest.skip("oracle/_ref/clref_runner.so not built")
+    out = str(tmp_path_factory.mktemp("clref") / "clref_bdpt.npz")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "clref_job.py"), out, "ieee", "bdpt"],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        pytest.fail("reference BDPT job failed:\n" + r.stdout + r.stderr)
+    return np.load(out, allow_pickle=False)
+
+
+def our_planes(raw, depths, N):
+    """(depths, 8, N, 4) float32 view of the product's vertex planes."""
+    return raw.view(np.float32).reshape(depths, 8, N, 4)
+
+
+def compare_vertices(ours, ref, counts, depths, N, label):
+    """Bit-exact comparison of the defined vertex fields; returns a list of mismatch messages."""
+    bad = []
+    f32 = lambda a: np.ascontiguousarray(a, np.float32).view(np.uint32)   # noqa: E731
+    for d in range(depths):
+        live = counts > d
+        if not live.any():
+            continue
+        o = ours[d]                         # (8, N, 4)
+        r = ref[:, d]                       # (N,) structured
+        typ = r["type"]
+        fields = {
+            "p": (o[0, :, :3], r["p"][:, :3]), "throughput": (o[6, :, :3], r["throughput"][:, :3]),
+            "pdfFwd": (o[1, :, 3], r["pdfFwd"]), "pdfRev": (o[2, :, 3], r["pdfRev"]),
+            "type": (o[7, :, 0].view(np.int32), typ), "flags": (o[7, :, 1].view(np.int32), r["flags"]),
+            "lightIdx": (o[7, :, 2].view(np.int32), r["lightIdx"]),
+        }
+        surf = {
+            "gn": (o[1, :, :3], r["gn"][:, :3]), "sn": (o[2, :, :3], r["sn"][:, :3]),
+            "wo": (o[3, :, :3], r["wo"][:, :3]), "sdpdu": (o[4, :, :3], r["sdpdu"][:, :3]),
+            "sdpdv": (o[5, :, :3], r["sdpdv"][:, :3]), "uv": (np.stack([o[4, :, 3], o[5, :, 3]], -1), r["uv"]),
+            "traceErrorOffset": (o[0, :, 3], r["traceErrorOffset"]),
+            "materialIdx": (o[7, :, 3].view(np.int32), r["materialIdx"]),
+        }
+        light = {"gn": (o[1, :, :3], r["gn"][:, :3]), "pdfPos": (o[3, :, 3], r["pdfPos"])}
+        for group, sel in ((fields, live), (surf, live & (typ == 2)), (light, live & (typ == 1))):
+            for name, (a, b) in group.items():
+                a, b = np.asarray(a)[sel], np.asarray(b)[sel]
+                if a.dtype == np.float32:
+                    ne = f32(a) != f32(b)
+                    ne &= ~(np.isnan(a) & np.isnan(b))
+                else:
+                    ne = a != b
+                if ne.ndim > 1:
+                    ne = ne.any(-1)
+                if ne.any():
+                    bad.append(f"{label} depth {d} {name}: {int(ne.sum())}/{int(sel.sum())} differ")
+    return bad
+
+
+@pytest.mark.parametrize("case", BDPT_CASES, ids=[bdpt_key(c) for c in BDPT_CASES])
+def test_bdpt_matches_reference(hip_ctx, clref_bdpt, case):
+    from mcrt import lib
+    name, W, H, frames, D = case
+    key = bdpt_key(case)
+    N = W * H
+    ds = lib.DeviceScene(hip_ctx, build_scene(name))
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    cam = scene_camera(name, W, H)
+    report = []
+    for f in frames:
+        fb.render(ds, cam, frame=f, max_depth=D, sampler=T.SAMPLER_RANDOM, integrator=T.INTEGRATOR_BDPT)
+        g = fb.read(0)[..., :3]
+        ref = clref_bdpt[f"{key}_f{f}"][..., :3]
+        exact = (g.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(g) & np.isnan(ref))
+        close = np.abs(g - ref) <= REL_TOL * (np.abs(g) + np.abs(ref)) + 1e-30
+        close |= exact
+        # pixels no light-tracing splat landed on: the reference's sum order is the own (t, s)
+        # order there, so they must be bit-exact
+        nosplat = (fb.read_bdpt("splat").view(np.float32).reshape(H, W, 4)[..., :3] == 0).all(-1)
+        ex_ns = exact.all(-1)[nosplat]
+        report.append(f"frame {f}: bit-exact {exact.mean():.5f} (no-splat pixels {ex_ns.mean():.5f} of "
+                      f"{int(nosplat.sum())}), within {REL_TOL:g} {close.mean():.5f}, mean {g.mean():.6f} vs {ref.mean():.6f}")
+        if not ex_ns.all():
+            report.append(f"frame {f}: {int((~ex_ns).sum())} no-splat pixels outside bit-exactness")
+        if not close.all():
+            report.append(f"frame {f}: {int((~close).sum())} pixels outside tolerance")
+    # state of the last frame: counts and vertices
+    cc = fb.read_bdpt("camera_counts").view(np.int32)
+    lc = fb.read_bdpt("light_counts").view(np.int32)
+    rcc = clref_bdpt[f"{key}_camera_counts"].view(np.int32)
+    rlc = clref_bdpt[f"{key}_light_counts"].view(np.int32)
+    bad = [r for r in report if "outside" in r]
+    if (cc != rcc).any():
+        bad.append(f"camera counts differ at {int((cc != rcc).sum())} pixels")
+    if (lc != rlc).any():
+        bad.append(f"light counts differ at {int((lc != rlc).sum())} pixels")
+    bad += compare_vertices(our_planes(fb.read_bdpt("camera_vertices"), D + 2, N),
+                           clref_bdpt[f"{key}_camera_vertices"].view(po.REF_VERTEX_DTYPE).reshape(N, D + 2),
+                           cc, D + 2, N, "camera")
+    bad += compare_vertices(our_planes(fb.read_bdpt("light_vertices"), D + 1, N),
+                            clref_bdpt[f"{key}_light_vertices"].view(po.REF_VERTEX_DTYPE).reshape(N, D + 1),
+                            lc, D + 1, N, "light")
+    print(key, report)
+    fb.close()
+    ds.close()
+    assert not bad, (bad, report)
