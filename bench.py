@@ -1,5 +1,8 @@
 """Benchmark: Mpaths/s of the MI355X path tracer on the San-Miguel proxy at 1920x1080
 (BASELINE.json metric), PT with maxDepth 2 (the reference default), random sampler.
+`--integrator bdpt` measures the BDPT integrator instead: one path =
+one camera + one light subpath with all their connections; N GPUs split frames (each rank
+renders whole frames f = rank + N*i, "scaling": "weak"), since light-tracing splats land anywhere.
 
 One step = one 1-spp frame of the whole image (mcrt_render_frame + mcrt_accumulate).
 N GPUs: one process per GPU (torch.distributed.run), the image is tile-split into 8-row bands
@@ -106,6 +109,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     args = ap.parse_args()
 
     import torch
@@ -141,11 +145,18 @@ def main():
         f"{info['nodes']} nodes, {info['bytes'] / 1e6:.0f} MB)")
     fb = lib.FrameBuffer(ctx, W, H)
     filt = T.make_filter(T.BOX)
-    band = dict(band_rows=args.band_rows, num_bands=world, band_index=rank)
+    bdpt = args.integrator == "bdpt"
+    if bdpt:   # frame split: whole frames per rank
+        band = dict(band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_BDPT)
+    else:
+        band = dict(band_rows=args.band_rows, num_bands=world, band_index=rank)
+    first = [True]
 
-    def step(frame):
+    def step(i):
+        frame = rank + world * i if bdpt else i
         fb.render(ds, cam, frame=frame, max_depth=D, **band)
-        fb.accumulate(filt, frame)
+        fb.accumulate(filt, 0 if first[0] else frame)   # 0: the first accumulation overwrites
+        first[0] = False
 
     for f in range(args.warmup):
         step(f)
@@ -187,24 +198,25 @@ def main():
     kstats = ctx.kernel_stats() if not args.no_kernel_timing else {}
     ctx.set_profiling(False)
 
-    paths = W * H * args.steps
+    paths = W * H * args.steps * (world if bdpt else 1)
     value = paths / elapsed / 1e6
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "scaling": "weak" if bdpt else "strong", "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic: deterministic {args.scene} ({scene.num_triangles} tris, seeded generator mcrt/scenes.py)",
-        "config": {"workload": f"{args.scene} {W}x{H}, unidirectional PT, maxDepth {D}, random sampler, "
-                               f"1 spp per step, box-filter accumulate", "width": W, "height": H,
+        "config": {"workload": f"{args.scene} {W}x{H}, {'BDPT' if bdpt else 'unidirectional PT'}, maxDepth {D}, "
+                               f"random sampler, 1 spp per step, box-filter accumulate", "width": W, "height": H,
                    "triangles": scene.num_triangles, "max_depth": D, "spp_per_step": 1,
-                   "parallelism": f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce"},
+                   "parallelism": (f"frame split x {world} + 1 RCCL reduce" if bdpt else
+                                   f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce")},
     }
     if rank == 0:
         rays = {"closest": fstats["closest_rays"] / (W * H / world), "any": fstats["any_rays"] / (W * H / world),
                 "shaded": fstats["shaded_paths"] / (W * H / world)}
         out["rays_per_path"] = {k: round(v, 4) for k, v in rays.items()}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not bdpt:
             cpu = cpu_baseline(scene, cam, W, H, D, args.cpu_seconds)
             st = cpu["_stats"]
             V = {"k_primary": st[1] / max(st[0], 1), "k_extend": st[3] / max(st[2], 1),
