@@ -104,7 +104,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--max-depth", type=int, default=2)
-    ap.add_argument("--scene", default="san_miguel_proxy", choices=["san_miguel_proxy", "dragon_proxy"])
+    ap.add_argument("--scene", default="san_miguel_proxy", choices=["san_miguel_proxy", "dragon_proxy", "sponza_proxy"])
+    ap.add_argument("--sampler", default="random", choices=["random", "sobol"])
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -131,8 +132,13 @@ def main():
     t0 = time.perf_counter()
     if args.scene == "san_miguel_proxy":
         scene = scenes.san_miguel_proxy(tris=args.tris)
+    elif args.scene == "sponza_proxy":
+        scene = scenes.sponza_proxy()
     else:
-        scene = scenes.dragon_proxy(tris=args.tris)
+        scene = scenes.dragon_proxy(tris=min(args.tris, 871_414))
+    sampler = T.SAMPLER_SOBOL if args.sampler == "sobol" else T.SAMPLER_RANDOM
+    if sampler == T.SAMPLER_SOBOL:   # g_SobolMatrices32 (sobol.h:34), committed as a data fixture
+        scene.sobol = np.load(os.path.join(ROOT, "tests", "golden", "sobol_1024x52.npy"))
     gen_s = time.perf_counter() - t0
     cam = scene_camera(args.scene, W, H)
     log(f"[bench] scene {scene.name}: {scene.num_triangles} tris, gen {gen_s:.1f}s")
@@ -154,7 +160,7 @@ def main():
 
     def step(i):
         frame = rank + world * i if bdpt else i
-        fb.render(ds, cam, frame=frame, max_depth=D, **band)
+        fb.render(ds, cam, frame=frame, max_depth=D, sampler=sampler, **band)
         fb.accumulate(filt, 0 if first[0] else frame)   # 0: the first accumulation overwrites
         first[0] = False
 
@@ -206,7 +212,7 @@ def main():
         "scaling": "weak" if bdpt else "strong", "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic: deterministic {args.scene} ({scene.num_triangles} tris, seeded generator mcrt/scenes.py)",
         "config": {"workload": f"{args.scene} {W}x{H}, {'BDPT' if bdpt else 'unidirectional PT'}, maxDepth {D}, "
-                               f"random sampler, 1 spp per step, box-filter accumulate", "width": W, "height": H,
+                               f"{args.sampler} sampler, 1 spp per step, box-filter accumulate", "width": W, "height": H,
                    "triangles": scene.num_triangles, "max_depth": D, "spp_per_step": 1,
                    "parallelism": (f"frame split x {world} + 1 RCCL reduce" if bdpt else
                                    f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce")},
@@ -216,7 +222,7 @@ def main():
                 "shaded": fstats["shaded_paths"] / (W * H / world)}
         out["rays_per_path"] = {k: round(v, 4) for k, v in rays.items()}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and not bdpt:
+        if world == 1 and not args.no_cpu_baseline and not bdpt and sampler == T.SAMPLER_RANDOM:
             cpu = cpu_baseline(scene, cam, W, H, D, args.cpu_seconds)
             st = cpu["_stats"]
             V = {"k_primary": st[1] / max(st[0], 1), "k_extend": st[3] / max(st[2], 1),

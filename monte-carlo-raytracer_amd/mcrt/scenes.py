@@ -610,10 +610,86 @@ def san_miguel_proxy(tris=10_000_000, seed=4, tex_size=512):
     return b.build()
 
 
+def sponza_proxy(tris=262_267, seed=3, tex_size=1024):
+    """Crytek-Sponza proxy (config 3): a long atrium with two storeys of
+    arcades (columns and beams), hanging drapes, 25 materials and 16 RGBA8 1024^2 textures
+    (the reference's Sponza textures are mip-mapped; its LOD path is disabled,
+    textures.cl:207, so only level 0 is read).  Sun (intensity 40) + a triangle-mesh area light."""
+    rng = np.random.default_rng(SEED_BASE + seed)
+    b = SceneBuilder("sponza_proxy")
+    gens = [
+        lambda: tex_bricks(tex_size), lambda: tex_checker(tex_size, (200, 190, 170), (150, 130, 110), tiles=32),
+        lambda: tex_noise(tex_size, rng, (190, 170, 140), 30), lambda: tex_noise(tex_size, rng, (150, 150, 140), 45),
+        lambda: tex_noise(tex_size, rng, (160, 40, 40), 30), lambda: tex_noise(tex_size, rng, (40, 80, 150), 30),
+        lambda: tex_noise(tex_size, rng, (60, 120, 50), 30), lambda: tex_normalmap(tex_size, rng),
+    ]
+    texs = [b.add_texture(gens[i % len(gens)]()) for i in range(16)]
+    mats = []
+    for i in range(25):
+        k = i % 5
+        kd = tuple(rng.uniform(0.4, 0.9, 3))
+        if k == 0:
+            mats.append(b.add_material(kd=kd, ks=(0, 0, 0), diffuseTexId=texs[i % 7]))
+        elif k == 1:
+            mats.append(b.add_material(kd=kd, ks=(0.08, 0.08, 0.08), diffuseTexId=texs[(i + 2) % 7],
+                                       normalMapId=texs[7 + (i % 2) * 8], roughness=0.35))
+        elif k == 2:
+            mats.append(b.add_material(kd=kd, ks=tuple(rng.uniform(0.05, 0.3, 3)), roughness=float(rng.uniform(0.1, 0.5)),
+                                       diffuseTexId=texs[8 + (i % 7)]))
+        elif k == 3:   # drapes: coloured cloth
+            mats.append(b.add_material(kd=kd, ks=(0, 0, 0), diffuseTexId=texs[4 + (i % 3)]))
+        else:
+            mats.append(b.add_material(kd=kd, ks=(0.04, 0.04, 0.04), diffuseTexId=texs[9 + (i % 6)]))
+    budget = int(tris)
+    L, Wd, H = 30.0, 12.0, 14.0
+    parts_fixed = 0
+    # floor, walls, upper walls of the nave
+    ng = max(2, int(math.sqrt(budget * 0.10 / 2)))
+    b.add_mesh(*grid((-L / 2, 0, -Wd / 2), (L, 0, 0), (0, 0, Wd), ng, ng // 2 + 1, uv_scale=10.0, flip=True), mats[1])
+    parts_fixed += 2 * ng * (ng // 2 + 1)
+    nw = max(2, int(math.sqrt(budget * 0.12 / 2 / 4)))
+    for z, fl in ((-Wd / 2 - 3, False), (Wd / 2 + 3, True)):
+        b.add_mesh(*grid((-L / 2, 0, z), (L, 0, 0), (0, H, 0), nw, nw, uv_scale=6.0, flip=fl), mats[0])
+    for x, fl in ((-L / 2, True), (L / 2, False)):
+        b.add_mesh(*grid((x, 0, -Wd / 2 - 3), (0, 0, Wd + 6), (0, H, 0), nw, nw, uv_scale=4.0, flip=fl), mats[5])
+    parts_fixed += 4 * 2 * nw * nw
+    # two storeys of arcades on both sides: columns + beams
+    ncol = 11
+    col_budget = int(budget * 0.45)
+    per_col = max(64, col_budget // (2 * 2 * ncol))
+    nseg = max(8, int(math.sqrt(per_col / 2)))
+    for storey, (y0, hgt, rad) in enumerate(((0.0, 5.0, 0.45), (6.0, 4.0, 0.3))):
+        for side in (-1, 1):
+            for i in range(ncol):
+                x = -L / 2 + 2.0 + i * (L - 4.0) / (ncol - 1)
+                b.add_mesh(*cylinder((x, y0, side * Wd / 2), rad, hgt, nseg, nseg), mats[(2 + storey * 3 + i) % 25])
+            b.add_mesh(*box((-L / 2, y0 + hgt, side * Wd / 2 - 0.6), (L / 2, y0 + hgt + 1.0, side * Wd / 2 + 0.6), 12),
+                       mats[10 + storey])
+    # drapes between the upper columns (displaced cloth)
+    used = parts_fixed + 2 * 2 * ncol * 2 * nseg * nseg + 4 * 6 * 2 * 144
+    nd = 2 * (ncol - 1)
+    dr = max(2, int(math.sqrt(max(budget - used, nd * 8) / nd / 2)))
+    for side in (-1, 1):
+        for i in range(ncol - 1):
+            x0 = -L / 2 + 2.0 + i * (L - 4.0) / (ncol - 1) + 0.4
+            w = (L - 4.0) / (ncol - 1) - 0.8
+            P, N, UV, T_ = grid((x0, 6.2, side * (Wd / 2 - 0.2)), (w, 0, 0), (0, 3.6, 0), dr, dr, flip=side > 0)
+            ph = rng.uniform(0, 2 * np.pi)
+            P = P.copy()
+            P[:, 2] += side * 0.15 * np.sin(P[:, 0] * 6.0 + ph) * (1.0 - (P[:, 1] - 6.2) / 3.6)
+            b.add_mesh(P, N, UV, T_, mats[3 + 5 * (i % 4)])
+    lm = b.add_material(kd=(0.8, 0.8, 0.8), ks=(0, 0, 0))
+    ls = b.add_mesh(*grid((-2, H - 0.3, -1.5), (4, 0, 0), (0, 0, 3), 1, 1, flip=True), lm)
+    b.add_directional_light(euler_forward(70.0, 20.0), (40.0, 40.0, 40.0))
+    b.add_mesh_light(ls, (17.0, 12.0, 4.0))
+    return b.build()
+
+
 CAMERAS = {
     # name: (pos, look-at, fov_y) -- perspective 45 deg, near 0.3 (PathTracingApp.cpp:387)
     "cornell": ((0.0, 1.0, 3.4), (0.0, 1.0, 0.0), 45.0),
     "mixed": ((0.0, 3.0, -9.0), (0.0, 1.0, 0.5), 45.0),
     "dragon_proxy": ((-3.3, 3.2, -4.5), (0.0, 1.4, 0.0), 45.0),
     "san_miguel_proxy": ((8.2, 2.56, -6.6), (-2.0, 2.8, 3.0), 45.0),
+    "sponza_proxy": ((12.0, 3.0, 0.5), (-4.0, 4.5, -0.5), 45.0),
 }

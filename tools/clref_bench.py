@@ -1,5 +1,9 @@
-"""Times the REFERENCE's OpenCL pipeline (oracle/_ref, GPU box) on the bench workload, for a
-per-kernel comparison under rocprofv3.  usage: python tools/clref_bench.py [variant] [frames] [pt|bdpt]"""
+"""Times the REFERENCE's OpenCL pipeline (oracle/_ref, GPU box) on a bench workload, for a
+per-kernel comparison under rocprofv3.
+
+usage: python tools/clref_bench.py [--variant fast|ieee] [--frames K] [--integrator pt|bdpt]
+                                   [--scene san_miguel_proxy|dragon_proxy|sponza_proxy] [--width W --height H]"""
+import argparse
 import os
 import sys
 import time
@@ -10,22 +14,30 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", default="fast")
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
+    ap.add_argument("--scene", default="san_miguel_proxy")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--max-depth", type=int, default=2)
+    a = ap.parse_args()
     from mcrt import scenes
     from mcrt.camera import scene_camera
     from oracle import pyoracle as po
-    variant = sys.argv[1] if len(sys.argv) > 1 else "fast"
-    frames = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    integ = sys.argv[3] if len(sys.argv) > 3 else "pt"
-    sc = scenes.san_miguel_proxy()
-    cs = po.CLRefScene(sc, variant)
-    cam = scene_camera("san_miguel_proxy", 1920, 1080)
-    render = cs.render_bdpt if integ == "bdpt" else cs.render
-    render(cam, frame=0, max_depth=2)
+    sc = getattr(scenes, a.scene)()
+    cs = po.CLRefScene(sc, a.variant)
+    W, H = a.width, a.height
+    cam = scene_camera(a.scene, W, H)
+    render = cs.render_bdpt if a.integrator == "bdpt" else cs.render
+    render(cam, frame=0, max_depth=a.max_depth)
     t0 = time.perf_counter()
-    for f in range(frames):
-        render(cam, frame=f, max_depth=2)
-    dt = (time.perf_counter() - t0) / frames
-    print(f"reference OpenCL {integ} ({variant}) {dt * 1e3:.3f} ms/frame, {1920 * 1080 / dt / 1e6:.1f} Mpaths/s")
+    for f in range(a.frames):
+        render(cam, frame=f, max_depth=a.max_depth)
+    dt = (time.perf_counter() - t0) / a.frames
+    print(f"reference OpenCL {a.integrator} ({a.variant}) {a.scene} {W}x{H} D={a.max_depth}: "
+          f"{dt * 1e3:.3f} ms/frame, {W * H / dt / 1e6:.1f} Mpaths/s")
 
 
 if __name__ == "__main__":
