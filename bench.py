@@ -171,6 +171,7 @@ def main():
     step(args.warmup)
     ctx.sync()
     fstats = fb.stats()
+    qcounts = fb.queue_counts() if not bdpt else None
     frame0 = args.warmup + 1
 
     if not args.no_kernel_timing:
@@ -254,14 +255,26 @@ def main():
             out["kernels"] = {k: {"avg_ms": round(v["ms"] / max(v["launches"], 1), 4), "launches": v["launches"],
                                   "items_per_launch": round(v["items"] / max(v["launches"], 1), 1)}
                               for k, v in kstats.items()}
-            if V is not None and dom in V:
+            alg = None
+            if V is not None and dom == "k_shadow_extend":
+                # one launch = the extension rays for bounce 1 + the shadow rays of bounce 0
+                alg = (qcounts[1][0] * per_query_bytes("k_extend", V["k_extend"])
+                       + qcounts[0][0] * per_query_bytes("k_shadow", V["k_shadow"]))
+            elif V is not None and dom in V:
                 alg = items_per_launch * per_query_bytes(dom, V[dom])
+            if alg is not None:
                 achieved = alg / (avg_ms * 1e-3) / 1e9
                 tr = pmc_traffic(dom)
                 out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                                    "traffic": tr, "alg_bytes_per_launch": round(alg),
                                    "avg_launch_ms": round(avg_ms, 4)}
+                try:   # attainable HBM bandwidth of an in-repo stream copy
+                    att = ctx.stream_copy_gbps(2 << 30, 5)
+                    out["roofline"]["attainable"] = round(att, 1)
+                    out["roofline"]["frac_of_attainable"] = round(achieved / att, 4)
+                except Exception as e:   # noqa: BLE001 -- reported, not fatal
+                    log(f"[bench] stream copy failed: {e}")
         print(json.dumps(out), flush=True)
     fb.close()
     ds.close()

@@ -240,6 +240,10 @@ MCRT_API mcrt_status mcrt_ctx_kernel_stats(mcrt_ctx ctx, int max, const char** n
                                            double* total_ms, int64_t* launches,
                                            int64_t* items, int* count);
 MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx);
+/* Attainable HBM bandwidth: a float4 stream-copy kernel over `bytes` (>= 1 GiB recommended,
+ * well above the 256 MB Infinity Cache), best of `iters` launches; *gbps = (read + write)
+ * bytes / time.  The roofline's "attainable" figure next to the 8 TB/s spec peak. */
+MCRT_API mcrt_status mcrt_ctx_stream_copy(mcrt_ctx ctx, uint64_t bytes, int iters, double* gbps);
 
 /* ------------------------------------------------------------------------ */
 /* Scene (replaces RTScene upload + RadeonRays CreateMesh/AttachShape/SetId/
@@ -307,6 +311,9 @@ MCRT_API mcrt_status mcrt_framebuffer_set_accumulation(mcrt_framebuffer fb, cons
 /* Per-frame path statistics of the last render (paths, closest rays, any rays, ...). */
 MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closest_rays, int64_t* any_rays,
                                             int64_t* shaded_paths);
+/* Queue sizes of the last PT render, per bounce b < max: shadow[b] = shadow rays queued by
+ * bounce b's shading, extension[b] = extension rays queued for bounce b+1. */
+MCRT_API mcrt_status mcrt_framebuffer_queue_counts(mcrt_framebuffer fb, int32_t* shadow, int32_t* extension, int max);
 /* Host copy of a ray queue of the last render (the state the reference keeps in its
  * per-pixel trace_shadowRays / trace_rays / throughput buffers):
  *   which 0: shadow queue of the last bounce    -- origin.xyz|tmax, dir.xyz|pixel(int bits), throughput*L

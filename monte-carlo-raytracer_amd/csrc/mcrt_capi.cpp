@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -27,11 +28,12 @@ thread_local std::string g_lastError;
 
 enum KernelId {
     K_PRIMARY, K_SHADE0, K_SHADEN, K_SHADOW, K_EXTEND, K_ACCUM, K_TRACE_CLOSEST, K_TRACE_ANY,
-    K_BDPT_START, K_BDPT_VERTEX, K_BDPT_CONNECT, K_BDPT_VIS, K_BDPT_GATHER, K_COUNT
+    K_BDPT_START, K_BDPT_VERTEX, K_BDPT_CONNECT, K_BDPT_VIS, K_BDPT_GATHER, K_SHADOW_EXTEND, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {"k_primary",    "k_shade0",      "k_shadeN",       "k_shadow",   "k_extend",
                                      "k_accumulate", "k_trace_closest", "k_trace_any",  "k_bdpt_start",
-                                     "k_bdpt_vertex", "k_bdpt_connect", "k_bdpt_vis",   "k_bdpt_gather"};
+                                     "k_bdpt_vertex", "k_bdpt_connect", "k_bdpt_vis",   "k_bdpt_gather",
+                                     "k_shadow_extend"};
 
 }  // namespace
 
@@ -41,6 +43,7 @@ struct mcrt_ctx_s {
     hipStream_t stream = nullptr;
     int numCUs = 256;
     bool profiling = false;
+    bool fuseShadowExtend = true;   // MCRT_NO_FUSE=1 launches k_shadow and k_extend separately (A/B)
     std::string error;
     struct Pending {
         int kernel;
@@ -280,6 +283,7 @@ MCRT_API mcrt_status mcrt_ctx_create(int device, mcrt_ctx* out) {
     if (hipSetDevice(device) != hipSuccess) { delete c; return fail(nullptr, MCRT_ERROR_DEVICE, "hipSetDevice failed"); }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
+    if (const char* nf = std::getenv("MCRT_NO_FUSE")) c->fuseShadowExtend = nf[0] != '1';
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(nullptr, MCRT_ERROR_DEVICE, "hipStreamCreate failed");
@@ -332,6 +336,36 @@ MCRT_API mcrt_status mcrt_ctx_kernel_stats(mcrt_ctx ctx, int max, const char** n
         ++k;
     }
     if (count) *count = k;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_ctx_stream_copy(mcrt_ctx ctx, uint64_t bytes, int iters, double* gbps) {
+    if (!ctx || !gbps || bytes < 4096 || iters < 1) return fail(ctx, MCRT_ERROR_INVALID_ARG, "bad stream-copy args");
+    hipSetDevice(ctx->device);
+    const size_t n4 = (size_t)(bytes / 2 / 16);   // half the bytes read, half written
+    float4 *a = nullptr, *b = nullptr;
+    HIPCHK(ctx, hipMalloc(&a, n4 * 16));
+    if (hipMalloc(&b, n4 * 16) != hipSuccess) { hipFree(a); return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "stream copy"); }
+    hipMemsetAsync(a, 0, n4 * 16, ctx->stream);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    float best = 1e30f;
+    for (int i = 0; i < iters + 1; ++i) {
+        hipEventRecord(e0, ctx->stream);
+        mcrt::launch_stream_copy(a, b, n4, ctx->numCUs, ctx->stream);
+        hipEventRecord(e1, ctx->stream);
+        hipEventSynchronize(e1);
+        float ms = 0.0f;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (i > 0 && ms < best) best = ms;   // launch 0 warms up
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipFree(a);
+    hipFree(b);
+    HIPCHK(ctx, hipGetLastError());
+    *gbps = (double)(2 * n4 * 16) / (best * 1e-3) / 1e9;
     return MCRT_OK;
 }
 
@@ -811,7 +845,7 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
         HIPCHK(ctx, hipMemsetAsync(fb->radiance, 0, 16 * fb->N, st));
         return MCRT_OK;
     }
-    if (!ensure_spill(s, std::max((size_t)f.numTiles * 64, fb->N)))
+    if (!ensure_spill(s, std::max((size_t)f.numTiles * 64, 2 * fb->N + 64)))
         return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
     const TraceCtx tcs = trace_ctx(s);   // after ensure_spill (the buffer may have moved)
     fb->lastIntegrator = MCRT_INTEGRATOR_PT;
@@ -829,7 +863,7 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
             Timed t(ctx, K_SHADE0, nullptr, (int64_t)f.numTiles * 64);
             mcrt::launch_shade0(sa, f, dCam, fb->hitsP, fb->radiance, q, st);
         } else {
-            {
+            if (!ctx->fuseShadowExtend) {
                 Timed t(ctx, K_EXTEND, extCnt + b - 1, 0);
                 mcrt::launch_extend(tcs, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1], fb->hitsE,
                                     (int)fb->N, st);
@@ -838,7 +872,12 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
             mcrt::launch_shadeN(sa, f, b, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1],
                                 fb->eT[(b - 1) & 1], fb->hitsE, fb->radiance, q, (int)fb->N, st);
         }
-        {
+        if (ctx->fuseShadowExtend && b + 1 < p->max_depth) {
+            // shadow rays of bounce b + extension rays for bounce b+1 (both from this shading pass)
+            Timed t(ctx, K_SHADOW_EXTEND, nullptr, 0);
+            mcrt::launch_shadow_extend(tcs, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b, fb->sO,
+                                       fb->sD, fb->sL, fb->radiance, (int)fb->N, (int)fb->N, st);
+        } else {
             Timed t(ctx, K_SHADOW, shadowCnt + b, 0);
             mcrt::launch_shadow(tcs, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, (int)fb->N, st);
         }
@@ -935,6 +974,21 @@ MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closes
     if (closest_rays) *closest_rays = cl;
     if (any_rays) *any_rays = an;
     if (shaded_paths) *shaded_paths = sh;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_queue_counts(mcrt_framebuffer fb, int32_t* shadow, int32_t* extension, int max) {
+    if (!fb || max < 0) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    int c[64];
+    HIPCHK(ctx, hipMemcpy(c, fb->counters, sizeof(c), hipMemcpyDeviceToHost));
+    for (int b = 0; b < max && b < 32; ++b) {
+        const bool live = b < fb->lastMaxDepth && fb->lastIntegrator == MCRT_INTEGRATOR_PT;
+        if (shadow) shadow[b] = live ? c[b] : 0;
+        if (extension) extension[b] = live && b + 1 < fb->lastMaxDepth ? c[32 + b] : 0;
+    }
     return MCRT_OK;
 }
 

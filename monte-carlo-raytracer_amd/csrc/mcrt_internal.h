@@ -69,6 +69,9 @@ void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const 
                    hipStream_t st);
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st);
+void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
+                          const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
+                          float4* radiance, int maxExt, int maxShadow, hipStream_t st);
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st);
 void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,
@@ -77,6 +80,7 @@ void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int
 void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st);
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st);
+void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st);
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& q, hipStream_t st);
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,

@@ -138,6 +138,52 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     radiance[pix] = acc;
 }
 
+// Shadow rays of bounce b and extension rays of bounce b+1 in ONE launch: both only depend on
+// the shading of bounce b.  Extension workgroups come first (their rays are the longer ones),
+// shadow workgroups fill the extension launch's divergent tail instead of waiting for it.
+__global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __restrict__ extCount,
+                                                      const float4* __restrict__ qO, const float4* __restrict__ qD,
+                                                      float4* __restrict__ hitOut, const int* __restrict__ shadowCount,
+                                                      const float4* __restrict__ sO, const float4* __restrict__ sD,
+                                                      const float4* __restrict__ sL, float4* __restrict__ radiance) {
+    __shared__ uint32_t lds[STACK_LDS * 64];
+    const int ne = *extCount;
+    const int eb = (ne + 63) >> 6;
+    const int lane = threadIdx.x;
+    if ((int)blockIdx.x < eb) {
+        const int i = blockIdx.x * 64 + lane;
+        if (i >= ne) return;
+        const float4 o = qO[i], d = qD[i];
+        TraceRay r;
+        r.o = ld3(o);
+        r.d = ld3(d);
+        r.tmax = RT_MAX_TRACE_F;
+        r.mask = -1;
+        float t;
+        const int tri = traverse<false>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+        hitOut[i] = closestRecord(c.nodes, r, tri, t);
+    } else {
+        const int ns = *shadowCount;
+        const int i = ((int)blockIdx.x - eb) * 64 + lane;
+        if (i >= ns) return;
+        const float4 o = sO[i], d = sD[i], L = sL[i];
+        TraceRay r;
+        r.o = ld3(o);
+        r.d = ld3(d);
+        r.tmax = o.w;
+        r.mask = -1;
+        float t;
+        const int tri = traverse<true>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+        const float V = tri >= 0 ? 0.0f : 1.0f;
+        const int pix = __float_as_int(d.w);
+        float4 acc = radiance[pix];
+        acc.x += L.x * V;
+        acc.y += L.y * V;
+        acc.z += L.z * V;
+        radiance[pix] = acc;
+    }
+}
+
 // PathTracing kernel body (PathTracing.cl:52-184) for one path.
 // Returns the radiance term added at this vertex by emission (or by a NaN NEE term
 // with no shadow ray).  NEE terms go to the shadow queue.
@@ -332,6 +378,24 @@ __global__ __launch_bounds__(256) void k_resolve(int n, const float4* __restrict
     image[i] = make_float4(cl_div(s.x, w), cl_div(s.y, w), cl_div(s.z, w), cl_div(s.w, w));
 }
 
+// Attainable-bandwidth probe (mcrt_ctx_stream_copy): grid-stride float4 copy, 4 loads in flight
+// per lane before the stores so every wave keeps 4 KB of reads outstanding.
+__global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ src4, float4* __restrict__ dst4, size_t n) {
+    const f4* src = reinterpret_cast<const f4*>(src4);
+    f4* dst = reinterpret_cast<f4*>(dst4);
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const f4 a = __builtin_nontemporal_load(&src[i]), b = __builtin_nontemporal_load(&src[i + stride]);
+        const f4 c = __builtin_nontemporal_load(&src[i + 2 * stride]), d = __builtin_nontemporal_load(&src[i + 3 * stride]);
+        __builtin_nontemporal_store(a, &dst[i]);
+        __builtin_nontemporal_store(b, &dst[i + stride]);
+        __builtin_nontemporal_store(c, &dst[i + 2 * stride]);
+        __builtin_nontemporal_store(d, &dst[i + 3 * stride]);
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
@@ -354,6 +418,13 @@ void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const 
                    float4* radiance, int maxCount, hipStream_t st) {
     hipLaunchKernelGGL(k_shadow, dim3((maxCount + 63) / 64), dim3(64), 0, st, c, count, sO, sD, sL, radiance);
 }
+void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
+                          const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
+                          float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
+    const int blocks = (maxExt + 63) / 64 + (maxShadow + 63) / 64;
+    hipLaunchKernelGGL(k_shadow_extend, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, extCount, qO, qD, hits,
+                       shadowCount, sO, sD, sL, radiance);
+}
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + SHADE_BLOCK - 1) / SHADE_BLOCK;
@@ -370,6 +441,10 @@ void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* rad
                        float4* image, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + 255) / 256;
     hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(256), 0, st, f, frame, w, radiance, wsum, wts, image);
+}
+
+void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st) {
+    hipLaunchKernelGGL(k_stream_copy, dim3(numCUs * 8), dim3(256), 0, st, src, dst, n4);
 }
 
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st) {

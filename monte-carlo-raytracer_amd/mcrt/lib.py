@@ -32,6 +32,7 @@ SIGNATURES = {
     "mcrt_ctx_set_profiling": (_c.c_int, [_vp, _c.c_int]),
     "mcrt_ctx_kernel_stats": (_c.c_int, [_vp, _c.c_int, _vp, _vp, _vp, _vp, _c.POINTER(_c.c_int)]),
     "mcrt_ctx_reset_stats": (_c.c_int, [_vp]),
+    "mcrt_ctx_stream_copy": (_c.c_int, [_vp, _c.c_uint64, _c.c_int, _c.POINTER(_c.c_double)]),
     "mcrt_scene_create": (_c.c_int, [_vp, _vp, _c.POINTER(_vp)]),
     "mcrt_scene_destroy": (_c.c_int, [_vp]),
     "mcrt_scene_update_lights": (_c.c_int, [_vp, _vp, _c.c_uint32]),
@@ -51,6 +52,7 @@ SIGNATURES = {
     "mcrt_framebuffer_copy_device": (_c.c_int, [_vp, _c.c_int, _vp]),
     "mcrt_framebuffer_set_accumulation": (_c.c_int, [_vp, _vp, _vp]),
     "mcrt_framebuffer_read_queue": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int32)]),
+    "mcrt_framebuffer_queue_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.POINTER(_c.c_int32), _c.c_int]),
     "mcrt_framebuffer_read_bdpt": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64)]),
     "mcrt_make_pinhole_camera": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _c.c_float, _c.c_float, _c.c_uint32,
                                             _c.c_uint32, _vp, _vp]),
@@ -124,6 +126,12 @@ class Context:
 
     def reset_stats(self):
         _check(lib().mcrt_ctx_reset_stats(self.h), self.h)
+
+    def stream_copy_gbps(self, nbytes=2 << 30, iters=5):
+        """Attainable HBM GB/s of a stream copy (mcrt_ctx_stream_copy)."""
+        g = _c.c_double()
+        _check(lib().mcrt_ctx_stream_copy(self.h, nbytes, iters, _c.byref(g)), self.h)
+        return g.value
 
     def kernel_stats(self):
         n = 16
@@ -225,6 +233,13 @@ class FrameBuffer:
         a, b, c = _c.c_int64(), _c.c_int64(), _c.c_int64()
         _check(lib().mcrt_framebuffer_stats(self.h, _c.byref(a), _c.byref(b), _c.byref(c)), self.ctx.h)
         return {"closest_rays": a.value, "any_rays": b.value, "shaded_paths": c.value}
+
+    def queue_counts(self, max_bounces=8):
+        """(shadow[b], extension[b]) queue sizes of the last PT render."""
+        sh = (_c.c_int32 * max_bounces)()
+        ex = (_c.c_int32 * max_bounces)()
+        _check(lib().mcrt_framebuffer_queue_counts(self.h, sh, ex, max_bounces), self.ctx.h)
+        return list(sh), list(ex)
 
     def read_queue(self, which):
         """(a, b, c) float4 arrays of the last bounce's shadow (0) / extension (1) queue."""
