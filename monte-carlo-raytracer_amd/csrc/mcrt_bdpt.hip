@@ -17,10 +17,13 @@
 //   k_bdpt_gather         radiance = (own strategies summed in the reference's (t, s) order) + splats
 //
 // HBM layout (N = W*H pixels; all planes are float4 x N, so every access is coalesced):
-//   camera vertices  (D+2) depths x 8 planes, light vertices (D+1) x 8 planes:
+//   camera vertices  (D+2) depths x 13 planes, light vertices (D+1) x 13 planes:
 //     0 p.xyz|traceErrorOffset  1 gn.xyz|pdfFwd  2 sn.xyz|pdfRev  3 wo.xyz|pdfPos
 //     4 sdpdu.xyz|uv.x  5 sdpdv.xyz|uv.y  6 throughput.xyz|-  7 int4(type, flags, lightIdx, materialIdx)
-//   (the reference's 240-B RTBDPTVertex holds the same fields plus unused differentials).
+//     8-12 the vertex's uber-material properties (getUberMaterialProperties at its uv, computed
+//     once by k_bdpt_vertex): Kd|eta, Ks|Kt.w, Kr|alpha.x, Kt.xyz|alpha.y, opacity|material type.
+//   (the reference's 240-B RTBDPTVertex holds the first 8 planes' fields plus unused
+//   differentials, and re-reads up to 8 textures per material evaluation instead of plane 8-12).
 //   vertex counts: int x N per subpath.  sampled light vertex of the s = 1 strategy, persistent across
 //   frames (the reference reads it before overwriting it, BDPT.cl:585-586): D planes of float4
 //   (p.xyz | flags<<16 | lightIdx).  own-strategy slots: (C - D) planes of float4 (C = maxConnections).
@@ -52,12 +55,39 @@ struct BVertex {
     f3 wo, throughput;
     float traceErrorOffset, pdfFwd, pdfRev, pdfPos;
     int type, flags, lightIdx, materialIdx;
+    const float4* planes;   // where a surface vertex's material properties live (loadUber)
+    int depth;
 };
 
 // --- plane addressing ---------------------------------------------------------------------
-MCRT_DEV float4* vplane(float4* base, int depth, int k, int N) { return base + (size_t)(depth * 8 + k) * N; }
+MCRT_DEV float4* vplane(float4* base, int depth, int k, int N) {
+    return base + (size_t)(depth * BDPT_VERTEX_PLANES + k) * N;
+}
 MCRT_DEV const float4* vplane(const float4* base, int depth, int k, int N) {
-    return base + (size_t)(depth * 8 + k) * N;
+    return base + (size_t)(depth * BDPT_VERTEX_PLANES + k) * N;
+}
+// material properties of a surface vertex (planes 8-12); matType = RTMaterial::type
+MCRT_DEV void storeUber(float4* base, int depth, int pix, int N, const Uber& u, int matType) {
+    vplane(base, depth, 8, N)[pix] = make_float4(u.Kd.x, u.Kd.y, u.Kd.z, u.eta);
+    vplane(base, depth, 9, N)[pix] = make_float4(u.Ks.x, u.Ks.y, u.Ks.z, u.Kt.w);
+    vplane(base, depth, 10, N)[pix] = make_float4(u.Kr.x, u.Kr.y, u.Kr.z, u.roughness.x);
+    vplane(base, depth, 11, N)[pix] = make_float4(u.Kt.x, u.Kt.y, u.Kt.z, u.roughness.y);
+    vplane(base, depth, 12, N)[pix] = make_float4(u.opacity.x, u.opacity.y, u.opacity.z, __int_as_float(matType));
+}
+MCRT_DEV Uber loadUber(const float4* base, int depth, int pix, int N, int* matType) {
+    const float4 a = vplane(base, depth, 8, N)[pix], b = vplane(base, depth, 9, N)[pix];
+    const float4 c = vplane(base, depth, 10, N)[pix], d = vplane(base, depth, 11, N)[pix];
+    const float4 e = vplane(base, depth, 12, N)[pix];
+    Uber u;
+    u.Kd = ld3(a);
+    u.eta = a.w;
+    u.Ks = ld3(b);
+    u.Kt = f4{d.x, d.y, d.z, b.w};
+    u.Kr = ld3(c);
+    u.roughness = f2{c.w, d.w};
+    u.opacity = ld3(e);
+    *matType = __float_as_int(e.w);
+    return u;
 }
 
 MCRT_DEV BVertex loadVertex(const float4* base, int depth, int pix, int N) {
@@ -83,6 +113,8 @@ MCRT_DEV BVertex loadVertex(const float4* base, int depth, int pix, int N) {
     v.flags = h.y;
     v.lightIdx = h.z;
     v.materialIdx = h.w;
+    v.planes = base;
+    v.depth = depth;
     return v;
 }
 // Position / geometric normal / flags only (the "next" or "prev" vertex of a pdf evaluation)
@@ -237,17 +269,20 @@ MCRT_DEV LightLe sampleLightLe(const SceneArgs& s, const mcrt_light& light, f2 u
 }
 
 // --- materials.cl with transport modes ----------------------------------------------------
-MCRT_DEV f3 evaluateMaterial(const SceneArgs& s, int materialIdx, f3 wo, f3 wi, const Frame& si, int mode) {
-    const mcrt_material mat = s.materials[materialIdx];
-    if (mat.type != 0) return splat3(0.0f);   // materials.cl:131-142: only RT_UBER_MATERIAL
-    const Uber um = uberProps(s, mat, si.uv);
-    return evaluateUberBSDF(um, si, wo, wi, mode);
+// evaluateMaterial / evaluateMaterialPdf (materials.cl:120-142) of a stored surface vertex: the
+// uber properties come from the vertex's planes 8-12 (the same getUberMaterialProperties values
+// the reference recomputes from the textures at every call).  Non-uber materials evaluate to 0.
+MCRT_DEV f3 evaluateMaterialV(const BVertex& v, int pix, int N, f3 wo, f3 wi, int mode) {
+    int type;
+    const Uber um = loadUber(v.planes, v.depth, pix, N, &type);
+    if (type != 0) return splat3(0.0f);
+    return evaluateUberBSDF(um, v.fr, wo, wi, mode);
 }
-MCRT_DEV float evaluateMaterialPdf(const SceneArgs& s, int materialIdx, f3 wo, f3 wi, const Frame& si) {
-    const mcrt_material mat = s.materials[materialIdx];
-    if (mat.type != 0) return 0.0f;
-    const Uber um = uberProps(s, mat, si.uv);
-    return evaluateUberBSDF_Pdf(um, si, wo, wi);
+MCRT_DEV float evaluateMaterialPdfV(const BVertex& v, int pix, int N, f3 wo, f3 wi) {
+    int type;
+    const Uber um = loadUber(v.planes, v.depth, pix, N, &type);
+    if (type != 0) return 0.0f;
+    return evaluateUberBSDF_Pdf(um, v.fr, wo, wi);
 }
 // hasMaterialNonDeltaComponents (materials.cl:163-183)
 MCRT_DEV bool hasMaterialNonDeltaComponents(const SceneArgs& s, int materialIdx, const Frame& si) {
@@ -316,8 +351,8 @@ MCRT_DEV float evalVertexPdfLightOrigin(const SceneArgs& s, f3 thisP, f3 thisGn,
     return pdfPos * light.choicePdf;
 }
 // evalVertexPdf(this, prev (may be null), next)
-MCRT_DEV float evalVertexPdf(const SceneArgs& s, const mcrt_camera& cam, const BVertex& v, bool hasPrev, f3 prevP,
-                             const BVertexPos& next) {
+MCRT_DEV float evalVertexPdf(const SceneArgs& s, const mcrt_camera& cam, const BVertex& v, int pix, int N, bool hasPrev,
+                             f3 prevP, const BVertexPos& next) {
     if (v.type == RT_BDPT_LIGHT_VERTEX) return evalVertexPdfLight(s, v.fr.p, v.fr.gn, v.flags, v.lightIdx, next);
     f3 wn = next.p - v.fr.p;
     float lenSq = cl_dot(wn, wn);
@@ -334,18 +369,18 @@ MCRT_DEV float evalVertexPdf(const SceneArgs& s, const mcrt_camera& cam, const B
             if (isNearZero(lenSq)) return 0.0f;
             wp = cl_div(wp, cl_sqrt(lenSq));
         }
-        pdf = evaluateMaterialPdf(s, v.materialIdx, wp, wn, v.fr);
+        pdf = evaluateMaterialPdfV(v, pix, N, wp, wn);
     }
     return convertVertexDensity(pdf, v.fr.p, next);
 }
 // evalVertex_f(this, next, mode) (BDPT.cl:215-235)
-MCRT_DEV f3 evalVertex_f(const SceneArgs& s, const BVertex& v, f3 nextP, int mode) {
+MCRT_DEV f3 evalVertex_f(const BVertex& v, int pix, int N, f3 nextP, int mode) {
     f3 wi = nextP - v.fr.p;
     const float lenSq = cl_dot(wi, wi);
     if (isNearZero(lenSq)) return splat3(0.0f);
     wi = cl_div(wi, cl_sqrt(lenSq));
     if (v.type == RT_BDPT_SURFACE_VERTEX) {
-        const f3 f = evaluateMaterial(s, v.materialIdx, v.wo, wi, v.fr, mode);
+        const f3 f = evaluateMaterialV(v, pix, N, v.wo, wi, mode);
         return f * shadingNormalCorrection(v.fr, v.wo, wi, mode);
     }
     return f3{1.0f, 0.0784f, 0.5765f};
@@ -484,6 +519,16 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
             const int materialIdx = shape->materialId;
             const mcrt_material mat = s.materials[materialIdx];
             if (mat.uber_normalMapId != -1) applyNormalMapping(s, mat.uber_normalMapId, cur.fr);
+            Uber um;
+            if (mat.type == 0) {
+                um = uberProps(s, mat, cur.fr.uv);
+            } else {
+                um.Kd = um.Ks = um.Kr = um.opacity = splat3(0.0f);
+                um.Kt = f4{0.0f, 0.0f, 0.0f, 0.0f};
+                um.roughness = f2{0.0f, 0.0f};
+                um.eta = 0.0f;
+            }
+            storeUber(V, depth, pix, N, um, mat.type);
             const int mode = isCamera ? TRANSPORT_MODE_RADIANCE : TRANSPORT_MODE_IMPORTANCE;
             const BVertexPos prev = loadVertexPos(V, depth - 1, pix, N);
             float pdfFwd = Dd.w;
@@ -514,10 +559,8 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                 const f2 bsdfSample = getSample2D(sampler);
                 f3 wi = splat3(0.0f), fv = splat3(0.0f);
                 int sampledType = 0, numNonDelta = 0;
-                if (mat.type == 0) {
-                    const Uber um = uberProps(s, mat, cur.fr.uv);
+                if (mat.type == 0)
                     fv = sampleUberBSDF(um, cur.fr, bsdfSample, wo, &wi, &pdfFwd, &sampledType, mode, &numNonDelta);
-                }
                 if (numNonDelta > 0) cur.flags |= VF_CONNECTIBLE;
                 if (isBlack(fv) || isNearZero(pdfFwd)) {
                     storeVertex(V, depth, pix, N, cur);
@@ -529,7 +572,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                         pdfFwd = 0.0f;
                         pdfRev = 0.0f;
                     } else {
-                        pdfRev = evaluateMaterialPdf(s, materialIdx, wi, wo, cur.fr);
+                        pdfRev = mat.type == 0 ? evaluateUberBSDF_Pdf(um, cur.fr, wi, wo) : 0.0f;
                     }
                     float off = cur.traceErrorOffset;
                     if ((sampledType & BSDF_TRANSMISSION) != 0 && cl_dot(cur.fr.gn, wi) * cl_sign(off) < 0.0f) off *= -1.0f;
@@ -613,7 +656,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                             ix = min(max(ix, 0), (int)f.W - 1);
                             iy = min(max(iy, 0), (int)f.H - 1);
                             code = ~(ix + iy * (int)f.W);
-                            L = lv.throughput * samp.throughput * evalVertex_f(s, lv, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                            L = lv.throughput * samp.throughput * evalVertex_f(lv, pix, N, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
                             if (isVertexOnSurface(lv.fr.gn)) L *= absDot(wi, lv.fr.sn);
                             rayO = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
                             rayT = cl_distance(rayO, ld3(cam.pos));
@@ -641,7 +684,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                                                      pdfFwdS, light.flags);
                             *stale = make_float4(samp.fr.p.x, samp.fr.p.y, samp.fr.p.z,
                                                  __int_as_float((samp.flags << 16) | (chosen & 0xffff)));
-                            const f3 fm = evaluateMaterial(s, cv.materialIdx, cv.wo, ls.wi, cv.fr, TRANSPORT_MODE_RADIANCE);
+                            const f3 fm = evaluateMaterialV(cv, pix, N, cv.wo, ls.wi, TRANSPORT_MODE_RADIANCE);
                             L = cv.throughput * samp.throughput * fm;
                             if (isVertexOnSurface(cv.fr.gn)) L *= absDot(ls.wi, cv.fr.sn);
                             if (ls.shadowSet) {
@@ -655,8 +698,8 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                 } else {
                     const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
                     if (isConnectible(cv.flags) && isConnectible(lv.flags)) {
-                        const f3 lvf = evalVertex_f(s, lv, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
-                        const f3 cvf = evalVertex_f(s, cv, lv.fr.p, TRANSPORT_MODE_RADIANCE);
+                        const f3 lvf = evalVertex_f(lv, pix, N, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                        const f3 cvf = evalVertex_f(cv, pix, N, lv.fr.p, TRANSPORT_MODE_RADIANCE);
                         const f3 lp = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
                         const f3 cp = cv.fr.p + cv.fr.gn * cv.traceErrorOffset;
                         f3 w = cp - lp;
@@ -691,14 +734,14 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                     if (sI > 1) qsPrev = loadVertexPos(b.lightV, sI - 2, pix, N);
                     pt.flags &= ~VF_DELTA;
                     if (sI > 0) qs.flags &= ~VF_DELTA;
-                    const float ptRev = sI > 0 ? evalVertexPdf(s, cam, qs, sI > 1, qsPrev.p, posOf(pt))
+                    const float ptRev = sI > 0 ? evalVertexPdf(s, cam, qs, pix, N, sI > 1, qsPrev.p, posOf(pt))
                                                : evalVertexPdfLightOrigin(s, pt.fr.p, pt.fr.gn, pt.flags, pt.lightIdx, ptPrev.p);
                     float ptPrevRev = 0.0f, qsRev = 0.0f, qsPrevRev = 0.0f;
                     if (t > 1)
-                        ptPrevRev = sI > 0 ? evalVertexPdf(s, cam, pt, true, qs.fr.p, ptPrev)
+                        ptPrevRev = sI > 0 ? evalVertexPdf(s, cam, pt, pix, N, true, qs.fr.p, ptPrev)
                                            : evalVertexPdfLight(s, pt.fr.p, pt.fr.gn, pt.flags, pt.lightIdx, ptPrev);
-                    if (sI > 0) qsRev = evalVertexPdf(s, cam, pt, t > 1, ptPrev.p, posOf(qs));
-                    if (sI > 1) qsPrevRev = evalVertexPdf(s, cam, qs, true, pt.fr.p, qsPrev);
+                    if (sI > 0) qsRev = evalVertexPdf(s, cam, pt, pix, N, t > 1, ptPrev.p, posOf(qs));
+                    if (sI > 1) qsPrevRev = evalVertexPdf(s, cam, qs, pix, N, true, pt.fr.p, qsPrev);
                     float sumRi = 0.0f;
                     // camera subpath (BDPT.cl:819-827)
                     float ri = 1.0f;

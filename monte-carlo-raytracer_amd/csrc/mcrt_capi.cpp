@@ -634,8 +634,8 @@ static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D) {
     auto A = [&](auto** p, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
     };
-    A(&fb->camV, 16 * N * 8 * (D + 2));
-    A(&fb->lightV, 16 * N * 8 * (D + 1));
+    A(&fb->camV, 16 * N * BDPT_VERTEX_PLANES * (D + 2));
+    A(&fb->lightV, 16 * N * BDPT_VERTEX_PLANES * (D + 1));
     A(&fb->sampLight, 16 * N * D);
     A(&fb->slots, 16 * N * (C - D));
     A(&fb->splat, 16 * N);
@@ -649,8 +649,8 @@ static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D) {
     A(&fb->cL, 16 * N * C);
     if (e == hipSuccess) e = hipMemset(fb->sampLight, 0, 16 * N * D);
     if (e == hipSuccess) e = hipMemset(fb->splat, 0, 16 * N);
-    if (e == hipSuccess) e = hipMemset(fb->camV, 0, 16 * N * 8 * (D + 2));
-    if (e == hipSuccess) e = hipMemset(fb->lightV, 0, 16 * N * 8 * (D + 1));
+    if (e == hipSuccess) e = hipMemset(fb->camV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 2));
+    if (e == hipSuccess) e = hipMemset(fb->lightV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 1));
     if (e != hipSuccess) { fb_free_bdpt(fb); return e; }
     fb->bdptDepth = D;
     return hipSuccess;
@@ -1026,8 +1026,8 @@ MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, 
     const void* src = nullptr;
     size_t sz = 0;
     switch (which) {
-    case 0: src = fb->camV; sz = 16 * N * 8 * (D + 2); break;
-    case 1: src = fb->lightV; sz = 16 * N * 8 * (D + 1); break;
+    case 0: src = fb->camV; sz = 16 * N * BDPT_VERTEX_PLANES * (D + 2); break;
+    case 1: src = fb->lightV; sz = 16 * N * BDPT_VERTEX_PLANES * (D + 1); break;
     case 2: src = fb->camCount; sz = 4 * N; break;
     case 3: src = fb->lightCount; sz = 4 * N; break;
     case 4: src = fb->slots; sz = 16 * N * (C - D); break;

@@ -38,6 +38,8 @@ struct QueueArgs {
     float4 *eOout, *eDout, *eTout;
 };
 
+// float4 planes per BDPT vertex: 8 for the vertex, 5 for its uber-material properties
+#define BDPT_VERTEX_PLANES 13
 // BDPT per-frame state (mcrt_bdpt.hip header comment has the layout)
 struct BdptArgs {
     float4* camV;        // (D+2) x 8 planes x N

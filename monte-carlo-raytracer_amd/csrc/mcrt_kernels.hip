@@ -378,22 +378,17 @@ __global__ __launch_bounds__(256) void k_resolve(int n, const float4* __restrict
     image[i] = make_float4(cl_div(s.x, w), cl_div(s.y, w), cl_div(s.z, w), cl_div(s.w, w));
 }
 
-// Attainable-bandwidth probe (mcrt_ctx_stream_copy): grid-stride float4 copy, 4 loads in flight
-// per lane before the stores so every wave keeps 4 KB of reads outstanding.
-__global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ src4, float4* __restrict__ dst4, size_t n) {
-    const f4* src = reinterpret_cast<const f4*>(src4);
-    f4* dst = reinterpret_cast<f4*>(dst4);
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const f4 a = __builtin_nontemporal_load(&src[i]), b = __builtin_nontemporal_load(&src[i + stride]);
-        const f4 c = __builtin_nontemporal_load(&src[i + 2 * stride]), d = __builtin_nontemporal_load(&src[i + 3 * stride]);
-        __builtin_nontemporal_store(a, &dst[i]);
-        __builtin_nontemporal_store(b, &dst[i + stride]);
-        __builtin_nontemporal_store(c, &dst[i + 2 * stride]);
-        __builtin_nontemporal_store(d, &dst[i + 3 * stride]);
-    }
-    for (; i < n; i += stride) dst[i] = src[i];
+// Attainable-bandwidth probe (mcrt_ctx_stream_copy): one float4 per thread, 4 per lane in flight
+// through 4 independent loads; the grid covers the array (no grid-stride loop).
+__global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
+    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
+    float4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + 256 * k < n) v[k] = src[base + 256 * k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + 256 * k < n) dst[base + 256 * k] = v[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -444,7 +439,8 @@ void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* rad
 }
 
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st) {
-    hipLaunchKernelGGL(k_stream_copy, dim3(numCUs * 8), dim3(256), 0, st, src, dst, n4);
+    (void)numCUs;
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n4 + 1023) / 1024)), dim3(256), 0, st, src, dst, n4);
 }
 
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st) {
