@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
+    ap.add_argument("--device-build", action="store_true", help="on-device linear BVH instead of the RR-identical host build")
     args = ap.parse_args()
 
     import torch
@@ -145,7 +146,7 @@ def main():
 
     ctx = lib.Context(local)
     t0 = time.perf_counter()
-    ds = lib.DeviceScene(ctx, scene)
+    ds = lib.DeviceScene(ctx, scene, device_build=args.device_build)
     info = ds.info()
     log(f"[bench] upload+BVH {time.perf_counter() - t0:.1f}s (build {info['build_ms'] / 1e3:.1f}s, "
         f"{info['nodes']} nodes, {info['bytes'] / 1e6:.0f} MB)")
@@ -215,6 +216,8 @@ def main():
         "config": {"workload": f"{args.scene} {W}x{H}, {'BDPT' if bdpt else 'unidirectional PT'}, maxDepth {D}, "
                                f"{args.sampler} sampler, 1 spp per step, box-filter accumulate", "width": W, "height": H,
                    "triangles": scene.num_triangles, "max_depth": D, "spp_per_step": 1,
+                   "bvh": "device LBVH" if args.device_build else "host RadeonRays-identical SAH",
+                   "bvh_build_ms": round(info["build_ms"], 1),
                    "parallelism": (f"frame split x {world} + 1 RCCL reduce" if bdpt else
                                    f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce")},
     }

@@ -190,6 +190,11 @@ typedef struct {
     float traversal_cost;   /* "bvh.sah.traversal_cost", default 10 */
     int   num_bins;         /* "bvh.sah.num_bins", default 64 */
     int   use_sah;          /* "bvh.builder" == "sah", default 1 */
+    /* 0 (default): host build that reproduces RadeonRays' Bvh2 node for node (bit-exact parity,
+     * seconds for 10 M triangles).  1: on-device linear BVH (Morton order, rocPRIM radix sort;
+     * tens of ms), same record format and triangle data, different tree (equal-t hit ties may
+     * resolve differently from the reference).  Ignores the three SAH fields. */
+    int   device_build;
 } mcrt_accel_opts;
 
 #define MCRT_SAMPLER_SOBOL  0   /* KRN/samplers.cl:16 */

@@ -504,6 +504,8 @@ MCRT_API mcrt_status mcrt_scene_update_shapes(mcrt_scene s, const mcrt_shape* sh
     return replace_array(s, &s->dShapes, sh, sizeof(mcrt_shape) * n);
 }
 
+static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_point t0);
+
 MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts) {
     if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
     mcrt_ctx ctx = s->ctx;
@@ -516,6 +518,25 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     for (auto& sh : s->shapes) n += sh.numTriangles;
     if (n == 0) return fail(ctx, MCRT_ERROR_INVALID_ARG, "scene has no triangles (RR: Commit on empty scene throws)");
     if (n > (size_t)0x7fffffff) return fail(ctx, MCRT_ERROR_INVALID_ARG, "too many triangles");
+    if (opts && opts->device_build) {   // on-device linear BVH (mcrt_gpubuild.hip)
+        hipSetDevice(ctx->device);
+        std::vector<uint32_t> first(s->shapes.size());
+        uint32_t acc = 0;
+        for (size_t si = 0; si < s->shapes.size(); ++si) { first[si] = acc; acc += s->shapes[si].numTriangles; }
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        float4* nodes = nullptr;
+        int depth = 0;
+        HIPCHK(ctx, mcrt::gpu_build_bvh((const mcrt_shape*)s->dShapes, first, (const uint32_t*)s->dIndices,
+                                        (const float4*)s->dPositions, n, ctx->stream, &nodes, &depth));
+        if (s->dNodes) hipFree(s->dNodes);
+        if (s->dTris) hipFree(s->dTris);
+        s->dTris = nullptr;
+        s->dNodes = nodes;
+        s->numNodes = 2 * n - 1;
+        s->numTris = (uint32_t)n;
+        s->bvhDepth = depth;
+        return finish_accel(s, t0);
+    }
     std::vector<float> tri(9 * n);
     std::vector<int32_t> shapeOf(n), primOf(n);
     size_t k = 0;
@@ -545,8 +566,13 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     s->bvhDepth = bvh.depth;
     mcrt::free_bvh(bvh);
     if (e != hipSuccess) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, std::string("BVH upload: ") + hipGetErrorString(e));
-    // traversal scratch: overflow flag; per-ray spill columns deep enough for the tree
-    // (allocated by ensure_spill for the largest launch)
+    return finish_accel(s, t0);
+}
+
+// traversal scratch: overflow flag; per-ray spill columns deep enough for the tree
+// (allocated by ensure_spill for the largest launch)
+static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_point t0) {
+    mcrt_ctx ctx = s->ctx;
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
     const int needCap = ((s->bvhDepth + 2 + 14) / 15) * 15;

@@ -94,6 +94,12 @@ void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance,
 void launch_bdpt_clear_splat(int n, float4* splat, hipStream_t st);
 }  // namespace mcrt
 
+// Device BVH builder (mcrt_gpubuild.hip): linear BVH in the mcrt_bvh.cpp record format
+#include <vector>
+namespace mcrt {
+hipError_t gpu_build_bvh(const mcrt_shape* dShapes, const std::vector<uint32_t>& shapeFirst, const uint32_t* dIndices,
+                         const float4* dPositions, size_t n, hipStream_t st, float4** nodesOut, int* depthOut);
+}
 // Host BVH builder (mcrt_bvh.cpp)
 namespace mcrt {
 struct BvhOut {

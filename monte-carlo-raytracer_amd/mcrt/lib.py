@@ -146,7 +146,7 @@ class Context:
 
 
 class DeviceScene:
-    def __init__(self, ctx, scene, build=True, cost=10.0, bins=64, sah=True):
+    def __init__(self, ctx, scene, build=True, cost=10.0, bins=64, sah=True, device_build=False):
         self.ctx = ctx
         self.scene = scene
         self._desc = scene.desc()
@@ -155,10 +155,10 @@ class DeviceScene:
         self.h = h
         ctx._adopt(self)
         if build:
-            self.build(cost, bins, sah)
+            self.build(cost, bins, sah, device_build)
 
-    def build(self, cost=10.0, bins=64, sah=True):
-        opts = T.AccelOpts(cost, bins, 1 if sah else 0)
+    def build(self, cost=10.0, bins=64, sah=True, device_build=False):
+        opts = T.AccelOpts(cost, bins, 1 if sah else 0, 1 if device_build else 0)
         _check(lib().mcrt_accel_build(self.h, _c.byref(opts)), self.ctx.h)
 
     def info(self):

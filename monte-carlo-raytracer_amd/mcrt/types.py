@@ -130,7 +130,8 @@ class SceneDesc(ctypes.Structure):
 
 
 class AccelOpts(ctypes.Structure):
-    _fields_ = [("traversal_cost", ctypes.c_float), ("num_bins", ctypes.c_int), ("use_sah", ctypes.c_int)]
+    _fields_ = [("traversal_cost", ctypes.c_float), ("num_bins", ctypes.c_int), ("use_sah", ctypes.c_int),
+                ("device_build", ctypes.c_int)]
 
 
 class FrameParams(ctypes.Structure):
