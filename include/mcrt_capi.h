@@ -304,7 +304,22 @@ MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* fil
 /* Device pointers of the frame buffer's arrays (float4 x W*H, float x W*H). */
 MCRT_API mcrt_status mcrt_framebuffer_device_ptrs(mcrt_framebuffer fb, void** radiance, void** weighted_sum,
                                                   void** weight_sum, void** image);
-/* Copies device -> host (RGBA32F, W*H*4 floats).  which: 0 radiance, 1 weighted sum, 2 image. */
+/* Post-process of the accumulated image, the passes after RTReconstructionPass in the
+ * reference pipeline (PathTracingApp.cpp:240-254): RTDenoisePass (BilateralDenoise,
+ * KRN/Denoise.cl:6-47, RTDenoisePass.cpp) then RTToneMappingPass (ReinhardToneMapping,
+ * KRN/ToneMapping.cl:42-63, RTToneMappingPass.cpp; the pass passes GI.minLuminance as Lwhite).
+ * Result: the display image (mcrt_framebuffer_read which = 3), = the image when both are off. */
+typedef struct {
+    int32_t use_denoise;        /* GI.useDenoise (default 0) */
+    int32_t denoise_radius;     /* GI.denoiseKernelRadius (default 1) */
+    float   sigma_spatial;      /* GI.bilateralDenoiseSigmaSpatial (default 1.0) */
+    float   sigma_range;        /* GI.bilateralDenoiseSigmaRange (default 0.1) */
+    int32_t use_tonemapping;    /* GI.useTonemapping (default 0) */
+    float   min_luminance;      /* GI.minLuminance (default 2.0), Reinhard's Lwhite */
+} mcrt_postprocess_params;
+MCRT_API mcrt_status mcrt_postprocess(mcrt_framebuffer fb, const mcrt_postprocess_params* params);
+/* Copies device -> host (RGBA32F, W*H*4 floats).  which: 0 radiance, 1 weighted sum, 2 image,
+ * 3 display image (mcrt_postprocess). */
 MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float* host_rgba);
 /* Device-to-device copy of one frame-buffer array into caller memory (e.g. a torch/RCCL
  * buffer for the multi-GPU reduce): which 0 radiance (float4), 1 weighted sum (float4),

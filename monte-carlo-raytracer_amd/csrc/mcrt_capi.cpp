@@ -98,6 +98,8 @@ struct mcrt_framebuffer_s {
     float4* wsum = nullptr;
     float* wts = nullptr;
     float4* image = nullptr;
+    float4* denoised = nullptr;  // RTDenoisePass output (persistent: the reference keeps its image)
+    float4* display = nullptr;   // post-processed image (mcrt_postprocess)
     float4* hitsP = nullptr;     // primary hits by pixel
     float4* hitsE = nullptr;     // extension hits by queue slot
     float4* eO[2] = {};
@@ -641,8 +643,9 @@ static void fb_free_bdpt(mcrt_framebuffer fb) {
 }
 
 static void fb_free(mcrt_framebuffer fb) {
-    void* ptrs[] = {fb->radiance, fb->wsum, fb->wts, fb->image, fb->hitsP, fb->hitsE, fb->eO[0], fb->eO[1],
-                    fb->eD[0],    fb->eD[1], fb->eT[0], fb->eT[1], fb->sO,   fb->sD,   fb->sL,    fb->counters};
+    void* ptrs[] = {fb->radiance, fb->wsum, fb->wts,   fb->image, fb->hitsP, fb->hitsE,    fb->eO[0],
+                    fb->eO[1],    fb->eD[0], fb->eD[1], fb->eT[0], fb->eT[1], fb->sO,       fb->sD,
+                    fb->sL,       fb->counters, fb->denoised, fb->display};
     for (void* p : ptrs)
         if (p) hipFree(p);
     fb_free_bdpt(fb);
@@ -700,6 +703,8 @@ MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint3
     A(&fb->wsum, 16 * N);
     A(&fb->wts, 4 * N);
     A(&fb->image, 16 * N);
+    A(&fb->denoised, 16 * N);
+    A(&fb->display, 16 * N);
     A(&fb->hitsP, 16 * N);
     A(&fb->hitsE, 16 * N);
     for (int i = 0; i < 2; ++i) { A(&fb->eO[i], 16 * N); A(&fb->eD[i], 16 * N); A(&fb->eT[i], 16 * N); }
@@ -711,6 +716,8 @@ MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint3
     if (e == hipSuccess) e = hipMemset(fb->wsum, 0, 16 * N);
     if (e == hipSuccess) e = hipMemset(fb->wts, 0, 4 * N);
     if (e == hipSuccess) e = hipMemset(fb->image, 0, 16 * N);
+    if (e == hipSuccess) e = hipMemset(fb->denoised, 0, 16 * N);
+    if (e == hipSuccess) e = hipMemset(fb->display, 0, 16 * N);
     if (e == hipSuccess) e = hipMemset(fb->counters, 0, 256 * sizeof(int));
     if (e != hipSuccess) {
         fb_free(fb);
@@ -944,11 +951,35 @@ MCRT_API mcrt_status mcrt_framebuffer_device_ptrs(mcrt_framebuffer fb, void** ra
     return MCRT_OK;
 }
 
-MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float* host_rgba) {
-    if (!fb || !host_rgba || which < 0 || which > 2) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+MCRT_API mcrt_status mcrt_postprocess(mcrt_framebuffer fb, const mcrt_postprocess_params* p) {
+    if (!fb || !p) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
     mcrt_ctx ctx = fb->ctx;
     hipSetDevice(ctx->device);
-    const void* src = which == 0 ? (const void*)fb->radiance : which == 1 ? (const void*)fb->wsum : (const void*)fb->image;
+    const int W = (int)fb->W, H = (int)fb->H;
+    const float4* src = fb->image;
+    if (p->use_denoise) {
+        // RTDenoisePass (RTDenoisePass.cpp:21-60): the kernel writes nothing for a non-positive
+        // radius or sigma (Denoise.cl:18-19), so the pass then shows its image's old content.
+        if (p->denoise_radius > 16) return fail(ctx, MCRT_ERROR_INVALID_ARG, "denoise_radius > 16 (the GUI allows <= 10)");
+        if (p->denoise_radius > 0 && p->sigma_spatial > 0.0f && p->sigma_range > 0.0f)
+            mcrt::launch_denoise(W, H, p->denoise_radius, p->sigma_spatial, p->sigma_range, fb->image, fb->denoised,
+                                 ctx->stream);
+        src = fb->denoised;
+    }
+    if (p->use_tonemapping)   // RTToneMappingPass::applyReinhardToneMapping (RTToneMappingPass.cpp:38-72)
+        mcrt::launch_tonemap(W * H, p->min_luminance, src, fb->display, ctx->stream);
+    else
+        HIPCHK(ctx, hipMemcpyAsync(fb->display, src, 16 * fb->N, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipGetLastError());
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float* host_rgba) {
+    if (!fb || !host_rgba || which < 0 || which > 3) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    const void* src = which == 0 ? (const void*)fb->radiance : which == 1 ? (const void*)fb->wsum
+                      : which == 2 ? (const void*)fb->image : (const void*)fb->display;
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipMemcpy(host_rgba, src, 16 * fb->N, hipMemcpyDeviceToHost));
     return MCRT_OK;

@@ -82,6 +82,8 @@ void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int
 void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st);
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st);
+void launch_denoise(int W, int H, int r, float ss, float sr, const float4* in, float4* out, hipStream_t st);
+void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStream_t st);
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st);
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& q, hipStream_t st);

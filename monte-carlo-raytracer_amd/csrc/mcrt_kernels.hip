@@ -378,6 +378,63 @@ __global__ __launch_bounds__(256) void k_resolve(int n, const float4* __restrict
     image[i] = make_float4(cl_div(s.x, w), cl_div(s.y, w), cl_div(s.z, w), cl_div(s.w, w));
 }
 
+// ---------------------------------------------------------------------------
+// Post-process (the reference's RTDenoisePass + RTToneMappingPass after reconstruction)
+// ---------------------------------------------------------------------------
+#define DENOISE_TILE 16
+#define DENOISE_RMAX 16
+// BilateralDenoise (KRN/Denoise.cl:6-47): a 16x16 tile plus its clamped apron staged in LDS
+// once (the reference re-reads the (2r+1)^2 window through the image unit per pixel); the
+// window is walked in the reference's order (x outer, y inner) so the sums round identically.
+__global__ __launch_bounds__(DENOISE_TILE * DENOISE_TILE) void k_denoise(int W, int H, int r, float ss, float sr,
+                                                                         const float4* __restrict__ in,
+                                                                         float4* __restrict__ out) {
+    __shared__ float4 tile[(DENOISE_TILE + 2 * DENOISE_RMAX) * (DENOISE_TILE + 2 * DENOISE_RMAX)];
+    const int TW = DENOISE_TILE + 2 * r;
+    const int x0 = blockIdx.x * DENOISE_TILE - r, y0 = blockIdx.y * DENOISE_TILE - r;
+    const int tid = threadIdx.y * DENOISE_TILE + threadIdx.x;
+    for (int i = tid; i < TW * TW; i += DENOISE_TILE * DENOISE_TILE) {
+        const int gx = min(max(x0 + i % TW, 0), W - 1), gy = min(max(y0 + i / TW, 0), H - 1);
+        tile[i] = in[(size_t)gy * W + gx];
+    }
+    __syncthreads();
+    const int gx = blockIdx.x * DENOISE_TILE + threadIdx.x, gy = blockIdx.y * DENOISE_TILE + threadIdx.y;
+    if (gx >= W || gy >= H) return;
+    const float sdSq = ss * ss, srSq = sr * sr;
+    const float4 oc = tile[(gy - y0) * TW + (gx - x0)];
+    const f4 o = f4{oc.x, oc.y, oc.z, oc.w};
+    f4 fc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    float weightSum = 0.0f;
+    for (int rx = -r; rx <= r; ++rx) {
+        const int x = min(max(rx + gx, 0), W - 1);
+        for (int ry = -r; ry <= r; ++ry) {
+            const int y = min(max(ry + gy, 0), H - 1);
+            const float4 kc = tile[(y - y0) * TW + (x - x0)];
+            const f4 k = f4{kc.x, kc.y, kc.z, kc.w};
+            const f4 cd = o - k;
+            const float d2 = fmaf(cd.w, cd.w, fmaf(cd.z, cd.z, fmaf(cd.y, cd.y, cd.x * cd.x)));   // dot(float4)
+            const int sp = (gx - x) * (gx - x) + (gy - y) * (gy - y);
+            const float w = expf(cl_div((float)(-sp), (2.0f * sdSq)) - cl_div(d2, (2.0f * srSq)));
+            weightSum += w;
+            fc += w * k;
+        }
+    }
+    fc = cl_div(fc, weightSum);
+    out[(size_t)gy * W + gx] = make_float4(fc.x, fc.y, fc.z, fc.w);
+}
+
+// ReinhardToneMapping (KRN/ToneMapping.cl:42-63), luminance of KRN/colors.cl:19-22
+__global__ __launch_bounds__(256) void k_tonemap(int n, float Lwhite, const float4* __restrict__ in,
+                                                 float4* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = in[i];
+    const float L = 0.212671f * p.x + 0.715160f * p.y + 0.072169f * p.z;
+    const float tL = cl_div(L * (1.0f + cl_div(L, (Lwhite * Lwhite))), (1.0f + L));
+    const float s = cl_div(tL, L);
+    out[i] = make_float4(p.x * s, p.y * s, p.z * s, p.w);
+}
+
 // Attainable-bandwidth probe (mcrt_ctx_stream_copy): one float4 per thread, 4 per lane in flight
 // through 4 independent loads; the grid covers the array (no grid-stride loop).
 __global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
@@ -438,6 +495,13 @@ void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* rad
     hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(256), 0, st, f, frame, w, radiance, wsum, wts, image);
 }
 
+void launch_denoise(int W, int H, int r, float ss, float sr, const float4* in, float4* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_denoise, dim3((W + DENOISE_TILE - 1) / DENOISE_TILE, (H + DENOISE_TILE - 1) / DENOISE_TILE),
+                       dim3(DENOISE_TILE, DENOISE_TILE), 0, st, W, H, r, ss, sr, in, out);
+}
+void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_tonemap, dim3((n + 255) / 256), dim3(256), 0, st, n, Lwhite, in, out);
+}
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st) {
     (void)numCUs;
     hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n4 + 1023) / 1024)), dim3(256), 0, st, src, dst, n4);

@@ -53,6 +53,7 @@ SIGNATURES = {
     "mcrt_framebuffer_set_accumulation": (_c.c_int, [_vp, _vp, _vp]),
     "mcrt_framebuffer_read_queue": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int32)]),
     "mcrt_framebuffer_queue_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.POINTER(_c.c_int32), _c.c_int]),
+    "mcrt_postprocess": (_c.c_int, [_vp, _c.POINTER(T.PostprocessParams)]),
     "mcrt_framebuffer_read_bdpt": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64)]),
     "mcrt_make_pinhole_camera": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _c.c_float, _c.c_float, _c.c_uint32,
                                             _c.c_uint32, _vp, _vp]),
@@ -211,6 +212,13 @@ class FrameBuffer:
     def accumulate(self, filt, frame):
         filt = np.ascontiguousarray(filt)
         _check(lib().mcrt_accumulate(self.h, _p(filt), frame), self.ctx.h)
+
+    def postprocess(self, denoise=False, radius=1, sigma_spatial=1.0, sigma_range=0.1, tonemap=False,
+                    min_luminance=2.0):
+        """RTDenoisePass + RTToneMappingPass on the accumulated image -> read(3)."""
+        p = T.PostprocessParams(1 if denoise else 0, radius, sigma_spatial, sigma_range, 1 if tonemap else 0,
+                                min_luminance)
+        _check(lib().mcrt_postprocess(self.h, _c.byref(p)), self.ctx.h)
 
     def read(self, which=0):
         out = np.zeros((self.H, self.W, 4), np.float32)

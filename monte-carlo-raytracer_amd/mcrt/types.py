@@ -143,6 +143,12 @@ class FrameParams(ctypes.Structure):
     ]
 
 
+class PostprocessParams(ctypes.Structure):
+    _fields_ = [("use_denoise", ctypes.c_int32), ("denoise_radius", ctypes.c_int32),
+                ("sigma_spatial", ctypes.c_float), ("sigma_range", ctypes.c_float),
+                ("use_tonemapping", ctypes.c_int32), ("min_luminance", ctypes.c_float)]
+
+
 INTEGRATOR_PT = 0
 INTEGRATOR_BDPT = 1
 

@@ -1663,6 +1663,45 @@ static float filterWeight(const mcrt_filter* f) {
     }
     return 1.0f;
 }
+/* KRN/Denoise.cl:6-47 (BilateralDenoise); the reference writes nothing when a parameter is
+ * non-positive (the output keeps its previous content: here, left untouched). */
+void orc_denoise(int W, int H, int radius, float ss, float sr, const float* in, float* out) {
+    if (radius <= 0 || ss <= 0.0f || sr <= 0.0f) return;
+    const float sdSq = ss * ss, srSq = sr * sr;
+    for (int gy = 0; gy < H; ++gy)
+        for (int gx = 0; gx < W; ++gx) {
+            const float* o = &in[4 * ((size_t)gy * W + gx)];
+            float fc[4] = {0, 0, 0, 0}, wsum = 0.0f;
+            for (int rx = -radius; rx <= radius; ++rx) {
+                const int x = rx + gx < 0 ? 0 : (rx + gx > W - 1 ? W - 1 : rx + gx);
+                for (int ry = -radius; ry <= radius; ++ry) {
+                    const int y = ry + gy < 0 ? 0 : (ry + gy > H - 1 ? H - 1 : ry + gy);
+                    const float* k = &in[4 * ((size_t)y * W + x)];
+                    float d2 = 0.0f;
+                    for (int c = 0; c < 4; ++c) d2 += (o[c] - k[c]) * (o[c] - k[c]);
+                    const int sp = (gx - x) * (gx - x) + (gy - y) * (gy - y);
+                    const float w = expf((float)(-sp) / (2.0f * sdSq) - d2 / (2.0f * srSq));
+                    wsum += w;
+                    for (int c = 0; c < 4; ++c) fc[c] += w * k[c];
+                }
+            }
+            for (int c = 0; c < 4; ++c) out[4 * ((size_t)gy * W + gx) + c] = fc[c] / wsum;
+        }
+}
+
+/* KRN/ToneMapping.cl:42-63 with computeLuminanceFromRGB (KRN/colors.cl:19-22) and
+ * toneMapControlled (ToneMapping.cl:37-40); alpha passes through. */
+void orc_tonemap(int W, int H, float Lwhite, const float* in, float* out) {
+    for (size_t i = 0; i < (size_t)W * H; ++i) {
+        const float* p = &in[4 * i];
+        const float L = 0.212671f * p[0] + 0.715160f * p[1] + 0.072169f * p[2];
+        const float tL = L * (1.0f + L / (Lwhite * Lwhite)) / (1.0f + L);
+        const float s = tL / L;
+        for (int c = 0; c < 3; ++c) out[4 * i + c] = p[c] * s;
+        out[4 * i + 3] = p[3];
+    }
+}
+
 void orc_accumulate(int W, int H, int frame, const mcrt_filter* f, const float* radiance,
                     float* wsum, float* wts, float* image) {
     float w = filterWeight(f);

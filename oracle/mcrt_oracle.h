@@ -2,7 +2,7 @@
  * mcrt_oracle.h -- TEST INFRASTRUCTURE ONLY.
  *
  * CPU restatement of the reference hot path (compix/Monte-Carlo-Raytracer):
- * the OpenCL path tracer (assets/kernels/*.cl) and the RadeonRays Bvh2 +
+ * the OpenCL path tracer (assets/kernels/ sources) and the RadeonRays Bvh2 +
  * LDS traversal it calls (third_party/RadeonRays/RadeonRays/src/...).
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
  * load this library, and only as the checker / CPU baseline -- the product
@@ -80,6 +80,11 @@ float orc_pdf_uber(const float kd[3], const float ks[3], const float kr[3], cons
                    const float rough_alpha[2], const float opacity[3], float eta,
                    const float wo[3], const float wi[3]);
 float orc_roughness_to_alpha(float r);
+
+/* Post-process passes (test restatements): BilateralDenoise (KRN/Denoise.cl:6-47) and
+ * ReinhardToneMapping (KRN/ToneMapping.cl:42-63) on RGBA32F images (W*H float4). */
+void orc_denoise(int W, int H, int radius, float sigma_spatial, float sigma_range, const float* in, float* out);
+void orc_tonemap(int W, int H, float Lwhite, const float* in, float* out);
 
 #ifdef __cplusplus
 }

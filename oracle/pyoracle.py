@@ -50,6 +50,8 @@ def lib():
         L.orc_render_frame.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _vp, _vp]
         L.orc_render_rows.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _c.c_int, _c.c_int, _vp, _vp]
         L.orc_accumulate.argtypes = [_c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp, _vp]
+        L.orc_denoise.argtypes = [_c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float, _vp, _vp]
+        L.orc_tonemap.argtypes = [_c.c_int, _c.c_int, _c.c_float, _vp, _vp]
         L.orc_sample_uber.argtypes = [_vp] * 6 + [_c.c_float, _vp, _vp, _vp]
         L.orc_eval_uber.argtypes = [_vp] * 5 + [_c.c_float, _vp, _vp, _vp]
         L.orc_pdf_uber.restype = _c.c_float
@@ -145,6 +147,22 @@ def accumulate(radiance, frame, filt, wsum=None, wts=None):
     image = np.zeros((H, W, 4), np.float32)
     lib().orc_accumulate(W, H, frame, _p(filt), _p(radiance), _p(wsum), _p(wts), _p(image))
     return wsum, wts, image
+
+
+def denoise(img, radius, sigma_spatial, sigma_range):
+    """BilateralDenoise (Denoise.cl:6-47) on an (H, W, 4) float32 image."""
+    img = np.ascontiguousarray(img, np.float32)
+    out = img.copy()
+    lib().orc_denoise(img.shape[1], img.shape[0], radius, sigma_spatial, sigma_range, _p(img), _p(out))
+    return out
+
+
+def tonemap(img, l_white):
+    """ReinhardToneMapping (ToneMapping.cl:42-63) on an (H, W, 4) float32 image."""
+    img = np.ascontiguousarray(img, np.float32)
+    out = np.empty_like(img)
+    lib().orc_tonemap(img.shape[1], img.shape[0], l_white, _p(img), _p(out))
+    return out
 
 
 def wang_hash(x):

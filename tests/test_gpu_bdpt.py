@@ -41,8 +41,9 @@ def clref_bdpt(tmp_path_factory):
 
 
 def our_planes(raw, depths, N):
-    """(depths, 8, N, 4) float32 view of the product's vertex planes."""
-    return raw.view(np.float32).reshape(depths, 8, N, 4)
+    """(depths, planes, N, 4) float32 view of the product's vertex planes (planes 0-7 = the vertex)."""
+    f = raw.view(np.float32)
+    return f.reshape(depths, f.size // (depths * N * 4), N, 4)
 
 
 def compare_vertices(ours, ref, counts, depths, N, label):
