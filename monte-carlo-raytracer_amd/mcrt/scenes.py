@@ -129,10 +129,17 @@ class SceneBuilder:
         self.materials.append(default_material(**kw))
         return len(self.materials) - 1
 
-    def add_texture(self, rgba, wrap=0):
+    def add_texture(self, rgba, wrap=0, mips=False):
+        """RGBA8 texture; mips=True stores its glGenerateMipmap chain after level 0 the way
+        RTScene::uploadTextures packs it (RTScene.cpp:680-766; only level 0 is sampled, the
+        reference's LOD path is disabled at textures.cl:207)."""
         rgba = np.ascontiguousarray(rgba, np.uint8)
         assert rgba.ndim == 3 and rgba.shape[2] == 4
-        self.textures.append((rgba, wrap))
+        if mips:
+            from .objload import mip_chain
+            self.textures.append((mip_chain(rgba), wrap))
+        else:
+            self.textures.append((rgba, wrap))
         return len(self.textures) - 1
 
     def add_mesh(self, P, N, UV, tris, material, transform=None):
@@ -249,10 +256,12 @@ class SceneBuilder:
         descs = np.zeros(len(self.textures), T.TEXDESC_DTYPE)
         chunks, off = [], 0
         for i, (img, wrap) in enumerate(self.textures):
-            h, w = img.shape[:2]
-            descs[i] = (w, h, 1, 3, wrap, 0, off)
-            chunks.append(img.reshape(-1))
-            off += img.nbytes
+            levels = img if isinstance(img, list) else [img]
+            h, w = levels[0].shape[:2]
+            descs[i] = (w, h, len(levels), 3, wrap, 0, off)
+            for lv in levels:
+                chunks.append(lv.reshape(-1))
+                off += lv.nbytes
         tex_data = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
         materials = np.array(self.materials, T.MATERIAL_DTYPE) if self.materials else np.zeros(0, T.MATERIAL_DTYPE)
         return Scene(shapes, indices, positions, uvs, normals, tangents, binormals, None, descs,
