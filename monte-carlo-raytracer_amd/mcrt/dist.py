@@ -40,6 +40,14 @@ def band_rows_of(height, band_rows, num_bands, band_index):
     return rows[rows < height]
 
 
+def frame_split(num_frames, world, rank):
+    """Frame split (BDPT, whose light-tracing splats land anywhere in the image): rank r renders
+    whole frames r, r + N, r + 2N, ... of the sequence 0 .. num_frames-1."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    return np.arange(rank, num_frames, world, dtype=np.int64)
+
+
 def reduce_accumulators(wsum, wts, dst=0, group=None):
     """Sum the per-rank accumulators into rank `dst` (torch tensors, in place on dst)."""
     import torch.distributed as dist

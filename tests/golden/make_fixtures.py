@@ -14,6 +14,12 @@ own C++ (oracle/_ref/librrref.so, built from /root/reference by oracle/refbuild)
                         (source/application/PathTracer/raytracing/sampling/sobol.h:34)
   rr_bvh_mixed.npz      node array of the reference Bvh2 (bvh2.cpp) over mcrt.scenes.test_scene()
 
+Generated on the GPU box instead (the reference's OpenCL kernels need the MI355X):
+  clref_{ieee,fast}.npz       python tests/clref_job.py OUT VARIANT
+  clref_bdpt_{ieee,fast}.npz  python tests/clref_job.py OUT VARIANT bdpt, then
+                              tests/clref_job.py:strip_bdpt_golden(OUT, FIXTURE) keeps the
+                              radiance frames and vertex counts
+
 usage: python tests/golden/make_fixtures.py
 """
 import ctypes

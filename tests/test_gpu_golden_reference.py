@@ -56,3 +56,55 @@ def test_tolerance_vs_reference_fast_math_build(frames):
         d = np.abs(g[..., :3] - ref)
         frac = (d <= 1e-4 * np.maximum(1.0, np.abs(ref))).all(-1).mean()
         assert frac >= 0.995, (k, frac)
+
+
+# --- BDPT: committed outputs of the reference's BDPT.cl (tests/golden/clref_bdpt_{ieee,fast}.npz,
+#     tests/clref_job.py OUT VARIANT bdpt, stripped to radiance frames + vertex counts) ---------
+@pytest.fixture(scope="module")
+def bdpt_frames(hip_ctx):
+    from clref_job import BDPT_CASES, bdpt_key
+    from mcrt import lib
+    out = {}
+    for case in BDPT_CASES:
+        name, W, H, fr, D = case
+        ds = lib.DeviceScene(hip_ctx, build_scene(name))
+        fb = lib.FrameBuffer(hip_ctx, W, H)   # fresh buffers: frames in order, as the fixture
+        cam = scene_camera(name, W, H)
+        for f in fr:
+            fb.render(ds, cam, frame=f, max_depth=D, sampler=T.SAMPLER_RANDOM, integrator=T.INTEGRATOR_BDPT)
+            splat = fb.read_bdpt("splat").view(np.float32).reshape(H, W, 4)
+            out[f"{bdpt_key(case)}_f{f}"] = (fb.read(0), (splat[..., :3] == 0).all(-1))
+        out[f"{bdpt_key(case)}_camera_counts"] = fb.read_bdpt("camera_counts").view(np.int32)
+        out[f"{bdpt_key(case)}_light_counts"] = fb.read_bdpt("light_counts").view(np.int32)
+        fb.close()
+        ds.close()
+    return out
+
+
+def test_bdpt_vs_reference_ieee(bdpt_frames):
+    """Vertex counts bit-exact; radiance bit-exact where no light-tracing splat landed, else
+    within 4e-6 relative (the reference's CAS-atomic sum order is scheduling-dependent)."""
+    z = np.load(os.path.join(GOLDEN, "clref_bdpt_ieee.npz"), allow_pickle=False)
+    assert sorted(z.files) == sorted(bdpt_frames)
+    for k, v in bdpt_frames.items():
+        ref = z[k]
+        if k.endswith("_counts"):
+            np.testing.assert_array_equal(v, ref.view(np.int32), err_msg=k)
+            continue
+        g, nosplat = v
+        g, ref = g[..., :3], ref[..., :3]
+        exact = (g.view(np.uint32) == ref.view(np.uint32)).all(-1)
+        assert exact[nosplat].all(), (k, int((~exact[nosplat]).sum()))
+        close = np.abs(g - ref) <= 4e-6 * (np.abs(g) + np.abs(ref)) + 1e-30
+        assert close.all(), (k, int((~close).sum()))
+
+
+def test_bdpt_vs_reference_fast_math_build(bdpt_frames):
+    z = np.load(os.path.join(GOLDEN, "clref_bdpt_fast.npz"), allow_pickle=False)
+    for k, v in bdpt_frames.items():
+        if k.endswith("_counts"):
+            continue
+        ref = z[k][..., :3].astype(np.float64)
+        d = np.abs(v[0][..., :3] - ref)
+        frac = (d <= 1e-4 * np.maximum(1.0, np.abs(ref))).all(-1).mean()
+        assert frac >= 0.99, (k, frac)
