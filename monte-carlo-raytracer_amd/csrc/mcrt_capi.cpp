@@ -44,6 +44,7 @@ struct mcrt_ctx_s {
     int numCUs = 256;
     bool profiling = false;
     bool fuseShadowExtend = true;   // MCRT_NO_FUSE=1 launches k_shadow and k_extend separately (A/B)
+    bool sortRays = false;          // MCRT_SORT_RAYS=1: global sort of the extension queue (mcrt_raysort.hip)
     std::string error;
     struct Pending {
         int kernel;
@@ -88,6 +89,7 @@ struct mcrt_scene_s {
     int spillCap = 0;
     size_t spillRays = 0;           // rays the spill buffer covers (spillCap words each)
     int* dScratch = nullptr;   // [0] overflow flag, [1..] work counters for API queries
+    float bbLo[3] = {0, 0, 0}, bbHi[3] = {0, 0, 0};   // world bounds (root record of the BVH)
 };
 
 struct mcrt_framebuffer_s {
@@ -99,6 +101,9 @@ struct mcrt_framebuffer_s {
     float* wts = nullptr;
     float4* image = nullptr;
     float4* denoised = nullptr;  // RTDenoisePass output (persistent: the reference keeps its image)
+    float4 *sortO = nullptr, *sortD = nullptr, *sortT = nullptr;   // sorted extension queue (MCRT_SORT_RAYS)
+    void* sortScratch = nullptr;
+    size_t sortTemp = 0;
     float4* display = nullptr;   // post-processed image (mcrt_postprocess)
     float4* hitsP = nullptr;     // primary hits by pixel
     float4* hitsE = nullptr;     // extension hits by queue slot
@@ -286,6 +291,7 @@ MCRT_API mcrt_status mcrt_ctx_create(int device, mcrt_ctx* out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
     if (const char* nf = std::getenv("MCRT_NO_FUSE")) c->fuseShadowExtend = nf[0] != '1';
+    if (const char* sr = std::getenv("MCRT_SORT_RAYS")) c->sortRays = sr[0] == '1';
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(nullptr, MCRT_ERROR_DEVICE, "hipStreamCreate failed");
@@ -584,6 +590,22 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
         s->spillRays = 0;
         s->spillCap = needCap;
     }
+    // world bounds = the root record's two child boxes (or its triangle)
+    float r[16];
+    HIPCHK(ctx, hipMemcpy(r, s->dNodes, 64, hipMemcpyDeviceToHost));
+    int32_t mark;
+    std::memcpy(&mark, &r[12], 4);
+    if (mark >= 0) {
+        const float lo[3] = {std::min(r[0], r[4]), std::min(r[2], r[6]), std::min(r[8], r[10])};
+        const float hi[3] = {std::max(r[1], r[5]), std::max(r[3], r[7]), std::max(r[9], r[11])};
+        for (int a = 0; a < 3; ++a) { s->bbLo[a] = lo[a]; s->bbHi[a] = hi[a]; }
+    } else {
+        for (int a = 0; a < 3; ++a) {
+            const float v0 = r[a], v1 = r[a] + r[4 + a], v2 = r[a] + r[8 + a];
+            s->bbLo[a] = std::min(v0, std::min(v1, v2));
+            s->bbHi[a] = std::max(v0, std::max(v1, v2));
+        }
+    }
     s->buildMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MCRT_OK;
 }
@@ -645,7 +667,8 @@ static void fb_free_bdpt(mcrt_framebuffer fb) {
 static void fb_free(mcrt_framebuffer fb) {
     void* ptrs[] = {fb->radiance, fb->wsum, fb->wts,   fb->image, fb->hitsP, fb->hitsE,    fb->eO[0],
                     fb->eO[1],    fb->eD[0], fb->eD[1], fb->eT[0], fb->eT[1], fb->sO,       fb->sD,
-                    fb->sL,       fb->counters, fb->denoised, fb->display};
+                    fb->sL,       fb->counters, fb->denoised, fb->display, fb->sortO, fb->sortD,
+                    fb->sortT,    fb->sortScratch};
     for (void* p : ptrs)
         if (p) hipFree(p);
     fb_free_bdpt(fb);
@@ -904,6 +927,23 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
             Timed t(ctx, K_SHADEN, extCnt + b - 1, 0);
             mcrt::launch_shadeN(sa, f, b, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1],
                                 fb->eT[(b - 1) & 1], fb->hitsE, fb->radiance, q, (int)fb->N, st);
+        }
+        if (ctx->sortRays && b + 1 < p->max_depth) {   // reorder the extension queue of bounce b
+            if (!fb->sortO) {
+                fb->sortTemp = mcrt::ray_sort_temp_bytes((int)fb->N);
+                HIPCHK(ctx, hipMalloc(&fb->sortO, 16 * fb->N));
+                HIPCHK(ctx, hipMalloc(&fb->sortD, 16 * fb->N));
+                HIPCHK(ctx, hipMalloc(&fb->sortT, 16 * fb->N));
+                HIPCHK(ctx, hipMalloc(&fb->sortScratch, 16 * fb->N + fb->sortTemp));
+            }
+            const float3 lo = make_float3(s->bbLo[0], s->bbLo[1], s->bbLo[2]);
+            const float3 hi = make_float3(s->bbHi[0], s->bbHi[1], s->bbHi[2]);
+            HIPCHK(ctx, mcrt::sort_ray_queue(extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->eT[b & 1], fb->sortO,
+                                             fb->sortD, fb->sortT, (int)fb->N, lo, hi, fb->sortScratch, fb->sortTemp,
+                                             st));
+            std::swap(fb->eO[b & 1], fb->sortO);
+            std::swap(fb->eD[b & 1], fb->sortD);
+            std::swap(fb->eT[b & 1], fb->sortT);
         }
         if (ctx->fuseShadowExtend && b + 1 < p->max_depth) {
             // shadow rays of bounce b + extension rays for bounce b+1 (both from this shading pass)

@@ -102,6 +102,13 @@ namespace mcrt {
 hipError_t gpu_build_bvh(const mcrt_shape* dShapes, const std::vector<uint32_t>& shapeFirst, const uint32_t* dIndices,
                          const float4* dPositions, size_t n, hipStream_t st, float4** nodesOut, int* depthOut);
 }
+// Optional extension-queue sort (mcrt_raysort.hip)
+namespace mcrt {
+size_t ray_sort_temp_bytes(int maxCount);
+hipError_t sort_ray_queue(const int* count, const float4* o, const float4* d, const float4* t, float4* o2, float4* d2,
+                          float4* t2, int maxCount, float3 sceneLo, float3 sceneHi, void* scratch, size_t tempBytes,
+                          hipStream_t st);
+}
 // Host BVH builder (mcrt_bvh.cpp)
 namespace mcrt {
 struct BvhOut {

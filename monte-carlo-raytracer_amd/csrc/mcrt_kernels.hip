@@ -21,6 +21,10 @@
 #ifndef SHADE_BLOCK
 #define SHADE_BLOCK 256
 #endif
+// Group the extension queue by ray-direction octant within each shading block (1 = on).
+#ifndef MCRT_SORT_OCTANT
+#define MCRT_SORT_OCTANT 1
+#endif
 // Occupancy target of the shading kernels (waves per SIMD); 0 = compiler's choice.
 #ifndef MCRT_SHADE_WAVES
 #define MCRT_SHADE_WAVES 0
@@ -294,8 +298,12 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
     int x = 0, y = 0;
     bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y);
     __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
+#if MCRT_SORT_OCTANT
+    __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];
+#endif
     ShadeOut o;
     o.pushS = o.pushE = false;
+    o.eD = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (valid) {
         const mcrt_camera& cam = *camp;
         const int pix = y * (int)f.W + x;
@@ -305,7 +313,13 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
     }
     const int ss = blockAppend<SHADE_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
+#if MCRT_SORT_OCTANT
+    // extension rays grouped by direction octant inside the block's queue slice
+    const int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
+    const int es = blockAppendGrouped<SHADE_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
+#else
     const int es = blockAppend<SHADE_BLOCK / 64>(q.extCountOut, o.pushE, ldsWave);
+#endif
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 
@@ -317,9 +331,13 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shadeN(SceneArg
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = *countIn;
     __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
+#if MCRT_SORT_OCTANT
+    __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];
+#endif
     if ((int)blockIdx.x * SHADE_BLOCK >= n) return;   // whole block past the queue: uniform exit
     ShadeOut o;
     o.pushS = o.pushE = false;
+    o.eD = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (i < n) {
         const float4 O = qO[i], D = qD[i], Tp = qT[i];
         const int pix = __float_as_int(O.w);
@@ -332,7 +350,13 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shadeN(SceneArg
     }
     const int ss = blockAppend<SHADE_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
+#if MCRT_SORT_OCTANT
+    // extension rays grouped by direction octant inside the block's queue slice
+    const int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
+    const int es = blockAppendGrouped<SHADE_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
+#else
     const int es = blockAppend<SHADE_BLOCK / 64>(q.extCountOut, o.pushE, ldsWave);
+#endif
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 

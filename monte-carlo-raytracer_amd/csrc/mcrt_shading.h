@@ -117,6 +117,37 @@ MCRT_DEV int blockAppend(int* counter, bool pred, int* ldsWave /* NW + 1 ints */
     return slot;
 }
 
+// Block-aggregated append grouped by a small key (G groups): within the block's slice of the
+// queue the records are ordered by group (then wave, then lane), so the traversal waves that
+// read the queue see rays of one group (e.g. the direction octant) together.  One global
+// atomic per block; every thread of the block must call.  lds: NW * G + 1 ints.
+template <int NW, int G>
+MCRT_DEV int blockAppendGrouped(int* counter, bool pred, int group, int* lds) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const unsigned long long m = __ballot(pred && group == g);
+        if (g == group) mine = m;
+        if (lane == 0) lds[g * NW + wv] = __popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int sum = 0;
+        for (int i = 0; i < G * NW; ++i) {   // (group, wave) order
+            const int c = lds[i];
+            lds[i] = sum;
+            sum += c;
+        }
+        lds[G * NW] = sum ? atomicAdd(counter, sum) : 0;
+    }
+    __syncthreads();
+    const int prefix = __builtin_amdgcn_mbcnt_hi((unsigned)(mine >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mine, 0u));
+    const int slot = lds[G * NW] + (pred ? lds[group * NW + wv] : 0) + prefix;
+    __syncthreads();
+    return slot;
+}
+
 // May be called under divergent control flow: only active lanes take part.
 MCRT_DEV int waveAppend(int* counter, bool pred) {
     const unsigned long long m = __ballot(pred);
