@@ -583,7 +583,7 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
     mcrt_ctx ctx = s->ctx;
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
-    const int needCap = ((s->bvhDepth + 2 + 14) / 15) * 15;
+    const int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries
     if (needCap != s->spillCap) {
         if (s->dSpill) hipFree(s->dSpill);
         s->dSpill = nullptr;

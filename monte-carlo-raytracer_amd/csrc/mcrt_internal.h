@@ -59,7 +59,7 @@ struct BdptQueue {
 struct TraceCtx {
     const float4* nodes;   // 4 float4 per node (mcrt_bvh.cpp): internal = child boxes + indices, leaf = triangle
     uint32_t* spill;
-    int spillCap;           // spill entries per ray (multiple of STACK_LDS - 1)
+    int spillCap;           // spill entries per ray (a multiple of STACK_LDS)
     int* overflow;
 };
 
