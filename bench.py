@@ -111,6 +111,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
+    ap.add_argument("--save-image", default=None, help="rank 0 saves the final accumulated image (.npy)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, the product path); gloo only rehearses N ranks on one GPU")
     ap.add_argument("--device-build", action="store_true", help="on-device linear BVH instead of the RR-identical host build")
     args = ap.parse_args()
 
@@ -121,8 +124,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "gloo":   # rehearsal: every rank on cuda:0 of a 1-GPU box
+            local = local % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from mcrt import dist as mdist
     from mcrt import lib, scenes
@@ -203,6 +211,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if args.save_image and rank == 0:
+        np.save(args.save_image, fb.read(2))
     kstats = ctx.kernel_stats() if not args.no_kernel_timing else {}
     ctx.set_profiling(False)
 

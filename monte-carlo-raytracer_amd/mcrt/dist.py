@@ -51,6 +51,13 @@ def frame_split(num_frames, world, rank):
 def reduce_accumulators(wsum, wts, dst=0, group=None):
     """Sum the per-rank accumulators into rank `dst` (torch tensors, in place on dst)."""
     import torch.distributed as dist
+    if wsum.is_cuda and dist.get_backend(group) == "gloo":   # gloo rehearsal: reduce via host copies
+        hs, hw = wsum.cpu(), wts.cpu()
+        dist.reduce(hs, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        dist.reduce(hw, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        wsum.copy_(hs)
+        wts.copy_(hw)
+        return
     dist.reduce(wsum, dst=dst, op=dist.ReduceOp.SUM, group=group)
     dist.reduce(wts, dst=dst, op=dist.ReduceOp.SUM, group=group)
 
