@@ -195,6 +195,19 @@ typedef struct {
      * tens of ms), same record format and triangle data, different tree (equal-t hit ties may
      * resolve differently from the reference).  Ignores the three SAH fields. */
     int   device_build;
+    /* Two-level (instanced) structure: RadeonRays' IntersectorTwoLevel, which RR selects when a
+     * shape is an instance (RTScene::attachMesh -> CreateInstance for every further entity that
+     * shares a mesh, APP/raytracing/scene/RTScene.cpp:572-596) unless "bvh.forceflat"; forced by
+     * "bvh.force2level" (RR/src/device/calc_intersection_device.cpp:68-105, defaults off,
+     * PathTracingSettings.h:239-240).  Shapes with equal (startIdx, startVertex, numTriangles)
+     * are instances of the first one; each keeps its own transform, shape id and material.
+     * Host-built (device_build applies to the flat structure only). */
+    int   force_2level;
+    int   force_flat;
+    /* Per-shape world-to-local matrices (Shape::SetTransform's minv, RR/include/radeon_rays.h;
+     * the reference passes Transform::getWorldToLocalMatrix).  NULL: the transpose of each
+     * shape's toWorldInverseTranspose.  Used by the two-level structure only. */
+    const mcrt_mat4* world_to_local;
 } mcrt_accel_opts;
 
 #define MCRT_SAMPLER_SOBOL  0   /* KRN/samplers.cl:16 */
@@ -270,6 +283,17 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene scene, const mcrt_accel_opts* o
 /* Build statistics: node count, bytes on device, host build milliseconds. */
 MCRT_API mcrt_status mcrt_accel_info(mcrt_scene scene, uint64_t* num_nodes, uint64_t* device_bytes,
                                      double* build_ms, uint32_t* num_triangles);
+/* Which structure mcrt_accel_build made: two_level 0 (flat Bvh2) / 1 (instanced), distinct
+ * meshes and instances of the two-level one, deepest traversal path. */
+MCRT_API mcrt_status mcrt_accel_layout(mcrt_scene scene, int32_t* two_level, uint32_t* num_meshes,
+                                       uint32_t* num_instances, int32_t* depth);
+/* Host-only build of the structure mcrt_accel_build would upload (no device needed): 64-B
+ * records (mcrt_bvh.cpp / mcrt_bvh2l.cpp layouts) into out_records (up to max_records; may be
+ * NULL to query *num_records); info[4] = {two_level, top-level records, depth, meshes}.
+ * For tools and tests (e.g. pinning the trees against the reference builders). */
+MCRT_API mcrt_status mcrt_accel_build_host_records(const mcrt_scene_desc* desc, const mcrt_accel_opts* opts,
+                                                   float* out_records, uint64_t max_records,
+                                                   uint64_t* num_records, int32_t* info);
 
 /* ------------------------------------------------------------------------ */
 /* Ray queries on DEVICE buffers (IntersectionApi::QueryIntersection /

@@ -501,13 +501,8 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
         const bool isCamera = (tag & 1) == 0;
         float4* V = isCamera ? b.camV : b.lightV;
         const float4 hit = hits[i];
-        const int tri = __float_as_int(hit.w);
-        int shapeIdx = -1, primIdx = -1;
-        if (tri >= 0) {
-            shapeIdx = __float_as_int(s.nodes[4 * tri].w);
-            primIdx = __float_as_int(s.nodes[4 * tri + 1].w);
-        }
-        const mcrt_shape* shape = tri >= 0 ? &s.shapes[shapeIdx] : nullptr;
+        const int shapeIdx = __float_as_int(hit.z), primIdx = __float_as_int(hit.w);
+        const mcrt_shape* shape = shapeIdx >= 0 ? &s.shapes[shapeIdx] : nullptr;
         if (shape && shape->materialId != -1) {
             (isCamera ? b.camCount : b.lightCount)[pix] = depth + 1;
             const f3 rayD = ld3(Dd);
@@ -815,6 +810,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
 
 // Any hit over the connection queue (RR occluded_main semantics): occluded own strategies are
 // zeroed in their slot, unoccluded light-tracing strategies splatted (BDPT.cl:888-899).
+template <bool TL>
 __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const int* __restrict__ count,
                                                  const float4* __restrict__ sO, const float4* __restrict__ sD,
                                                  const float4* __restrict__ sL) {
@@ -830,12 +826,11 @@ __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const i
     r.d = ld3(d);
     r.tmax = o.w;
     r.mask = -1;
-    float t;
-    const int tri = traverse<true>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+    const bool occluded = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow);
     const int code = __float_as_int(d.w);
     if (code >= 0) {
-        if (tri >= 0) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    } else if (tri < 0) {
+        if (occluded) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    } else if (!occluded) {
         const float4 L = sL[i];
         float* dst = reinterpret_cast<float*>(&b.splat[~code]);
         atomicAdd(dst + 0, L.x);
@@ -889,8 +884,9 @@ void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
     hipLaunchKernelGGL(k_bdpt_connect, dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, q);
 }
 void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st) {
-    hipLaunchKernelGGL(k_bdpt_vis, dim3((maxCount + 63) / 64 > 0 ? (maxCount + 63) / 64 : 1), dim3(64), 0, st, c, b,
-                       q.count, q.o, q.d, q.t);
+    const int blocks = (maxCount + 63) / 64 > 0 ? (maxCount + 63) / 64 : 1;
+    hipLaunchKernelGGL(c.twoLevel ? k_bdpt_vis<true> : k_bdpt_vis<false>, dim3(blocks), dim3(64), 0, st, c, b, q.count,
+                       q.o, q.d, q.t);
 }
 void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + 255) / 256;

@@ -84,6 +84,8 @@ struct mcrt_scene_s {
     uint32_t numTris = 0;
     double buildMs = 0.0;
     int bvhDepth = 0;
+    bool twoLevel = false;          // instanced scene: two-level records (mcrt_bvh2l.cpp)
+    int numMeshes = 0, numInstances = 0;
     // traversal scratch
     uint32_t* dSpill = nullptr;
     int spillCap = 0;
@@ -251,6 +253,7 @@ static TraceCtx trace_ctx(mcrt_scene s) {
     c.spill = s->dSpill;
     c.spillCap = s->spillCap;
     c.overflow = s->dScratch;
+    c.twoLevel = s->twoLevel ? 1 : 0;
     return c;
 }
 
@@ -512,7 +515,7 @@ MCRT_API mcrt_status mcrt_scene_update_shapes(mcrt_scene s, const mcrt_shape* sh
     return replace_array(s, &s->dShapes, sh, sizeof(mcrt_shape) * n);
 }
 
-static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_point t0);
+static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_point t0, const float* box6);
 
 MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts) {
     if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
@@ -526,6 +529,34 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     for (auto& sh : s->shapes) n += sh.numTriangles;
     if (n == 0) return fail(ctx, MCRT_ERROR_INVALID_ARG, "scene has no triangles (RR: Commit on empty scene throws)");
     if (n > (size_t)0x7fffffff) return fail(ctx, MCRT_ERROR_INVALID_ARG, "too many triangles");
+    // IntersectorTwoLevel when forced or when a mesh is shared, unless flat is forced
+    // (CalcIntersectionDevice::Preprocess, RR/src/device/calc_intersection_device.cpp:68-105)
+    const bool use2 = (opts && opts->force_2level) ||
+                      (!(opts && opts->force_flat) && mcrt::shapes_are_instanced(s->shapes.data(), s->shapes.size()));
+    if (use2) {
+        int threads = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+        mcrt::Bvh2lOut b2;
+        if (!mcrt::build_bvh2l(s->shapes.data(), s->shapes.size(), s->indices.data(), s->positions.data(),
+                               opts ? opts->world_to_local : nullptr, cost, bins, sah, threads, b2))
+            return fail(ctx, MCRT_ERROR_INVALID_ARG, "two-level BVH build failed");
+        hipSetDevice(ctx->device);
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (s->dNodes) hipFree(s->dNodes);
+        if (s->dTris) hipFree(s->dTris);
+        s->dNodes = s->dTris = nullptr;
+        hipError_t e = hipMalloc(&s->dNodes, 64 * b2.numNodes);
+        if (e == hipSuccess) e = hipMemcpy(s->dNodes, b2.records.data(), 64 * b2.numNodes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, std::string("BVH upload: ") + hipGetErrorString(e));
+        s->numNodes = b2.numNodes;
+        s->numTris = (uint32_t)n;
+        s->bvhDepth = b2.depth;
+        s->twoLevel = true;
+        s->numMeshes = b2.numMeshes;
+        s->numInstances = b2.numInstances;
+        return finish_accel(s, t0, b2.topBox);
+    }
+    s->twoLevel = false;
+    s->numMeshes = s->numInstances = 0;
     if (opts && opts->device_build) {   // on-device linear BVH (mcrt_gpubuild.hip)
         hipSetDevice(ctx->device);
         std::vector<uint32_t> first(s->shapes.size());
@@ -543,7 +574,7 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
         s->numNodes = 2 * n - 1;
         s->numTris = (uint32_t)n;
         s->bvhDepth = depth;
-        return finish_accel(s, t0);
+        return finish_accel(s, t0, nullptr);
     }
     std::vector<float> tri(9 * n);
     std::vector<int32_t> shapeOf(n), primOf(n);
@@ -574,12 +605,12 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     s->bvhDepth = bvh.depth;
     mcrt::free_bvh(bvh);
     if (e != hipSuccess) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, std::string("BVH upload: ") + hipGetErrorString(e));
-    return finish_accel(s, t0);
+    return finish_accel(s, t0, nullptr);
 }
 
 // traversal scratch: overflow flag; per-ray spill columns deep enough for the tree
 // (allocated by ensure_spill for the largest launch)
-static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_point t0) {
+static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_point t0, const float* box6) {
     mcrt_ctx ctx = s->ctx;
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
@@ -589,6 +620,11 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
         s->dSpill = nullptr;
         s->spillRays = 0;
         s->spillCap = needCap;
+    }
+    if (box6) {
+        for (int a = 0; a < 3; ++a) { s->bbLo[a] = box6[a]; s->bbHi[a] = box6[3 + a]; }
+        s->buildMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return MCRT_OK;
     }
     // world bounds = the root record's two child boxes (or its triangle)
     float r[16];
@@ -617,6 +653,78 @@ MCRT_API mcrt_status mcrt_accel_info(mcrt_scene s, uint64_t* num_nodes, uint64_t
     if (device_bytes) *device_bytes = 64ull * s->numNodes;
     if (build_ms) *build_ms = s->buildMs;
     if (num_triangles) *num_triangles = s->numTris;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_accel_layout(mcrt_scene s, int32_t* two_level, uint32_t* num_meshes,
+                                       uint32_t* num_instances, int32_t* depth) {
+    if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
+    if (!s->dNodes) return fail(s->ctx, MCRT_ERROR_NOT_READY, "mcrt_accel_build has not been called");
+    if (two_level) *two_level = s->twoLevel ? 1 : 0;
+    if (num_meshes) *num_meshes = (uint32_t)s->numMeshes;
+    if (num_instances) *num_instances = (uint32_t)s->numInstances;
+    if (depth) *depth = s->bvhDepth;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_accel_build_host_records(const mcrt_scene_desc* d, const mcrt_accel_opts* opts,
+                                                   float* out_records, uint64_t max_records, uint64_t* num_records,
+                                                   int32_t* info) {
+    if (!d || !d->shapes || !d->indices || !d->positions || !num_records)
+        return fail(nullptr, MCRT_ERROR_INVALID_ARG, "invalid arguments");
+    const float cost = opts ? opts->traversal_cost : 10.0f;
+    const int bins = opts ? opts->num_bins : 64;
+    const bool sah = opts ? opts->use_sah != 0 : true;
+    if (bins < 2 || bins > 4096) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "num_bins out of range");
+    for (uint32_t i = 0; i < d->num_shapes; ++i) {
+        const mcrt_shape& sh = d->shapes[i];
+        if ((uint64_t)sh.startIdx + 3ull * sh.numTriangles > d->num_indices)
+            return fail(nullptr, MCRT_ERROR_INVALID_ARG, "shape indices out of range");
+        for (uint64_t k = 0; k < 3ull * sh.numTriangles; ++k)
+            if ((uint64_t)sh.startVertex + d->indices[sh.startIdx + k] >= d->num_vertices)
+                return fail(nullptr, MCRT_ERROR_INVALID_ARG, "vertex index out of range");
+    }
+    const int threads = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+    const bool use2 = (opts && opts->force_2level) ||
+                      (!(opts && opts->force_flat) && mcrt::shapes_are_instanced(d->shapes, d->num_shapes));
+    int32_t inf[4] = {use2 ? 1 : 0, 0, 0, 0};
+    if (use2) {
+        mcrt::Bvh2lOut b2;
+        if (!mcrt::build_bvh2l(d->shapes, d->num_shapes, d->indices, d->positions, opts ? opts->world_to_local : nullptr,
+                               cost, bins, sah, threads, b2))
+            return fail(nullptr, MCRT_ERROR_INVALID_ARG, "two-level BVH build failed");
+        *num_records = b2.numNodes;
+        if (out_records) std::memcpy(out_records, b2.records.data(), 64 * std::min<uint64_t>(max_records, b2.numNodes));
+        inf[1] = (int32_t)b2.topNodes;
+        inf[2] = b2.depth;
+        inf[3] = b2.numMeshes;
+    } else {
+        size_t n = 0;
+        for (uint32_t i = 0; i < d->num_shapes; ++i) n += d->shapes[i].numTriangles;
+        if (n == 0) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene has no triangles");
+        std::vector<float> tri(9 * n);
+        std::vector<int32_t> shapeOf(n), primOf(n);
+        size_t k = 0;
+        for (uint32_t si = 0; si < d->num_shapes; ++si) {
+            const mcrt_shape& sh = d->shapes[si];
+            for (uint32_t f = 0; f < sh.numTriangles; ++f, ++k) {
+                for (int c = 0; c < 3; ++c)
+                    xformPoint(sh.toWorldTransform, d->positions[sh.startVertex + d->indices[sh.startIdx + 3 * f + c]],
+                               &tri[9 * k + 3 * c]);
+                shapeOf[k] = (int32_t)si;
+                primOf[k] = (int32_t)f;
+            }
+        }
+        mcrt::BvhOut bvh;
+        if (!mcrt::build_bvh(tri.data(), shapeOf.data(), primOf.data(), n, cost, bins, sah, threads, bvh))
+            return fail(nullptr, MCRT_ERROR_INVALID_ARG, "BVH build failed");
+        *num_records = bvh.numNodes;
+        if (out_records) std::memcpy(out_records, bvh.nodes, 64 * std::min<uint64_t>(max_records, bvh.numNodes));
+        inf[1] = (int32_t)bvh.numNodes;
+        inf[2] = bvh.depth;
+        mcrt::free_bvh(bvh);
+    }
+    if (info) std::memcpy(info, inf, sizeof(inf));
     return MCRT_OK;
 }
 

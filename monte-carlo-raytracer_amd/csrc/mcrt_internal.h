@@ -58,6 +58,8 @@ struct BdptQueue {
 
 struct TraceCtx {
     const float4* nodes;   // 4 float4 per node (mcrt_bvh.cpp): internal = child boxes + indices, leaf = triangle
+                           // two-level (mcrt_bvh2l.cpp): + instance records (world->object rows, bottom root)
+    int twoLevel;          // selects the kernels' two-level instantiation (launch-time, not per lane)
     uint32_t* spill;
     int spillCap;           // spill entries per ray (a multiple of STACK_LDS)
     int* overflow;
@@ -123,4 +125,19 @@ struct BvhOut {
 bool build_bvh(const float* tri, const int32_t* shapeOf, const int32_t* primOf, std::size_t n, float cost, int bins,
                bool sah, int threads, BvhOut& out);
 void free_bvh(BvhOut& out);
+}  // namespace mcrt
+// Host two-level (instanced) build (mcrt_bvh2l.cpp)
+namespace mcrt {
+struct Bvh2lOut {
+    std::vector<float> records;   // 16 floats per record
+    std::size_t numNodes = 0, topNodes = 0;
+    int numMeshes = 0, numInstances = 0;
+    int depth = 0;                // deepest top + bottom path (+ the return marker)
+    float topBox[6] = {};         // world bounds (lo xyz, hi xyz)
+};
+// true when two shapes share (startIdx, startVertex, numTriangles): RTScene::attachMesh then
+// creates RadeonRays instances and RR switches to its two-level intersector
+bool shapes_are_instanced(const mcrt_shape* shapes, std::size_t n);
+bool build_bvh2l(const mcrt_shape* shapes, std::size_t nshapes, const uint32_t* indices, const mcrt_float4* positions,
+                 const mcrt_mat4* worldToLocal, float cost, int bins, bool sah, int threads, Bvh2lOut& out);
 }  // namespace mcrt

@@ -41,7 +41,7 @@
 // 8 waves per SIMD resident and refills them as they finish -- measured faster on MI355X
 // than a persistent grid pulling work from an atomic queue.
 // ---------------------------------------------------------------------------
-template <bool ANY>
+template <bool ANY, bool TL>
 __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* __restrict__ rays, int n,
                                                    mcrt_intersection* __restrict__ hits, int* __restrict__ occl) {
     __shared__ uint32_t lds[STACK_LDS * 64];
@@ -55,15 +55,16 @@ __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* _
     r.d = ld3(rr.d);
     r.tmax = rr.o.w;
     r.mask = rr.extra[0];
-    float t;
-    const int tri = traverse<ANY>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
     if (ANY) {
-        occl[i] = tri >= 0 ? 1 : -1;
-    } else if (tri >= 0) {
-        const float4 h4 = closestRecord(c.nodes, r, tri, t);
+        occl[i] = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow) ? 1 : -1;
+        return;
+    }
+    float t;
+    const float4 h4 = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+    if (__float_as_int(h4.z) >= 0) {
         mcrt_intersection h;
-        h.shapeid = __float_as_int(c.nodes[4 * tri].w);
-        h.primid = __float_as_int(c.nodes[4 * tri + 1].w);
+        h.shapeid = __float_as_int(h4.z);
+        h.primid = __float_as_int(h4.w);
         h.padding[0] = h.padding[1] = 0;
         h.uvwt.x = h4.x; h.uvwt.y = h4.y; h.uvwt.z = 0.0f; h.uvwt.w = t;
         hits[i] = h;
@@ -75,6 +76,7 @@ __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* _
 
 // Camera ray generation fused with the first closest-hit query (RTPrimaryRaysPass):
 // one workgroup = one wave = one 8x8 pixel tile of the rank's bands.
+template <bool TL>
 __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 float4* __restrict__ hitOut) {
     __shared__ uint32_t lds[STACK_LDS * 64];
@@ -89,12 +91,12 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
     r.tmax = 1000.0f;
     r.mask = -1;
     float t;
-    const int tri = traverse<false>(c.nodes, r, lds + lane, raySpill(c, tile, lane), c.spillCap, c.overflow, t);
-    hitOut[(size_t)y * f.W + x] = closestRecord(c.nodes, r, tri, t);
+    hitOut[(size_t)y * f.W + x] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, tile, lane), c.spillCap, c.overflow, t);
 }
 
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
 // The grid covers the queue's capacity; workgroups past the device-side count exit at once.
+template <bool TL>
 __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ qO,
                                                const float4* __restrict__ qD, float4* __restrict__ hitOut) {
     __shared__ uint32_t lds[STACK_LDS * 64];
@@ -110,12 +112,12 @@ __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict
     r.tmax = RT_MAX_TRACE_F;
     r.mask = -1;
     float t;
-    const int tri = traverse<false>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
-    hitOut[i] = closestRecord(c.nodes, r, tri, t);
+    hitOut[i] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
 }
 
 // Any hit over the shadow queue + ShadowPass (PathTracing.cl:186-217):
 // sO = (o.xyz, tmax), sD = (d.xyz, pix), sL = throughput * L; radiance[pix] += L * V.
+template <bool TL>
 __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ sO,
                                                const float4* __restrict__ sD, const float4* __restrict__ sL,
                                                float4* __restrict__ radiance) {
@@ -131,9 +133,7 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     r.d = ld3(d);
     r.tmax = o.w;
     r.mask = -1;
-    float t;
-    const int tri = traverse<true>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
-    const float V = tri >= 0 ? 0.0f : 1.0f;
+    const float V = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow) ? 0.0f : 1.0f;
     const int pix = __float_as_int(d.w);
     float4 acc = radiance[pix];
     acc.x += L.x * V;
@@ -145,6 +145,7 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
 // Shadow rays of bounce b and extension rays of bounce b+1 in ONE launch: both only depend on
 // the shading of bounce b.  Extension workgroups come first (their rays are the longer ones),
 // shadow workgroups fill the extension launch's divergent tail instead of waiting for it.
+template <bool TL>
 __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __restrict__ extCount,
                                                       const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                       float4* __restrict__ hitOut, const int* __restrict__ shadowCount,
@@ -164,8 +165,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.tmax = RT_MAX_TRACE_F;
         r.mask = -1;
         float t;
-        const int tri = traverse<false>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
-        hitOut[i] = closestRecord(c.nodes, r, tri, t);
+        hitOut[i] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
     } else {
         const int ns = *shadowCount;
         const int i = ((int)blockIdx.x - eb) * 64 + lane;
@@ -176,9 +176,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.d = ld3(d);
         r.tmax = o.w;
         r.mask = -1;
-        float t;
-        const int tri = traverse<true>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
-        const float V = tri >= 0 ? 0.0f : 1.0f;
+        const float V = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow) ? 0.0f : 1.0f;
         const int pix = __float_as_int(d.w);
         float4 acc = radiance[pix];
         acc.x += L.x * V;
@@ -200,10 +198,8 @@ struct ShadeOut {
 MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pix, float4 hit, f3 dir, f3 throughput,
                       int prevFlags, ShadeOut& o) {
     f3 add = splat3(0.0f);
-    const int tri = __float_as_int(hit.w);
-    if (tri < 0 || s.numLights <= 0) return add;
-    const float4 A = s.nodes[4 * tri], E1 = s.nodes[4 * tri + 1];
-    const int shapeIdx = __float_as_int(A.w), primIdx = __float_as_int(E1.w);
+    const int shapeIdx = __float_as_int(hit.z), primIdx = __float_as_int(hit.w);
+    if (shapeIdx < 0 || s.numLights <= 0) return add;
     const mcrt_shape& shape = s.shapes[shapeIdx];
     Frame si = computeSurfaceInteraction(s, shapeIdx, primIdx, f2{hit.x, hit.y});
     const f3 wo = -dir;
@@ -480,26 +476,34 @@ namespace mcrt {
 void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, mcrt_intersection* hits, int* occl,
                        hipStream_t st) {
     const dim3 g((n + 63) / 64), b(64);
-    if (any) hipLaunchKernelGGL(k_trace_rays<true>, g, b, 0, st, c, rays, n, hits, occl);
-    else hipLaunchKernelGGL(k_trace_rays<false>, g, b, 0, st, c, rays, n, hits, occl);
+    if (c.twoLevel) {
+        if (any) hipLaunchKernelGGL((k_trace_rays<true, true>), g, b, 0, st, c, rays, n, hits, occl);
+        else hipLaunchKernelGGL((k_trace_rays<false, true>), g, b, 0, st, c, rays, n, hits, occl);
+    } else {
+        if (any) hipLaunchKernelGGL((k_trace_rays<true, false>), g, b, 0, st, c, rays, n, hits, occl);
+        else hipLaunchKernelGGL((k_trace_rays<false, false>), g, b, 0, st, c, rays, n, hits, occl);
+    }
 }
 void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st) {
-    hipLaunchKernelGGL(k_primary, dim3(f.numTiles), dim3(64), 0, st, c, f, cam, hits);
+    hipLaunchKernelGGL(c.twoLevel ? k_primary<true> : k_primary<false>, dim3(f.numTiles), dim3(64), 0, st, c, f, cam,
+                       hits);
 }
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
                    hipStream_t st) {
-    hipLaunchKernelGGL(k_extend, dim3((maxCount + 63) / 64), dim3(64), 0, st, c, count, qO, qD, hits);
+    hipLaunchKernelGGL(c.twoLevel ? k_extend<true> : k_extend<false>, dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+                       count, qO, qD, hits);
 }
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st) {
-    hipLaunchKernelGGL(k_shadow, dim3((maxCount + 63) / 64), dim3(64), 0, st, c, count, sO, sD, sL, radiance);
+    hipLaunchKernelGGL(c.twoLevel ? k_shadow<true> : k_shadow<false>, dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+                       count, sO, sD, sL, radiance);
 }
 void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
                           const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
                           float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
     const int blocks = (maxExt + 63) / 64 + (maxShadow + 63) / 64;
-    hipLaunchKernelGGL(k_shadow_extend, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, extCount, qO, qD, hits,
-                       shadowCount, sO, sD, sL, radiance);
+    hipLaunchKernelGGL(c.twoLevel ? k_shadow_extend<true> : k_shadow_extend<false>, dim3(blocks > 0 ? blocks : 1),
+                       dim3(64), 0, st, c, extCount, qO, qD, hits, shadowCount, sO, sD, sL, radiance);
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {

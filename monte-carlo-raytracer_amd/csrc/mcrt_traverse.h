@@ -140,13 +140,178 @@ MCRT_DEV f2 triBary(f3 p, float4 A, float4 E1, float4 E2) {
     return f2{b1, b2};
 }
 
-// hit record of the closest-hit kernels: (u, v, t, triangle) -- intersect_bvh2_lds.cl:200-215
+// Hit record of the closest-hit kernels: (u, v, shape index bits, primitive index bits), shape
+// = -1 on a miss (barycentrics: intersect_bvh2_lds.cl:200-215).  The shading kernels read the
+// shape and primitive from here, not from the BVH.
 MCRT_DEV float4 closestRecord(const float4* __restrict__ nodes, const TraceRay& r, int tri, float t) {
-    if (tri < 0) return make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+    if (tri < 0) return make_float4(0.f, 0.f, __int_as_float(-1), __int_as_float(-1));
     const float4 A = nodes[4 * tri], E1 = nodes[4 * tri + 1], E2 = nodes[4 * tri + 2];
     const f3 p = r.o + t * r.d;
     const f2 uv = triBary(p, A, E1, E2);
-    return make_float4(uv.x, uv.y, t, __int_as_float(tri));
+    return make_float4(uv.x, uv.y, A.w, E1.w);
+}
+
+// ---------------------------------------------------------------------------
+// Two-level (instanced) traversal over the mcrt_bvh2l.cpp records: RadeonRays'
+// IntersectorTwoLevel semantics (intersect_bvh2level_skiplinks.cl:112-318) -- at a top-level
+// leaf the ray moves into the shape's object space (world-to-local rows), the shape's own
+// BVH is traversed, then the world ray is restored -- on our nearest-first stack traversal
+// (the reference walks fixed-order skip links; the closest hit does not depend on the order
+// except between triangles at exactly the same t).
+// ---------------------------------------------------------------------------
+#define BVH_INSTANCE_MARK (-2)
+
+// transform_point / transform_vector (intersect_bvh2level_skiplinks.cl:88-106); ext-vector
+// arithmetic contracts exactly like the OpenCL source
+MCRT_DEV f3 xfPoint(float4 m0, float4 m1, float4 m2, f3 p) {
+    f3 r;
+    r.x = m0.x * p.x + m0.y * p.y + m0.z * p.z + m0.w;
+    r.y = m1.x * p.x + m1.y * p.y + m1.z * p.z + m1.w;
+    r.z = m2.x * p.x + m2.y * p.y + m2.z * p.z + m2.w;
+    return r;
+}
+MCRT_DEV f3 xfVector(float4 m0, float4 m1, float4 m2, f3 p) {
+    f3 r;
+    r.x = m0.x * p.x + m0.y * p.y + m0.z * p.z;
+    r.y = m1.x * p.x + m1.y * p.y + m1.z * p.z;
+    r.z = m2.x * p.x + m2.y * p.y + m2.z * p.z;
+    return r;
+}
+
+// Returns the hit triangle record or -1; hitInst = the instance record it was hit through.
+template <bool ANY>
+MCRT_DEV int traverse2L(const float4* __restrict__ nodes, const TraceRay& r, uint32_t* stk, uint32_t* spill,
+                        int spillCap, int* overflowFlag, float& tHit, int& hitInst) {
+    constexpr int DONE = -1, POP = -2, RESTORE = -3;
+    const f3 winv = safeInvDir(r.d);
+    const f3 woxi = -r.o * winv;
+    TraceRay cr = r;   // current-space ray (world at the top level, object below an instance)
+    f3 inv = winv, oxi = woxi;
+    float t = r.tmax;
+    int hit = -1, hinst = -1, inst = -1;
+    int node = 0;
+    stk[0] = (uint32_t)DONE;
+    int sp = 1, spillTop = 0;
+    auto push = [&](int v) {
+        if (sp == STACK_LDS) {
+            if (spillTop + STACK_LDS - 1 <= spillCap) {
+                for (int k = 1; k < STACK_LDS; ++k) spill[(size_t)(spillTop + k - 1) * 64] = stk[k * 64];
+                spillTop += STACK_LDS - 1;
+            } else {
+                *overflowFlag = 1;
+            }
+            sp = 1;
+        }
+        stk[sp * 64] = (uint32_t)v;
+        ++sp;
+    };
+    auto pop = [&]() -> int {
+        --sp;
+        int v = (int)stk[sp * 64];
+        if (v == DONE && spillTop > 0) {
+            spillTop -= STACK_LDS - 1;
+            for (int k = 1; k < STACK_LDS; ++k) stk[k * 64] = spill[(size_t)(spillTop + k - 1) * 64];
+            sp = STACK_LDS - 1;
+            v = (int)stk[sp * 64];
+        }
+        return v;
+    };
+    while (node != DONE) {
+        const float4 n0 = nodes[4 * node + 0];
+        const float4 n1 = nodes[4 * node + 1];
+        const float4 n2 = nodes[4 * node + 2];
+        const int4 n3 = *reinterpret_cast<const int4*>(&nodes[4 * node + 3]);
+        asm volatile("" ::"v"(n1.w), "v"(n2.w));
+        int next;
+        if (n3.x >= 0) {
+            const float ax0 = fmaf(n0.x, inv.x, oxi.x), ax1 = fmaf(n0.y, inv.x, oxi.x);
+            const float ay0 = fmaf(n0.z, inv.y, oxi.y), ay1 = fmaf(n0.w, inv.y, oxi.y);
+            const float az0 = fmaf(n2.x, inv.z, oxi.z), az1 = fmaf(n2.y, inv.z, oxi.z);
+            const float bx0 = fmaf(n1.x, inv.x, oxi.x), bx1 = fmaf(n1.y, inv.x, oxi.x);
+            const float by0 = fmaf(n1.z, inv.y, oxi.y), by1 = fmaf(n1.w, inv.y, oxi.y);
+            const float bz0 = fmaf(n2.z, inv.z, oxi.z), bz1 = fmaf(n2.w, inv.z, oxi.z);
+            const float a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
+            const float a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), t);
+            const float b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
+            const float b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), t);
+            const bool h0 = a0 <= a1, h1 = b0 <= b1;
+            const bool c1first = h1 && (a0 > b0);
+            if (h0 && h1) push(c1first ? n3.x : n3.y);
+            next = (h0 || h1) ? ((c1first || !h0) ? n3.y : n3.x) : POP;
+        } else if (n3.x == BVH_INSTANCE_MARK) {
+            next = POP;
+            if (r.mask != n3.z) {   // RR_RAY_MASK at the shape (skiplinks.cl:225-230)
+                cr.o = xfPoint(n0, n1, n2, r.o);
+                cr.d = xfVector(n0, n1, n2, r.d);
+                inv = safeInvDir(cr.d);
+                oxi = -cr.o * inv;
+                inst = node;
+                push(RESTORE);
+                next = n3.y;
+            }
+        } else {
+            next = POP;
+            const float th = triHit(cr, n0, n1, n2, t);
+            if (th < t) {
+                t = th;
+                hit = node;
+                hinst = inst;
+                if (ANY) next = DONE;
+            }
+        }
+        if (next == POP) {
+            next = pop();
+            if (next == RESTORE) {   // back to the top level (skiplinks.cl:287-297)
+                cr = r;
+                inv = winv;
+                oxi = woxi;
+                inst = -1;
+                next = pop();
+            }
+        }
+        node = next;
+    }
+    tHit = t;
+    hitInst = hinst;
+    return hit;
+}
+
+// Closest-hit record through an instance: the object-space ray is recomputed from the instance
+// rows (same arithmetic as during traversal), barycentrics in object space as the reference.
+MCRT_DEV float4 closestRecord2L(const float4* __restrict__ nodes, const TraceRay& r, int tri, int inst, float t) {
+    if (tri < 0) return make_float4(0.f, 0.f, __int_as_float(-1), __int_as_float(-1));
+    const float4 m0 = nodes[4 * inst], m1 = nodes[4 * inst + 1], m2 = nodes[4 * inst + 2];
+    const int shape = reinterpret_cast<const int4*>(&nodes[4 * inst + 3])->z;
+    TraceRay cr = r;
+    cr.o = xfPoint(m0, m1, m2, r.o);
+    cr.d = xfVector(m0, m1, m2, r.d);
+    const float4 A = nodes[4 * tri], E1 = nodes[4 * tri + 1], E2 = nodes[4 * tri + 2];
+    const f3 p = cr.o + t * cr.d;
+    const f2 uv = triBary(p, A, E1, E2);
+    return make_float4(uv.x, uv.y, __int_as_float(shape), E1.w);
+}
+
+// Closest / any hit over either layout; TL selects the two-level instantiation.
+template <bool TL>
+MCRT_DEV float4 traceClosest(const float4* __restrict__ nodes, const TraceRay& r, uint32_t* stk, uint32_t* spill,
+                             int spillCap, int* overflowFlag, float& t) {
+    if (TL) {
+        int inst;
+        const int tri = traverse2L<false>(nodes, r, stk, spill, spillCap, overflowFlag, t, inst);
+        return closestRecord2L(nodes, r, tri, inst, t);
+    }
+    const int tri = traverse<false>(nodes, r, stk, spill, spillCap, overflowFlag, t);
+    return closestRecord(nodes, r, tri, t);
+}
+template <bool TL>
+MCRT_DEV bool traceAny(const float4* __restrict__ nodes, const TraceRay& r, uint32_t* stk, uint32_t* spill,
+                       int spillCap, int* overflowFlag) {
+    float t;
+    if (TL) {
+        int inst;
+        return traverse2L<true>(nodes, r, stk, spill, spillCap, overflowFlag, t, inst) >= 0;
+    }
+    return traverse<true>(nodes, r, stk, spill, spillCap, overflowFlag, t) >= 0;
 }
 
 // Per-ray spill column: rays are grouped 64 to a wave; lane l of wave w owns entries

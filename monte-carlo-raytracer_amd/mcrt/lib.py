@@ -40,6 +40,8 @@ SIGNATURES = {
     "mcrt_scene_update_shapes": (_c.c_int, [_vp, _vp, _c.c_uint32]),
     "mcrt_accel_build": (_c.c_int, [_vp, _vp]),
     "mcrt_accel_info": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "mcrt_accel_layout": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "mcrt_accel_build_host_records": (_c.c_int, [_vp, _vp, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64), _vp]),
     "mcrt_trace_closest": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
     "mcrt_trace_any": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
     "mcrt_framebuffer_create": (_c.c_int, [_vp, _c.c_uint32, _c.c_uint32, _c.POINTER(_vp)]),
@@ -146,8 +148,35 @@ class Context:
                 for i in range(cnt.value)}
 
 
+def accel_opts(cost=10.0, bins=64, sah=True, device_build=False, force_2level=False, force_flat=False,
+               world_to_local=None):
+    """mcrt_accel_opts; world_to_local: optional (num_shapes, 4, 4) float32 array (kept alive by
+    the caller until the build returns)."""
+    w2l = None if world_to_local is None else world_to_local.ctypes.data
+    return T.AccelOpts(cost, bins, 1 if sah else 0, 1 if device_build else 0, 1 if force_2level else 0,
+                       1 if force_flat else 0, w2l)
+
+
+def build_host_records(scene, **opts):
+    """Host-only build (no GPU): (records float32 (n, 16), info dict) of the structure
+    mcrt_accel_build would upload for `scene` (mcrt.scenes.Scene)."""
+    desc = scene.desc()
+    w2l = opts.get("world_to_local")
+    if w2l is not None:
+        opts["world_to_local"] = np.ascontiguousarray(w2l, np.float32)
+    o = accel_opts(**opts)
+    n = _c.c_uint64()
+    _check(lib().mcrt_accel_build_host_records(_c.byref(desc), _c.byref(o), None, 0, _c.byref(n), None))
+    rec = np.zeros((n.value, 16), np.float32)
+    info = np.zeros(4, np.int32)
+    _check(lib().mcrt_accel_build_host_records(_c.byref(desc), _c.byref(o), _p(rec), n.value, _c.byref(n), _p(info)))
+    return rec, {"two_level": int(info[0]), "top_records": int(info[1]), "depth": int(info[2]),
+                 "meshes": int(info[3])}
+
+
 class DeviceScene:
-    def __init__(self, ctx, scene, build=True, cost=10.0, bins=64, sah=True, device_build=False):
+    def __init__(self, ctx, scene, build=True, cost=10.0, bins=64, sah=True, device_build=False,
+                 force_2level=False, force_flat=False, world_to_local=None):
         self.ctx = ctx
         self.scene = scene
         self._desc = scene.desc()
@@ -156,11 +185,18 @@ class DeviceScene:
         self.h = h
         ctx._adopt(self)
         if build:
-            self.build(cost, bins, sah, device_build)
+            self.build(cost, bins, sah, device_build, force_2level, force_flat, world_to_local)
 
-    def build(self, cost=10.0, bins=64, sah=True, device_build=False):
-        opts = T.AccelOpts(cost, bins, 1 if sah else 0, 1 if device_build else 0)
+    def build(self, cost=10.0, bins=64, sah=True, device_build=False, force_2level=False, force_flat=False,
+              world_to_local=None):
+        w2l = None if world_to_local is None else np.ascontiguousarray(world_to_local, np.float32)
+        opts = accel_opts(cost, bins, sah, device_build, force_2level, force_flat, w2l)
         _check(lib().mcrt_accel_build(self.h, _c.byref(opts)), self.ctx.h)
+
+    def layout(self):
+        tl, nm, ni, dp = _c.c_int32(), _c.c_uint32(), _c.c_uint32(), _c.c_int32()
+        _check(lib().mcrt_accel_layout(self.h, _c.byref(tl), _c.byref(nm), _c.byref(ni), _c.byref(dp)), self.ctx.h)
+        return {"two_level": tl.value, "meshes": nm.value, "instances": ni.value, "depth": dp.value}
 
     def info(self):
         nn, nb, ms, nt = _c.c_uint64(), _c.c_uint64(), _c.c_double(), _c.c_uint32()

@@ -111,7 +111,12 @@ class Scene:
         return np.concatenate(out) if out else np.zeros((0, 3, 3), np.float32)
 
     def bbox(self):
-        P = self.positions[:, :3]
+        """World-space bounds of the shapes (transforms applied)."""
+        M = self.shapes["toWorldTransform"]
+        if np.array_equal(M, np.broadcast_to(np.eye(4, dtype=np.float32), M.shape)):
+            P = self.positions[:, :3]
+        else:
+            P = self.world_triangles().reshape(-1, 3)
         return P.min(0), P.max(0)
 
 
@@ -150,6 +155,19 @@ class SceneBuilder:
         self.meshes.append((P, N, UV, tris, int(material), transform))
         return len(self.meshes) - 1
 
+    def add_instance(self, mesh, transform, material=None):
+        """Another shape that shares mesh `mesh`'s vertex and index data (same startIdx,
+        startVertex, numTriangles) under its own transform: what RTScene::attachMesh records for
+        every further entity of an already attached mesh (RTScene.cpp:572-596), which makes
+        RadeonRays build its two-level structure.  material None = the first entity's material,
+        as the reference's instance shapes carry (sharedShapeInfo.materialId)."""
+        base = mesh
+        while self.meshes[base][0] is None:
+            base = self.meshes[base][1]
+        mat = self.meshes[base][4] if material is None else int(material)
+        self.meshes.append((None, base, None, None, mat, transform))
+        return len(self.meshes) - 1
+
     def add_directional_light(self, direction, intensity):
         self.lights.append({"type": T.DIRECTIONAL, "d": np.asarray(direction, np.float64), "intensity": intensity})
         return len(self.lights) - 1
@@ -170,8 +188,8 @@ class SceneBuilder:
     def build(self, sobol=None):
         nshape = len(self.meshes)
         shapes = np.zeros(nshape, T.SHAPE_DTYPE)
-        nv = sum(m[0].shape[0] for m in self.meshes)
-        ni = sum(m[3].size for m in self.meshes)
+        nv = sum(m[0].shape[0] for m in self.meshes if m[0] is not None)
+        ni = sum(m[3].size for m in self.meshes if m[0] is not None)
         positions = np.zeros((nv, 4), np.float32)
         normals = np.zeros((nv, 4), np.float32)
         tangents = np.zeros((nv, 4), np.float32)
@@ -180,6 +198,20 @@ class SceneBuilder:
         indices = np.zeros(ni, np.uint32)
         v0 = i0 = 0
         for k, (P, N, UV, tris, mat, M) in enumerate(self.meshes):
+            if P is None:   # instance of shape N (= base mesh index)
+                base = self.meshes[N]
+                s = shapes[k]
+                Mw = np.eye(4, dtype=np.float32) if M is None else np.asarray(M, np.float32)
+                s["toWorldTransform"] = Mw
+                s["toWorldInverseTranspose"] = np.linalg.inv(Mw.astype(np.float64)).T.astype(np.float32)
+                for f in ("startIdx", "startVertex", "numTriangles"):
+                    s[f] = shapes[N][f]
+                s["materialId"] = mat
+                s["lightID"] = -1
+                Pw = base[0] @ Mw[:3, :3].T + Mw[:3, 3]
+                tri = Pw[base[3].astype(np.int64)]
+                s["area"] = 0.5 * np.linalg.norm(np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]), axis=1).sum()
+                continue
             n = P.shape[0]
             positions[v0:v0 + n, :3] = P
             normals[v0:v0 + n, :3] = N
@@ -212,6 +244,8 @@ class SceneBuilder:
             Pw_all = []
             for k, (P, N, UV, tris, mat, M) in enumerate(self.meshes):
                 Mw = shapes[k]["toWorldTransform"]
+                if P is None:
+                    P = self.meshes[N][0]
                 Pw_all.append((P @ Mw[:3, :3].T + Mw[:3, 3]).astype(np.float32))
             Pw_all = np.concatenate(Pw_all)
             bmin, bmax = Pw_all.min(0), Pw_all.max(0)
@@ -534,6 +568,91 @@ def dragon_proxy(tris=871_414, seed=2):
     return b.build()
 
 
+def _affine(scale, yaw_deg, t, tilt_deg=0.0):
+    """4x4 float32 local-to-world: translate(t) * rotY(yaw) * rotX(tilt) * scale."""
+    a, b = math.radians(yaw_deg), math.radians(tilt_deg)
+    ry = np.array([[math.cos(a), 0, math.sin(a)], [0, 1, 0], [-math.sin(a), 0, math.cos(a)]])
+    rx = np.array([[1, 0, 0], [0, math.cos(b), -math.sin(b)], [0, math.sin(b), math.cos(b)]])
+    M = np.eye(4)
+    M[:3, :3] = ry @ rx * scale
+    M[:3, 3] = t
+    return M.astype(np.float32)
+
+
+def instanced_proxy(grid_n=8, body_tris=60_000, seed=5):
+    """Instancing workload: a field of grid_n x grid_n copies of two
+    shared meshes (a displaced 'rock' and a column) under rotated / scaled / translated
+    transforms, on a ground plane with a mesh light -- the scene shape for which RTScene
+    creates RadeonRays instances and RR switches to its two-level intersector.  ~2 x grid_n^2
+    x body_tris effective triangles from 2 x body_tris stored."""
+    rng = np.random.default_rng(SEED_BASE + seed)
+    b = SceneBuilder("instanced_proxy")
+    ground_tex = b.add_texture(tex_checker(128, (190, 190, 190), (80, 80, 90), tiles=16))
+    ground = b.add_material(kd=(0.8, 0.8, 0.8), ks=(0.05, 0.05, 0.05), diffuseTexId=ground_tex, roughness=0.5)
+    rock = b.add_material(kd=(0.5, 0.42, 0.3), ks=(0.3, 0.28, 0.2), roughness=0.3)
+    metal = b.add_material(kd=(0.1, 0.1, 0.1), ks=(0.9, 0.85, 0.7), roughness=0.15)
+    half = grid_n * 1.5
+    b.add_mesh(*grid((-half - 2, 0, -half - 2), (2 * half + 4, 0, 0), (0, 0, 2 * half + 4), 8, 8, uv_scale=6.0,
+                     flip=True), ground)
+    nu = max(8, int(round(math.sqrt(body_tris))))
+    nv = max(4, body_tris // (2 * nu) + 1)
+    rock_mesh = None
+    col_mesh = None
+    for i in range(grid_n):
+        for j in range(grid_n):
+            x, z = -half + 3.0 * i + 1.5, -half + 3.0 * j + 1.5
+            if (i + j) % 2 == 0:
+                M = _affine(rng.uniform(0.6, 1.1), rng.uniform(0, 360), (x, 0.9, z), rng.uniform(-20, 20))
+                if rock_mesh is None:
+                    P, N, UV, tris = displaced_sphere(np.zeros(3), 1.0, nu, nv, rng, amp=0.25, octaves=6)
+                    rock_mesh = b.add_mesh(P, N, UV, tris, rock, transform=M)
+                else:
+                    b.add_instance(rock_mesh, M)
+            else:
+                M = _affine(rng.uniform(0.8, 1.2), rng.uniform(0, 360), (x, 0.0, z))
+                if col_mesh is None:
+                    P, N, UV, tris = cylinder(np.zeros(3), 0.5, 2.5, nseg=max(16, body_tris // 64), nh=16, cap=True)
+                    col_mesh = b.add_mesh(P, N, UV, tris, metal, transform=M)
+                else:
+                    b.add_instance(col_mesh, M)
+    lm = b.add_material(kd=(0.8, 0.8, 0.8), ks=(0, 0, 0))
+    ls = b.add_mesh(*grid((-2.0, 7.0, -2.0), (4, 0, 0), (0, 0, 4), 1, 1, flip=True), lm)
+    b.add_directional_light(euler_forward(50.0, 60.0), (6.0, 6.0, 6.0))
+    b.add_mesh_light(ls, (20.0, 16.0, 12.0))
+    return b.build()
+
+
+def instances_test_scene(seed=0):
+    """Small instancing parity scene: meshes and instances interleaved in attach order (the
+    std::partition order of IntersectorTwoLevel::Process matters), a single-triangle mesh
+    (bottom tree = one leaf), scaled / rotated / tilted instances with per-instance materials,
+    a mesh light and a point light."""
+    rng = np.random.default_rng(SEED_BASE + 100 + seed)
+    b = SceneBuilder("instances_test")
+    tex = b.add_texture(tex_checker(64, (220, 220, 220), (60, 60, 150)))
+    m0 = b.add_material(kd=(0.7, 0.6, 0.5), ks=(0.2, 0.2, 0.2), roughness=0.3)
+    m1 = b.add_material(kd=(0.2, 0.5, 0.7), ks=(0.6, 0.6, 0.6), roughness=0.1)
+    floor = b.add_material(kd=(1, 1, 1), diffuseTexId=tex)
+    b.add_mesh(*grid((-9, 0, -9), (18, 0, 0), (0, 0, 18), 4, 4, uv_scale=4.0, flip=True), floor)
+    A = b.add_mesh(*displaced_sphere(np.zeros(3), 1.0, 24, 12, rng), m0, transform=_affine(1.0, 10.0, (0, 1, 0)))
+    b.add_instance(A, _affine(0.5, 45.0, (3, 1, 0), 30.0))
+    B = b.add_mesh(*grid((-1, 0, -1), (2, 0, 0), (0, 0, 2), 3, 3), m1, transform=_affine(1.0, 0.0, (0, 0.01, -4)))
+    b.add_instance(A, _affine(2.0, -70.0, (-4, 2, 1)), material=m1)
+    b.add_instance(B, _affine(1.0, 90.0, (0, 3, 5), 80.0))
+    C = b.add_mesh(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32), np.tile([0, 0, 1], (3, 1)),
+                   np.zeros((3, 2)), np.array([[0, 1, 2]]), m0, transform=_affine(1.0, 0.0, (2, 0, -3)))
+    b.add_instance(C, _affine(3.0, 33.0, (-2, 0, -3), 12.0))
+    for i in range(6):
+        b.add_instance(A, _affine(rng.uniform(0.3, 1.5), rng.uniform(0, 360), rng.uniform(-7, 7, 3) * (1, 0, 1)
+                                  + (0, 1.2, 0), rng.uniform(-40, 40)))
+    lm = b.add_material(kd=(0.8, 0.8, 0.8), ks=(0, 0, 0))
+    ls = b.add_mesh(*grid((-1, 6.0, -1), (2, 0, 0), (0, 0, 2), 1, 1, flip=True), lm)
+    b.add_mesh_light(ls, (14.0, 12.0, 10.0))
+    b.add_point_light((3.0, 5.0, -3.0), (6.0, 6.0, 6.0))
+    b.add_directional_light(euler_forward(50.0, 30.0), (3.0, 3.0, 3.0))
+    return b.build()
+
+
 def san_miguel_proxy(tris=10_000_000, seed=4, tex_size=512):
     """San-Miguel proxy (configs 4/5 and the headline metric): courtyard with arcades,
     tables, ~70 % of the triangles in foliage quads with alpha cut-out leaves, >= 64
@@ -701,4 +820,6 @@ CAMERAS = {
     "dragon_proxy": ((-3.3, 3.2, -4.5), (0.0, 1.4, 0.0), 45.0),
     "san_miguel_proxy": ((8.2, 2.56, -6.6), (-2.0, 2.8, 3.0), 45.0),
     "sponza_proxy": ((12.0, 3.0, 0.5), (-4.0, 4.5, -0.5), 45.0),
+    "instanced_proxy": ((0.0, 9.0, -17.0), (0.0, 0.5, 0.0), 45.0),
+    "instances_test": ((0.0, 5.0, -13.0), (0.0, 1.0, 0.0), 45.0),
 }

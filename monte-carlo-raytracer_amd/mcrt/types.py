@@ -131,7 +131,8 @@ class SceneDesc(ctypes.Structure):
 
 class AccelOpts(ctypes.Structure):
     _fields_ = [("traversal_cost", ctypes.c_float), ("num_bins", ctypes.c_int), ("use_sah", ctypes.c_int),
-                ("device_build", ctypes.c_int)]
+                ("device_build", ctypes.c_int), ("force_2level", ctypes.c_int), ("force_flat", ctypes.c_int),
+                ("world_to_local", ctypes.c_void_p)]
 
 
 class FrameParams(ctypes.Structure):

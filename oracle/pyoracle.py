@@ -210,6 +210,11 @@ def ref():
         L.rr_obj_num_shapes.argtypes = [_vp]
         L.rr_obj_shape.argtypes = [_vp, _c.c_int, _vp, _vp, _vp, _vp]
         L.rr_obj_free.argtypes = [_vp]
+        L.rr2l_build.restype = _vp
+        L.rr2l_build.argtypes = [_c.c_int, _vp, _vp, _vp, _vp, _vp, _c.c_float, _c.c_int, _c.c_int]
+        L.rr2l_sizes.argtypes = [_vp, _vp]
+        L.rr2l_copy.argtypes = [_vp, _vp, _vp, _vp, _vp]
+        L.rr2l_free.argtypes = [_vp]
         _ref = L
     return _ref
 
@@ -234,6 +239,42 @@ class _RefShapes:
 
     def args(self):
         return (len(self.P), self.pp, _p(self.nv), 16, self.ip, _p(self.nf), _p(self.mt))
+
+
+# IntersectorTwoLevel's buffers (intersect_bvh2level_skiplinks.cl kernel arguments)
+RR2L_SHAPE_DTYPE = np.dtype([("id", "<i4"), ("bvhidx", "<i4"), ("shapeDisabled", "<u4"), ("padding1", "<i4"),
+                             ("minv", "<f4", (4, 4)), ("lv", "<f4", 4), ("av", "<f4", 4)])
+RR2L_FACE_DTYPE = np.dtype([("idx", "<i4", 3), ("shape_id", "<i4"), ("prim_id", "<i4")])
+
+
+def ref_bvh2l(scene, world_to_local=None, cost=10.0, bins=64, sah=True):
+    """The reference's two-level structure for `scene` (oracle/_ref/librrref.so: RR Bvh +
+    PlainBvhTranslator run by the Process mirror in rrref_driver.cpp).  world_to_local:
+    (S, 4, 4) float32 (default: transpose of toWorldInverseTranspose, as the product's default).
+    Returns dict(nodes (K, 8) float32 = bbox pmin/pmax xyzw, vertices (V, 4), faces, shapes, root,
+    meshes, instances)."""
+    sh = scene.shapes
+    keys = np.ascontiguousarray(np.stack([sh["startIdx"], sh["startVertex"], sh["numTriangles"]], 1).astype(np.uint32))
+    m = np.ascontiguousarray(sh["toWorldTransform"].astype(np.float32))
+    if world_to_local is None:
+        world_to_local = np.transpose(sh["toWorldInverseTranspose"], (0, 2, 1))
+    minv = np.ascontiguousarray(world_to_local, np.float32)
+    idx = np.ascontiguousarray(scene.indices, np.uint32)
+    pos = np.ascontiguousarray(scene.positions, np.float32)
+    L = ref()
+    h = L.rr2l_build(len(sh), _p(keys), _p(m), _p(minv), _p(idx), _p(pos), cost, bins, 1 if sah else 0)
+    try:
+        sz = np.zeros(7, np.int64)
+        L.rr2l_sizes(h, _p(sz))
+        nodes = np.zeros((sz[0], 8), np.float32)
+        verts = np.zeros((sz[1], 4), np.float32)
+        faces = np.zeros(sz[2], RR2L_FACE_DTYPE)
+        shapes = np.zeros(sz[3], RR2L_SHAPE_DTYPE)
+        L.rr2l_copy(h, _p(nodes), _p(verts), _p(faces), _p(shapes))
+    finally:
+        L.rr2l_free(h)
+    return {"nodes": nodes, "vertices": verts, "faces": faces, "shapes": shapes, "root": int(sz[4]),
+            "meshes": int(sz[5]), "instances": int(sz[6])}
 
 
 def ref_bvh_nodes(scene, cost=10.0, bins=64, sah=True):
@@ -315,6 +356,8 @@ def clref(variant="ieee"):
         L.clref_bdpt_render.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _vp]
         L.clref_bdpt_read.restype = _c.c_int64
         L.clref_bdpt_read.argtypes = [_vp, _c.c_int, _vp]
+        L.clref_scene_set_two_level.argtypes = [_vp, _vp, _c.c_int64, _vp, _c.c_int64, _vp, _c.c_int64, _vp,
+                                                _c.c_int64, _c.c_int]
         st = L.clref_init(os.path.join(HERE, "_ref").encode(), variant.encode())
         if st != 0:
             raise RuntimeError(f"clref_init({variant}) = {st}: {L.clref_error().decode()}")
@@ -326,10 +369,14 @@ class CLRefScene:
     """A scene on the reference OpenCL pipeline; BVH nodes from the reference Bvh2 builder
     (librrref.so) when available, else from the oracle's bit-identical restatement."""
 
-    def __init__(self, scene, variant="ieee", nodes=None):
+    def __init__(self, scene, variant="ieee", nodes=None, two_level=False, world_to_local=None):
+        """two_level: ray queries go through RadeonRays' IntersectorTwoLevel kernels over the
+        reference's own two-level build (ref_bvh2l), as RR does for instanced scenes."""
         self.L = clref(variant)
         self.scene = scene
         self._desc = scene.desc()
+        if two_level and nodes is None:
+            nodes = np.zeros((1, 16), np.float32)   # flat structure unused
         if nodes is None:
             o = OracleScene(scene)
             o.build()
@@ -338,6 +385,13 @@ class CLRefScene:
         self.h = self.L.clref_scene_create(ctypes.byref(self._desc), _p(self.nodes), len(self.nodes))
         if not self.h:
             raise RuntimeError(self.L.clref_error().decode())
+        if two_level:
+            r = self.two_level = ref_bvh2l(scene, world_to_local=world_to_local)
+            st = self.L.clref_scene_set_two_level(self.h, _p(r["nodes"]), len(r["nodes"]), _p(r["vertices"]),
+                                                  len(r["vertices"]), _p(r["faces"]), len(r["faces"]),
+                                                  _p(r["shapes"]), len(r["shapes"]), r["root"])
+            if st != 0:
+                raise RuntimeError(f"clref_scene_set_two_level {st}: {self.L.clref_error().decode()}")
 
     def render(self, cam, frame=0, max_depth=2):
         W, H = int(cam["width"][0]), int(cam["height"][0])

@@ -48,7 +48,10 @@ struct Runtime {
     cl_program pt = nullptr, rr = nullptr, recon = nullptr, bdpt = nullptr;
     cl_kernel kGen = nullptr, kPT = nullptr, kShadow = nullptr, kIsect = nullptr, kOccl = nullptr, kRecon = nullptr;
     cl_kernel kBStart = nullptr, kBSec = nullptr, kBPrep = nullptr, kBConn = nullptr, kBCopy = nullptr;
-    std::string deviceName;
+    // RadeonRays IntersectorTwoLevel (intersect_bvh2level_skiplinks.cl), loaded on first use
+    cl_program rr2l = nullptr;
+    cl_kernel kIsect2 = nullptr, kOccl2 = nullptr;
+    std::string deviceName, dir;
 } R;
 
 cl_program loadProgram(const std::string& path) {
@@ -99,6 +102,10 @@ struct Scene {
            lightThr = nullptr, lightPdf = nullptr, lightCnt = nullptr, connRays = nullptr, connVis = nullptr,
            sampCamV = nullptr, sampLightV = nullptr, bTemp = nullptr, bStack = nullptr, bCount = nullptr,
            bConnCount = nullptr;
+    // two-level mode: IntersectorTwoLevel's buffers (intersector_2level.cpp:300-470)
+    bool twoLevel = false;
+    cl_mem n2 = nullptr, v2 = nullptr, f2 = nullptr, s2 = nullptr;
+    int root2 = -1;
 };
 
 template <class T>
@@ -109,7 +116,25 @@ bool launch2D(cl_kernel k, int W, int H) {
     return ok(clEnqueueNDRangeKernel(R.q, k, 2, nullptr, gs, ls, 0, nullptr, nullptr), "launch2D") &&
            ok(clFinish(R.q), "clFinish");
 }
+// IntersectorTwoLevel::Intersect / Occluded argument order (intersector_2level.cpp:640-690)
+bool launchRR2(cl_kernel k, Scene* s, cl_mem rays, cl_mem out, cl_mem count, int n) {
+    k = (k == R.kIsect) ? R.kIsect2 : R.kOccl2;
+    cl_int e = 0;
+    e |= arg(k, 0, s->n2);
+    e |= arg(k, 1, s->v2);
+    e |= arg(k, 2, s->f2);
+    e |= arg(k, 3, s->s2);
+    e |= arg(k, 4, s->root2);
+    e |= arg(k, 5, rays);
+    e |= arg(k, 6, count);
+    e |= arg(k, 7, out);
+    if (!ok(e, "set RR2L args")) return false;
+    size_t gs = (size_t)(n + 63) / 64 * 64, ls = 64;
+    return ok(clEnqueueNDRangeKernel(R.q, k, 1, nullptr, &gs, &ls, 0, nullptr, nullptr), "launchRR2") &&
+           ok(clFinish(R.q), "clFinish");
+}
 bool launchRR(cl_kernel k, Scene* s, cl_mem rays, cl_mem out, int n) {
+    if (s->twoLevel) return launchRR2(k, s, rays, out, s->count, n);
     cl_int e = 0;
     e |= arg(k, 0, s->nodes);
     e |= arg(k, 1, rays);
@@ -185,6 +210,7 @@ __attribute__((visibility("default"))) int clref_init(const char* dir, const cha
     R.q = clCreateCommandQueue(R.ctx, R.dev, 0, &e);
     if (!ok(e, "clCreateCommandQueue")) return -4;
     std::string d(dir);
+    R.dir = d;
     R.pt = loadProgram(d + "/clref_pt_" + variant + ".hsaco");
     R.rr = loadProgram(d + "/clref_rr.hsaco");
     R.recon = loadProgram(d + "/clref_recon.hsaco");
@@ -235,6 +261,35 @@ __attribute__((visibility("default"))) void* clref_scene_create(const mcrt_scene
     s->numLights = (int)d->num_lights;
     if (!s->shapes || !s->nodes) { delete s; return nullptr; }
     return s;
+}
+
+// Switch the scene's ray queries to RadeonRays' two-level intersector over the reference's own
+// two-level buffers (oracle/_ref/librrref.so rr2l_build): nodes 32 B, vertices 16 B, faces 20 B,
+// shapes 112 B.
+__attribute__((visibility("default"))) int clref_scene_set_two_level(void* sp, const void* nodes, int64_t nn,
+                                                                     const void* verts, int64_t nv, const void* faces,
+                                                                     int64_t nf, const void* shapes, int64_t ns,
+                                                                     int root) {
+    Scene* s = (Scene*)sp;
+    if (!R.rr2l) {
+        R.rr2l = loadProgram(R.dir + "/clref_rr2l.hsaco");
+        if (!R.rr2l) return -1;
+        cl_int e = 0;
+        R.kIsect2 = clCreateKernel(R.rr2l, "intersect_main", &e);
+        if (!ok(e, "kernel intersect_main (2l)")) return -2;
+        R.kOccl2 = clCreateKernel(R.rr2l, "occluded_main", &e);
+        if (!ok(e, "kernel occluded_main (2l)")) return -2;
+    }
+    cl_mem* old[] = {&s->n2, &s->v2, &s->f2, &s->s2};
+    for (auto* m : old)
+        if (*m) clReleaseMemObject(*m), *m = nullptr;
+    s->n2 = buf(32ull * nn, nodes);
+    s->v2 = buf(16ull * nv, verts);
+    s->f2 = buf(20ull * nf, faces);
+    s->s2 = buf(112ull * ns, shapes);
+    s->root2 = root;
+    s->twoLevel = s->n2 && s->v2 && s->f2 && s->s2;
+    return s->twoLevel ? 0 : -3;
 }
 
 static bool setSceneArgs(cl_kernel k, Scene* s, int& a) {   // RTScene::setSceneArgs, RTScene.cpp:178-197
@@ -448,6 +503,7 @@ static bool ensureBdptBuffers(Scene* s, int W, int H, int D) {
 }
 
 static bool launchRRn(cl_kernel k, Scene* s, cl_mem rays, cl_mem out, cl_mem count, int n) {
+    if (s->twoLevel) return launchRR2(k, s, rays, out, count, n);
     cl_int e = 0;
     e |= arg(k, 0, s->nodes);
     e |= arg(k, 1, rays);

@@ -67,6 +67,51 @@ def strip_bdpt_golden(src, dst):
     np.savez_compressed(dst, **keep)
 
 
+# Two-level (instanced) scenes: RadeonRays' IntersectorTwoLevel kernels over the reference's own
+# two-level build (oracle/_ref/librrref.so rr2l_build)
+TL_CASES = [  # (scene, W, H, frames, max_depth)
+    ("instances_test", 96, 64, (0, 1), 2),
+    ("instances_test", 64, 48, (0,), 5),
+    ("instanced_small", 80, 60, (0,), 2),
+]
+TL_BDPT_CASES = [("instances_test", 64, 48, (0, 1), 2)]
+
+
+def tl_rays(scene, n=20000, seed=11):
+    """Random rays; every 8th ray carries a shape id as its mask (RR_RAY_MASK at the instance)."""
+    rays = random_rays(scene, n, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    sel = np.arange(n) % 8 == 3
+    rays["extra"][sel, 0] = rng.integers(0, len(scene.shapes), sel.sum())
+    return rays
+
+
+def tl_job(out_path, variant):
+    res = {}
+    cache = {}
+    for case in TL_CASES:
+        name, W, H, frames, D = case
+        if name not in cache:
+            cache[name] = po.CLRefScene(build_scene(name), variant, two_level=True)
+        cs = cache[name]
+        cam = scene_camera("instanced_proxy" if name == "instanced_small" else name, W, H)
+        for f in frames:
+            res[f"{name}_{W}x{H}_d{D}_f{f}"] = cs.render(cam, frame=f, max_depth=D)
+    for name, cs in cache.items():
+        rays = tl_rays(cs.scene)
+        res[f"{name}_rays"] = rays
+        res[f"{name}_closest"] = cs.trace(rays)
+        res[f"{name}_any"] = cs.trace(rays, any_hit=True)
+    for case in TL_BDPT_CASES:
+        name, W, H, frames, D = case
+        cs = po.CLRefScene(build_scene(name), variant, two_level=True)
+        cam = scene_camera(name, W, H)
+        for f in frames:
+            res[f"bdpt_{name}_{W}x{H}_d{D}_f{f}"] = cs.render_bdpt(cam, frame=f, max_depth=D)
+    np.savez_compressed(out_path, **res)
+    print(f"clref two-level job ({variant}): {len(res)} arrays -> {out_path}")
+
+
 def build_scene(name):
     if name == "mixed":
         return scenes.test_scene()
@@ -74,6 +119,10 @@ def build_scene(name):
         return scenes.cornell_box(os.path.join(ROOT, "tests", "golden", "cornell_original.npz"))
     if name == "dragon_small":
         return scenes.dragon_proxy(tris=20000)
+    if name == "instances_test":
+        return scenes.instances_test_scene()
+    if name == "instanced_small":
+        return scenes.instanced_proxy(grid_n=4, body_tris=6000)
     raise KeyError(name)
 
 
@@ -89,6 +138,9 @@ def main():
     variant = sys.argv[2] if len(sys.argv) > 2 else "ieee"
     if len(sys.argv) > 3 and sys.argv[3] == "bdpt":
         bdpt_job(out_path, variant)
+        return
+    if len(sys.argv) > 3 and sys.argv[3] == "2l":
+        tl_job(out_path, variant)
         return
     if len(sys.argv) > 3 and sys.argv[3] == "sm":
         sm_job(out_path, variant, int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6]))
