@@ -104,7 +104,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--tris", type=int, default=10_000_000)
     ap.add_argument("--max-depth", type=int, default=2)
-    ap.add_argument("--scene", default="san_miguel_proxy", choices=["san_miguel_proxy", "dragon_proxy", "sponza_proxy"])
+    ap.add_argument("--scene", default="san_miguel_proxy", choices=["san_miguel_proxy", "dragon_proxy", "sponza_proxy",
+                                                                   "instanced_proxy"])
     ap.add_argument("--sampler", default="random", choices=["random", "sobol"])
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,6 +116,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the product path); gloo only rehearses N ranks on one GPU")
     ap.add_argument("--device-build", action="store_true", help="on-device linear BVH instead of the RR-identical host build")
+    ap.add_argument("--force-flat", action="store_true",
+                    help="flat BVH even for instanced scenes (RR bvh.forceflat); default: RR's auto selection")
     args = ap.parse_args()
 
     import torch
@@ -143,6 +146,8 @@ def main():
         scene = scenes.san_miguel_proxy(tris=args.tris)
     elif args.scene == "sponza_proxy":
         scene = scenes.sponza_proxy()
+    elif args.scene == "instanced_proxy":
+        scene = scenes.instanced_proxy()
     else:
         scene = scenes.dragon_proxy(tris=min(args.tris, 871_414))
     sampler = T.SAMPLER_SOBOL if args.sampler == "sobol" else T.SAMPLER_RANDOM
@@ -154,8 +159,9 @@ def main():
 
     ctx = lib.Context(local)
     t0 = time.perf_counter()
-    ds = lib.DeviceScene(ctx, scene, device_build=args.device_build)
+    ds = lib.DeviceScene(ctx, scene, device_build=args.device_build, force_flat=args.force_flat)
     info = ds.info()
+    two_level = ds.layout()["two_level"] == 1
     log(f"[bench] upload+BVH {time.perf_counter() - t0:.1f}s (build {info['build_ms'] / 1e3:.1f}s, "
         f"{info['nodes']} nodes, {info['bytes'] / 1e6:.0f} MB)")
     fb = lib.FrameBuffer(ctx, W, H)
@@ -226,7 +232,8 @@ def main():
         "config": {"workload": f"{args.scene} {W}x{H}, {'BDPT' if bdpt else 'unidirectional PT'}, maxDepth {D}, "
                                f"{args.sampler} sampler, 1 spp per step, box-filter accumulate", "width": W, "height": H,
                    "triangles": scene.num_triangles, "max_depth": D, "spp_per_step": 1,
-                   "bvh": "device LBVH" if args.device_build else "host RadeonRays-identical SAH",
+                   "bvh": ("two-level (instanced), RadeonRays-identical Bvh trees" if two_level else
+                           "device LBVH" if args.device_build else "host RadeonRays-identical SAH"),
                    "bvh_build_ms": round(info["build_ms"], 1),
                    "parallelism": (f"frame split x {world} + 1 RCCL reduce" if bdpt else
                                    f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce")},
@@ -236,7 +243,8 @@ def main():
                 "shaded": fstats["shaded_paths"] / (W * H / world)}
         out["rays_per_path"] = {k: round(v, 4) for k, v in rays.items()}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and not bdpt and sampler == T.SAMPLER_RANDOM:
+        # (the CPU oracle and the roofline's visit counts price the flat structure)
+        if world == 1 and not args.no_cpu_baseline and not bdpt and sampler == T.SAMPLER_RANDOM and not two_level:
             cpu = cpu_baseline(scene, cam, W, H, D, args.cpu_seconds)
             st = cpu["_stats"]
             V = {"k_primary": st[1] / max(st[0], 1), "k_extend": st[3] / max(st[2], 1),
