@@ -233,6 +233,12 @@ typedef struct {
      * APP/.../RTBDPTPass.cpp:67-128) needs the whole image in one band (num_bands = 1): its
      * light-tracing strategies splat into any pixel.  Multi-GPU BDPT splits frames instead. */
     int32_t integrator;
+    /* 1: textures at camera-ray hits are read mip-mapped over the pixel footprint (ray
+     * differentials, computeSurfaceInteractionWithDifferentials + readTexture2Df_lod +
+     * computeMipmapLOD: KRN/geometry.cl:92-175, KRN/textures.cl:148-202).  The reference carries
+     * this path switched off (KRN/textures.cl:204-209); 0 (default) = its bilinear level-0
+     * reads.  PT only; needs the textures' mip chains (mcrt_texture_desc.numMipLevels). */
+    int32_t texture_lod;
 } mcrt_frame_params;
 
 typedef struct mcrt_ctx_s*         mcrt_ctx;
@@ -342,6 +348,16 @@ typedef struct {
     float   min_luminance;      /* GI.minLuminance (default 2.0), Reinhard's Lwhite */
 } mcrt_postprocess_params;
 MCRT_API mcrt_status mcrt_postprocess(mcrt_framebuffer fb, const mcrt_postprocess_params* params);
+/* Per-pixel outputs at the camera-ray hits (camera rays traced by this call; no shading):
+ *  MCRT_AOV_ALBEDO:      float4 per pixel = (uber diffuse Kd incl. texture, opacity.x), zero on
+ *                        a miss; mip-mapped when params->texture_lod (an albedo guide for denoisers)
+ *  MCRT_AOV_TEXTURE_LOD: 3 float4 per pixel = (duvdx, duvdy), (diffuse-texture LOD, shape index
+ *                        bits, uv), the diffuse texture read at that LOD (zeros where untextured).
+ * host_out: W*H*{1|3}*4 floats.  Band fields of params select the rows as in mcrt_render_frame. */
+#define MCRT_AOV_ALBEDO      0
+#define MCRT_AOV_TEXTURE_LOD 1
+MCRT_API mcrt_status mcrt_render_aov(mcrt_scene scene, mcrt_framebuffer fb, const mcrt_camera* camera,
+                                     const mcrt_frame_params* params, int aov, float* host_out);
 /* Copies device -> host (RGBA32F, W*H*4 floats).  which: 0 radiance, 1 weighted sum, 2 image,
  * 3 display image (mcrt_postprocess). */
 MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float* host_rgba);

@@ -877,6 +877,7 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
     f.sampler = p->sampler;
     f.russianRoulette = p->russian_roulette;
     f.rrStartDepth = p->rr_start_depth;
+    f.textureLod = p->texture_lod ? 1 : 0;
     f.numBands = p->num_bands <= 0 ? 1 : p->num_bands;
     f.bandIndex = p->band_index;
     f.bandRows = f.numBands == 1 ? 8 : p->band_rows;
@@ -1068,11 +1069,44 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
     return MCRT_OK;
 }
 
+MCRT_API mcrt_status mcrt_render_aov(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cam,
+                                     const mcrt_frame_params* p, int aov, float* host_out) {
+    if (!s || !fb || !cam || !p || !host_out) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    mcrt_ctx ctx = s->ctx;
+    if (!s->dNodes) return fail(ctx, MCRT_ERROR_NOT_READY, "mcrt_accel_build has not been called");
+    if (aov != MCRT_AOV_ALBEDO && aov != MCRT_AOV_TEXTURE_LOD) return fail(ctx, MCRT_ERROR_INVALID_ARG, "unknown aov");
+    if (cam->width != fb->W || cam->height != fb->H)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "camera size differs from the frame buffer");
+    FrameArgs f;
+    std::string err;
+    if (!frame_args(fb, p, f, err)) return fail(ctx, MCRT_ERROR_INVALID_ARG, err);
+    hipSetDevice(ctx->device);
+    hipStream_t st = ctx->stream;
+    mcrt_camera* dCam = reinterpret_cast<mcrt_camera*>(fb->counters + 128);
+    HIPCHK(ctx, hipMemcpyAsync(dCam, cam, sizeof(mcrt_camera), hipMemcpyHostToDevice, st));
+    if (!ensure_spill(s, std::max((size_t)f.numTiles * 64, 2 * fb->N + 64)))
+        return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
+    const TraceCtx tcs = trace_ctx(s);
+    mcrt::launch_primary(tcs, f, dCam, fb->hitsP, st);
+    const size_t stride = aov == MCRT_AOV_TEXTURE_LOD ? 3 : 1;
+    float4* dOut = nullptr;
+    HIPCHK(ctx, hipMallocAsync((void**)&dOut, 16 * stride * fb->N, st));
+    HIPCHK(ctx, hipMemsetAsync(dOut, 0, 16 * stride * fb->N, st));
+    mcrt::launch_aov(scene_args(s), f, dCam, fb->hitsP, aov, dOut, st);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(host_out, dOut, 16 * stride * fb->N, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    hipFreeAsync(dOut, st);
+    hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(ctx, MCRT_ERROR_DEVICE, std::string("aov: ") + hipGetErrorString(e));
+    return MCRT_OK;
+}
+
 MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* filter, int32_t frame_index) {
     if (!fb || !filter) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
     mcrt_ctx ctx = fb->ctx;
     if (!fb->haveBands) {   // no frame rendered yet: whole image
-        mcrt_frame_params p;
+        mcrt_frame_params p{};
         std::memset(&p, 0, sizeof(p));
         p.num_bands = 1;
         std::string err;

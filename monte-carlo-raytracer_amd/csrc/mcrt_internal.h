@@ -29,6 +29,7 @@ struct FrameArgs {
     int russianRoulette, rrStartDepth;
     int bandRows, numBands, bandIndex;
     int tilesX, numTiles;   // 8x8 tiles of this rank's bands
+    int textureLod;         // mip-mapped texture reads at camera-ray hits (PT)
 };
 
 struct QueueArgs {
@@ -81,6 +82,8 @@ void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* ca
 void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,
                    const float4* qD, const float4* qT, const float4* hits, float4* radiance, const QueueArgs& q,
                    int maxCount, hipStream_t st);
+void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits, int which,
+                float4* out, hipStream_t st);
 void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st);
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st);

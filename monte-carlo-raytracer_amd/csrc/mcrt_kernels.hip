@@ -195,13 +195,20 @@ struct ShadeOut {
     float4 eO, eD, eT;   // extension ray + throughput
 };
 
+// LOD (k_shade0 with mcrt_frame_params.texture_lod): textures at this camera-ray hit are read
+// mip-mapped over the pixel footprint given by the ray differentials (ro, dxDir, dyDir).
+template <bool LOD = false>
 MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pix, float4 hit, f3 dir, f3 throughput,
-                      int prevFlags, ShadeOut& o) {
+                      int prevFlags, ShadeOut& o, f3 ro = f3{0, 0, 0}, f3 dxDir = f3{0, 0, 0}, f3 dyDir = f3{0, 0, 0}) {
     f3 add = splat3(0.0f);
     const int shapeIdx = __float_as_int(hit.z), primIdx = __float_as_int(hit.w);
     if (shapeIdx < 0 || s.numLights <= 0) return add;
     const mcrt_shape& shape = s.shapes[shapeIdx];
-    Frame si = computeSurfaceInteraction(s, shapeIdx, primIdx, f2{hit.x, hit.y});
+    f3 dpdu, dpdv;
+    Frame si = computeSurfaceInteraction(s, shapeIdx, primIdx, f2{hit.x, hit.y}, LOD ? &dpdu : nullptr,
+                                         LOD ? &dpdv : nullptr);
+    TexLod lod{{0.0f, 0.0f}, {0.0f, 0.0f}, false};
+    if (LOD) lod = surfaceUVDifferentials(si, dpdu, dpdv, ro, dxDir, dyDir);
     const f3 wo = -dir;
     const bool isBackfacing = cl_dot(si.gn, wo) < 0.0f;
     const float traceErrorOffset = isBackfacing ? -RT_TRACE_OFFSET_F : RT_TRACE_OFFSET_F;
@@ -209,7 +216,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
     mcrt_material mat;
     if (materialId != -1) {
         mat = s.materials[materialId];
-        if (mat.uber_normalMapId != -1) applyNormalMapping(s, mat.uber_normalMapId, si);
+        if (mat.uber_normalMapId != -1) applyNormalMapping(s, mat.uber_normalMapId, si, lod);
     }
     if (bounce == 0) throughput = splat3(1.0f);
     // emission (PathTracing.cl:82-101)
@@ -223,7 +230,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
     Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, bounce, f.W, f.H, s.sobol);
     const bool isUber = materialId != -1 && mat.type == 0;   // materials.cl:130-142: other types evaluate to 0
     Uber um;
-    if (isUber) um = uberProps(s, mat, si.uv);
+    if (isUber) um = uberProps(s, mat, si.uv, lod);
     // next-event estimation, one light (PathTracing.cl:107-136)
     {
         uint32_t lightIdx = (uint32_t)floorf(getSample1D(sampler) * s.numLights);
@@ -286,6 +293,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
 }
 
 // Bounce 0: every pixel of the band (tile order); writes radiance[pix] (= `=` of ShadowPass).
+template <bool LOD>
 __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArgs s, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 const float4* __restrict__ hits, float4* __restrict__ radiance,
                                                 QueueArgs q) {
@@ -304,7 +312,9 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
         const mcrt_camera& cam = *camp;
         const int pix = y * (int)f.W + x;
         const f3 dir = cameraDir(cam, x, y);
-        const f3 add = shadePath(s, f, 0, pix, hits[pix], dir, splat3(1.0f), 0, o);
+        f3 dx = splat3(0.0f), dy = splat3(0.0f);
+        if (LOD) cameraDiffDirs(cam, x, y, dx, dy);
+        const f3 add = shadePath<LOD>(s, f, 0, pix, hits[pix], dir, splat3(1.0f), 0, o, ld3(cam.pos), dx, dy);
         radiance[pix] = make_float4(add.x, add.y, add.z, 0.0f);
     }
     const int ss = blockAppend<SHADE_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
@@ -354,6 +364,52 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shadeN(SceneArg
     const int es = blockAppend<SHADE_BLOCK / 64>(q.extCountOut, o.pushE, ldsWave);
 #endif
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
+}
+
+// ---------------------------------------------------------------------------
+// Per-pixel outputs of the camera-ray hits (mcrt_render_aov), tile order as k_shade0.
+//   MCRT_AOV_ALBEDO:     1 float4 = (uber Kd incl. texture, opacity.x); LOD per f.textureLod
+//   MCRT_AOV_TEXTURE_LOD: 3 float4 = (duvdx, duvdy), (diffuse-texture LOD, shape, uv),
+//                         the diffuse texture read mip-mapped (zeros where untextured)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_aov(SceneArgs s, FrameArgs f, const mcrt_camera* __restrict__ camp,
+                                             const float4* __restrict__ hits, int which, float4* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int x, y;
+    if (tile >= f.numTiles || !tilePixel(f, tile, lane, x, y)) return;
+    const int pix = y * (int)f.W + x;
+    const int stride = which == MCRT_AOV_TEXTURE_LOD ? 3 : 1;
+    float4* o = out + (size_t)pix * stride;
+    for (int k = 0; k < stride; ++k) o[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float4 hit = hits[pix];
+    const int shapeIdx = __float_as_int(hit.z), primIdx = __float_as_int(hit.w);
+    if (shapeIdx < 0) return;
+    const mcrt_camera& cam = *camp;
+    f3 dpdu, dpdv, dx, dy;
+    const Frame si = computeSurfaceInteraction(s, shapeIdx, primIdx, f2{hit.x, hit.y}, &dpdu, &dpdv);
+    cameraDiffDirs(cam, x, y, dx, dy);
+    TexLod L = surfaceUVDifferentials(si, dpdu, dpdv, ld3(cam.pos), dx, dy);
+    const int materialId = s.shapes[shapeIdx].materialId;
+    if (which == MCRT_AOV_TEXTURE_LOD) {
+        float lod = 0.0f;
+        f4 c = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (materialId != -1 && s.materials[materialId].uber_diffuseTexId != -1) {
+            const int t = s.materials[materialId].uber_diffuseTexId;
+            const mcrt_texture_desc tex = s.textures[t];
+            lod = mipLod(tex, L.duvdx, L.duvdy);
+            c = readTexLodDesc(s, tex, si.uv, lod);
+        }
+        o[0] = make_float4(L.duvdx.x, L.duvdx.y, L.duvdy.x, L.duvdy.y);
+        o[1] = make_float4(lod, __int_as_float(shapeIdx), si.uv.x, si.uv.y);
+        o[2] = make_float4(c.x, c.y, c.z, c.w);
+    } else {
+        L.on = f.textureLod != 0;
+        if (materialId != -1 && s.materials[materialId].type == 0) {
+            const Uber u = uberProps(s, s.materials[materialId], si.uv, L);
+            o[0] = make_float4(u.Kd.x, u.Kd.y, u.Kd.z, u.opacity.x);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -508,7 +564,8 @@ void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* 
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + SHADE_BLOCK - 1) / SHADE_BLOCK;
-    hipLaunchKernelGGL(k_shade0, dim3(blocks), dim3(SHADE_BLOCK), 0, st, s, f, cam, hits, radiance, q);
+    hipLaunchKernelGGL(f.textureLod ? k_shade0<true> : k_shade0<false>, dim3(blocks), dim3(SHADE_BLOCK), 0, st, s, f,
+                       cam, hits, radiance, q);
 }
 void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,
                    const float4* qD, const float4* qT, const float4* hits, float4* radiance, const QueueArgs& q,
@@ -516,6 +573,11 @@ void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int
     const int blocks = (maxCount + SHADE_BLOCK - 1) / SHADE_BLOCK;
     hipLaunchKernelGGL(k_shadeN, dim3(blocks > 0 ? blocks : 1), dim3(SHADE_BLOCK), 0, st, s, f, bounce, countIn, qO, qD,
                        qT, hits, radiance, q);
+}
+void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits, int which,
+                float4* out, hipStream_t st) {
+    const int blocks = (f.numTiles * 64 + 255) / 256;
+    hipLaunchKernelGGL(k_aov, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, s, f, cam, hits, which, out);
 }
 void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st) {

@@ -27,8 +27,7 @@ MCRT_DEV f3 cameraDir(const mcrt_camera& cam, int x, int y) {   // PathTracing.c
 // shading
 // ---------------------------------------------------------------------------
 // KRN/textures.cl:70-125 (readTexture2Df_linear: bilinear RGBA8, wrap modes)
-MCRT_DEV f4 readTex(const SceneArgs& s, int texId, f2 uv) {
-    const mcrt_texture_desc tex = s.textures[texId];
+MCRT_DEV f4 readTexDesc(const SceneArgs& s, const mcrt_texture_desc& tex, f2 uv) {
     const int w = tex.width, h = tex.height;
     // The reference's compiled kernel folds `-(1/w)` into `-1/w` and so loses the 2.5-ulp
     // metadata: these two reciprocals are correctly rounded there (and here).
@@ -69,23 +68,107 @@ MCRT_DEV f4 readTex(const SceneArgs& s, int texId, f2 uv) {
                     fmaf(m1.w - m0.w, t.y, m0.w)};
     return m * (1.0f / 255.0f);
 }
+MCRT_DEV f4 readTex(const SceneArgs& s, int texId, f2 uv) { return readTexDesc(s, s.textures[texId], uv); }
+
+// ---------------------------------------------------------------------------
+// Mip-mapped texture reads at camera-ray hits (opt-in, mcrt_frame_params.texture_lod).  The
+// reference carries this path but leaves it off (textures.cl:204-209 keeps the bilinear level-0
+// read); these restate its pieces: ray differentials (PathTracing.cl:29-33), the pixel's uv
+// footprint (computeSurfaceInteractionWithDifferentials, geometry.cl:126-168), the LOD
+// (computeMipmapLOD, textures.cl:198-202) and the trilinear read (readTexture2Df_lod,
+// textures.cl:148-196).  Pinned against those reference functions compiled into a probe kernel
+// (oracle/refbuild/clprobe_lod.cl, tests/test_gpu_texture_lod.py).
+// ---------------------------------------------------------------------------
+struct TexLod {
+    f2 duvdx, duvdy;
+    bool on;
+};
+
+// computeMipmapLOD (textures.cl:198-202)
+MCRT_DEV float mipLod(const mcrt_texture_desc& t, f2 dx, f2 dy) {
+    const float w = fmaxf(fmaxf(fabsf(dx.x), fabsf(dx.y)), fmaxf(fabsf(dy.x), fabsf(dy.y)));
+    return (float)t.numMipLevels - 1.0f + log2f(fmaxf(w, 1e-8f));
+}
+
+// readTexture2Df_lod (textures.cl:148-196); texel stride 4 (computeTexelStride, textures.cl:24-27)
+MCRT_DEV f4 readTexLodDesc(const SceneArgs& s, const mcrt_texture_desc& tex, f2 uv, float lod) {
+    if (lod < 1e-8f || tex.numMipLevels < 2) return readTexDesc(s, tex, uv);
+    if (lod >= (float)(tex.numMipLevels - 1)) {   // the reference reads the last level as 1 x 1
+        mcrt_texture_desc top = tex;
+        uint16_t w = tex.width, h = tex.height;
+        int off = 0;
+        for (int i = 0; i < tex.numMipLevels - 1; ++i) {
+            off += w * h * 4;
+            w = (uint16_t)max(w / 2, 1);
+            h = (uint16_t)max(h / 2, 1);
+        }
+        top.width = 1;
+        top.height = 1;
+        top.memOffset += off;
+        return readTexDesc(s, top, uv);
+    }
+    const int lower = (int)floorf(lod);
+    uint16_t w = tex.width, h = tex.height;
+    int off = 0;
+    for (int i = 0; i < lower; ++i) {
+        off += w * h * 4;
+        w = (uint16_t)max(w / 2, 1);
+        h = (uint16_t)max(h / 2, 1);
+    }
+    mcrt_texture_desc lo = tex, hi = tex;
+    lo.width = w;
+    lo.height = h;
+    lo.memOffset += off;
+    const int offHi = off + w * h * 4;
+    hi.width = (uint16_t)max(w / 2, 1);
+    hi.height = (uint16_t)max(h / 2, 1);
+    hi.memOffset += offHi;
+    const f4 v0 = readTexDesc(s, lo, uv), v1 = readTexDesc(s, hi, uv);
+    const float t = lod - (float)lower;
+    return f4{fmaf(v1.x - v0.x, t, v0.x), fmaf(v1.y - v0.y, t, v0.y), fmaf(v1.z - v0.z, t, v0.z),
+              fmaf(v1.w - v0.w, t, v0.w)};
+}
+
+// readTexture2Df with the LOD path switched on (textures.cl:204-209 with line 207 active)
+MCRT_DEV f4 readTexL(const SceneArgs& s, int texId, f2 uv, const TexLod& L) {
+    if (!L.on) return readTex(s, texId, uv);
+    const mcrt_texture_desc tex = s.textures[texId];
+    return readTexLodDesc(s, tex, uv, mipLod(tex, L.duvdx, L.duvdy));
+}
+
+// solveLinearSystem2x2 (matrix.cl:72-83) with A = makeMat2(a00, a01, a10, a11)
+MCRT_DEV bool solve2x2(float a00, float a01, float a10, float a11, f2 B, f2* x) {
+    const float det = a00 * a11 - a10 * a01;
+    if (fabsf(det) < 1e-8f) return false;
+    *x = f2{cl_div(a11 * B.x - a01 * B.y, det), cl_div(a00 * B.y - a10 * B.x, det)};
+    return true;
+}
+
+// Ray differentials of the camera ray through pixel (x, y) (GeneratePerspectiveRays,
+// PathTracing.cl:22-33): both offset rays start at the camera position.
+MCRT_DEV void cameraDiffDirs(const mcrt_camera& cam, int x, int y, f3& dx, f3& dy) {
+    const f2 r = f2{cl_div(1.0f, (float)cam.width), cl_div(1.0f, (float)cam.height)};
+    const f2 uv = f2{(float)x * r.x, (float)y * r.y};
+    dx = lerpDirection(ld3(cam.r00), ld3(cam.r10), ld3(cam.r11), ld3(cam.r01), uv.x + r.x, uv.y);
+    dy = lerpDirection(ld3(cam.r00), ld3(cam.r10), ld3(cam.r11), ld3(cam.r01), uv.x, uv.y + r.y);
+}
 
 // KRN/materials.cl:76-91 (getUberMaterialProperties)
-MCRT_DEV Uber uberProps(const SceneArgs& s, const mcrt_material& material, f2 uv) {
+MCRT_DEV Uber uberProps(const SceneArgs& s, const mcrt_material& material, f2 uv, const TexLod& L = TexLod{{0, 0}, {0, 0}, false}) {
     Uber u;
-    const f4 Kd_opacity = material.uber_diffuseTexId != -1 ? readTex(s, material.uber_diffuseTexId, uv) : f4{1.0f, 1.0f, 1.0f, 1.0f};
+    const f4 Kd_opacity = material.uber_diffuseTexId != -1 ? readTexL(s, material.uber_diffuseTexId, uv, L) : f4{1.0f, 1.0f, 1.0f, 1.0f};
     u.Kd = Kd_opacity.xyz * ld3(material.uber_kd);
-    u.Ks = (material.uber_glossyTexId != -1 ? readTex(s, material.uber_glossyTexId, uv).xyz : splat3(1.0f)) * ld3(material.uber_ks);
-    u.Kr = (material.uber_specReflectionTexId != -1 ? readTex(s, material.uber_specReflectionTexId, uv).xyz : splat3(1.0f)) *
+    u.Ks = (material.uber_glossyTexId != -1 ? readTexL(s, material.uber_glossyTexId, uv, L).xyz : splat3(1.0f)) * ld3(material.uber_ks);
+    u.Kr = (material.uber_specReflectionTexId != -1 ? readTexL(s, material.uber_specReflectionTexId, uv, L).xyz : splat3(1.0f)) *
            ld3(material.uber_kr);
-    u.Kt.xyz = (material.uber_transmissionTexId != -1 ? readTex(s, material.uber_transmissionTexId, uv).xyz : splat3(1.0f)) *
+    u.Kt.xyz = (material.uber_transmissionTexId != -1 ? readTexL(s, material.uber_transmissionTexId, uv, L).xyz : splat3(1.0f)) *
                ld3(material.uber_kt);
     u.Kt.w = material.uber_kt.w;
-    u.opacity = (material.uber_opacityTexId != -1 ? readTex(s, material.uber_opacityTexId, uv).xyz : splat3(1.0f)) *
+    u.opacity = (material.uber_opacityTexId != -1 ? readTexL(s, material.uber_opacityTexId, uv, L).xyz : splat3(1.0f)) *
                 ld3(material.uber_opacity) * Kd_opacity.w;
-    u.roughness = material.uber_roughnessTexId != -1 ? readTex(s, material.uber_roughnessTexId, uv).xy
+    u.roughness = material.uber_roughnessTexId != -1 ? readTexL(s, material.uber_roughnessTexId, uv, L).xy
                                                       : f2{material.uber_roughness.x, material.uber_roughness.y};
-    u.eta = material.uber_iorTexId != -1 ? readTex(s, material.uber_iorTexId, uv).x : material.uber_eta;
+    u.eta = material.uber_iorTexId != -1 ? readTexL(s, material.uber_iorTexId, uv, L).x : material.uber_eta;
     u.roughness = f2{roughnessToAlpha(u.roughness.x), roughnessToAlpha(u.roughness.y)};
     return u;
 }
@@ -201,7 +284,8 @@ MCRT_DEV f3 sampleTriangle(f3 p0, f3 p1, f3 p2, f2 u, f3* gn) {
 }
 
 // computeSurfaceInteraction (geometry.cl:177-215)
-MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, int shapeIdx, int primIdx, f2 barycentrics) {
+MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, int shapeIdx, int primIdx, f2 barycentrics,
+                                         f3* dpduOut = nullptr, f3* dpdvOut = nullptr) {
     Frame si;
     const mcrt_shape& shape = s.shapes[shapeIdx];
     const uint32_t i0 = s.indices[shape.startIdx + 3 * primIdx];
@@ -223,12 +307,46 @@ MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, int shapeIdx, int p
     computeTrianglePartialDerivates(uv0, uv1, uv2, p0, p1, p2, si.sn, &dpdu, &dpdv);
     si.sdpdu = cl_normalize(dpdu - cl_dot(si.sn, dpdu) * si.sn);
     si.sdpdv = cl_normalize(dpdv - cl_dot(si.sn, dpdv) * si.sn - cl_dot(si.sdpdu, dpdv) * si.sdpdu);
+    if (dpduOut) *dpduOut = dpdu;
+    if (dpdvOut) *dpdvOut = dpdv;
     return si;
 }
 
+// The pixel's uv footprint at a camera-ray hit (computeSurfaceInteractionWithDifferentials,
+// geometry.cl:126-168): intersect the two offset rays with the tangent plane, express the
+// offsets in (dpdu, dpdv) on the two axes the geometric normal is least aligned with.
+// dpdu, dpdv: computeTrianglePartialDerivates' (unnormalised) output.
+MCRT_DEV TexLod surfaceUVDifferentials(const Frame& si, f3 dpdu, f3 dpdv, f3 o, f3 dxDir, f3 dyDir) {
+    TexLod L;
+    L.on = true;
+    const float d = cl_dot(si.gn, si.p);
+    const float tx = cl_div(-(cl_dot(si.gn, o) - d), cl_dot(si.gn, dxDir));
+    const f3 px = o + tx * dxDir;
+    const float ty = cl_div(-(cl_dot(si.gn, o) - d), cl_dot(si.gn, dyDir));
+    const f3 py = o + ty * dyDir;
+    float a00, a01, a10, a11;
+    f2 Bx, By;
+    if (fabsf(si.gn.x) > fabsf(si.gn.y) && fabsf(si.gn.x) > fabsf(si.gn.z)) {
+        a00 = dpdu.y; a01 = dpdv.y; a10 = dpdu.z; a11 = dpdv.z;
+        Bx = f2{px.y, px.z} - f2{si.p.y, si.p.z};
+        By = f2{py.y, py.z} - f2{si.p.y, si.p.z};
+    } else if (fabsf(si.gn.y) > fabsf(si.gn.z)) {
+        a00 = dpdu.x; a01 = dpdv.x; a10 = dpdu.z; a11 = dpdv.z;
+        Bx = f2{px.x, px.z} - f2{si.p.x, si.p.z};
+        By = f2{py.x, py.z} - f2{si.p.x, si.p.z};
+    } else {
+        a00 = dpdu.x; a01 = dpdv.x; a10 = dpdu.y; a11 = dpdv.y;
+        Bx = f2{px.x, px.y} - f2{si.p.x, si.p.y};
+        By = f2{py.x, py.y} - f2{si.p.x, si.p.y};
+    }
+    if (!solve2x2(a00, a01, a10, a11, Bx, &L.duvdx)) L.duvdx = f2{0.0f, 0.0f};
+    if (!solve2x2(a00, a01, a10, a11, By, &L.duvdy)) L.duvdy = f2{0.0f, 0.0f};
+    return L;
+}
+
 // applyNormalMapping_internal (materials.cl:11-19)
-MCRT_DEV void applyNormalMapping(const SceneArgs& s, int texId, Frame& si) {
-    const f3 nm = 2.0f * readTex(s, texId, si.uv).xyz - 1.0f;
+MCRT_DEV void applyNormalMapping(const SceneArgs& s, int texId, Frame& si, const TexLod& L = TexLod{{0, 0}, {0, 0}, false}) {
+    const f3 nm = 2.0f * readTexL(s, texId, si.uv, L).xyz - 1.0f;
     si.sn = cl_normalize(si.sdpdu * nm.x + si.sdpdv * nm.y + si.sn * nm.z);
     si.sdpdu = cl_normalize(cl_cross(si.sn, si.sdpdv));
     si.sdpdv = cl_normalize(cl_cross(si.sdpdu, si.sn));

@@ -56,6 +56,7 @@ SIGNATURES = {
     "mcrt_framebuffer_read_queue": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int32)]),
     "mcrt_framebuffer_queue_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.POINTER(_c.c_int32), _c.c_int]),
     "mcrt_postprocess": (_c.c_int, [_vp, _c.POINTER(T.PostprocessParams)]),
+    "mcrt_render_aov": (_c.c_int, [_vp, _vp, _vp, _vp, _c.c_int, _vp]),
     "mcrt_framebuffer_read_bdpt": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64)]),
     "mcrt_make_pinhole_camera": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _c.c_float, _c.c_float, _c.c_uint32,
                                             _c.c_uint32, _vp, _vp]),
@@ -239,11 +240,20 @@ class FrameBuffer:
         ctx._adopt(self)
 
     def render(self, dscene, cam, frame=0, max_depth=2, sampler=T.SAMPLER_RANDOM, rr=False, rr_start=3,
-               band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_PT):
+               band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_PT, texture_lod=False):
         p = T.FrameParams(frame, max_depth, sampler, 1 if rr else 0, rr_start, band_rows, num_bands, band_index,
-                          integrator)
+                          integrator, 1 if texture_lod else 0)
         cam = np.ascontiguousarray(cam)
         _check(lib().mcrt_render_frame(dscene.h, self.h, _p(cam), _c.byref(p)), self.ctx.h)
+
+    def render_aov(self, dscene, cam, aov=T.AOV_ALBEDO, texture_lod=False):
+        """mcrt_render_aov: (H, W, 4) albedo or (H, W, 3, 4) texture-footprint records."""
+        p = T.FrameParams(0, 1, T.SAMPLER_RANDOM, 0, 3, 8, 1, 0, T.INTEGRATOR_PT, 1 if texture_lod else 0)
+        cam = np.ascontiguousarray(cam)
+        shape = (self.H, self.W, 3, 4) if aov == T.AOV_TEXTURE_LOD else (self.H, self.W, 4)
+        out = np.zeros(shape, np.float32)
+        _check(lib().mcrt_render_aov(dscene.h, self.h, _p(cam), _c.byref(p), aov, _p(out)), self.ctx.h)
+        return out
 
     def accumulate(self, filt, frame):
         filt = np.ascontiguousarray(filt)

@@ -653,6 +653,31 @@ def instances_test_scene(seed=0):
     return b.build()
 
 
+def lod_test_scene(seed=0):
+    """Texture-LOD workload: a large checker floor and a brick wall seen at grazing angles
+    (strong minification), textured spheres with normal maps, every texture with its full mip
+    chain (numMipLevels > 1), plus one untextured sphere."""
+    rng = np.random.default_rng(SEED_BASE + 200 + seed)
+    b = SceneBuilder("lod_test")
+    checker = b.add_texture(tex_checker(256, (230, 230, 230), (30, 30, 120), tiles=32), mips=True)
+    bricks = b.add_texture(tex_bricks(128), mips=True)
+    normal = b.add_texture(tex_normalmap(64, rng), mips=True)
+    leaf = b.add_texture(tex_leaf(64), wrap=2, mips=True)
+    floor = b.add_material(kd=(1, 1, 1), ks=(0.04, 0.04, 0.04), roughness=0.4, diffuseTexId=checker)
+    wall = b.add_material(kd=(1, 1, 1), diffuseTexId=bricks, normalMapId=normal)
+    b.add_mesh(*grid((-40, 0, -10), (80, 0, 0), (0, 0, 120), 8, 8, uv_scale=12.0, flip=True), floor)
+    b.add_mesh(*grid((-40, 0, 60), (80, 0, 0), (0, 12, 0), 4, 4, uv_scale=6.0, flip=True), wall)
+    for i in range(5):
+        m = b.add_material(kd=(0.9, 0.9, 0.9), ks=(0.2, 0.2, 0.2), roughness=0.3,
+                           diffuseTexId=(leaf if i % 2 else checker), normalMapId=normal if i == 2 else -1)
+        b.add_mesh(*displaced_sphere(np.array([-6.0 + 3.0 * i, 1.0, 4.0 + 2.0 * i]), 1.0, 32, 16, rng, amp=0.05), m)
+    plain = b.add_material(kd=(0.7, 0.3, 0.2))
+    b.add_mesh(*displaced_sphere(np.array([8.0, 1.0, 2.0]), 1.0, 32, 16, rng, amp=0.05), plain)
+    b.add_directional_light(euler_forward(40.0, 20.0), (5.0, 5.0, 5.0))
+    b.add_point_light((0.0, 6.0, 0.0), (20.0, 20.0, 20.0))
+    return b.build()
+
+
 def san_miguel_proxy(tris=10_000_000, seed=4, tex_size=512):
     """San-Miguel proxy (configs 4/5 and the headline metric): courtyard with arcades,
     tables, ~70 % of the triangles in foliage quads with alpha cut-out leaves, >= 64
@@ -822,4 +847,5 @@ CAMERAS = {
     "sponza_proxy": ((12.0, 3.0, 0.5), (-4.0, 4.5, -0.5), 45.0),
     "instanced_proxy": ((0.0, 9.0, -17.0), (0.0, 0.5, 0.0), 45.0),
     "instances_test": ((0.0, 5.0, -13.0), (0.0, 1.0, 0.0), 45.0),
+    "lod_test": ((0.0, 2.0, -9.0), (0.0, 1.0, 10.0), 45.0),
 }

@@ -140,7 +140,7 @@ class FrameParams(ctypes.Structure):
         ("frame_index", ctypes.c_int32), ("max_depth", ctypes.c_int32), ("sampler", ctypes.c_int32),
         ("russian_roulette", ctypes.c_int32), ("rr_start_depth", ctypes.c_int32),
         ("band_rows", ctypes.c_int32), ("num_bands", ctypes.c_int32), ("band_index", ctypes.c_int32),
-        ("integrator", ctypes.c_int32),
+        ("integrator", ctypes.c_int32), ("texture_lod", ctypes.c_int32),
     ]
 
 
@@ -174,3 +174,6 @@ def make_filter(kind=BOX, radius=(2.0, 2.0), pixel_offset=(0.0, 0.0), B=1.0 / 3,
     f["gaussianExpY"] = np.exp(-alpha * radius[1] * radius[1])
     f["pixelOffset"] = pixel_offset
     return f
+
+AOV_ALBEDO = 0        # MCRT_AOV_ALBEDO
+AOV_TEXTURE_LOD = 1   # MCRT_AOV_TEXTURE_LOD

@@ -356,6 +356,7 @@ def clref(variant="ieee"):
         L.clref_bdpt_render.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _vp]
         L.clref_bdpt_read.restype = _c.c_int64
         L.clref_bdpt_read.argtypes = [_vp, _c.c_int, _vp]
+        L.clref_probe_lod.argtypes = [_vp, _c.c_char_p, _vp, _vp, _c.c_int, _c.c_int, _vp]
         L.clref_scene_set_two_level.argtypes = [_vp, _vp, _c.c_int64, _vp, _c.c_int64, _vp, _c.c_int64, _vp,
                                                 _c.c_int64, _c.c_int]
         st = L.clref_init(os.path.join(HERE, "_ref").encode(), variant.encode())
@@ -409,7 +410,7 @@ class CLRefScene:
         return img
 
     READ = {"rays": (0, 48), "isect": (1, 32), "shadow_rays": (2, 48), "temp": (3, 16), "throughput": (4, 32),
-            "occlusion": (5, 4), "radiance": (6, 16)}
+            "occlusion": (5, 4), "radiance": (6, 16), "ray_differentials": (7, 64)}
 
     def read(self, which, W, H):
         """Raw bytes of an intermediate buffer of the last frame (diagnostics)."""
@@ -418,6 +419,21 @@ class CLRefScene:
         st = self.L.clref_read(self.h, idx, _p(out))
         if st != 0:
             raise RuntimeError(f"clref_read {st}: {self.L.clref_error().decode()}")
+        return out
+
+    def probe_lod(self, cam):
+        """The reference's (unused) texture-LOD functions at its own primary hits: renders one
+        depth-1 frame (GeneratePerspectiveRays + intersect), then runs clprobe_lod.cl's ProbeLOD
+        on its intersections and ray differentials.  Returns (H, W, 3, 4) float32."""
+        W, H = int(cam["width"][0]), int(cam["height"][0])
+        self.render(cam, frame=0, max_depth=1)
+        isect = self.read("isect", W, H)
+        diffs = self.read("ray_differentials", W, H)
+        out = np.zeros((H, W, 3, 4), np.float32)
+        st = self.L.clref_probe_lod(self.h, os.path.join(HERE, "_ref", "clref_probe_lod.hsaco").encode(), _p(isect),
+                                    _p(diffs), W, H, _p(out))
+        if st != 0:
+            raise RuntimeError(f"clref_probe_lod {st}: {self.L.clref_error().decode()}")
         return out
 
     def render_bdpt(self, cam, frame=0, max_depth=2):

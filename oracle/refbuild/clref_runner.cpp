@@ -412,9 +412,9 @@ __attribute__((visibility("default"))) int clref_trace(void* sp, const void* ray
 __attribute__((visibility("default"))) int clref_read(void* sp, int which, void* out) {
     Scene* s = (Scene*)sp;
     const size_t n = (size_t)s->W * s->H;
-    cl_mem m[7] = {s->rays, s->isect, s->shadowRays, s->temp, s->thr, s->occl, s->radiance};
-    size_t sz[7] = {48, 32, 48, 16, 32, 4, 16};
-    if (which < 0 || which > 6 || !m[which]) { g_err = "clref_read: bad buffer"; return -1; }
+    cl_mem m[8] = {s->rays, s->isect, s->shadowRays, s->temp, s->thr, s->occl, s->radiance, s->rayDiff};
+    size_t sz[8] = {48, 32, 48, 16, 32, 4, 16, 64};
+    if (which < 0 || which > 7 || !m[which]) { g_err = "clref_read: bad buffer"; return -1; }
     return ok(clEnqueueReadBuffer(R.q, m[which], CL_TRUE, 0, sz[which] * n, out, 0, nullptr, nullptr), "read") ? 0 : -2;
 }
 
@@ -453,6 +453,42 @@ __attribute__((visibility("default"))) int clref_probe(void* sp, const char* hsa
     clReleaseMemObject(bi);
     clReleaseMemObject(bd);
     clReleaseMemObject(bs);
+    clReleaseMemObject(bo);
+    return good ? 0 : -5;
+}
+
+// Texture-LOD probe (clprobe_lod.cl, test infrastructure): the reference's unused LOD functions
+// over given primary intersections (32 B) and ray differentials (64 B); out: 3 float4 / pixel.
+__attribute__((visibility("default"))) int clref_probe_lod(void* sp, const char* hsaco, const void* isects,
+                                                           const void* diffs, int W, int H, float* out) {
+    Scene* s = (Scene*)sp;
+    static cl_program prog = nullptr;
+    static cl_kernel k = nullptr;
+    cl_int e = 0;
+    if (!k) {
+        prog = loadProgram(hsaco);
+        if (!prog) return -1;
+        k = clCreateKernel(prog, "ProbeLOD", &e);
+        if (!ok(e, "kernel ProbeLOD")) return -2;
+    }
+    const size_t n = (size_t)W * H;
+    cl_mem bi = buf(32 * n, isects), bd = buf(64 * n, diffs);
+    std::vector<float> zero(12 * n, 0.0f);
+    cl_mem bo = buf(12 * 4 * n, zero.data());
+    int a = 0;
+    if (!setSceneArgs(k, s, a)) return -3;
+    e = 0;
+    e |= arg(k, a++, W);
+    e |= arg(k, a++, H);
+    e |= arg(k, a++, bi);
+    e |= arg(k, a++, bd);
+    e |= arg(k, a++, bo);
+    if (!ok(e, "probe lod args")) return -4;
+    size_t gs = (n + 63) / 64 * 64, ls = 64;
+    bool good = ok(clEnqueueNDRangeKernel(R.q, k, 1, nullptr, &gs, &ls, 0, nullptr, nullptr), "probe lod launch") &&
+                ok(clEnqueueReadBuffer(R.q, bo, CL_TRUE, 0, 12 * 4 * n, out, 0, nullptr, nullptr), "probe lod read");
+    clReleaseMemObject(bi);
+    clReleaseMemObject(bd);
     clReleaseMemObject(bo);
     return good ? 0 : -5;
 }

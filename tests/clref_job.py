@@ -112,6 +112,19 @@ def tl_job(out_path, variant):
     print(f"clref two-level job ({variant}): {len(res)} arrays -> {out_path}")
 
 
+LOD_CASES = [("lod_test", 160, 120), ("mixed", 96, 64)]
+
+
+def lod_job(out_path, variant):
+    """The reference's texture-LOD functions at its own primary hits (clprobe_lod.cl)."""
+    res = {}
+    for name, W, H in LOD_CASES:
+        cs = po.CLRefScene(build_scene(name), variant)
+        res[f"lod_{name}_{W}x{H}"] = cs.probe_lod(scene_camera(name, W, H))
+    np.savez_compressed(out_path, **res)
+    print(f"clref lod job ({variant}): {len(res)} arrays -> {out_path}")
+
+
 def build_scene(name):
     if name == "mixed":
         return scenes.test_scene()
@@ -119,6 +132,8 @@ def build_scene(name):
         return scenes.cornell_box(os.path.join(ROOT, "tests", "golden", "cornell_original.npz"))
     if name == "dragon_small":
         return scenes.dragon_proxy(tris=20000)
+    if name == "lod_test":
+        return scenes.lod_test_scene()
     if name == "instances_test":
         return scenes.instances_test_scene()
     if name == "instanced_small":
@@ -138,6 +153,9 @@ def main():
     variant = sys.argv[2] if len(sys.argv) > 2 else "ieee"
     if len(sys.argv) > 3 and sys.argv[3] == "bdpt":
         bdpt_job(out_path, variant)
+        return
+    if len(sys.argv) > 3 and sys.argv[3] == "lod":
+        lod_job(out_path, variant)
         return
     if len(sys.argv) > 3 and sys.argv[3] == "2l":
         tl_job(out_path, variant)
