@@ -12,6 +12,8 @@
 // boxes, leaves their triangle), one flat loop per ray with a per-lane LDS short stack
 // (16 entries, [entry][lane] layout -> conflict free) spilling to a per-ray global column;
 // one wave per workgroup, the hardware dispatcher schedules the waves.
+#include <algorithm>
+
 #include "mcrt_device.h"
 #include "mcrt_internal.h"
 #include "mcrt_traverse.h"
@@ -511,17 +513,19 @@ __global__ __launch_bounds__(256) void k_tonemap(int n, float Lwhite, const floa
     out[i] = make_float4(p.x * s, p.y * s, p.z * s, p.w);
 }
 
-// Attainable-bandwidth probe (mcrt_ctx_stream_copy): one float4 per thread, 4 per lane in flight
-// through 4 independent loads; the grid covers the array (no grid-stride loop).
-__global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
-    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
-    float4 v[4];
+// Attainable-bandwidth probe (mcrt_ctx_stream_copy): a persistent grid (8 workgroups per CU)
+// strides over the array; each lane keeps 4 independent 16-B nontemporal loads in flight.
+__global__ __launch_bounds__(256) void k_stream_copy(const f4* __restrict__ src, f4* __restrict__ dst, size_t n) {
+    const size_t step = (size_t)gridDim.x * 1024;
+    for (size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x; base < n; base += step) {
+        f4 v[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (base + 256 * k < n) v[k] = src[base + 256 * k];
+        for (int k = 0; k < 4; ++k)
+            if (base + 256 * k < n) v[k] = __builtin_nontemporal_load(src + base + 256 * k);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (base + 256 * k < n) dst[base + 256 * k] = v[k];
+        for (int k = 0; k < 4; ++k)
+            if (base + 256 * k < n) __builtin_nontemporal_store(v[k], dst + base + 256 * k);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -593,8 +597,10 @@ void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStrea
     hipLaunchKernelGGL(k_tonemap, dim3((n + 255) / 256), dim3(256), 0, st, n, Lwhite, in, out);
 }
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st) {
-    (void)numCUs;
-    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n4 + 1023) / 1024)), dim3(256), 0, st, src, dst, n4);
+    const size_t need = (n4 + 1023) / 1024;
+    const size_t blocks = std::min(need, (size_t)std::max(numCUs, 1) * 8);
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const f4*>(src),
+                       reinterpret_cast<f4*>(dst), n4);
 }
 
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st) {
