@@ -193,8 +193,7 @@ def main():
         ctx.set_profiling(True)
     ctx.reset_stats()
     if world > 1:
-        acc_s = torch.empty(W * H * 4, dtype=torch.float32, device="cuda")
-        acc_w = torch.empty(W * H, dtype=torch.float32, device="cuda")
+        acc_buf, acc_s, acc_w = mdist.packed_accumulators(W * H, "cuda")   # one buffer -> one reduce
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
@@ -204,7 +203,7 @@ def main():
         fb.copy_device(1, acc_s.data_ptr())
         fb.copy_device(3, acc_w.data_ptr())
         ctx.sync()
-        mdist.reduce_accumulators(acc_s, acc_w, dst=0)
+        mdist.reduce_packed(acc_buf, dst=0)
         if rank == 0:
             torch.cuda.synchronize()
             fb.set_accumulation(acc_s.data_ptr(), acc_w.data_ptr())

@@ -324,6 +324,16 @@ MCRT_API mcrt_status mcrt_trace_any(mcrt_scene scene, const mcrt_ray* d_rays, in
 MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint32_t height,
                                              mcrt_framebuffer* out);
 MCRT_API mcrt_status mcrt_framebuffer_destroy(mcrt_framebuffer fb);
+/* Frames in flight (PT): mcrt_render_frame for frame i uses buffer slot i mod n on its own HIP
+ * stream and returns at once; mcrt_accumulate runs on the context stream in call order, after
+ * that frame's render, so n frames overlap on the GPU and the image is unchanged bit for bit
+ * (the reference's pass sequence per frame, RTPathTracingPass::update then
+ * RTReconstructionPass::updateReconstruction, is kept; only its clFinish after every launch is
+ * gone).  0 = auto: one slot per band share (num_bands), at most MCRT_MAX_FRAMES_IN_FLIGHT --
+ * a whole-image frame fills the GPU alone, a 1/N band share does not.  Reads of the frame
+ * buffer synchronise every slot.  No reference counterpart (its passes are synchronous). */
+#define MCRT_MAX_FRAMES_IN_FLIGHT 4
+MCRT_API mcrt_status mcrt_framebuffer_set_frames_in_flight(mcrt_framebuffer fb, int32_t n);
 /* Renders one 1-spp frame: PrimaryRays + maxDepth x (shade, shadow, extend).
  * Result: per-pixel frame radiance ("RadianceBufferCL"). */
 MCRT_API mcrt_status mcrt_render_frame(mcrt_scene scene, mcrt_framebuffer fb, const mcrt_camera* camera,

@@ -13,9 +13,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
+#include <vector>
+#include <map>
+#include <tuple>
 #include <vector>
 
 #include "mcrt_internal.h"
@@ -45,6 +50,7 @@ struct mcrt_ctx_s {
     bool profiling = false;
     bool fuseShadowExtend = true;   // MCRT_NO_FUSE=1 launches k_shadow and k_extend separately (A/B)
     bool sortRays = false;          // MCRT_SORT_RAYS=1: global sort of the extension queue (mcrt_raysort.hip)
+    int envFramesInFlight = 0;      // MCRT_FRAMES_IN_FLIGHT=n overrides the frame buffers' setting (A/B)
     std::string error;
     struct Pending {
         int kernel;
@@ -75,6 +81,9 @@ struct mcrt_scene_s {
     void* dSobol = nullptr;
     void* dLights = nullptr;
     void* dMaterials = nullptr;
+    void* dSurf = nullptr;       // surface records (SceneArgs::surf), 128 B per distinct mesh triangle
+    void* dSurfBase = nullptr;   // per shape: its first surface record
+    void* dSurfMeshes = nullptr; // build scratch: startIdx | startVertex | base per distinct mesh
     uint32_t numLights = 0, numMaterials = 0, numTextures = 0;
     bool hasSobol = false;
     // BVH
@@ -94,10 +103,38 @@ struct mcrt_scene_s {
     float bbLo[3] = {0, 0, 0}, bbHi[3] = {0, 0, 0};   // world bounds (root record of the BVH)
 };
 
+// One frame in flight (PT): the per-frame buffers of mcrt_render_frame, its own stream and
+// spill columns.  Frame i renders in slot i mod S on that slot's stream while mcrt_accumulate
+// runs on the context stream in frame order (it waits for the slot's `done` event and records
+// `free` after reading the slot's radiance), so S frames overlap on the GPU -- each frame's
+// arithmetic and the per-pixel accumulation order are unchanged, so the image is the same bit
+// for bit.  Small per-rank frames (tile split over many GPUs) do not fill 256 CUs alone.
+struct FrameSlot {
+    float4* radiance = nullptr;
+    float4* hitsP = nullptr;     // primary hits by pixel
+    float4* hitsE = nullptr;     // extension hits by queue slot
+    float4* eO[2] = {};
+    float4* eD[2] = {};
+    float4* eT[2] = {};
+    float4 *sO = nullptr, *sD = nullptr, *sL = nullptr;
+    int* counters = nullptr;     // [0..31] shadow counts, [32..63] ext counts, [64..] work counters, camera @128
+    uint32_t* spill = nullptr;   // per-ray traversal spill columns of this slot's launches
+    size_t spillWords = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;   // recorded after the slot's last render
+    hipEvent_t free = nullptr;   // recorded on the context stream after the slot's buffers were last read
+    int lastMaxDepth = 0;
+    int64_t lastPixels = 0;
+};
+
 struct mcrt_framebuffer_s {
     mcrt_ctx ctx = nullptr;
     uint32_t W = 0, H = 0;
     size_t N = 0;
+    std::vector<FrameSlot> slot;   // slot[0] always allocated; others on first use
+    int cur = 0, next = 0;         // slot of the last rendered frame / of the next one
+    int framesInFlight = 0;        // 0 = auto (mcrt_framebuffer_set_frames_in_flight)
+    // views of slot[cur] (the last rendered frame)
     float4* radiance = nullptr;
     float4* wsum = nullptr;
     float* wts = nullptr;
@@ -113,7 +150,7 @@ struct mcrt_framebuffer_s {
     float4* eD[2] = {};
     float4* eT[2] = {};
     float4 *sO = nullptr, *sD = nullptr, *sL = nullptr;
-    int* counters = nullptr;     // [0..31] shadow counts, [32..63] ext counts, [64..] work counters
+    int* counters = nullptr;
     int lastMaxDepth = 0;
     int64_t lastPixels = 0;
     FrameArgs bands{};      // band layout of the last mcrt_render_frame (used by mcrt_accumulate)
@@ -160,16 +197,18 @@ struct Timed {
     hipEvent_t a = nullptr, b = nullptr;
     const int* countDev;
     int64_t items;
-    Timed(mcrt_ctx ctx, int kernel, const int* countDev_, int64_t items_) : c(ctx), k(kernel), countDev(countDev_), items(items_) {
+    hipStream_t st;
+    Timed(mcrt_ctx ctx, int kernel, const int* countDev_, int64_t items_, hipStream_t stream = nullptr)
+        : c(ctx), k(kernel), countDev(countDev_), items(items_), st(stream ? stream : ctx->stream) {
         if (c->profiling) {
             hipEventCreate(&a);
             hipEventCreate(&b);
-            hipEventRecord(a, c->stream);
+            hipEventRecord(a, st);
         }
     }
     ~Timed() {
         if (c->profiling) {
-            hipEventRecord(b, c->stream);
+            hipEventRecord(b, st);
             c->pending.push_back({k, a, b, countDev, items});
         }
     }
@@ -177,8 +216,8 @@ struct Timed {
 
 static void drain_pending(mcrt_ctx ctx) {
     if (ctx->pending.empty()) return;
-    hipStreamSynchronize(ctx->stream);
     for (auto& p : ctx->pending) {
+        hipEventSynchronize(p.b);   // events may sit on frame-slot streams
         float ms = 0.0f;
         hipEventElapsedTime(&ms, p.a, p.b);
         ctx->totalMs[p.kernel] += ms;
@@ -270,6 +309,8 @@ static SceneArgs scene_args(mcrt_scene s) {
     a.lights = (const mcrt_light*)s->dLights;
     a.materials = (const mcrt_material*)s->dMaterials;
     a.nodes = (const float4*)s->dNodes;
+    a.surf = (const float4*)s->dSurf;
+    a.surfBase = (const uint32_t*)s->dSurfBase;
     a.numLights = (int)s->numLights;
     return a;
 }
@@ -295,6 +336,7 @@ MCRT_API mcrt_status mcrt_ctx_create(int device, mcrt_ctx* out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
     if (const char* nf = std::getenv("MCRT_NO_FUSE")) c->fuseShadowExtend = nf[0] != '1';
     if (const char* sr = std::getenv("MCRT_SORT_RAYS")) c->sortRays = sr[0] == '1';
+    if (const char* fi = std::getenv("MCRT_FRAMES_IN_FLIGHT")) c->envFramesInFlight = std::atoi(fi);
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(nullptr, MCRT_ERROR_DEVICE, "hipStreamCreate failed");
@@ -316,7 +358,9 @@ MCRT_API mcrt_status mcrt_ctx_destroy(mcrt_ctx ctx) {
 
 MCRT_API mcrt_status mcrt_ctx_synchronize(mcrt_ctx ctx) {
     if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
+    hipSetDevice(ctx->device);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipDeviceSynchronize());   // frame-slot streams of the context's frame buffers
     return MCRT_OK;
 }
 
@@ -392,7 +436,8 @@ MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx) {
 // ---------------------------------------------------------------------------
 static void scene_free_device(mcrt_scene s) {
     void** ptrs[] = {&s->dShapes, &s->dIndices, &s->dPositions, &s->dUvs, &s->dNormals, &s->dTextures,
-                     &s->dTexData, &s->dSobol, &s->dLights, &s->dMaterials, &s->dNodes, &s->dTris};
+                     &s->dTexData, &s->dSobol, &s->dLights, &s->dMaterials, &s->dNodes, &s->dTris,
+                     &s->dSurf, &s->dSurfBase, &s->dSurfMeshes};
     for (void** p : ptrs) {
         if (*p) hipFree(*p);
         *p = nullptr;
@@ -402,6 +447,54 @@ static void scene_free_device(mcrt_scene s) {
     s->dSpill = nullptr;
     s->spillRays = 0;
     s->dScratch = nullptr;
+}
+
+// Surface records (SceneArgs::surf): shapes with the same (startIdx, startVertex, numTriangles)
+// -- RTScene's instances of one mesh -- share one record range; the records are gathered on the
+// device from the uploaded index/vertex arrays.  Rebuilt when shapes change.
+static hipError_t build_surface_records(mcrt_scene s) {
+    hipStream_t st = s->ctx->stream;
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> meshOf;
+    std::vector<uint32_t> mStart, mVert, mBase, shapeBase(s->shapes.size());
+    uint32_t total = 0;
+    for (size_t i = 0; i < s->shapes.size(); ++i) {
+        const mcrt_shape& sh = s->shapes[i];
+        auto key = std::make_tuple((uint32_t)sh.startIdx, (uint32_t)sh.startVertex, (uint32_t)sh.numTriangles);
+        auto it = meshOf.find(key);
+        if (it == meshOf.end()) {
+            it = meshOf.emplace(key, total).first;
+            if (sh.numTriangles > 0) {
+                mStart.push_back(sh.startIdx);
+                mVert.push_back(sh.startVertex);
+                mBase.push_back(total);
+            }
+            total += sh.numTriangles;
+        }
+        shapeBase[i] = it->second;
+    }
+    hipError_t e = hipStreamSynchronize(st);   // the old records may still be read
+    void** old[] = {&s->dSurf, &s->dSurfBase, &s->dSurfMeshes};
+    for (void** p : old) {
+        if (*p) hipFree(*p);
+        *p = nullptr;
+    }
+    const int nm = (int)mBase.size();
+    std::vector<uint32_t> meshes(3 * (size_t)std::max(nm, 1));
+    std::copy(mStart.begin(), mStart.end(), meshes.begin());
+    std::copy(mVert.begin(), mVert.end(), meshes.begin() + nm);
+    std::copy(mBase.begin(), mBase.end(), meshes.begin() + 2 * nm);
+    if (e == hipSuccess) e = hipMalloc(&s->dSurf, (size_t)std::max(total, 1u) * 128);
+    if (e == hipSuccess) e = upload(&s->dSurfBase, shapeBase.data(), shapeBase.size(), st);
+    if (e == hipSuccess) e = upload(&s->dSurfMeshes, meshes.data(), meshes.size(), st);
+    if (e == hipSuccess && nm > 0) {
+        const uint32_t* m = (const uint32_t*)s->dSurfMeshes;
+        mcrt::launch_surface_records(m, m + nm, m + 2 * nm, nm, total, (const uint32_t*)s->dIndices,
+                                     (const float4*)s->dPositions, (const float2*)s->dUvs, (const float4*)s->dNormals,
+                                     (float4*)s->dSurf, st);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e;
 }
 
 MCRT_API mcrt_status mcrt_scene_create(mcrt_ctx ctx, const mcrt_scene_desc* d, mcrt_scene* out) {
@@ -455,6 +548,7 @@ MCRT_API mcrt_status mcrt_scene_create(mcrt_ctx ctx, const mcrt_scene_desc* d, m
     UP(dMaterials, d->materials, d->num_materials);
 #undef UP
     if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = build_surface_records(s);
     if (e != hipSuccess) {
         scene_free_device(s);
         delete s;
@@ -512,7 +606,10 @@ MCRT_API mcrt_status mcrt_scene_update_shapes(mcrt_scene s, const mcrt_shape* sh
         if (sh[i].startIdx != s->shapes[i].startIdx || sh[i].numTriangles != s->shapes[i].numTriangles)
             return fail(s->ctx, MCRT_ERROR_INVALID_ARG, "shape topology must not change");
     s->shapes.assign(sh, sh + n);
-    return replace_array(s, &s->dShapes, sh, sizeof(mcrt_shape) * n);
+    mcrt_status st = replace_array(s, &s->dShapes, sh, sizeof(mcrt_shape) * n);
+    if (st != MCRT_OK) return st;
+    HIPCHK(s->ctx, build_surface_records(s));   // startVertex may have moved
+    return MCRT_OK;
 }
 
 static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_point t0, const float* box6);
@@ -772,14 +869,79 @@ static void fb_free_bdpt(mcrt_framebuffer fb) {
     fb->bdptDepth = 0;
 }
 
+static void slot_free(FrameSlot& k) {
+    if (k.stream) hipStreamSynchronize(k.stream);
+    void* ptrs[] = {k.radiance, k.hitsP, k.hitsE, k.eO[0], k.eO[1], k.eD[0], k.eD[1], k.eT[0], k.eT[1],
+                    k.sO,       k.sD,    k.sL,    k.counters, k.spill};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    if (k.done) hipEventDestroy(k.done);
+    if (k.free) hipEventDestroy(k.free);
+    if (k.stream) hipStreamDestroy(k.stream);
+    k = FrameSlot();
+}
+
 static void fb_free(mcrt_framebuffer fb) {
-    void* ptrs[] = {fb->radiance, fb->wsum, fb->wts,   fb->image, fb->hitsP, fb->hitsE,    fb->eO[0],
-                    fb->eO[1],    fb->eD[0], fb->eD[1], fb->eT[0], fb->eT[1], fb->sO,       fb->sD,
-                    fb->sL,       fb->counters, fb->denoised, fb->display, fb->sortO, fb->sortD,
-                    fb->sortT,    fb->sortScratch};
+    for (auto& k : fb->slot) slot_free(k);
+    void* ptrs[] = {fb->wsum, fb->wts, fb->image, fb->denoised, fb->display, fb->sortO, fb->sortD, fb->sortT,
+                    fb->sortScratch};
     for (void* p : ptrs)
         if (p) hipFree(p);
     fb_free_bdpt(fb);
+}
+
+static hipError_t slot_alloc(FrameSlot& k, size_t N) {
+    hipError_t e = hipSuccess;
+    auto A = [&](auto** p, size_t bytes) {
+        if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
+    };
+    A(&k.radiance, 16 * N);
+    A(&k.hitsP, 16 * N);
+    A(&k.hitsE, 16 * N);
+    for (int i = 0; i < 2; ++i) { A(&k.eO[i], 16 * N); A(&k.eD[i], 16 * N); A(&k.eT[i], 16 * N); }
+    A(&k.sO, 16 * N);
+    A(&k.sD, 16 * N);
+    A(&k.sL, 16 * N);
+    A(&k.counters, 256 * sizeof(int));
+    if (e == hipSuccess) e = hipMemset(k.radiance, 0, 16 * N);
+    if (e == hipSuccess) e = hipMemset(k.counters, 0, 256 * sizeof(int));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&k.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&k.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&k.free, hipEventDisableTiming);
+    if (e != hipSuccess) slot_free(k);
+    return e;
+}
+
+// The fb's radiance/queue/counter fields view slot k (the last rendered frame).
+static void fb_bind(mcrt_framebuffer fb, int k) {
+    FrameSlot& s = fb->slot[k];
+    fb->cur = k;
+    fb->radiance = s.radiance;
+    fb->hitsP = s.hitsP;
+    fb->hitsE = s.hitsE;
+    for (int i = 0; i < 2; ++i) { fb->eO[i] = s.eO[i]; fb->eD[i] = s.eD[i]; fb->eT[i] = s.eT[i]; }
+    fb->sO = s.sO;
+    fb->sD = s.sD;
+    fb->sL = s.sL;
+    fb->counters = s.counters;
+    fb->lastMaxDepth = s.lastMaxDepth;
+    fb->lastPixels = s.lastPixels;
+}
+
+// Host reads and context-stream work that touch the slots: all slot streams first.
+static hipError_t fb_sync(mcrt_framebuffer fb) {
+    hipError_t e = hipSuccess;
+    for (auto& k : fb->slot)
+        if (k.stream && e == hipSuccess) e = hipStreamSynchronize(k.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(fb->ctx->stream);
+    return e;
+}
+
+// Makes the context stream wait for every slot's last render (work on the context stream
+// that reads or rewrites slot buffers: BDPT, AOVs, device copies).
+static void ctx_wait_slots(mcrt_framebuffer fb) {
+    for (auto& k : fb->slot)
+        if (k.stream) hipStreamWaitEvent(fb->ctx->stream, k.done, 0);
 }
 
 // RTBDPTPass::createBuffers (RTBDPTPass.cpp:442-479), sized for max depth D.  The persistent
@@ -830,26 +992,19 @@ MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint3
     auto A = [&](auto** p, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
     };
-    A(&fb->radiance, 16 * N);
     A(&fb->wsum, 16 * N);
     A(&fb->wts, 4 * N);
     A(&fb->image, 16 * N);
     A(&fb->denoised, 16 * N);
     A(&fb->display, 16 * N);
-    A(&fb->hitsP, 16 * N);
-    A(&fb->hitsE, 16 * N);
-    for (int i = 0; i < 2; ++i) { A(&fb->eO[i], 16 * N); A(&fb->eD[i], 16 * N); A(&fb->eT[i], 16 * N); }
-    A(&fb->sO, 16 * N);
-    A(&fb->sD, 16 * N);
-    A(&fb->sL, 16 * N);
-    A(&fb->counters, 256 * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(fb->radiance, 0, 16 * N);
+    fb->slot.resize(MCRT_MAX_FRAMES_IN_FLIGHT);
+    if (e == hipSuccess) e = slot_alloc(fb->slot[0], N);
+    if (e == hipSuccess) fb_bind(fb, 0);
     if (e == hipSuccess) e = hipMemset(fb->wsum, 0, 16 * N);
     if (e == hipSuccess) e = hipMemset(fb->wts, 0, 4 * N);
     if (e == hipSuccess) e = hipMemset(fb->image, 0, 16 * N);
     if (e == hipSuccess) e = hipMemset(fb->denoised, 0, 16 * N);
     if (e == hipSuccess) e = hipMemset(fb->display, 0, 16 * N);
-    if (e == hipSuccess) e = hipMemset(fb->counters, 0, 256 * sizeof(int));
     if (e != hipSuccess) {
         fb_free(fb);
         delete fb;
@@ -860,10 +1015,17 @@ MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint3
     return MCRT_OK;
 }
 
+MCRT_API mcrt_status mcrt_framebuffer_set_frames_in_flight(mcrt_framebuffer fb, int32_t n) {
+    if (!fb || n < 0 || n > MCRT_MAX_FRAMES_IN_FLIGHT)
+        return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "frames in flight must be 0 (auto) .. 4");
+    fb->framesInFlight = n;
+    return MCRT_OK;
+}
+
 MCRT_API mcrt_status mcrt_framebuffer_destroy(mcrt_framebuffer fb) {
     if (!fb) return MCRT_OK;
     hipSetDevice(fb->ctx->device);
-    hipStreamSynchronize(fb->ctx->stream);
+    fb_sync(fb);
     fb_free(fb);
     delete fb;
     return MCRT_OK;
@@ -893,6 +1055,16 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
     // tile ids are dealt in the kernel as tb -> gb; count the band-local blocks that map inside
     f.numTiles = myBlocks * f.tilesX;
     return true;
+}
+
+// Frames in flight for a render with band layout f: the frame buffer's setting (or the
+// MCRT_FRAMES_IN_FLIGHT override); auto = one per band share, up to 4 (MI355X: 4 hardware queues
+// per process) -- a whole-image frame alone fills the GPU, a 1/N band share does not.
+static int frames_in_flight(mcrt_framebuffer fb, const FrameArgs& f) {
+    int n = fb->ctx->envFramesInFlight > 0 ? fb->ctx->envFramesInFlight : fb->framesInFlight;
+    if (n <= 0) n = f.numBands;
+    if (fb->ctx->sortRays) n = 1;   // one set of sort buffers
+    return std::max(1, std::min(n, MCRT_MAX_FRAMES_IN_FLIGHT));
 }
 
 // RTBDPTPass::update (RTBDPTPass.cpp:67-128): start vertices, D+1 rounds of (trace, vertex),
@@ -993,10 +1165,38 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
     std::string err;
     if (!frame_args(fb, p, f, err)) return fail(ctx, MCRT_ERROR_INVALID_ARG, err);
     hipSetDevice(ctx->device);
-    if (p->integrator == MCRT_INTEGRATOR_BDPT) return render_bdpt(s, fb, cam, p, f);
-    hipStream_t st = ctx->stream;
-    fb->lastMaxDepth = p->max_depth;
-    fb->lastPixels = 0;
+    if (p->integrator == MCRT_INTEGRATOR_BDPT) {
+        ctx_wait_slots(fb);   // BDPT runs on the context stream in slot 0's buffers
+        fb_bind(fb, 0);
+        fb->next = 1 % frames_in_flight(fb, f);
+        mcrt_status r = render_bdpt(s, fb, cam, p, f);
+        hipEventRecord(fb->slot[0].done, ctx->stream);
+        hipEventRecord(fb->slot[0].free, ctx->stream);
+        fb->slot[0].lastMaxDepth = fb->lastMaxDepth;
+        fb->slot[0].lastPixels = fb->lastPixels;
+        return r;
+    }
+    // frame slot: its buffers are free once the accumulation of its previous frame has read them
+    const int S = frames_in_flight(fb, f);
+    const int ks = fb->next % S;
+    FrameSlot& slot = fb->slot[ks];
+    if (!slot.stream) HIPCHK(ctx, slot_alloc(slot, fb->N));
+    const int cap = s->spillCap;
+    const size_t spillRays = (std::max((size_t)f.numTiles * 64, 2 * fb->N + 64) + 63) / 64 * 64;
+    if (!slot.spill || slot.spillWords < spillRays * cap) {
+        HIPCHK(ctx, hipStreamSynchronize(slot.stream));
+        if (slot.spill) hipFree(slot.spill);
+        slot.spill = nullptr;
+        slot.spillWords = 0;
+        HIPCHK(ctx, hipMalloc(&slot.spill, spillRays * cap * sizeof(uint32_t)));
+        slot.spillWords = spillRays * cap;
+    }
+    hipStream_t st = slot.stream;
+    HIPCHK(ctx, hipStreamWaitEvent(st, slot.free, 0));
+    fb_bind(fb, ks);
+    fb->next = (ks + 1) % S;
+    fb->lastMaxDepth = slot.lastMaxDepth = p->max_depth;
+    fb->lastPixels = slot.lastPixels = 0;
     fb->bands = f;
     fb->haveBands = true;
     // camera goes to device through a kernel argument copy (no host sync, no staging race)
@@ -1006,16 +1206,19 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
     int* shadowCnt = fb->counters;          // [b]
     int* extCnt = fb->counters + 32;        // [b]
     const SceneArgs sa = scene_args(s);
+    fb->lastIntegrator = MCRT_INTEGRATOR_PT;
     if (s->numLights == 0) {   // RTPathTracingPass.cpp:42: no lights -> pass skipped; radiance = 0 here
         HIPCHK(ctx, hipMemsetAsync(fb->radiance, 0, 16 * fb->N, st));
+        HIPCHK(ctx, hipEventRecord(slot.done, st));
         return MCRT_OK;
     }
-    if (!ensure_spill(s, std::max((size_t)f.numTiles * 64, 2 * fb->N + 64)))
-        return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
-    const TraceCtx tcs = trace_ctx(s);   // after ensure_spill (the buffer may have moved)
-    fb->lastIntegrator = MCRT_INTEGRATOR_PT;
+    TraceCtx tcs = trace_ctx(s);
+    tcs.spill = slot.spill;
+    // the queues hold at most the band's paths: size the ray grids to them, not to the image
+    const int bandPaths = f.numTiles * 64;
+    const int qCap = (int)std::min<size_t>(fb->N, (size_t)bandPaths);
     {
-        Timed t(ctx, K_PRIMARY, nullptr, (int64_t)f.numTiles * 64);
+        Timed t(ctx, K_PRIMARY, nullptr, (int64_t)f.numTiles * 64, st);
         mcrt::launch_primary(tcs, f, dCam, fb->hitsP, st);
     }
     for (int b = 0; b < p->max_depth; ++b) {
@@ -1025,17 +1228,17 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
         q.extCountOut = extCnt + b;
         q.eOout = fb->eO[b & 1]; q.eDout = fb->eD[b & 1]; q.eTout = fb->eT[b & 1];
         if (b == 0) {
-            Timed t(ctx, K_SHADE0, nullptr, (int64_t)f.numTiles * 64);
+            Timed t(ctx, K_SHADE0, nullptr, (int64_t)f.numTiles * 64, st);
             mcrt::launch_shade0(sa, f, dCam, fb->hitsP, fb->radiance, q, st);
         } else {
             if (!ctx->fuseShadowExtend) {
-                Timed t(ctx, K_EXTEND, extCnt + b - 1, 0);
+                Timed t(ctx, K_EXTEND, extCnt + b - 1, 0, st);
                 mcrt::launch_extend(tcs, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1], fb->hitsE,
-                                    (int)fb->N, st);
+                                    qCap, st);
             }
-            Timed t(ctx, K_SHADEN, extCnt + b - 1, 0);
+            Timed t(ctx, K_SHADEN, extCnt + b - 1, 0, st);
             mcrt::launch_shadeN(sa, f, b, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1],
-                                fb->eT[(b - 1) & 1], fb->hitsE, fb->radiance, q, (int)fb->N, st);
+                                fb->eT[(b - 1) & 1], fb->hitsE, fb->radiance, q, qCap, st);
         }
         if (ctx->sortRays && b + 1 < p->max_depth) {   // reorder the extension queue of bounce b
             if (!fb->sortO) {
@@ -1050,22 +1253,24 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
             HIPCHK(ctx, mcrt::sort_ray_queue(extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->eT[b & 1], fb->sortO,
                                              fb->sortD, fb->sortT, (int)fb->N, lo, hi, fb->sortScratch, fb->sortTemp,
                                              st));
-            std::swap(fb->eO[b & 1], fb->sortO);
-            std::swap(fb->eD[b & 1], fb->sortD);
-            std::swap(fb->eT[b & 1], fb->sortT);
+            std::swap(slot.eO[b & 1], fb->sortO);
+            std::swap(slot.eD[b & 1], fb->sortD);
+            std::swap(slot.eT[b & 1], fb->sortT);
+            fb_bind(fb, ks);
         }
         if (ctx->fuseShadowExtend && b + 1 < p->max_depth) {
             // shadow rays of bounce b + extension rays for bounce b+1 (both from this shading pass)
-            Timed t(ctx, K_SHADOW_EXTEND, nullptr, 0);
+            Timed t(ctx, K_SHADOW_EXTEND, nullptr, 0, st);
             mcrt::launch_shadow_extend(tcs, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b, fb->sO,
-                                       fb->sD, fb->sL, fb->radiance, (int)fb->N, (int)fb->N, st);
+                                       fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
-            Timed t(ctx, K_SHADOW, shadowCnt + b, 0);
-            mcrt::launch_shadow(tcs, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, (int)fb->N, st);
+            Timed t(ctx, K_SHADOW, shadowCnt + b, 0, st);
+            mcrt::launch_shadow(tcs, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, qCap, st);
         }
     }
     HIPCHK(ctx, hipGetLastError());
-    fb->lastPixels = (int64_t)f.numTiles * 64;
+    HIPCHK(ctx, hipEventRecord(slot.done, st));
+    fb->lastPixels = slot.lastPixels = (int64_t)f.numTiles * 64;
     return MCRT_OK;
 }
 
@@ -1082,6 +1287,7 @@ MCRT_API mcrt_status mcrt_render_aov(mcrt_scene s, mcrt_framebuffer fb, const mc
     if (!frame_args(fb, p, f, err)) return fail(ctx, MCRT_ERROR_INVALID_ARG, err);
     hipSetDevice(ctx->device);
     hipStream_t st = ctx->stream;
+    ctx_wait_slots(fb);   // the AOV pass reuses the bound slot's camera and primary-hit buffers
     mcrt_camera* dCam = reinterpret_cast<mcrt_camera*>(fb->counters + 128);
     HIPCHK(ctx, hipMemcpyAsync(dCam, cam, sizeof(mcrt_camera), hipMemcpyHostToDevice, st));
     if (!ensure_spill(s, std::max((size_t)f.numTiles * 64, 2 * fb->N + 64)))
@@ -1114,12 +1320,15 @@ MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* fil
         fb->haveBands = true;
     }
     hipSetDevice(ctx->device);
+    FrameSlot& slot = fb->slot[fb->cur];
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, slot.done, 0));   // the frame's render (its slot stream)
     {
         Timed t(ctx, K_ACCUM, nullptr, (int64_t)fb->bands.numTiles * 64);
         mcrt::launch_accumulate(fb->bands, frame_index, filter_weight(*filter), fb->radiance, fb->wsum, fb->wts,
                                 fb->image, ctx->stream);
     }
     HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(slot.free, ctx->stream));   // the slot may take its next frame
     return MCRT_OK;
 }
 
@@ -1162,7 +1371,7 @@ MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float
     hipSetDevice(ctx->device);
     const void* src = which == 0 ? (const void*)fb->radiance : which == 1 ? (const void*)fb->wsum
                       : which == 2 ? (const void*)fb->image : (const void*)fb->display;
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, fb_sync(fb));
     HIPCHK(ctx, hipMemcpy(host_rgba, src, 16 * fb->N, hipMemcpyDeviceToHost));
     return MCRT_OK;
 }
@@ -1173,6 +1382,7 @@ MCRT_API mcrt_status mcrt_framebuffer_copy_device(mcrt_framebuffer fb, int which
     hipSetDevice(ctx->device);
     const void* src = which == 0 ? (const void*)fb->radiance : which == 1 ? (const void*)fb->wsum
                       : which == 2 ? (const void*)fb->image : (const void*)fb->wts;
+    if (which == 0) ctx_wait_slots(fb);
     HIPCHK(ctx, hipMemcpyAsync(d_dst, src, (which == 3 ? 4 : 16) * fb->N, hipMemcpyDeviceToDevice, ctx->stream));
     return MCRT_OK;
 }
@@ -1193,7 +1403,7 @@ MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closes
     if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
     mcrt_ctx ctx = fb->ctx;
     hipSetDevice(ctx->device);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, fb_sync(fb));
     int c[64];
     if (fb->lastIntegrator == MCRT_INTEGRATOR_BDPT) {   // closest: all subpath rays; any: connection rays
         HIPCHK(ctx, hipMemcpy(c, fb->bdptCounters, sizeof(c), hipMemcpyDeviceToHost));
@@ -1220,7 +1430,7 @@ MCRT_API mcrt_status mcrt_framebuffer_queue_counts(mcrt_framebuffer fb, int32_t*
     if (!fb || max < 0) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
     mcrt_ctx ctx = fb->ctx;
     hipSetDevice(ctx->device);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, fb_sync(fb));
     int c[64];
     HIPCHK(ctx, hipMemcpy(c, fb->counters, sizeof(c), hipMemcpyDeviceToHost));
     for (int b = 0; b < max && b < 32; ++b) {
@@ -1239,7 +1449,7 @@ MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which,
     if (max_records < 0 || (max_records > 0 && !host_dst)) return fail(ctx, MCRT_ERROR_INVALID_ARG, "bad destination");
     if (fb->lastMaxDepth <= 0) return fail(ctx, MCRT_ERROR_INVALID_ARG, "nothing rendered yet");
     hipSetDevice(ctx->device);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, fb_sync(fb));
     int c[64];
     HIPCHK(ctx, hipMemcpy(c, fb->counters, sizeof(c), hipMemcpyDeviceToHost));
     const int b = which == 0 ? fb->lastMaxDepth - 1 : fb->lastMaxDepth - 2;   // last shadow / last extension queue
@@ -1277,7 +1487,7 @@ MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, 
     if (needed) *needed = sz;
     if (!host_dst || bytes == 0) return MCRT_OK;
     hipSetDevice(ctx->device);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, fb_sync(fb));
     HIPCHK(ctx, hipMemcpy(host_dst, src, std::min<size_t>(sz, bytes), hipMemcpyDeviceToHost));
     return MCRT_OK;
 }

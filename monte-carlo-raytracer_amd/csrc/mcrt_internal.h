@@ -20,6 +20,13 @@ struct SceneArgs {
     const mcrt_light* lights;
     const mcrt_material* materials;
     const float4* nodes;  // unified BVH (mcrt_bvh.cpp): leaf k = (v0, shape), (e1, prim), (e2, -), marker
+    // Surface records (built at scene upload, mcrt_build_surface_records): one 128-B record per
+    // triangle of each distinct (startIdx, startVertex) mesh with the object-space p0..p2,
+    // uv0..uv2 and n0..n2 computeSurfaceInteraction reads (geometry.cl:180-191), so a hit costs
+    // one cache line instead of an index line + 9 scattered vertex lines.  Shape k's triangle p
+    // is record surfBase[k] + p.
+    const float4* surf;
+    const uint32_t* surfBase;
     int numLights;
 };
 
@@ -69,6 +76,9 @@ struct TraceCtx {
 namespace mcrt {
 void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, mcrt_intersection* hits, int* occl,
                        hipStream_t st);
+void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshStartVertex, const uint32_t* meshBase,
+                            int numMeshes, uint32_t numRecords, const uint32_t* indices, const float4* positions,
+                            const float2* uvs, const float4* normals, float4* surf, hipStream_t st);
 void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st);
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
                    hipStream_t st);

@@ -76,6 +76,38 @@ __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* _
     }
 }
 
+// Surface records (SceneArgs::surf): record r of mesh m (meshBase[m] <= r < meshBase[m+1]) is
+// triangle p = r - meshBase[m] of the (startIdx, startVertex) range, packed as
+// (p0 p1.x | p1.yz p2.xy | p2.z uv0 uv1.x | uv1.y uv2 n0.x | n0.yz n1.xy | n1.z n2) + 2 pad float4.
+__global__ void k_surface_records(const uint32_t* __restrict__ meshStartIdx, const uint32_t* __restrict__ meshStartVertex,
+                                  const uint32_t* __restrict__ meshBase, int numMeshes, uint32_t numRecords,
+                                  const uint32_t* __restrict__ indices, const float4* __restrict__ positions,
+                                  const float2* __restrict__ uvs, const float4* __restrict__ normals,
+                                  float4* __restrict__ surf) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= numRecords) return;
+    int lo = 0, hi = numMeshes - 1;   // last mesh with meshBase <= r
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (meshBase[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t p = r - meshBase[lo];
+    const uint32_t* ix = indices + meshStartIdx[lo] + 3 * p;
+    const uint32_t sv = meshStartVertex[lo];
+    const float4 a = positions[sv + ix[0]], b = positions[sv + ix[1]], c = positions[sv + ix[2]];
+    const float2 ta = uvs[sv + ix[0]], tb = uvs[sv + ix[1]], tc = uvs[sv + ix[2]];
+    const float4 na = normals[sv + ix[0]], nb = normals[sv + ix[1]], nc = normals[sv + ix[2]];
+    float4* R = surf + 8 * (size_t)r;
+    R[0] = make_float4(a.x, a.y, a.z, b.x);
+    R[1] = make_float4(b.y, b.z, c.x, c.y);
+    R[2] = make_float4(c.z, ta.x, ta.y, tb.x);
+    R[3] = make_float4(tb.y, tc.x, tc.y, na.x);
+    R[4] = make_float4(na.y, na.z, nb.x, nb.y);
+    R[5] = make_float4(nb.z, nc.x, nc.y, nc.z);
+    R[6] = make_float4(0.f, 0.f, 0.f, 0.f);
+    R[7] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // Camera ray generation fused with the first closest-hit query (RTPrimaryRaysPass):
 // one workgroup = one wave = one 8x8 pixel tile of the rank's bands.
 template <bool TL>
@@ -544,6 +576,14 @@ void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n,
         else hipLaunchKernelGGL((k_trace_rays<false, false>), g, b, 0, st, c, rays, n, hits, occl);
     }
 }
+void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshStartVertex, const uint32_t* meshBase,
+                            int numMeshes, uint32_t numRecords, const uint32_t* indices, const float4* positions,
+                            const float2* uvs, const float4* normals, float4* surf, hipStream_t st) {
+    if (numRecords == 0) return;
+    k_surface_records<<<(numRecords + 255) / 256, 256, 0, st>>>(meshStartIdx, meshStartVertex, meshBase, numMeshes,
+                                                                numRecords, indices, positions, uvs, normals, surf);
+}
+
 void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st) {
     hipLaunchKernelGGL(c.twoLevel ? k_primary<true> : k_primary<false>, dim3(f.numTiles), dim3(64), 0, st, c, f, cam,
                        hits);

@@ -288,17 +288,16 @@ MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, int shapeIdx, int p
                                          f3* dpduOut = nullptr, f3* dpdvOut = nullptr) {
     Frame si;
     const mcrt_shape& shape = s.shapes[shapeIdx];
-    const uint32_t i0 = s.indices[shape.startIdx + 3 * primIdx];
-    const uint32_t i1 = s.indices[shape.startIdx + 3 * primIdx + 1];
-    const uint32_t i2 = s.indices[shape.startIdx + 3 * primIdx + 2];
-    const f3 p0 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i0]));
-    const f3 p1 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i1]));
-    const f3 p2 = transformPoint3(shape.toWorldTransform, ld3(s.positions[shape.startVertex + i2]));
-    const float2 t0 = s.uvs[shape.startVertex + i0], t1 = s.uvs[shape.startVertex + i1], t2 = s.uvs[shape.startVertex + i2];
-    const f2 uv0 = f2{t0.x, t0.y}, uv1 = f2{t1.x, t1.y}, uv2 = f2{t2.x, t2.y};
-    const f3 n0 = transformVector3(shape.toWorldInverseTranspose, ld3(s.normals[shape.startVertex + i0]));
-    const f3 n1 = transformVector3(shape.toWorldInverseTranspose, ld3(s.normals[shape.startVertex + i1]));
-    const f3 n2 = transformVector3(shape.toWorldInverseTranspose, ld3(s.normals[shape.startVertex + i2]));
+    // the triangle's surface record (SceneArgs::surf): the same floats the index path gathers
+    const float4* R = s.surf + 8 * ((size_t)s.surfBase[shapeIdx] + (uint32_t)primIdx);
+    const float4 r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3], r4 = R[4], r5 = R[5];
+    const f3 p0 = transformPoint3(shape.toWorldTransform, mk3(r0.x, r0.y, r0.z));
+    const f3 p1 = transformPoint3(shape.toWorldTransform, mk3(r0.w, r1.x, r1.y));
+    const f3 p2 = transformPoint3(shape.toWorldTransform, mk3(r1.z, r1.w, r2.x));
+    const f2 uv0 = f2{r2.y, r2.z}, uv1 = f2{r2.w, r3.x}, uv2 = f2{r3.y, r3.z};
+    const f3 n0 = transformVector3(shape.toWorldInverseTranspose, mk3(r3.w, r4.x, r4.y));
+    const f3 n1 = transformVector3(shape.toWorldInverseTranspose, mk3(r4.z, r4.w, r5.x));
+    const f3 n2 = transformVector3(shape.toWorldInverseTranspose, mk3(r5.y, r5.z, r5.w));
     si.p = p0 * (1.0f - barycentrics.x - barycentrics.y) + p1 * barycentrics.x + p2 * barycentrics.y;
     si.uv = uv0 * (1.0f - barycentrics.x - barycentrics.y) + uv1 * barycentrics.x + uv2 * barycentrics.y;
     si.gn = cl_normalize(cl_cross(p0 - p2, p1 - p2));

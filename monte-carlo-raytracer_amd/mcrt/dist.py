@@ -48,18 +48,30 @@ def frame_split(num_frames, world, rank):
     return np.arange(rank, num_frames, world, dtype=np.int64)
 
 
-def reduce_accumulators(wsum, wts, dst=0, group=None):
-    """Sum the per-rank accumulators into rank `dst` (torch tensors, in place on dst)."""
+def packed_accumulators(num_pixels, device):
+    """One contiguous float32 buffer holding sum(w*L) (4 per pixel) then sum(w) (1 per pixel), so
+    the end-of-job reduction is a single collective; returns (buf, wsum view, wts view)."""
+    import torch
+    buf = torch.empty(num_pixels * 5, dtype=torch.float32, device=device)
+    return buf, buf[:num_pixels * 4], buf[num_pixels * 4:]
+
+
+def reduce_packed(buf, dst=0, group=None):
+    """ONE sum-reduce of a packed accumulator buffer into rank `dst` (in place on dst)."""
     import torch.distributed as dist
-    if wsum.is_cuda and dist.get_backend(group) == "gloo":   # gloo rehearsal: reduce via host copies
-        hs, hw = wsum.cpu(), wts.cpu()
-        dist.reduce(hs, dst=dst, op=dist.ReduceOp.SUM, group=group)
-        dist.reduce(hw, dst=dst, op=dist.ReduceOp.SUM, group=group)
-        wsum.copy_(hs)
-        wts.copy_(hw)
+    if buf.is_cuda and dist.get_backend(group) == "gloo":   # gloo rehearsal: reduce via a host copy
+        h = buf.cpu()
+        dist.reduce(h, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        buf.copy_(h)
         return
-    dist.reduce(wsum, dst=dst, op=dist.ReduceOp.SUM, group=group)
-    dist.reduce(wts, dst=dst, op=dist.ReduceOp.SUM, group=group)
+    dist.reduce(buf, dst=dst, op=dist.ReduceOp.SUM, group=group)
+
+
+def reduce_accumulators(wsum, wts, dst=0, group=None):
+    """Sum separate per-rank accumulator tensors into rank `dst` (two collectives; the bench
+    packs both into one buffer with packed_accumulators and calls reduce_packed once)."""
+    reduce_packed(wsum, dst, group)
+    reduce_packed(wts, dst, group)
 
 
 def resolve(wsum, wts):

@@ -46,6 +46,7 @@ SIGNATURES = {
     "mcrt_trace_any": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
     "mcrt_framebuffer_create": (_c.c_int, [_vp, _c.c_uint32, _c.c_uint32, _c.POINTER(_vp)]),
     "mcrt_framebuffer_destroy": (_c.c_int, [_vp]),
+    "mcrt_framebuffer_set_frames_in_flight": (_c.c_int, [_vp, _c.c_int32]),
     "mcrt_render_frame": (_c.c_int, [_vp, _vp, _vp, _vp]),
     "mcrt_accumulate": (_c.c_int, [_vp, _vp, _c.c_int32]),
     "mcrt_framebuffer_device_ptrs": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
@@ -238,6 +239,10 @@ class FrameBuffer:
         _check(lib().mcrt_framebuffer_create(ctx.h, width, height, _c.byref(h)), ctx.h)
         self.h = h
         ctx._adopt(self)
+
+    def set_frames_in_flight(self, n):
+        """mcrt_framebuffer_set_frames_in_flight: 0 = auto (one slot per band share, <= 4)."""
+        _check(lib().mcrt_framebuffer_set_frames_in_flight(self.h, n), self.ctx.h)
 
     def render(self, dscene, cam, frame=0, max_depth=2, sampler=T.SAMPLER_RANDOM, rr=False, rr_start=3,
                band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_PT, texture_lod=False):

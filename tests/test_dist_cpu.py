@@ -60,10 +60,13 @@ def _worker(rank, world, port, out_path):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     wsum, wts = _accumulate_band(rank, world)
-    ts, tw = torch.from_numpy(wsum), torch.from_numpy(wts)
-    mdist.reduce_accumulators(ts, tw, dst=0)
+    # the bench's path: both accumulators in one packed buffer, ONE reduce
+    buf, ts, tw = mdist.packed_accumulators(H * W, "cpu")
+    ts.copy_(torch.from_numpy(wsum).reshape(-1))
+    tw.copy_(torch.from_numpy(wts).reshape(-1))
+    mdist.reduce_packed(buf, dst=0)
     if rank == 0:
-        np.savez(out_path, wsum=ts.numpy(), wts=tw.numpy())
+        np.savez(out_path, wsum=ts.numpy().reshape(H, W, 4), wts=tw.numpy().reshape(H, W))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -131,3 +131,36 @@ def test_frame_stats_and_no_lights(hip_ctx, mixed):
     assert not fb.read(0).any()
     fb.close()
     ds.close()
+
+
+@pytest.mark.parametrize("num_bands,band_index", [(1, 0), (3, 1)])
+def test_frames_in_flight_accumulate_bit_exact(hip_ctx, mixed, num_bands, band_index):
+    """mcrt_framebuffer_set_frames_in_flight: frames rendered in 2..4 overlapping slots and
+    accumulated in call order give the one-slot accumulators and last radiance bit for bit."""
+    from mcrt import lib
+    sc, _ = mixed
+    W, H = 96, 72
+    ds = lib.DeviceScene(hip_ctx, sc)
+    cam = scene_camera("mixed", W, H)
+    filt = T.make_filter(T.BOX)
+    out = {}
+    for fif in (1, 2, 4):
+        fb = lib.FrameBuffer(hip_ctx, W, H)
+        fb.set_frames_in_flight(fif)
+        for frame in range(9):
+            fb.render(ds, cam, frame=frame, max_depth=3, band_rows=8, num_bands=num_bands, band_index=band_index)
+            fb.accumulate(filt, frame)
+        out[fif] = (fb.read(0), fb.read(1), fb.read(2), fb.stats())
+        fb.close()
+    for fif in (2, 4):
+        for k in range(3):
+            np.testing.assert_array_equal(out[fif][k].view(np.uint32), out[1][k].view(np.uint32))
+        assert out[fif][3] == out[1][3]
+    assert out[1][2][..., :3].max() > 0
+    with pytest.raises(lib.MCRTError):
+        fb = lib.FrameBuffer(hip_ctx, W, H)
+        try:
+            fb.set_frames_in_flight(5)
+        finally:
+            fb.close()
+    ds.close()

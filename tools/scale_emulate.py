@@ -1,0 +1,65 @@
+"""Per-rank work of the N-GPU tile split, emulated on ONE GPU.
+
+For N in --ns, renders K frames of each rank's bands (band_index = r of num_bands = N) one rank
+at a time on cuda:0 and reports the slowest rank's ms/frame next to the 1-GPU ms/frame.  The
+ratio is the compute part of the strong-scaling efficiency (the final RCCL reduce and the
+launch gaps of concurrent processes are not in it).  Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "monte-carlo-raytracer_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--scene", default="san_miguel_proxy")
+    ap.add_argument("--fif", type=int, default=0, help="frames in flight (0 = the library's auto choice)")
+    args = ap.parse_args()
+    from mcrt import lib, scenes
+    from mcrt import types as T
+    from mcrt.camera import scene_camera
+    W, H = 1920, 1080
+    scene = scenes.san_miguel_proxy() if args.scene == "san_miguel_proxy" else scenes.dragon_proxy()
+    cam = scene_camera(args.scene, W, H)
+    ctx = lib.Context(0)
+    ds = lib.DeviceScene(ctx, scene)
+    fb = lib.FrameBuffer(ctx, W, H)
+    filt = T.make_filter(T.BOX)
+    fb.set_frames_in_flight(args.fif)
+    out = {"fif": args.fif, "scene": args.scene, "steps": args.steps, "band_rows": args.band_rows, "per_n": {}}
+    for n in [int(x) for x in args.ns.split(",")]:
+        per_rank = []
+        for r in range(n):
+            band = dict(band_rows=args.band_rows, num_bands=n, band_index=r)
+            for f in range(3):
+                fb.render(ds, cam, frame=f, max_depth=2, **band)
+                fb.accumulate(filt, f)
+            ctx.sync()
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                fb.render(ds, cam, frame=3 + i, max_depth=2, **band)
+                fb.accumulate(filt, 3 + i)
+            ctx.sync()
+            per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
+        out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
+                           "min_ms": round(min(per_rank), 4)}
+    base = out["per_n"][min(out["per_n"])]["max_ms"]
+    for n, v in out["per_n"].items():
+        v["compute_eff"] = round(base / (n * v["max_ms"]), 4)
+    print(json.dumps(out), flush=True)
+    fb.close()
+    ds.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
