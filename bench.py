@@ -72,13 +72,22 @@ def cpu_baseline(scene, cam, W, H, D, target_s=15.0):
     t0 = time.perf_counter()
     rad, st = o.render_rows(cam, rows, frame=0, max_depth=D, threads=threads)
     el = time.perf_counter() - t0
-    paths = len(rows) * W
+    paths0 = paths = len(rows) * W
+    frames = 1
+    # a whole frame can take well under target_s: render further frames (1, 2, ...) of the same
+    # rows until the sample is ~target_s of CPU work
+    while len(rows) == H and el + el / frames <= target_s:
+        t0 = time.perf_counter()
+        o.render_rows(cam, rows, frame=frames, max_depth=D, threads=threads)
+        el += time.perf_counter() - t0
+        paths += paths0
+        frames += 1
     return {
         "value": paths / el / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
-        "sample": f"{len(rows)} of {H} rows (evenly spaced) of frame 0, {paths} paths, D={D}, random sampler; "
-                  f"oracle = C restatement of PathTracing.cl + RR Bvh2/LDS traversal, {threads} threads, {el:.1f}s "
-                  f"(BVH build {build_s:.1f}s not timed)",
-        "_rows": rows, "_radiance": rad, "_stats": st, "_paths": paths,
+        "sample": f"{len(rows)} of {H} rows (evenly spaced) of frames 0..{frames - 1}, {paths} paths, D={D}, "
+                  f"random sampler; oracle = C restatement of PathTracing.cl + RR Bvh2/LDS traversal, {threads} "
+                  f"threads, {el:.1f}s (BVH build {build_s:.1f}s not timed)",
+        "_rows": rows, "_radiance": rad, "_stats": st, "_paths": paths0,
     }
 
 
@@ -118,6 +127,12 @@ def main():
     ap.add_argument("--device-build", action="store_true", help="on-device linear BVH instead of the RR-identical host build")
     ap.add_argument("--force-flat", action="store_true",
                     help="flat BVH even for instanced scenes (RR bvh.forceflat); default: RR's auto selection")
+    ap.add_argument("--russian-roulette", action="store_true",
+                    help="opt-in RR on extension rays (perf mode; the reference has none, so not a parity run)")
+    ap.add_argument("--rr-start", type=int, default=1, help="first bounce whose extension rays RR may cut")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="PT frames per mcrt_render_frames call (one launch sequence for all of them); "
+                         "0 = auto (min(16, 4 x ranks))")
     args = ap.parse_args()
 
     import torch
@@ -172,22 +187,39 @@ def main():
     else:
         band = dict(band_rows=args.band_rows, num_bands=world, band_index=rank)
     first = [True]
+    # auto: 4 frames per launch on one GPU, 16 from 4 GPUs on (a 1/N band share x 16 frames keeps
+    # every launch at >= 4 whole images of paths; tools/scale_emulate.py sweeps)
+    batch = 1 if bdpt else (args.batch if args.batch > 0 else min(16, 4 * world))
 
-    def step(i):
+    def step(i, n=1):
+        """frames i .. i+n-1 (one mcrt_render_frames call when n > 1)"""
         frame = rank + world * i if bdpt else i
-        fb.render(ds, cam, frame=frame, max_depth=D, sampler=sampler, **band)
+        kw = dict(max_depth=D, sampler=sampler, rr=args.russian_roulette, rr_start=args.rr_start, **band)
+        if n == 1:
+            fb.render(ds, cam, frame=frame, **kw)
+        else:
+            fb.render_frames(ds, [cam] * n, frame=frame, **kw)
         fb.accumulate(filt, 0 if first[0] else frame)   # 0: the first accumulation overwrites
         first[0] = False
 
-    for f in range(args.warmup):
-        step(f)
+    def run(i0, count):
+        i = 0
+        while i < count:
+            n = min(batch, count - i)
+            step(i0 + i, n)
+            i += n
+
+    # warmup: at least one call per frame slot (MCRT_MAX_FRAMES_IN_FLIGHT = 4), so no slot
+    # allocation falls inside the timed region
+    warm = max(args.warmup, 4 * batch)
+    run(0, warm)
     ctx.sync()
     # per-frame path statistics (device queue sizes) from one untimed frame
-    step(args.warmup)
+    step(warm)
     ctx.sync()
     fstats = fb.stats()
     qcounts = fb.queue_counts() if not bdpt else None
-    frame0 = args.warmup + 1
+    frame0 = warm + 1
 
     if not args.no_kernel_timing:
         ctx.set_profiling(True)
@@ -197,8 +229,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for i in range(args.steps):
-        step(frame0 + i)
+    run(frame0, args.steps)
     if world > 1:   # single RCCL reduce of the tile accumulators (north star)
         fb.copy_device(1, acc_s.data_ptr())
         fb.copy_device(3, acc_w.data_ptr())
@@ -229,13 +260,16 @@ def main():
         "scaling": "weak" if bdpt else "strong", "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic: deterministic {args.scene} ({scene.num_triangles} tris, seeded generator mcrt/scenes.py)",
         "config": {"workload": f"{args.scene} {W}x{H}, {'BDPT' if bdpt else 'unidirectional PT'}, maxDepth {D}, "
-                               f"{args.sampler} sampler, 1 spp per step, box-filter accumulate", "width": W, "height": H,
+                               f"{args.sampler} sampler, 1 spp per step, box-filter accumulate"
+                               + (f", Russian roulette from bounce {args.rr_start} (perf mode)"
+                                  if args.russian_roulette and not bdpt else ""), "width": W, "height": H,
                    "triangles": scene.num_triangles, "max_depth": D, "spp_per_step": 1,
                    "bvh": ("two-level (instanced), RadeonRays-identical Bvh trees" if two_level else
                            "device LBVH" if args.device_build else "host RadeonRays-identical SAH"),
                    "bvh_build_ms": round(info["build_ms"], 1),
                    "parallelism": (f"frame split x {world} + 1 RCCL reduce" if bdpt else
-                                   f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce")},
+                                   f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce"),
+                   "frames_per_launch": batch},
     }
     if rank == 0:
         rays = {"closest": fstats["closest_rays"] / (W * H / world), "any": fstats["any_rays"] / (W * H / world),
@@ -276,10 +310,11 @@ def main():
                                   "items_per_launch": round(v["items"] / max(v["launches"], 1), 1)}
                               for k, v in kstats.items()}
             alg = None
+            fpl = args.steps / max(ks["launches"], 1)   # frames per launch (mcrt_render_frames batches)
             if V is not None and dom == "k_shadow_extend":
-                # one launch = the extension rays for bounce 1 + the shadow rays of bounce 0
-                alg = (qcounts[1][0] * per_query_bytes("k_extend", V["k_extend"])
-                       + qcounts[0][0] * per_query_bytes("k_shadow", V["k_shadow"]))
+                # one launch = the extension rays for bounce 1 + the shadow rays of bounce 0, of fpl frames
+                alg = fpl * (qcounts[1][0] * per_query_bytes("k_extend", V["k_extend"])
+                             + qcounts[0][0] * per_query_bytes("k_shadow", V["k_shadow"]))
             elif V is not None and dom in V:
                 alg = items_per_launch * per_query_bytes(dom, V[dom])
             if alg is not None:

@@ -329,8 +329,8 @@ MCRT_API mcrt_status mcrt_framebuffer_destroy(mcrt_framebuffer fb);
  * that frame's render, so n frames overlap on the GPU and the image is unchanged bit for bit
  * (the reference's pass sequence per frame, RTPathTracingPass::update then
  * RTReconstructionPass::updateReconstruction, is kept; only its clFinish after every launch is
- * gone).  0 = auto: one slot per band share (num_bands), at most MCRT_MAX_FRAMES_IN_FLIGHT --
- * a whole-image frame fills the GPU alone, a 1/N band share does not.  Reads of the frame
+ * gone).  0 = auto = 2: each launch's divergent tail of long rays is filled by the next
+ * frame's launches (small band shares are better widened by mcrt_render_frames).  Reads of the frame
  * buffer synchronise every slot.  No reference counterpart (its passes are synchronous). */
 #define MCRT_MAX_FRAMES_IN_FLIGHT 4
 MCRT_API mcrt_status mcrt_framebuffer_set_frames_in_flight(mcrt_framebuffer fb, int32_t n);
@@ -339,8 +339,26 @@ MCRT_API mcrt_status mcrt_framebuffer_set_frames_in_flight(mcrt_framebuffer fb, 
 MCRT_API mcrt_status mcrt_render_frame(mcrt_scene scene, mcrt_framebuffer fb, const mcrt_camera* camera,
                                        const mcrt_frame_params* params);
 /* ReconstructionPass (KRN/reconstruction.cl:6-60): clamp [0,1000] (NaN->0),
- * frame_index 0 overwrites, else accumulates sum(w*L), sum(w); image = ratio. */
+ * frame_index 0 overwrites, else accumulates sum(w*L), sum(w); image = ratio.
+ * After mcrt_render_frames it accumulates every frame of that batch in frame order
+ * (frame_index = the batch's first frame), all with this filter. */
 MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* filter, int32_t frame_index);
+/* Batched frames (PT): renders the `count` (1..16) consecutive 1-spp frames
+ * params->frame_index + k, k < count, with cameras[k] (per-frame TAA jitter), in ONE pass --
+ * every launch (camera rays, shading, shadow + extension rays) covers all count frames' paths,
+ * so a small per-rank band share (tile split over N GPUs) still fills the 256 CUs and the
+ * divergent tail of each launch is paid once per batch.  Per frame the arithmetic, the RNG
+ * streams (keyed by pixel, frame_index + k, bounce) and the radiance are exactly those of
+ * mcrt_render_frame; mcrt_accumulate_frames (or mcrt_accumulate) then sums them in frame order,
+ * so the image equals count x (mcrt_render_frame + mcrt_accumulate) bit for bit.  Radiance read
+ * back (mcrt_framebuffer_read 0) is the batch's first frame.  The reference renders one frame
+ * per RTPathTracingPass::update; this is the same sequence, launched wider. */
+MCRT_API mcrt_status mcrt_render_frames(mcrt_scene scene, mcrt_framebuffer fb, const mcrt_camera* cameras,
+                                        int32_t count, const mcrt_frame_params* params);
+/* filters: `count` filters (one per frame of the last mcrt_render_frames; the per-frame filter
+ * props of RTReconstructionPass) or 1 shared by all; frame_index = the batch's first frame. */
+MCRT_API mcrt_status mcrt_accumulate_frames(mcrt_framebuffer fb, const mcrt_filter* filters, int32_t count,
+                                            int32_t frame_index);
 /* Device pointers of the frame buffer's arrays (float4 x W*H, float x W*H). */
 MCRT_API mcrt_status mcrt_framebuffer_device_ptrs(mcrt_framebuffer fb, void** radiance, void** weighted_sum,
                                                   void** weight_sum, void** image);

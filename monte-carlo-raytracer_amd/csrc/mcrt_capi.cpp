@@ -125,7 +125,11 @@ struct FrameSlot {
     hipEvent_t free = nullptr;   // recorded on the context stream after the slot's buffers were last read
     int lastMaxDepth = 0;
     int64_t lastPixels = 0;
+    int lastBatch = 1;           // frames of the slot's last render (mcrt_render_frames)
+    int frames = 1;              // radiance / primary-hit planes of W*H allocated (batch capacity)
+    size_t queueCap = 0;         // entries of each ray-queue buffer
 };
+#define SLOT_COUNTER_BYTES 4096   // [0..127] ints: counters; cameras (176 B each, <= 16) from byte 512
 
 struct mcrt_framebuffer_s {
     mcrt_ctx ctx = nullptr;
@@ -890,21 +894,25 @@ static void fb_free(mcrt_framebuffer fb) {
     fb_free_bdpt(fb);
 }
 
-static hipError_t slot_alloc(FrameSlot& k, size_t N) {
+// Per-frame planes (radiance, primary hits) for `frames` frames of N pixels; ray queues of Q entries.
+static hipError_t slot_alloc(FrameSlot& k, size_t N, int frames = 1, size_t Q = 0) {
     hipError_t e = hipSuccess;
+    if (Q < N) Q = N;
     auto A = [&](auto** p, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
     };
-    A(&k.radiance, 16 * N);
-    A(&k.hitsP, 16 * N);
-    A(&k.hitsE, 16 * N);
-    for (int i = 0; i < 2; ++i) { A(&k.eO[i], 16 * N); A(&k.eD[i], 16 * N); A(&k.eT[i], 16 * N); }
-    A(&k.sO, 16 * N);
-    A(&k.sD, 16 * N);
-    A(&k.sL, 16 * N);
-    A(&k.counters, 256 * sizeof(int));
-    if (e == hipSuccess) e = hipMemset(k.radiance, 0, 16 * N);
-    if (e == hipSuccess) e = hipMemset(k.counters, 0, 256 * sizeof(int));
+    A(&k.radiance, 16 * N * frames);
+    A(&k.hitsP, 16 * N * frames);
+    A(&k.hitsE, 16 * Q);
+    for (int i = 0; i < 2; ++i) { A(&k.eO[i], 16 * Q); A(&k.eD[i], 16 * Q); A(&k.eT[i], 16 * Q); }
+    A(&k.sO, 16 * Q);
+    A(&k.sD, 16 * Q);
+    A(&k.sL, 16 * Q);
+    A(&k.counters, SLOT_COUNTER_BYTES);
+    k.frames = frames;
+    k.queueCap = Q;
+    if (e == hipSuccess) e = hipMemset(k.radiance, 0, 16 * N * frames);
+    if (e == hipSuccess) e = hipMemset(k.counters, 0, SLOT_COUNTER_BYTES);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&k.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&k.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&k.free, hipEventDisableTiming);
@@ -1040,6 +1048,7 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
     f.russianRoulette = p->russian_roulette;
     f.rrStartDepth = p->rr_start_depth;
     f.textureLod = p->texture_lod ? 1 : 0;
+    f.batch = 1;
     f.numBands = p->num_bands <= 0 ? 1 : p->num_bands;
     f.bandIndex = p->band_index;
     f.bandRows = f.numBands == 1 ? 8 : p->band_rows;
@@ -1057,12 +1066,15 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
     return true;
 }
 
-// Frames in flight for a render with band layout f: the frame buffer's setting (or the
-// MCRT_FRAMES_IN_FLIGHT override); auto = one per band share, up to 4 (MI355X: 4 hardware queues
-// per process) -- a whole-image frame alone fills the GPU, a 1/N band share does not.
+// Frames in flight for a render: the frame buffer's setting (or the MCRT_FRAMES_IN_FLIGHT
+// override); auto = 2.  Each launch of a frame ends in a divergent tail of long rays that the next
+// frame's launches fill (San-Miguel proxy 1080p: 2.33 -> 1.91 ms/frame with 2 slots, 2.06 with 4;
+// tools/scale_emulate.py).  Small per-rank band shares are widened by batching frames
+// (mcrt_render_frames) rather than by more slots: 4 slots of 1/8-image frames reach 0.49 ms per
+// frame at N = 8, 2 slots of 16-frame batches 0.25.
 static int frames_in_flight(mcrt_framebuffer fb, const FrameArgs& f) {
     int n = fb->ctx->envFramesInFlight > 0 ? fb->ctx->envFramesInFlight : fb->framesInFlight;
-    if (n <= 0) n = f.numBands;
+    if (n <= 0) n = 2;
     if (fb->ctx->sortRays) n = 1;   // one set of sort buffers
     return std::max(1, std::min(n, MCRT_MAX_FRAMES_IN_FLIGHT));
 }
@@ -1144,14 +1156,21 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     return MCRT_OK;
 }
 
-MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cam,
-                                       const mcrt_frame_params* p) {
+static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cam, int count,
+                                 const mcrt_frame_params* p) {
     if (!s || !fb || !cam || !p) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
     mcrt_ctx ctx = s->ctx;
     if (fb->ctx != ctx) return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame buffer belongs to another context");
     if (!s->dNodes) return fail(ctx, MCRT_ERROR_NOT_READY, "mcrt_accel_build has not been called");
-    if (cam->width != fb->W || cam->height != fb->H)
-        return fail(ctx, MCRT_ERROR_INVALID_ARG, "camera size differs from the frame buffer");
+    if (count < 1 || count > MCRT_MAX_BATCH_FRAMES)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame count must be 1 .. 16");
+    for (int k = 0; k < count; ++k)
+        if (cam[k].width != fb->W || cam[k].height != fb->H)
+            return fail(ctx, MCRT_ERROR_INVALID_ARG, "camera size differs from the frame buffer");
+    if (count > 1 && p->integrator != MCRT_INTEGRATOR_PT)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "batched frames are PT only");
+    if ((uint64_t)fb->N * count >= (1ull << 31))
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame count x pixels must stay below 2^31 (path ids are int32)");
     if (p->max_depth < 1 || p->max_depth > MCRT_MAX_BOUNCES) return fail(ctx, MCRT_ERROR_INVALID_ARG, "max_depth out of range");
     if (p->sampler != MCRT_SAMPLER_RANDOM && p->sampler != MCRT_SAMPLER_SOBOL)
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "unknown sampler");
@@ -1174,15 +1193,26 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
         hipEventRecord(fb->slot[0].free, ctx->stream);
         fb->slot[0].lastMaxDepth = fb->lastMaxDepth;
         fb->slot[0].lastPixels = fb->lastPixels;
+        fb->slot[0].lastBatch = 1;
         return r;
     }
+    f.batch = count;
     // frame slot: its buffers are free once the accumulation of its previous frame has read them
     const int S = frames_in_flight(fb, f);
     const int ks = fb->next % S;
     FrameSlot& slot = fb->slot[ks];
-    if (!slot.stream) HIPCHK(ctx, slot_alloc(slot, fb->N));
+    // the queues hold at most the batch's paths of the band: size the ray grids to them
+    const int bandPaths = f.numTiles * 64 * count;
+    const size_t qNeed = std::max(fb->N, (size_t)bandPaths);
+    if (!slot.stream) {
+        HIPCHK(ctx, slot_alloc(slot, fb->N, count, qNeed));
+    } else if (slot.frames < count || slot.queueCap < qNeed) {   // grow for a larger batch
+        HIPCHK(ctx, hipEventSynchronize(slot.free));
+        slot_free(slot);
+        HIPCHK(ctx, slot_alloc(slot, fb->N, count, qNeed));
+    }
     const int cap = s->spillCap;
-    const size_t spillRays = (std::max((size_t)f.numTiles * 64, 2 * fb->N + 64) + 63) / 64 * 64;
+    const size_t spillRays = (std::max((size_t)bandPaths, 2 * qNeed + 64) + 63) / 64 * 64;
     if (!slot.spill || slot.spillWords < spillRays * cap) {
         HIPCHK(ctx, hipStreamSynchronize(slot.stream));
         if (slot.spill) hipFree(slot.spill);
@@ -1197,11 +1227,11 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
     fb->next = (ks + 1) % S;
     fb->lastMaxDepth = slot.lastMaxDepth = p->max_depth;
     fb->lastPixels = slot.lastPixels = 0;
+    slot.lastBatch = count;
     fb->bands = f;
     fb->haveBands = true;
-    // camera goes to device through a kernel argument copy (no host sync, no staging race)
-    mcrt_camera* dCam = reinterpret_cast<mcrt_camera*>(fb->counters + 128);   // 176 B slot after the counters
-    HIPCHK(ctx, hipMemcpyAsync(dCam, cam, sizeof(mcrt_camera), hipMemcpyHostToDevice, st));
+    mcrt_camera* dCam = reinterpret_cast<mcrt_camera*>(fb->counters + 128);   // 176 B per frame after the counters
+    HIPCHK(ctx, hipMemcpyAsync(dCam, cam, sizeof(mcrt_camera) * count, hipMemcpyHostToDevice, st));
     HIPCHK(ctx, hipMemsetAsync(fb->counters, 0, 128 * sizeof(int), st));
     int* shadowCnt = fb->counters;          // [b]
     int* extCnt = fb->counters + 32;        // [b]
@@ -1214,11 +1244,9 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
     }
     TraceCtx tcs = trace_ctx(s);
     tcs.spill = slot.spill;
-    // the queues hold at most the band's paths: size the ray grids to them, not to the image
-    const int bandPaths = f.numTiles * 64;
-    const int qCap = (int)std::min<size_t>(fb->N, (size_t)bandPaths);
+    const int qCap = bandPaths;
     {
-        Timed t(ctx, K_PRIMARY, nullptr, (int64_t)f.numTiles * 64, st);
+        Timed t(ctx, K_PRIMARY, nullptr, (int64_t)bandPaths, st);
         mcrt::launch_primary(tcs, f, dCam, fb->hitsP, st);
     }
     for (int b = 0; b < p->max_depth; ++b) {
@@ -1228,7 +1256,7 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
         q.extCountOut = extCnt + b;
         q.eOout = fb->eO[b & 1]; q.eDout = fb->eD[b & 1]; q.eTout = fb->eT[b & 1];
         if (b == 0) {
-            Timed t(ctx, K_SHADE0, nullptr, (int64_t)f.numTiles * 64, st);
+            Timed t(ctx, K_SHADE0, nullptr, (int64_t)bandPaths, st);
             mcrt::launch_shade0(sa, f, dCam, fb->hitsP, fb->radiance, q, st);
         } else {
             if (!ctx->fuseShadowExtend) {
@@ -1270,8 +1298,18 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const 
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(slot.done, st));
-    fb->lastPixels = slot.lastPixels = (int64_t)f.numTiles * 64;
+    fb->lastPixels = slot.lastPixels = (int64_t)bandPaths;
     return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_render_frame(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cam,
+                                       const mcrt_frame_params* p) {
+    return render_frames(s, fb, cam, 1, p);
+}
+
+MCRT_API mcrt_status mcrt_render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cameras, int32_t count,
+                                        const mcrt_frame_params* p) {
+    return render_frames(s, fb, cameras, count, p);
 }
 
 MCRT_API mcrt_status mcrt_render_aov(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cam,
@@ -1308,8 +1346,8 @@ MCRT_API mcrt_status mcrt_render_aov(mcrt_scene s, mcrt_framebuffer fb, const mc
     return MCRT_OK;
 }
 
-MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* filter, int32_t frame_index) {
-    if (!fb || !filter) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+static mcrt_status accumulate(mcrt_framebuffer fb, const mcrt_filter* filters, int nfilters, int32_t frame_index) {
+    if (!fb || !filters) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
     mcrt_ctx ctx = fb->ctx;
     if (!fb->haveBands) {   // no frame rendered yet: whole image
         mcrt_frame_params p{};
@@ -1321,15 +1359,30 @@ MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* fil
     }
     hipSetDevice(ctx->device);
     FrameSlot& slot = fb->slot[fb->cur];
+    const int batch = fb->lastIntegrator == MCRT_INTEGRATOR_PT ? slot.lastBatch : 1;
+    if (nfilters != 1 && nfilters != batch)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "one filter, or one per frame of the last mcrt_render_frames");
+    BatchWeights w{};
+    for (int k = 0; k < batch; ++k) w.w[k] = filter_weight(filters[nfilters == 1 ? 0 : k]);
+    FrameArgs f = fb->bands;
+    f.batch = batch;
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, slot.done, 0));   // the frame's render (its slot stream)
     {
-        Timed t(ctx, K_ACCUM, nullptr, (int64_t)fb->bands.numTiles * 64);
-        mcrt::launch_accumulate(fb->bands, frame_index, filter_weight(*filter), fb->radiance, fb->wsum, fb->wts,
-                                fb->image, ctx->stream);
+        Timed t(ctx, K_ACCUM, nullptr, (int64_t)f.numTiles * 64 * batch);
+        mcrt::launch_accumulate(f, frame_index, w, fb->radiance, fb->wsum, fb->wts, fb->image, ctx->stream);
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(slot.free, ctx->stream));   // the slot may take its next frame
     return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* filter, int32_t frame_index) {
+    return accumulate(fb, filter, 1, frame_index);
+}
+
+MCRT_API mcrt_status mcrt_accumulate_frames(mcrt_framebuffer fb, const mcrt_filter* filters, int32_t count,
+                                            int32_t frame_index) {
+    return accumulate(fb, filters, count, frame_index);
 }
 
 MCRT_API mcrt_status mcrt_framebuffer_device_ptrs(mcrt_framebuffer fb, void** radiance, void** weighted_sum,

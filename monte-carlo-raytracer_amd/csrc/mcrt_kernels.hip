@@ -115,17 +115,19 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
                                                 float4* __restrict__ hitOut) {
     __shared__ uint32_t lds[STACK_LDS * 64];
     const int lane = threadIdx.x;
-    const int tile = blockIdx.x;
+    const int tileAll = xcdRemap(blockIdx.x, gridDim.x);   // batch frame k = tileAll / numTiles
+    const int k = tileAll / f.numTiles, tile = tileAll - k * f.numTiles;
     int x, y;
     if (!tilePixel(f, tile, lane, x, y)) return;
-    const mcrt_camera& cam = *camp;
+    const mcrt_camera& cam = camp[k];
     TraceRay r;
     r.o = ld3(cam.pos);
     r.d = cameraDir(cam, x, y);
     r.tmax = 1000.0f;
     r.mask = -1;
     float t;
-    hitOut[(size_t)y * f.W + x] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, tile, lane), c.spillCap, c.overflow, t);
+    hitOut[(size_t)k * f.W * f.H + (size_t)y * f.W + x] =
+        traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, tileAll, lane), c.spillCap, c.overflow, t);
 }
 
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
@@ -137,7 +139,8 @@ __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict
     const int n = *count;
     if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
-    const int i = blockIdx.x * 64 + lane;
+    const int blk = xcdRemap(blockIdx.x, (n + 63) >> 6);
+    const int i = blk * 64 + lane;
     if (i >= n) return;
     const float4 o = qO[i], d = qD[i];
     TraceRay r;
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict
     r.tmax = RT_MAX_TRACE_F;
     r.mask = -1;
     float t;
-    hitOut[i] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+    hitOut[i] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blk, lane), c.spillCap, c.overflow, t);
 }
 
 // Any hit over the shadow queue + ShadowPass (PathTracing.cl:186-217):
@@ -159,7 +162,8 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     const int n = *count;
     if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
-    const int i = blockIdx.x * 64 + lane;
+    const int blk = xcdRemap(blockIdx.x, (n + 63) >> 6);
+    const int i = blk * 64 + lane;
     if (i >= n) return;
     const float4 o = sO[i], d = sD[i], L = sL[i];
     TraceRay r;
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     r.d = ld3(d);
     r.tmax = o.w;
     r.mask = -1;
-    const float V = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow) ? 0.0f : 1.0f;
+    const float V = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blk, lane), c.spillCap, c.overflow) ? 0.0f : 1.0f;
     const int pix = __float_as_int(d.w);
     float4 acc = radiance[pix];
     acc.x += L.x * V;
@@ -190,7 +194,8 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
     const int eb = (ne + 63) >> 6;
     const int lane = threadIdx.x;
     if ((int)blockIdx.x < eb) {
-        const int i = blockIdx.x * 64 + lane;
+        const int blk = xcdRemap(blockIdx.x, eb);
+        const int i = blk * 64 + lane;
         if (i >= ne) return;
         const float4 o = qO[i], d = qD[i];
         TraceRay r;
@@ -199,10 +204,12 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.tmax = RT_MAX_TRACE_F;
         r.mask = -1;
         float t;
-        hitOut[i] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+        hitOut[i] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blk, lane), c.spillCap, c.overflow, t);
     } else {
         const int ns = *shadowCount;
-        const int i = ((int)blockIdx.x - eb) * 64 + lane;
+        const int sb = (ns + 63) >> 6;
+        if ((int)blockIdx.x - eb >= sb) return;
+        const int i = xcdRemap((int)blockIdx.x - eb, sb) * 64 + lane;
         if (i >= ns) return;
         const float4 o = sO[i], d = sD[i], L = sL[i];
         TraceRay r;
@@ -261,7 +268,13 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
             Le = ld3(L.intensity);
         return throughput * Le;
     }
-    Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, bounce, f.W, f.H, s.sobol);
+    int px = pix, frame = f.frame;
+    if (f.batch > 1) {   // batched launch: path id -> (frame k, pixel)
+        const int k = (int)((uint32_t)pix / (f.W * f.H));
+        px = pix - k * (int)(f.W * f.H);
+        frame += k;
+    }
+    Sampler sampler = makeSampler(f.sampler, (uint32_t)px, frame, bounce, f.W, f.H, s.sobol);
     const bool isUber = materialId != -1 && mat.type == 0;   // materials.cl:130-142: other types evaluate to 0
     Uber um;
     if (isUber) um = uberProps(s, mat, si.uv, lod);
@@ -310,7 +323,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
                 f3 tp1 = nt;
                 if (f.russianRoulette && bounce + 1 >= f.rrStartDepth) {   // opt-in perf mode
                     const float qr = fmaxf(0.05f, 1.0f - fmaxf(nt.x, fmaxf(nt.y, nt.z)));
-                    const float ur = (float)wangHash((uint32_t)pix * 9781u + (uint32_t)f.frame * 6271u + (uint32_t)bounce) * 0x1p-32f;
+                    const float ur = (float)wangHash((uint32_t)px * 9781u + (uint32_t)frame * 6271u + (uint32_t)bounce) * 0x1p-32f;
                     alive = ur >= qr;
                     tp1 = cl_div(nt, (1.0f - qr));
                 }
@@ -332,9 +345,10 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
                                                 const float4* __restrict__ hits, float4* __restrict__ radiance,
                                                 QueueArgs q) {
     const int lane = threadIdx.x & 63;
-    const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int tileAll = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int k = tileAll / f.numTiles, tile = tileAll - k * f.numTiles;   // batch frame k
     int x = 0, y = 0;
-    bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y);
+    bool valid = k < f.batch && tilePixel(f, tile, lane, x, y);
     __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
 #if MCRT_SORT_OCTANT
     __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];
@@ -343,8 +357,8 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
     o.pushS = o.pushE = false;
     o.eD = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (valid) {
-        const mcrt_camera& cam = *camp;
-        const int pix = y * (int)f.W + x;
+        const mcrt_camera& cam = camp[k];
+        const int pix = k * (int)(f.W * f.H) + y * (int)f.W + x;
         const f3 dir = cameraDir(cam, x, y);
         f3 dx = splat3(0.0f), dy = splat3(0.0f);
         if (LOD) cameraDiffDirs(cam, x, y, dx, dy);
@@ -450,27 +464,35 @@ __global__ __launch_bounds__(256) void k_aov(SceneArgs s, FrameArgs f, const mcr
 // ReconstructionPass (KRN/reconstruction.cl:6-60); weight precomputed on the host
 // (KRN/filters.cl, uniform per frame).  Band rows only.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, float w, const float4* __restrict__ radiance,
-                                                    float4* __restrict__ wsum, float* __restrict__ wts,
-                                                    float4* __restrict__ image) {
+// A batch of f.batch frames (mcrt_render_frames) is accumulated in frame order, frame + k with
+// weight bw.w[k]: per pixel the same operations as f.batch single-frame launches.
+__global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, BatchWeights bw,
+                                                    const float4* __restrict__ radiance, float4* __restrict__ wsum,
+                                                    float* __restrict__ wts, float4* __restrict__ image) {
     const int lane = threadIdx.x & 63;
     const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     int x, y;
     if (tile >= f.numTiles || !tilePixel(f, tile, lane, x, y)) return;
     const int pix = y * (int)f.W + x;
-    const float4 r4 = radiance[pix];
-    const f4 radiance4 = f4{cl_clamp(r4.x, 0.0f, 1000.0f), cl_clamp(r4.y, 0.0f, 1000.0f), cl_clamp(r4.z, 0.0f, 1000.0f),
-                            cl_clamp(r4.w, 0.0f, 1000.0f)};
     f4 s;
     float ws;
-    if (frame == 0) {
-        s = radiance4 * w;
-        ws = w;
-    } else {
+    if (frame != 0) {
         const float4 o = wsum[pix];
         s = f4{o.x, o.y, o.z, o.w};
-        s += radiance4 * w;
-        ws = wts[pix] + w;
+        ws = wts[pix];
+    }
+    for (int k = 0; k < f.batch; ++k) {
+        const float4 r4 = radiance[(size_t)k * f.W * f.H + pix];
+        const f4 radiance4 = f4{cl_clamp(r4.x, 0.0f, 1000.0f), cl_clamp(r4.y, 0.0f, 1000.0f),
+                                cl_clamp(r4.z, 0.0f, 1000.0f), cl_clamp(r4.w, 0.0f, 1000.0f)};
+        const float w = bw.w[k];
+        if (frame + k == 0) {
+            s = radiance4 * w;
+            ws = w;
+        } else {
+            s += radiance4 * w;
+            ws = ws + w;
+        }
     }
     wsum[pix] = make_float4(s.x, s.y, s.z, s.w);
     wts[pix] = ws;
@@ -585,7 +607,7 @@ void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshSt
 }
 
 void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st) {
-    hipLaunchKernelGGL(c.twoLevel ? k_primary<true> : k_primary<false>, dim3(f.numTiles), dim3(64), 0, st, c, f, cam,
+    hipLaunchKernelGGL(c.twoLevel ? k_primary<true> : k_primary<false>, dim3(f.numTiles * f.batch), dim3(64), 0, st, c, f, cam,
                        hits);
 }
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
@@ -607,7 +629,7 @@ void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* 
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {
-    const int blocks = (f.numTiles * 64 + SHADE_BLOCK - 1) / SHADE_BLOCK;
+    const int blocks = (f.numTiles * f.batch * 64 + SHADE_BLOCK - 1) / SHADE_BLOCK;
     hipLaunchKernelGGL(f.textureLod ? k_shade0<true> : k_shade0<false>, dim3(blocks), dim3(SHADE_BLOCK), 0, st, s, f,
                        cam, hits, radiance, q);
 }
@@ -623,8 +645,8 @@ void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, 
     const int blocks = (f.numTiles * 64 + 255) / 256;
     hipLaunchKernelGGL(k_aov, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, s, f, cam, hits, which, out);
 }
-void launch_accumulate(const FrameArgs& f, int frame, float w, const float4* radiance, float4* wsum, float* wts,
-                       float4* image, hipStream_t st) {
+void launch_accumulate(const FrameArgs& f, int frame, const BatchWeights& w, const float4* radiance, float4* wsum,
+                       float* wts, float4* image, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + 255) / 256;
     hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(256), 0, st, f, frame, w, radiance, wsum, wts, image);
 }

@@ -363,6 +363,29 @@ MCRT_DEV bool traceAny(const float4* __restrict__ nodes, const TraceRay& r, uint
     return traverse<true>(nodes, r, stk, spill, spillCap, overflowFlag, t) >= 0;
 }
 
+// XCD-aware workgroup order for the traversal launches.  Workgroups are dealt round-robin to the
+// 8 XCDs (block b runs on the XCD of b % 8, MI355X_MICROARCH "Workgroup dispatch"), so in
+// launch order every XCD's 4 MB L2 would see rays from the whole image.  xcdRemap turns the
+// physical block index `rel` of a section of S blocks into a logical one such that each XCD
+// walks contiguous runs of MCRT_XCD_SEG logical blocks (camera tiles / queue slices, which are
+// spatially coherent): the rays in flight on one XCD then share BVH nodes.  Runs of SEG blocks
+// are dealt to the XCDs in turn (XCD k gets runs k, k+8, ...), which keeps the per-XCD load
+// balanced across the image; the tail of < 8*SEG blocks is split in 8 contiguous parts.
+// A bijection on [0, S); SEG = 0 is the identity.
+#ifndef MCRT_XCD_SEG
+#define MCRT_XCD_SEG 128
+#endif
+MCRT_DEV int xcdRemap(int rel, int S) {
+    if (MCRT_XCD_SEG <= 0) return rel;
+    constexpr int R = 8 * MCRT_XCD_SEG;
+    const int round = rel / R, base = round * R;
+    const int w = rel - base;
+    const int xr = w & 7, pos = w >> 3;
+    if (base + R <= S) return base + xr * MCRT_XCD_SEG + pos;
+    const int T = S - base, q = T >> 3, rm = T & 7;   // partial round: 8 contiguous parts
+    return base + xr * q + min(xr, rm) + pos;
+}
+
 // Per-ray spill column: rays are grouped 64 to a wave; lane l of wave w owns entries
 // spill[(w * spillCap + k) * 64 + l], k < spillCap (coalesced across the wave).
 MCRT_DEV uint32_t* raySpill(const TraceCtx& c, int wave, int lane) {

@@ -49,6 +49,8 @@ SIGNATURES = {
     "mcrt_framebuffer_set_frames_in_flight": (_c.c_int, [_vp, _c.c_int32]),
     "mcrt_render_frame": (_c.c_int, [_vp, _vp, _vp, _vp]),
     "mcrt_accumulate": (_c.c_int, [_vp, _vp, _c.c_int32]),
+    "mcrt_render_frames": (_c.c_int, [_vp, _vp, _vp, _c.c_int32, _vp]),
+    "mcrt_accumulate_frames": (_c.c_int, [_vp, _vp, _c.c_int32, _c.c_int32]),
     "mcrt_framebuffer_device_ptrs": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_framebuffer_read": (_c.c_int, [_vp, _c.c_int, _vp]),
     "mcrt_framebuffer_stats": (_c.c_int, [_vp, _vp, _vp, _vp]),
@@ -91,6 +93,16 @@ def _check(status, ctx=None):
 
 def _p(a):
     return None if a is None else a.ctypes.data
+
+
+def _records(items):
+    """Stacks one-record structured arrays into one array of the SAME dtype (np.stack would promote
+    a padded dtype such as the 56-B filter layout to a packed one and shift its fields)."""
+    first = np.asarray(items[0])
+    out = np.empty(len(items), first.dtype)
+    for i, a in enumerate(items):
+        out[i] = np.asarray(a, first.dtype).reshape(-1)[0]
+    return out
 
 
 class Context:
@@ -241,7 +253,7 @@ class FrameBuffer:
         ctx._adopt(self)
 
     def set_frames_in_flight(self, n):
-        """mcrt_framebuffer_set_frames_in_flight: 0 = auto (one slot per band share, <= 4)."""
+        """mcrt_framebuffer_set_frames_in_flight: 0 = auto (2 slots)."""
         _check(lib().mcrt_framebuffer_set_frames_in_flight(self.h, n), self.ctx.h)
 
     def render(self, dscene, cam, frame=0, max_depth=2, sampler=T.SAMPLER_RANDOM, rr=False, rr_start=3,
@@ -250,6 +262,19 @@ class FrameBuffer:
                           integrator, 1 if texture_lod else 0)
         cam = np.ascontiguousarray(cam)
         _check(lib().mcrt_render_frame(dscene.h, self.h, _p(cam), _c.byref(p)), self.ctx.h)
+
+    def render_frames(self, dscene, cams, frame=0, max_depth=2, sampler=T.SAMPLER_RANDOM, rr=False, rr_start=3,
+                      band_rows=8, num_bands=1, band_index=0):
+        """mcrt_render_frames: len(cams) consecutive frames frame, frame+1, ... in one pass (PT)."""
+        p = T.FrameParams(frame, max_depth, sampler, 1 if rr else 0, rr_start, band_rows, num_bands, band_index,
+                          T.INTEGRATOR_PT, 0)
+        cams = _records(cams)
+        _check(lib().mcrt_render_frames(dscene.h, self.h, _p(cams), len(cams), _c.byref(p)), self.ctx.h)
+
+    def accumulate_frames(self, filters, frame):
+        """mcrt_accumulate_frames: one filter per frame of the last render_frames (or one shared)."""
+        filters = _records(filters)
+        _check(lib().mcrt_accumulate_frames(self.h, _p(filters), len(filters), frame), self.ctx.h)
 
     def render_aov(self, dscene, cam, aov=T.AOV_ALBEDO, texture_lod=False):
         """mcrt_render_aov: (H, W, 4) albedo or (H, W, 3, 4) texture-footprint records."""

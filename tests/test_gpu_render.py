@@ -164,3 +164,93 @@ def test_frames_in_flight_accumulate_bit_exact(hip_ctx, mixed, num_bands, band_i
         finally:
             fb.close()
     ds.close()
+
+
+def test_russian_roulette_off_below_start_depth(hip_ctx, mixed):
+    """RR is opt-in (the reference has none): with rr_start_depth >= maxDepth
+    no extension ray is tested, so the frame is the parity-mode frame bit for bit."""
+    from mcrt import lib
+    sc, _ = mixed
+    W, H = 64, 48
+    ds = lib.DeviceScene(hip_ctx, sc)
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    cam = scene_camera("mixed", W, H)
+    fb.render(ds, cam, frame=2, max_depth=3)
+    a = fb.read(0)
+    fb.render(ds, cam, frame=2, max_depth=3, rr=True, rr_start=3)
+    b = fb.read(0)
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    fb.close()
+    ds.close()
+
+
+def test_russian_roulette_unbiased(hip_ctx, mixed):
+    """RR perf mode (extension rays survive with p = min(0.95, max(throughput)) and carry
+    throughput / p).  Its coin is a separate hash, so the reference's per-(pixel, frame, bounce)
+    sample streams are untouched and each RR path is the parity path, cut short or rescaled.
+    Unbiasedness: over pixels x frames the mean of (RR - parity) radiance is zero within 4
+    standard errors; RR must trace fewer closest-hit rays."""
+    from mcrt import lib
+    sc, _ = mixed
+    W, H, D, F = 64, 48, 5, 24
+    ds = lib.DeviceScene(hip_ctx, sc)
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    cam = scene_camera("mixed", W, H)
+    diffs, base, rays = [], [], [0, 0]
+    for frame in range(F):
+        fb.render(ds, cam, frame=frame, max_depth=D)
+        a = fb.read(0)[..., :3].astype(np.float64)
+        rays[0] += fb.stats()["closest_rays"]
+        fb.render(ds, cam, frame=frame, max_depth=D, rr=True, rr_start=1)
+        b = fb.read(0)[..., :3].astype(np.float64)
+        rays[1] += fb.stats()["closest_rays"]
+        assert np.isfinite(b).all()
+        diffs.append((b - a).sum(-1).ravel())
+        base.append(a.sum(-1).ravel())
+    d = np.concatenate(diffs)
+    se = d.std() / np.sqrt(d.size)
+    assert abs(d.mean()) <= 4 * se + 1e-7, (d.mean(), se)
+    assert (d != 0).any()                               # RR did act
+    assert abs(d.mean()) <= 0.02 * np.concatenate(base).mean()
+    assert rays[1] < rays[0], rays
+    fb.close()
+    ds.close()
+
+
+@pytest.mark.parametrize("num_bands,band_index,count", [(1, 0, 2), (1, 0, 5), (4, 3, 8)])
+def test_batched_frames_bit_exact(hip_ctx, mixed, num_bands, band_index, count):
+    """mcrt_render_frames + mcrt_accumulate_frames over `count` frames (per-frame jittered
+    cameras, per-frame filter weights) give the accumulators of `count` single-frame renders
+    and accumulations bit for bit, and the batch's first-frame radiance."""
+    from mcrt import lib
+    sc, _ = mixed
+    W, H, D = 96, 72, 3
+    ds = lib.DeviceScene(hip_ctx, sc)
+    band = dict(band_rows=8, num_bands=num_bands, band_index=band_index)
+    cams = [scene_camera("mixed", W, H, frame=f, jitter=True) for f in range(2 * count)]
+    filts = [T.make_filter(T.GAUSSIAN, pixel_offset=(0.1 * (f % 5) - 0.2, 0.05 * f - 0.3)) for f in range(2 * count)]
+    ref = lib.FrameBuffer(hip_ctx, W, H)
+    rad0 = {}
+    for f in range(2 * count):
+        ref.render(ds, cams[f], frame=f, max_depth=D, **band)
+        if f % count == 0:
+            rad0[f] = ref.read(0)
+        ref.accumulate(filts[f], f)
+    want = (ref.read(1), ref.read(2))
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    for f0 in (0, count):
+        fb.render_frames(ds, cams[f0:f0 + count], frame=f0, max_depth=D, **band)
+        np.testing.assert_array_equal(fb.read(0).view(np.uint32), rad0[f0].view(np.uint32))
+        fb.accumulate_frames(filts[f0:f0 + count], f0)
+    np.testing.assert_array_equal(fb.read(1).view(np.uint32), want[0].view(np.uint32))
+    np.testing.assert_array_equal(fb.read(2).view(np.uint32), want[1].view(np.uint32))
+    assert want[1][..., :3].max() > 0
+    st = fb.stats()
+    assert st["closest_rays"] > 0
+    with pytest.raises(lib.MCRTError):
+        fb.accumulate_frames(filts[:2] if count != 2 else filts[:3], 0)   # neither 1 nor count filters
+    with pytest.raises(lib.MCRTError):
+        fb.render_frames(ds, [cams[0]] * 17, frame=0, max_depth=D)
+    fb.close()
+    ref.close()
+    ds.close()

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--scene", default="san_miguel_proxy")
     ap.add_argument("--fif", type=int, default=0, help="frames in flight (0 = the library's auto choice)")
+    ap.add_argument("--batch", type=int, default=1, help="frames per mcrt_render_frames call (0 = N)")
     args = ap.parse_args()
     from mcrt import lib, scenes
     from mcrt import types as T
@@ -35,19 +36,27 @@ def main():
     fb = lib.FrameBuffer(ctx, W, H)
     filt = T.make_filter(T.BOX)
     fb.set_frames_in_flight(args.fif)
-    out = {"fif": args.fif, "scene": args.scene, "steps": args.steps, "band_rows": args.band_rows, "per_n": {}}
+    out = {"fif": args.fif, "batch": args.batch, "scene": args.scene, "steps": args.steps, "band_rows": args.band_rows, "per_n": {}}
     for n in [int(x) for x in args.ns.split(",")]:
         per_rank = []
         for r in range(n):
             band = dict(band_rows=args.band_rows, num_bands=n, band_index=r)
-            for f in range(3):
-                fb.render(ds, cam, frame=f, max_depth=2, **band)
-                fb.accumulate(filt, f)
+            B = args.batch if args.batch > 0 else n
+
+            def run(f0, count):
+                i = 0
+                while i < count:
+                    k = min(B, count - i)
+                    if k == 1:
+                        fb.render(ds, cam, frame=f0 + i, max_depth=2, **band)
+                    else:
+                        fb.render_frames(ds, [cam] * k, frame=f0 + i, max_depth=2, **band)
+                    fb.accumulate(filt, f0 + i)
+                    i += k
+            run(0, max(3, 4 * B))   # every frame slot allocated before timing
             ctx.sync()
             t0 = time.perf_counter()
-            for i in range(args.steps):
-                fb.render(ds, cam, frame=3 + i, max_depth=2, **band)
-                fb.accumulate(filt, 3 + i)
+            run(16, args.steps)
             ctx.sync()
             per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
         out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
