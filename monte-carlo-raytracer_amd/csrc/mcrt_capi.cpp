@@ -129,7 +129,18 @@ struct FrameSlot {
     int frames = 1;              // radiance / primary-hit planes of W*H allocated (batch capacity)
     size_t queueCap = 0;         // entries of each ray-queue buffer
 };
-#define SLOT_COUNTER_BYTES 4096   // [0..127] ints: counters; cameras (176 B each, <= 16) from byte 512
+#define SLOT_COUNTER_BYTES 4096
+
+// Per-frame BDPT arrays (RTBDPTPass::createBuffers, RTBDPTPass.cpp:442-479), one set per frame
+// slot so BDPT frames overlap like PT frames; layouts in mcrt_bdpt.hip.
+struct BdptSet {
+    float4 *camV = nullptr, *lightV = nullptr, *slots = nullptr, *splat = nullptr;
+    int *camCount = nullptr, *lightCount = nullptr, *bdptCounters = nullptr;
+    float4 *bqO[2] = {}, *bqD[2] = {}, *bqT[2] = {}, *bHits = nullptr;
+    float4 *cO = nullptr, *cD = nullptr, *cL = nullptr;
+    uint32_t* spill = nullptr;   // traversal spill columns of this set's launches
+    size_t spillWords = 0;
+};   // [0..127] ints: counters; cameras (176 B each, <= 16) from byte 512
 
 struct mcrt_framebuffer_s {
     mcrt_ctx ctx = nullptr;
@@ -159,8 +170,13 @@ struct mcrt_framebuffer_s {
     int64_t lastPixels = 0;
     FrameArgs bands{};      // band layout of the last mcrt_render_frame (used by mcrt_accumulate)
     bool haveBands = false;
-    // BDPT state (allocated on the first BDPT frame for a max depth; mcrt_bdpt.hip has the layout)
+    // BDPT state (allocated on the first BDPT frame for a max depth; mcrt_bdpt.hip has the layout):
+    // per-frame arrays per frame slot; the sampled-light-vertex planes carry state from frame to
+    // frame (BDPT.cl:585), so they are shared and the connect launches stay in frame order
     int bdptDepth = 0;
+    BdptSet bset[MCRT_MAX_FRAMES_IN_FLIGHT];
+    hipEvent_t bdptConnect = nullptr;   // recorded after the last enqueued frame's connect launch
+    // views of the set of the last BDPT frame (read-back API)
     float4 *camV = nullptr, *lightV = nullptr, *sampLight = nullptr, *slots = nullptr, *splat = nullptr;
     int *camCount = nullptr, *lightCount = nullptr, *bdptCounters = nullptr;
     float4 *bqO[2] = {}, *bqD[2] = {}, *bqT[2] = {}, *bHits = nullptr;
@@ -861,12 +877,19 @@ MCRT_API mcrt_status mcrt_trace_any(mcrt_scene s, const mcrt_ray* d_rays, int32_
 // ---------------------------------------------------------------------------
 // frame buffer + integrator
 // ---------------------------------------------------------------------------
-static void fb_free_bdpt(mcrt_framebuffer fb) {
-    void* ptrs[] = {fb->camV,   fb->lightV, fb->sampLight, fb->slots,  fb->splat,  fb->camCount, fb->lightCount,
-                    fb->bdptCounters, fb->bqO[0], fb->bqO[1], fb->bqD[0], fb->bqD[1], fb->bqT[0], fb->bqT[1],
-                    fb->bHits,  fb->cO,     fb->cD,        fb->cL};
+static void bset_free(BdptSet& b) {
+    void* ptrs[] = {b.camV,   b.lightV, b.slots,  b.splat,  b.camCount, b.lightCount, b.bdptCounters,
+                    b.bqO[0], b.bqO[1], b.bqD[0], b.bqD[1], b.bqT[0], b.bqT[1], b.bHits, b.cO, b.cD, b.cL, b.spill};
     for (void* p : ptrs)
         if (p) hipFree(p);
+    b = BdptSet();
+}
+
+static void fb_free_bdpt(mcrt_framebuffer fb) {
+    for (auto& b : fb->bset) bset_free(b);
+    if (fb->sampLight) hipFree(fb->sampLight);
+    if (fb->bdptConnect) hipEventDestroy(fb->bdptConnect);
+    fb->bdptConnect = nullptr;
     fb->camV = fb->lightV = fb->sampLight = fb->slots = fb->splat = fb->bHits = fb->cO = fb->cD = fb->cL = nullptr;
     fb->camCount = fb->lightCount = fb->bdptCounters = nullptr;
     for (int i = 0; i < 2; ++i) fb->bqO[i] = fb->bqD[i] = fb->bqT[i] = nullptr;
@@ -952,37 +975,57 @@ static void ctx_wait_slots(mcrt_framebuffer fb) {
         if (k.stream) hipStreamWaitEvent(fb->ctx->stream, k.done, 0);
 }
 
-// RTBDPTPass::createBuffers (RTBDPTPass.cpp:442-479), sized for max depth D.  The persistent
-// sampled-light-vertex planes start zeroed (the reference's buffer starts with whatever the
-// allocation holds; its clref runner zero-fills it too).
-static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D) {
-    if (fb->bdptDepth == D) return hipSuccess;
-    hipStreamSynchronize(fb->ctx->stream);
-    fb_free_bdpt(fb);
-    const size_t N = fb->N, C = (size_t)bdpt_max_connections(D);
+static hipError_t bset_alloc(BdptSet& b, size_t N, int D) {
+    const size_t C = (size_t)bdpt_max_connections(D);
     hipError_t e = hipSuccess;
     auto A = [&](auto** p, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
     };
-    A(&fb->camV, 16 * N * BDPT_VERTEX_PLANES * (D + 2));
-    A(&fb->lightV, 16 * N * BDPT_VERTEX_PLANES * (D + 1));
-    A(&fb->sampLight, 16 * N * D);
-    A(&fb->slots, 16 * N * (C - D));
-    A(&fb->splat, 16 * N);
-    A(&fb->camCount, 4 * N);
-    A(&fb->lightCount, 4 * N);
-    A(&fb->bdptCounters, 64 * sizeof(int));
-    for (int i = 0; i < 2; ++i) { A(&fb->bqO[i], 32 * N); A(&fb->bqD[i], 32 * N); A(&fb->bqT[i], 32 * N); }
-    A(&fb->bHits, 32 * N);
-    A(&fb->cO, 16 * N * C);
-    A(&fb->cD, 16 * N * C);
-    A(&fb->cL, 16 * N * C);
-    if (e == hipSuccess) e = hipMemset(fb->sampLight, 0, 16 * N * D);
-    if (e == hipSuccess) e = hipMemset(fb->splat, 0, 16 * N);
-    if (e == hipSuccess) e = hipMemset(fb->camV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 2));
-    if (e == hipSuccess) e = hipMemset(fb->lightV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 1));
-    if (e != hipSuccess) { fb_free_bdpt(fb); return e; }
-    fb->bdptDepth = D;
+    A(&b.camV, 16 * N * BDPT_VERTEX_PLANES * (D + 2));
+    A(&b.lightV, 16 * N * BDPT_VERTEX_PLANES * (D + 1));
+    A(&b.slots, 16 * N * (C - D));
+    A(&b.splat, 16 * N);
+    A(&b.camCount, 4 * N);
+    A(&b.lightCount, 4 * N);
+    A(&b.bdptCounters, 64 * sizeof(int));
+    for (int i = 0; i < 2; ++i) { A(&b.bqO[i], 32 * N); A(&b.bqD[i], 32 * N); A(&b.bqT[i], 32 * N); }
+    A(&b.bHits, 32 * N);
+    A(&b.cO, 16 * N * C);
+    A(&b.cD, 16 * N * C);
+    A(&b.cL, 16 * N * C);
+    if (e == hipSuccess) e = hipMemset(b.splat, 0, 16 * N);
+    if (e == hipSuccess) e = hipMemset(b.camV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 2));
+    if (e == hipSuccess) e = hipMemset(b.lightV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 1));
+    if (e != hipSuccess) bset_free(b);
+    return e;
+}
+
+// The fb's BDPT views show set k (the last BDPT frame).
+static void fb_bind_bdpt(mcrt_framebuffer fb, int k) {
+    const BdptSet& b = fb->bset[k];
+    fb->camV = b.camV; fb->lightV = b.lightV; fb->slots = b.slots; fb->splat = b.splat;
+    fb->camCount = b.camCount; fb->lightCount = b.lightCount; fb->bdptCounters = b.bdptCounters;
+    for (int i = 0; i < 2; ++i) { fb->bqO[i] = b.bqO[i]; fb->bqD[i] = b.bqD[i]; fb->bqT[i] = b.bqT[i]; }
+    fb->bHits = b.bHits; fb->cO = b.cO; fb->cD = b.cD; fb->cL = b.cL;
+}
+
+// RTBDPTPass::createBuffers (RTBDPTPass.cpp:442-479), sized for max depth D: set k of the
+// per-frame arrays, plus the persistent sampled-light-vertex planes, which start zeroed (the
+// reference's buffer starts with whatever the allocation holds; its clref runner zero-fills it too).
+static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k) {
+    const size_t N = fb->N;
+    if (fb->bdptDepth != D) {
+        for (auto& sl : fb->slot)
+            if (sl.stream) hipStreamSynchronize(sl.stream);
+        hipStreamSynchronize(fb->ctx->stream);
+        fb_free_bdpt(fb);
+        hipError_t e = hipMalloc(&fb->sampLight, 16 * N * D);
+        if (e == hipSuccess) e = hipMemset(fb->sampLight, 0, 16 * N * D);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&fb->bdptConnect, hipEventDisableTiming);
+        if (e != hipSuccess) { fb_free_bdpt(fb); return e; }
+        fb->bdptDepth = D;
+    }
+    if (!fb->bset[k].camV) return bset_alloc(fb->bset[k], N, D);
     return hipSuccess;
 }
 
@@ -1082,11 +1125,13 @@ static int frames_in_flight(mcrt_framebuffer fb, const FrameArgs& f) {
 // RTBDPTPass::update (RTBDPTPass.cpp:67-128): start vertices, D+1 rounds of (trace, vertex),
 // connections + MIS, visibility, gather.  Rays of both subpaths share one compacted queue.
 static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_camera* cam, const mcrt_frame_params* p,
-                               const FrameArgs& f) {
+                               const FrameArgs& f, int k, hipStream_t st) {
+    // frame slot k on stream st: per-frame arrays of set k; the connect launch (the only reader
+    // and writer of the shared sampled-light-vertex planes) waits for the previous frame's connect
     mcrt_ctx ctx = s->ctx;
-    hipStream_t st = ctx->stream;
     const int D = p->max_depth;
-    HIPCHK(ctx, fb_ensure_bdpt(fb, D));
+    HIPCHK(ctx, fb_ensure_bdpt(fb, D, k));
+    fb_bind_bdpt(fb, k);
     fb->lastMaxDepth = D;
     fb->lastPixels = 0;
     fb->bands = f;
@@ -1100,8 +1145,18 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         return MCRT_OK;
     }
     const size_t N = fb->N, C = (size_t)bdpt_max_connections(D);
-    if (!ensure_spill(s, std::max(2 * N, C * N))) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
-    const TraceCtx tcs = trace_ctx(s);
+    BdptSet& bs = fb->bset[k];
+    const size_t spillWords = (std::max(2 * N, C * N) + 63) / 64 * 64 * (size_t)s->spillCap;
+    if (bs.spillWords < spillWords) {
+        HIPCHK(ctx, hipStreamSynchronize(st));
+        if (bs.spill) hipFree(bs.spill);
+        bs.spill = nullptr;
+        bs.spillWords = 0;
+        HIPCHK(ctx, hipMalloc(&bs.spill, spillWords * sizeof(uint32_t)));
+        bs.spillWords = spillWords;
+    }
+    TraceCtx tcs = trace_ctx(s);
+    tcs.spill = bs.spill;
     const SceneArgs sa = scene_args(s);
     BdptArgs b;
     b.camV = fb->camV;
@@ -1122,16 +1177,16 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         return q;
     };
     {
-        Timed t(ctx, K_BDPT_START, nullptr, (int64_t)f.numTiles * 64);
+        Timed t(ctx, K_BDPT_START, nullptr, (int64_t)f.numTiles * 64, st);
         mcrt::launch_bdpt_start(sa, f, b, dCam, queue(0), st);
     }
     for (int d = 1; d <= D + 1; ++d) {
         const BdptQueue qIn = queue(d - 1), qOut = queue(d);
         {
-            Timed t(ctx, K_EXTEND, qIn.count, 0);
+            Timed t(ctx, K_EXTEND, qIn.count, 0, st);
             mcrt::launch_extend(tcs, qIn.count, qIn.o, qIn.d, fb->bHits, (int)(2 * N), st);
         }
-        Timed t(ctx, K_BDPT_VERTEX, qIn.count, 0);
+        Timed t(ctx, K_BDPT_VERTEX, qIn.count, 0, st);
         mcrt::launch_bdpt_vertex(sa, f, b, d, qIn, fb->bHits, qOut, (int)(2 * N), st);
     }
     BdptQueue cq;
@@ -1139,16 +1194,18 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     cq.o = fb->cO;
     cq.d = fb->cD;
     cq.t = fb->cL;
+    HIPCHK(ctx, hipStreamWaitEvent(st, fb->bdptConnect, 0));   // sampled-light planes in frame order
     {
-        Timed t(ctx, K_BDPT_CONNECT, nullptr, (int64_t)f.numTiles * 64);
+        Timed t(ctx, K_BDPT_CONNECT, nullptr, (int64_t)f.numTiles * 64, st);
         mcrt::launch_bdpt_connect(sa, f, b, dCam, cq, st);
     }
+    HIPCHK(ctx, hipEventRecord(fb->bdptConnect, st));
     {
-        Timed t(ctx, K_BDPT_VIS, cq.count, 0);
+        Timed t(ctx, K_BDPT_VIS, cq.count, 0, st);
         mcrt::launch_bdpt_vis(tcs, b, cq, (int)(C * N), st);
     }
     {
-        Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)f.numTiles * 64);
+        Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)f.numTiles * 64, st);
         mcrt::launch_bdpt_gather(f, b, fb->radiance, st);
     }
     HIPCHK(ctx, hipGetLastError());
@@ -1184,23 +1241,23 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     std::string err;
     if (!frame_args(fb, p, f, err)) return fail(ctx, MCRT_ERROR_INVALID_ARG, err);
     hipSetDevice(ctx->device);
-    if (p->integrator == MCRT_INTEGRATOR_BDPT) {
-        ctx_wait_slots(fb);   // BDPT runs on the context stream in slot 0's buffers
-        fb_bind(fb, 0);
-        fb->next = 1 % frames_in_flight(fb, f);
-        mcrt_status r = render_bdpt(s, fb, cam, p, f);
-        hipEventRecord(fb->slot[0].done, ctx->stream);
-        hipEventRecord(fb->slot[0].free, ctx->stream);
-        fb->slot[0].lastMaxDepth = fb->lastMaxDepth;
-        fb->slot[0].lastPixels = fb->lastPixels;
-        fb->slot[0].lastBatch = 1;
-        return r;
-    }
     f.batch = count;
     // frame slot: its buffers are free once the accumulation of its previous frame has read them
     const int S = frames_in_flight(fb, f);
     const int ks = fb->next % S;
     FrameSlot& slot = fb->slot[ks];
+    if (p->integrator == MCRT_INTEGRATOR_BDPT) {   // BDPT frames overlap the same way (set ks)
+        if (!slot.stream) HIPCHK(ctx, slot_alloc(slot, fb->N));
+        HIPCHK(ctx, hipStreamWaitEvent(slot.stream, slot.free, 0));
+        fb_bind(fb, ks);
+        fb->next = (ks + 1) % S;
+        slot.lastBatch = 1;
+        const mcrt_status r = render_bdpt(s, fb, cam, p, f, ks, slot.stream);
+        slot.lastMaxDepth = fb->lastMaxDepth;
+        slot.lastPixels = fb->lastPixels;
+        hipEventRecord(slot.done, slot.stream);
+        return r;
+    }
     // the queues hold at most the batch's paths of the band: size the ray grids to them
     const int bandPaths = f.numTiles * 64 * count;
     const size_t qNeed = std::max(fb->N, (size_t)bandPaths);
