@@ -11,10 +11,10 @@ reduce of the accumulators (sum) to rank 0 ends the job (inside the timed region
 Total work per step is fixed -> "scaling": "strong".
 
 Also reported (one JSON line on rank 0):
-  roofline      dominant kernel: algorithmic bytes per launch (rays x (48 + 32 + 64 V)
-                for closest, rays x (48 + 4 + 64 V) for any-hit, V = node visits per query of the
-                reference Bvh2 + LDS traversal measured by the oracle on the same scene/camera) over its
-                average HIP-event duration, vs the 8 TB/s HBM peak; traffic from rocprofv3 PMC if present
+  roofline      dominant kernel (k_shadow_extend): compulsory bytes per launch (ray I/O + 64 B per
+                DISTINCT BVH node the launch visits, counted by the oracle) over its average HIP-event
+                duration in an untimed one-slot pass, vs the 8 TB/s HBM peak; traffic = rocprofv3
+                memory-side bytes per launch from the committed counter summary (profiles/)
   cpu_baseline  the oracle (C restatement of the reference kernels) on a bounded sample of rows of
                 the same frame, all host cores (rank 0, N = 1 only)
 """
@@ -39,22 +39,9 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def per_query_bytes(kernel, V):
-    """SURVEY.md §8d algorithmic bytes per query."""
-    if kernel == "k_shadow":
-        return 48 + 4 + 64.0 * V
-    return 48 + 32 + 64.0 * V
-
-
-def b_path(stats_per_path, D):
-    """B_path = 112 + sum_closest(48+32+64V) + sum_any(48+4+64V) + sum_shade 388 + sum_bounce 132 + 72."""
-    s = stats_per_path
-    return (112 + s["closest"] * 80 + 64 * s["closest_visits"] + s["any"] * 52 + 64 * s["any_visits"]
-            + s["shaded"] * 388 + D * 132 + 72)
-
-
-def cpu_baseline(scene, cam, W, H, D, target_s=15.0):
-    """Times the oracle on a bounded, evenly spread sample of rows of frame 0."""
+def cpu_baseline(scene, cam_of, W, H, D, target_s=15.0):
+    """Times the oracle (C restatement of the reference kernels, oracle/mcrt_oracle.c) on a bounded,
+    evenly spread sample of rows of the bench's own frames (per-frame jittered cameras)."""
     from oracle import pyoracle as po
     # the box exposes all host CPUs but one GPU job owns a share of them (OMP_NUM_THREADS there)
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
@@ -62,15 +49,16 @@ def cpu_baseline(scene, cam, W, H, D, target_s=15.0):
     t0 = time.perf_counter()
     o.build()
     build_s = time.perf_counter() - t0
+    f0 = 0
     # calibrate on 8 rows, then size the sample to ~target_s
     cal_rows = np.linspace(0, H - 1, 8).astype(np.int32)
     t0 = time.perf_counter()
-    o.render_rows(cam, cal_rows, frame=0, max_depth=D, threads=threads)
+    o.render_rows(cam_of(f0), cal_rows, frame=f0, max_depth=D, threads=threads)
     dt = max(time.perf_counter() - t0, 1e-3)
     nrows = int(np.clip(8 * target_s / dt, 8, H))
     rows = np.unique(np.linspace(0, H - 1, nrows).astype(np.int32))
     t0 = time.perf_counter()
-    rad, st = o.render_rows(cam, rows, frame=0, max_depth=D, threads=threads)
+    rad, st = o.render_rows(cam_of(f0), rows, frame=f0, max_depth=D, threads=threads)
     el = time.perf_counter() - t0
     paths0 = paths = len(rows) * W
     frames = 1
@@ -78,28 +66,91 @@ def cpu_baseline(scene, cam, W, H, D, target_s=15.0):
     # rows until the sample is ~target_s of CPU work
     while len(rows) == H and el + el / frames <= target_s:
         t0 = time.perf_counter()
-        o.render_rows(cam, rows, frame=frames, max_depth=D, threads=threads)
+        o.render_rows(cam_of(f0 + frames), rows, frame=f0 + frames, max_depth=D, threads=threads)
         el += time.perf_counter() - t0
         paths += paths0
         frames += 1
     return {
         "value": paths / el / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
-        "sample": f"{len(rows)} of {H} rows (evenly spaced) of frames 0..{frames - 1}, {paths} paths, D={D}, "
-                  f"random sampler; oracle = C restatement of PathTracing.cl + RR Bvh2/LDS traversal, {threads} "
-                  f"threads, {el:.1f}s (BVH build {build_s:.1f}s not timed)",
-        "_rows": rows, "_radiance": rad, "_stats": st, "_paths": paths0,
+        "sample": f"{len(rows)} of {H} rows (evenly spaced) of frames {f0}..{f0 + frames - 1} (TAA-jittered cameras), "
+                  f"{paths} paths, D={D}, random sampler; oracle = C restatement of PathTracing.cl + RR Bvh2/LDS "
+                  f"traversal, {threads} threads, {el:.1f}s (BVH build {build_s:.1f}s not timed)",
+        "_rows": rows, "_radiance": rad, "_stats": st, "_paths": paths0, "_frame0": f0, "_oracle": o,
+        "_threads": threads,
     }
 
 
+def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, oracle=None):
+    """HBM roofline of k_shadow_extend (the dominant kernel): the shadow rays of bounce 0 and the
+    extension rays for bounce 1 of `batch` frames in one launch.
+
+    ALGORITHMIC bytes = the launch's compulsory traffic, which no cache can avoid:
+      extension ray: read (o, d) 32 B + write its hit record 16 B        = 48 B
+      shadow ray:    read (o, d, L) 48 B + radiance read-modify-write 32 B = 80 B
+      BVH:           64 B x the DISTINCT node records the launch's queries visit (each must come
+                     from HBM at least once per launch; re-reads of a node are cache traffic).
+    The distinct nodes are counted by the oracle (the reference's Bvh2 + LDS traversal, same tree,
+    same visit order) marking every node the queries of `batch` full frames visit.  The ray
+    counts are the product's own queue sizes.  traffic = the L2-to-memory bytes per launch from
+    rocprofv3 counters (profiles/, tools/pmc_json.py), for comparison: traffic / alg = the re-read
+    factor of the launch's node fetches."""
+    from oracle import pyoracle as po
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    o = oracle
+    if o is None:
+        o = po.OracleScene(scene)
+        o.build()
+    touched = o.track_touched(True)
+    t0 = time.perf_counter()
+    for f in range(batch):
+        o.render(cam_of(f), frame=f, max_depth=D, threads=threads)
+    el = time.perf_counter() - t0
+    o.track_touched(False)
+    n_nodes = int(((touched[1] | touched[2]) != 0).sum())
+    n_ext, n_sh = qcounts[1][0], qcounts[0][0]   # extension rays for bounce 1, shadow rays of bounce 0
+    alg = batch * (n_ext * 48 + n_sh * 80) + 64 * n_nodes
+    achieved = alg / (avg_ms * 1e-3) / 1e9
+    tr = pmc_traffic("k_shadow_extend")
+    out = {"bound": "hbm", "kernel": "k_shadow_extend", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "traffic": None if tr is None else round(tr["bytes_per_launch"]),
+           "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(avg_ms, 4),
+           "model": ("compulsory bytes per launch: 48 B per extension ray + 80 B per shadow ray + 64 B per "
+                     "DISTINCT BVH node the launch visits (oracle-counted over the launch's frames)"),
+           "distinct_nodes_per_launch": n_nodes, "nodes_total": int(o.num_nodes), "frames_per_launch": batch,
+           "rays_per_launch": {"extension": int(batch * n_ext), "shadow": int(batch * n_sh)},
+           "node_count_pass_s": round(el, 1)}
+    if tr is not None:
+        out["traffic_source"] = tr["source"]
+        out["traffic_rate_gbs"] = round(tr["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9, 1)
+        out["traffic_over_alg"] = round(tr["bytes_per_launch"] / alg, 2)
+        if "limiter" in tr:
+            out["limiter"] = tr["limiter"]
+    try:   # attainable HBM bandwidth of an in-repo stream copy (BASELINE.md §2)
+        att = ctx.stream_copy_gbps(2 << 30, 5)
+        out["attainable"] = round(att, 1)
+        out["frac_of_attainable"] = round(achieved / att, 4)
+    except Exception as e:   # noqa: BLE001 -- reported, not fatal
+        log(f"[bench] stream copy failed: {e}")
+    return out
+
+
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary (tools/pmc.py)."""
+    """Memory-side bytes per launch of `kernel` (and the SQ limiter summary, if measured) from the
+    committed rocprofv3 counter summary profiles/pmc_latest.json (tools/pmc_json.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
         k = d.get("kernels", {}).get(kernel)
-        return None if k is None else float(k["hbm_bytes_per_launch"])
+        if k is None:
+            return None
+        r = {"bytes_per_launch": float(k["hbm_bytes_per_launch"]),
+             "source": f"profiles/pmc_latest.json ({d.get('config', 'config not recorded')})"}
+        if "limiter" in k:
+            r["limiter"] = k["limiter"]
+        return r
     except Exception:
         return None
 
@@ -119,7 +170,11 @@ def main():
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-roofline-model", action="store_true",
+                    help="skip the oracle pass that counts the distinct BVH nodes of one launch")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--stats-launches", type=int, default=4,
+                    help="launch sequences of the untimed per-kernel timing pass (one frame slot)")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     ap.add_argument("--save-image", default=None, help="rank 0 saves the final accumulated image (.npy)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -166,10 +221,16 @@ def main():
     else:
         scene = scenes.dragon_proxy(tris=min(args.tris, 871_414))
     sampler = T.SAMPLER_SOBOL if args.sampler == "sobol" else T.SAMPLER_RANDOM
-    if sampler == T.SAMPLER_SOBOL:   # g_SobolMatrices32 (sobol.h:34), committed as a data fixture
-        scene.sobol = np.load(os.path.join(ROOT, "tests", "golden", "sobol_1024x52.npy"))
+    if sampler == T.SAMPLER_SOBOL:   # g_SobolMatrices32 (sobol.h:34), package data
+        from mcrt import sobol_matrices
+        scene.sobol = sobol_matrices()
     gen_s = time.perf_counter() - t0
-    cam = scene_camera(args.scene, W, H)
+    # TAA on (the reference default, PathTracingApp.cpp:208-215): every frame f has its own sub-pixel
+    # jittered camera; computed once for all frames before timing
+    ncams = 64
+    cams = [scene_camera(args.scene, W, H, frame=f, jitter=True) for f in range(ncams)]
+    cam_of = lambda f: cams[f % ncams]   # noqa: E731
+    cam = cams[0]
     log(f"[bench] scene {scene.name}: {scene.num_triangles} tris, gen {gen_s:.1f}s")
 
     ctx = lib.Context(local)
@@ -196,9 +257,9 @@ def main():
         frame = rank + world * i if bdpt else i
         kw = dict(max_depth=D, sampler=sampler, rr=args.russian_roulette, rr_start=args.rr_start, **band)
         if n == 1:
-            fb.render(ds, cam, frame=frame, **kw)
+            fb.render(ds, cam_of(frame), frame=frame, **kw)
         else:
-            fb.render_frames(ds, [cam] * n, frame=frame, **kw)
+            fb.render_frames(ds, [cam_of(frame + k) for k in range(n)], frame=frame, **kw)
         fb.accumulate(filt, 0 if first[0] else frame)   # 0: the first accumulation overwrites
         first[0] = False
 
@@ -221,8 +282,6 @@ def main():
     qcounts = fb.queue_counts() if not bdpt else None
     frame0 = warm + 1
 
-    if not args.no_kernel_timing:
-        ctx.set_profiling(True)
     ctx.reset_stats()
     if world > 1:
         acc_buf, acc_s, acc_w = mdist.packed_accumulators(W * H, "cuda")   # one buffer -> one reduce
@@ -249,8 +308,21 @@ def main():
         elapsed = float(t.item())
     if args.save_image and rank == 0:
         np.save(args.save_image, fb.read(2))
-    kstats = ctx.kernel_stats() if not args.no_kernel_timing else {}
-    ctx.set_profiling(False)
+    kstats = {}
+    if not args.no_kernel_timing:
+        # per-kernel HIP-event durations in a separate, untimed pass: one frame slot (kernels do not
+        # share the GPU with another frame's launches, so each duration is the kernel's own), the
+        # same frames per launch as the timed region
+        fb.set_frames_in_flight(1)
+        run(frame0 + args.steps, batch)   # the slot re-binds outside the profiled launches
+        ctx.sync()
+        ctx.set_profiling(True)
+        ctx.reset_stats()
+        run(frame0 + args.steps + batch, args.stats_launches * batch)
+        ctx.sync()
+        kstats = ctx.kernel_stats()
+        ctx.set_profiling(False)
+        fb.set_frames_in_flight(0)
 
     paths = W * H * args.steps * (world if bdpt else 1)
     value = paths / elapsed / 1e6
@@ -275,61 +347,37 @@ def main():
         rays = {"closest": fstats["closest_rays"] / (W * H / world), "any": fstats["any_rays"] / (W * H / world),
                 "shaded": fstats["shaded_paths"] / (W * H / world)}
         out["rays_per_path"] = {k: round(v, 4) for k, v in rays.items()}
+        # (the CPU oracle and the roofline's node counts price the flat structure)
+        oracle_ok = world == 1 and not bdpt and sampler == T.SAMPLER_RANDOM and not two_level
         cpu = None
-        # (the CPU oracle and the roofline's visit counts price the flat structure)
-        if world == 1 and not args.no_cpu_baseline and not bdpt and sampler == T.SAMPLER_RANDOM and not two_level:
-            cpu = cpu_baseline(scene, cam, W, H, D, args.cpu_seconds)
+        if oracle_ok and not args.no_cpu_baseline:
+            cpu = cpu_baseline(scene, cam_of, W, H, D, args.cpu_seconds)
             st = cpu["_stats"]
-            V = {"k_primary": st[1] / max(st[0], 1), "k_extend": st[3] / max(st[2], 1),
-                 "k_shadow": st[5] / max(st[4], 1)}
-            # parity spot check of the timed product frames is not possible (different frame
-            # indices); render frame 0 again and compare the sampled rows
-            fb.render(ds, cam, frame=0, max_depth=D, **band)
+            # parity spot check: the product renders the oracle's first sampled frame again
+            f0 = cpu["_frame0"]
+            fb.render(ds, cam_of(f0), frame=f0, max_depth=D, **band)
             g = fb.read(0)[cpu["_rows"]]
             r = cpu["_radiance"][cpu["_rows"]]
             dlt = np.abs(g[..., :3].astype(np.float64) - r[..., :3])
             ok = (dlt <= 1e-4 * np.maximum(1.0, np.abs(r[..., :3]))).all(-1).mean()
-            out["parity_vs_oracle"] = {"pixels_within_1e-4": round(float(ok), 5), "rows": int(len(cpu["_rows"]))}
-            per_path = {"closest": (st[0] + st[2]) / cpu["_paths"], "any": st[4] / cpu["_paths"],
-                        "closest_visits": (st[1] + st[3]) / cpu["_paths"], "any_visits": st[5] / cpu["_paths"],
-                        "shaded": (st[0] + st[2]) / cpu["_paths"]}
-            bp = b_path(per_path, D)
-            out["b_path_bytes"] = round(bp, 1)
-            out["achieved_hbm_gbs_alg"] = round(value * 1e6 * bp / 1e9, 1)
-            out["visits_per_query"] = {k: round(v, 2) for k, v in V.items()}
+            out["parity_vs_oracle"] = {"pixels_within_1e-4": round(float(ok), 5), "rows": int(len(cpu["_rows"])),
+                                       "frame": int(f0)}
+            out["visits_per_query"] = {"k_primary": round(st[1] / max(st[0], 1), 2),
+                                       "k_extend": round(st[3] / max(st[2], 1), 2),
+                                       "k_shadow": round(st[5] / max(st[4], 1), 2)}
             out["cpu_baseline"] = {k: v for k, v in cpu.items() if not k.startswith("_")}
             out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 4)
-        else:
-            V = None
         if kstats:
-            dom = max(kstats, key=lambda k: kstats[k]["ms"])
-            ks = kstats[dom]
-            avg_ms = ks["ms"] / max(ks["launches"], 1)
-            items_per_launch = ks["items"] / max(ks["launches"], 1)
             out["kernels"] = {k: {"avg_ms": round(v["ms"] / max(v["launches"], 1), 4), "launches": v["launches"],
                                   "items_per_launch": round(v["items"] / max(v["launches"], 1), 1)}
                               for k, v in kstats.items()}
-            alg = None
-            fpl = args.steps / max(ks["launches"], 1)   # frames per launch (mcrt_render_frames batches)
-            if V is not None and dom == "k_shadow_extend":
-                # one launch = the extension rays for bounce 1 + the shadow rays of bounce 0, of fpl frames
-                alg = fpl * (qcounts[1][0] * per_query_bytes("k_extend", V["k_extend"])
-                             + qcounts[0][0] * per_query_bytes("k_shadow", V["k_shadow"]))
-            elif V is not None and dom in V:
-                alg = items_per_launch * per_query_bytes(dom, V[dom])
-            if alg is not None:
-                achieved = alg / (avg_ms * 1e-3) / 1e9
-                tr = pmc_traffic(dom)
-                out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                                   "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                                   "traffic": tr, "alg_bytes_per_launch": round(alg),
-                                   "avg_launch_ms": round(avg_ms, 4)}
-                try:   # attainable HBM bandwidth of an in-repo stream copy
-                    att = ctx.stream_copy_gbps(2 << 30, 5)
-                    out["roofline"]["attainable"] = round(att, 1)
-                    out["roofline"]["frac_of_attainable"] = round(achieved / att, 4)
-                except Exception as e:   # noqa: BLE001 -- reported, not fatal
-                    log(f"[bench] stream copy failed: {e}")
+            out["kernels_note"] = ("HIP-event durations from an untimed pass after the timed region: one frame slot "
+                                   f"(no overlap with another frame's launches), {batch} frames per launch")
+            dom = max(kstats, key=lambda k: kstats[k]["ms"])
+            if oracle_ok and dom == "k_shadow_extend" and not args.no_roofline_model:
+                avg_ms = kstats[dom]["ms"] / max(kstats[dom]["launches"], 1)
+                out["roofline"] = roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx,
+                                                         cpu["_oracle"] if cpu else None)
         print(json.dumps(out), flush=True)
     fb.close()
     ds.close()

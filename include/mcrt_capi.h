@@ -359,7 +359,11 @@ MCRT_API mcrt_status mcrt_render_frames(mcrt_scene scene, mcrt_framebuffer fb, c
  * props of RTReconstructionPass) or 1 shared by all; frame_index = the batch's first frame. */
 MCRT_API mcrt_status mcrt_accumulate_frames(mcrt_framebuffer fb, const mcrt_filter* filters, int32_t count,
                                             int32_t frame_index);
-/* Device pointers of the frame buffer's arrays (float4 x W*H, float x W*H). */
+/* Device pointers of the frame buffer's arrays (float4 x W*H, float x W*H).  The radiance
+ * pointer is the plane of the LAST rendered frame: frames rotate through the frame slots
+ * (mcrt_framebuffer_set_frames_in_flight), so it is valid only until the next render call on this
+ * frame buffer, and work on another stream must first synchronise with the frame (e.g.
+ * mcrt_ctx_synchronize).  The accumulator and image pointers are fixed for the frame buffer's life. */
 MCRT_API mcrt_status mcrt_framebuffer_device_ptrs(mcrt_framebuffer fb, void** radiance, void** weighted_sum,
                                                   void** weight_sum, void** image);
 /* Post-process of the accumulated image, the passes after RTReconstructionPass in the
@@ -391,7 +395,8 @@ MCRT_API mcrt_status mcrt_render_aov(mcrt_scene scene, mcrt_framebuffer fb, cons
 MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float* host_rgba);
 /* Device-to-device copy of one frame-buffer array into caller memory (e.g. a torch/RCCL
  * buffer for the multi-GPU reduce): which 0 radiance (float4), 1 weighted sum (float4),
- * 2 image (float4), 3 weight sum (float).  Enqueued on the context stream. */
+ * 2 image (float4), 3 weight sum (float).  Enqueued on the context stream, ordered after the
+ * last render; the radiance copy keeps that frame's slot from taking a new frame until read. */
 MCRT_API mcrt_status mcrt_framebuffer_copy_device(mcrt_framebuffer fb, int which, void* d_dst);
 /* Inverse for multi-GPU: overwrite the weighted sums (float4) and weights (float) from device
  * memory (after a reduce) and recompute the image = sum / weight on the device. */
@@ -423,15 +428,33 @@ MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, 
 /* ------------------------------------------------------------------------ */
 /* Host helpers                                                              */
 /* ------------------------------------------------------------------------ */
-/* RTPrimaryRaysPass::generatePrimaryRays + RTUtil::screenToRay + Camera::screenToNDC
- * (APP/.../RTPrimaryRaysPass.cpp:81-104, APP/raytracing/util/RTUtil.cpp:9-41,
- * source/engine/camera/Camera.cpp:139-145) for a perspective camera with a
- * glm-style left-handed view (x right, y up, z forward).  pixel_offset is
- * the TAA jitter in pixels (PathTracingApp.cpp:208-215). */
+/* The reference host's RTPinholeCamera (kernel_data.h:246-264), bit for bit: CameraComponent
+ * (source/engine/camera/CameraComponent.cpp:61-134: glm::perspective -- left-handed, the vendored
+ * glm forces GLM_FORCE_LEFT_HANDED -- and the view matrix from the transform's rotation columns
+ * right / up / look), RTUtil::screenToRay for the four image corners at the near plane
+ * (APP/raytracing/util/RTUtil.cpp:9-41, RTPrimaryRaysPass.cpp:81-104) with pixel_offset = the
+ * TAA jitter in pixels (GI.filterSettings.curPixelOffset), worldToClip = viewProj (row major) and
+ * the z = 1 image-plane area of RTBDPTPass.cpp:158-166.  fov_y is the value the reference hands to
+ * glm::perspective, i.e. RADIANS (note: PathTracingApp.cpp:387 passes 45.0f, so the reference
+ * app's vertical field of view is 45 rad mod pi ~ 58.3 degrees).  float32 in glm's operation
+ * order (mcrt_camera.cpp), pinned against the reference's own glm (tests/test_camera_cpu.py). */
+MCRT_API mcrt_status mcrt_make_pinhole_camera_axes(const float pos[3], const float right[3], const float up[3],
+                                                   const float look[3], float fov_y, float near_z, float far_z,
+                                                   uint32_t width, uint32_t height, const float pixel_offset[2],
+                                                   mcrt_camera* out);
+/* Convenience form: a look-at camera (Camera::lookAt, source/engine/camera/Camera.cpp:58-63, with
+ * forward = target - position) and the field of view in DEGREES (glm::radians); otherwise
+ * mcrt_make_pinhole_camera_axes. */
 MCRT_API mcrt_status mcrt_make_pinhole_camera(const float pos[3], const float forward[3], const float up[3],
                                               float fov_y_deg, float near_z, float far_z,
                                               uint32_t width, uint32_t height,
                                               const float pixel_offset[2], mcrt_camera* out);
+/* TAA jitter of frame `frame` (PathTracingApp.cpp:208-215): pixel offset =
+ * (lerp(-rx, rx, sobol(frame, 0)), lerp(-ry, ry, sobol(frame, 1))), Sampler::sobolSample with
+ * scramble 0 over the 1024 x 52 g_SobolMatrices32 (the scene's sobol_matrices); radius = the
+ * reconstruction filter radius (GI.filterSettings.radius). */
+MCRT_API mcrt_status mcrt_taa_pixel_offset(const uint32_t* sobol_matrices, uint32_t frame, float radius_x,
+                                           float radius_y, float out[2]);
 /* Library version / build string. */
 MCRT_API const char* mcrt_version(void);
 

@@ -51,11 +51,13 @@ struct mcrt_ctx_s {
     bool fuseShadowExtend = true;   // MCRT_NO_FUSE=1 launches k_shadow and k_extend separately (A/B)
     bool sortRays = false;          // MCRT_SORT_RAYS=1: global sort of the extension queue (mcrt_raysort.hip)
     int envFramesInFlight = 0;      // MCRT_FRAMES_IN_FLIGHT=n overrides the frame buffers' setting (A/B)
+    int* dFlags = nullptr;          // device flags: [0] traversal-stack overflow (mcrt_traverse.h), set by any launch
     std::string error;
     struct Pending {
         int kernel;
         hipEvent_t a, b;
         const int* countDev;   // device counter holding the item count (or nullptr)
+        const int* countDev2;  // a second counter added to it (fused launches), or nullptr
         int64_t items;
     };
     std::vector<Pending> pending;
@@ -99,7 +101,7 @@ struct mcrt_scene_s {
     uint32_t* dSpill = nullptr;
     int spillCap = 0;
     size_t spillRays = 0;           // rays the spill buffer covers (spillCap words each)
-    int* dScratch = nullptr;   // [0] overflow flag, [1..] work counters for API queries
+    int* dScratch = nullptr;   // work counters for API queries
     float bbLo[3] = {0, 0, 0}, bbHi[3] = {0, 0, 0};   // world bounds (root record of the BVH)
 };
 
@@ -158,6 +160,7 @@ struct mcrt_framebuffer_s {
     float4 *sortO = nullptr, *sortD = nullptr, *sortT = nullptr;   // sorted extension queue (MCRT_SORT_RAYS)
     void* sortScratch = nullptr;
     size_t sortTemp = 0;
+    size_t sortCap = 0;          // entries of the sort buffers (= the slot's queueCap when allocated)
     float4* display = nullptr;   // post-processed image (mcrt_postprocess)
     float4* hitsP = nullptr;     // primary hits by pixel
     float4* hitsE = nullptr;     // extension hits by queue slot
@@ -182,6 +185,7 @@ struct mcrt_framebuffer_s {
     float4 *bqO[2] = {}, *bqD[2] = {}, *bqT[2] = {}, *bHits = nullptr;
     float4 *cO = nullptr, *cD = nullptr, *cL = nullptr;   // connection queue
     int lastIntegrator = MCRT_INTEGRATOR_PT;
+    bool bdptOneSet = false;     // a second BDPT set did not fit in HBM: BDPT frames use slot 0 only
 };
 
 static int bdpt_max_connections(int D) { const int t = D + 2; return t * (t + 1) / 2 - 2; }   // RTBDPTPass.cpp:404-408
@@ -218,8 +222,11 @@ struct Timed {
     const int* countDev;
     int64_t items;
     hipStream_t st;
-    Timed(mcrt_ctx ctx, int kernel, const int* countDev_, int64_t items_, hipStream_t stream = nullptr)
-        : c(ctx), k(kernel), countDev(countDev_), items(items_), st(stream ? stream : ctx->stream) {
+    const int* countDev2;
+    Timed(mcrt_ctx ctx, int kernel, const int* countDev_, int64_t items_, hipStream_t stream = nullptr,
+          const int* countDev2_ = nullptr)
+        : c(ctx), k(kernel), countDev(countDev_), items(items_), st(stream ? stream : ctx->stream),
+          countDev2(countDev2_) {
         if (c->profiling) {
             hipEventCreate(&a);
             hipEventCreate(&b);
@@ -229,7 +236,7 @@ struct Timed {
     ~Timed() {
         if (c->profiling) {
             hipEventRecord(b, st);
-            c->pending.push_back({k, a, b, countDev, items});
+            c->pending.push_back({k, a, b, countDev, countDev2, items});
         }
     }
 };
@@ -244,9 +251,10 @@ static void drain_pending(mcrt_ctx ctx) {
         ctx->launches[p.kernel] += 1;
         int64_t it = p.items;
         if (p.countDev) {
-            int v = 0;
+            int v = 0, v2 = 0;
             hipMemcpy(&v, p.countDev, sizeof(int), hipMemcpyDeviceToHost);
-            it = v;
+            if (p.countDev2) hipMemcpy(&v2, p.countDev2, sizeof(int), hipMemcpyDeviceToHost);
+            it = (int64_t)v + v2;
         }
         ctx->items[p.kernel] += it;
         hipEventDestroy(p.a);
@@ -311,7 +319,7 @@ static TraceCtx trace_ctx(mcrt_scene s) {
     c.nodes = (const float4*)s->dNodes;
     c.spill = s->dSpill;
     c.spillCap = s->spillCap;
-    c.overflow = s->dScratch;
+    c.overflow = s->ctx->dFlags;
     c.twoLevel = s->twoLevel ? 1 : 0;
     return c;
 }
@@ -362,7 +370,27 @@ MCRT_API mcrt_status mcrt_ctx_create(int device, mcrt_ctx* out) {
         return fail(nullptr, MCRT_ERROR_DEVICE, "hipStreamCreate failed");
     }
     c->stream = c->own;
+    if (hipMalloc(&c->dFlags, 64 * sizeof(int)) != hipSuccess || hipMemset(c->dFlags, 0, 64 * sizeof(int)) != hipSuccess) {
+        hipStreamDestroy(c->own);
+        delete c;
+        return fail(nullptr, MCRT_ERROR_OUT_OF_MEMORY, "device flags");
+    }
     *out = c;
+    return MCRT_OK;
+}
+
+// Device-side error flags raised by kernels since the last check (call after a synchronisation):
+// a traversal whose stack needed more entries than its spill column holds drops entries
+// (mcrt_traverse.h), so its hits may be wrong -- reported, never silent.
+static mcrt_status check_device_flags(mcrt_ctx ctx) {
+    int f = 0;
+    HIPCHK(ctx, hipMemcpy(&f, ctx->dFlags, sizeof(int), hipMemcpyDeviceToHost));
+    if (f != 0) {
+        HIPCHK(ctx, hipMemset(ctx->dFlags, 0, sizeof(int)));
+        return fail(ctx, MCRT_ERROR_DEVICE,
+                    "traversal stack overflow: a ray needed more stack entries than its spill column holds "
+                    "(results of the affected launches are unreliable)");
+    }
     return MCRT_OK;
 }
 
@@ -372,6 +400,7 @@ MCRT_API mcrt_status mcrt_ctx_destroy(mcrt_ctx ctx) {
     drain_pending(ctx);
     hipStreamSynchronize(ctx->stream);
     hipStreamDestroy(ctx->own);
+    if (ctx->dFlags) hipFree(ctx->dFlags);
     delete ctx;
     return MCRT_OK;
 }
@@ -381,7 +410,7 @@ MCRT_API mcrt_status mcrt_ctx_synchronize(mcrt_ctx ctx) {
     hipSetDevice(ctx->device);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipDeviceSynchronize());   // frame-slot streams of the context's frame buffers
-    return MCRT_OK;
+    return check_device_flags(ctx);
 }
 
 MCRT_API mcrt_status mcrt_ctx_set_stream(mcrt_ctx ctx, void* stream) {
@@ -731,7 +760,10 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
     mcrt_ctx ctx = s->ctx;
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
-    const int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries
+    int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries
+    // test hook: MCRT_TEST_SPILL_CAP=k caps the spill columns at k entries (0 = LDS stack only) so a
+    // test can drive a traversal past its capacity and check that the overflow is reported
+    if (const char* tc = std::getenv("MCRT_TEST_SPILL_CAP")) needCap = std::max(0, std::atoi(tc) / 16 * 16);
     if (needCap != s->spillCap) {
         if (s->dSpill) hipFree(s->dSpill);
         s->dSpill = nullptr;
@@ -1243,14 +1275,27 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     hipSetDevice(ctx->device);
     f.batch = count;
     // frame slot: its buffers are free once the accumulation of its previous frame has read them
-    const int S = frames_in_flight(fb, f);
-    const int ks = fb->next % S;
+    const bool bdpt = p->integrator == MCRT_INTEGRATOR_BDPT;
+    const int S = bdpt && fb->bdptOneSet ? 1 : frames_in_flight(fb, f);
+    int ks = fb->next % S;
+    if (bdpt && ks != 0 && fb->bdptDepth == p->max_depth && !fb->bset[ks].camV) {
+        // each BDPT set holds ~C x N x 48 B of connection rays (2.5 GB at 1080p, D = 2): when a
+        // second one does not fit, fall back to one frame in flight instead of failing the frame
+        const hipError_t e = bset_alloc(fb->bset[ks], fb->N, p->max_depth);
+        if (e == hipErrorOutOfMemory) {
+            hipGetLastError();
+            fb->bdptOneSet = true;
+            ks = 0;
+        } else if (e != hipSuccess) {
+            return fail(ctx, MCRT_ERROR_DEVICE, std::string("BDPT buffers: ") + hipGetErrorString(e));
+        }
+    }
     FrameSlot& slot = fb->slot[ks];
-    if (p->integrator == MCRT_INTEGRATOR_BDPT) {   // BDPT frames overlap the same way (set ks)
+    if (bdpt) {   // BDPT frames overlap the same way (set ks)
         if (!slot.stream) HIPCHK(ctx, slot_alloc(slot, fb->N));
         HIPCHK(ctx, hipStreamWaitEvent(slot.stream, slot.free, 0));
         fb_bind(fb, ks);
-        fb->next = (ks + 1) % S;
+        fb->next = (ks + 1) % (fb->bdptOneSet ? 1 : S);
         slot.lastBatch = 1;
         const mcrt_status r = render_bdpt(s, fb, cam, p, f, ks, slot.stream);
         slot.lastMaxDepth = fb->lastMaxDepth;
@@ -1295,7 +1340,8 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     const SceneArgs sa = scene_args(s);
     fb->lastIntegrator = MCRT_INTEGRATOR_PT;
     if (s->numLights == 0) {   // RTPathTracingPass.cpp:42: no lights -> pass skipped; radiance = 0 here
-        HIPCHK(ctx, hipMemsetAsync(fb->radiance, 0, 16 * fb->N, st));
+        // every frame plane of the batch: accumulate reads `count` of them
+        HIPCHK(ctx, hipMemsetAsync(fb->radiance, 0, 16 * fb->N * (size_t)count, st));
         HIPCHK(ctx, hipEventRecord(slot.done, st));
         return MCRT_OK;
     }
@@ -1326,18 +1372,29 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
                                 fb->eT[(b - 1) & 1], fb->hitsE, fb->radiance, q, qCap, st);
         }
         if (ctx->sortRays && b + 1 < p->max_depth) {   // reorder the extension queue of bounce b
-            if (!fb->sortO) {
-                fb->sortTemp = mcrt::ray_sort_temp_bytes((int)fb->N);
-                HIPCHK(ctx, hipMalloc(&fb->sortO, 16 * fb->N));
-                HIPCHK(ctx, hipMalloc(&fb->sortD, 16 * fb->N));
-                HIPCHK(ctx, hipMalloc(&fb->sortT, 16 * fb->N));
-                HIPCHK(ctx, hipMalloc(&fb->sortScratch, 16 * fb->N + fb->sortTemp));
+            // the queue holds up to the batch's paths (slot.queueCap >= count x band paths): the
+            // sort buffers, which are swapped into the slot's queue, must have the same capacity
+            if (fb->sortCap < slot.queueCap) {
+                HIPCHK(ctx, hipStreamSynchronize(st));
+                void* old[] = {fb->sortO, fb->sortD, fb->sortT, fb->sortScratch};
+                for (void* q : old)
+                    if (q) hipFree(q);
+                fb->sortO = fb->sortD = fb->sortT = nullptr;
+                fb->sortScratch = nullptr;
+                fb->sortCap = 0;
+                const size_t cap = slot.queueCap;
+                fb->sortTemp = mcrt::ray_sort_temp_bytes((int)cap);
+                HIPCHK(ctx, hipMalloc(&fb->sortO, 16 * cap));
+                HIPCHK(ctx, hipMalloc(&fb->sortD, 16 * cap));
+                HIPCHK(ctx, hipMalloc(&fb->sortT, 16 * cap));
+                HIPCHK(ctx, hipMalloc(&fb->sortScratch, 16 * cap + fb->sortTemp));
+                fb->sortCap = cap;
             }
             const float3 lo = make_float3(s->bbLo[0], s->bbLo[1], s->bbLo[2]);
             const float3 hi = make_float3(s->bbHi[0], s->bbHi[1], s->bbHi[2]);
             HIPCHK(ctx, mcrt::sort_ray_queue(extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->eT[b & 1], fb->sortO,
-                                             fb->sortD, fb->sortT, (int)fb->N, lo, hi, fb->sortScratch, fb->sortTemp,
-                                             st));
+                                             fb->sortD, fb->sortT, (int)slot.queueCap, lo, hi, fb->sortScratch,
+                                             fb->sortTemp, st));
             std::swap(slot.eO[b & 1], fb->sortO);
             std::swap(slot.eD[b & 1], fb->sortD);
             std::swap(slot.eT[b & 1], fb->sortT);
@@ -1345,7 +1402,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
         }
         if (ctx->fuseShadowExtend && b + 1 < p->max_depth) {
             // shadow rays of bounce b + extension rays for bounce b+1 (both from this shading pass)
-            Timed t(ctx, K_SHADOW_EXTEND, nullptr, 0, st);
+            Timed t(ctx, K_SHADOW_EXTEND, extCnt + b, 0, st, shadowCnt + b);   // items: extension + shadow rays
             mcrt::launch_shadow_extend(tcs, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b, fb->sO,
                                        fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
@@ -1483,7 +1540,7 @@ MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float
                       : which == 2 ? (const void*)fb->image : (const void*)fb->display;
     HIPCHK(ctx, fb_sync(fb));
     HIPCHK(ctx, hipMemcpy(host_rgba, src, 16 * fb->N, hipMemcpyDeviceToHost));
-    return MCRT_OK;
+    return check_device_flags(ctx);
 }
 
 MCRT_API mcrt_status mcrt_framebuffer_copy_device(mcrt_framebuffer fb, int which, void* d_dst) {
@@ -1494,6 +1551,8 @@ MCRT_API mcrt_status mcrt_framebuffer_copy_device(mcrt_framebuffer fb, int which
                       : which == 2 ? (const void*)fb->image : (const void*)fb->wts;
     if (which == 0) ctx_wait_slots(fb);
     HIPCHK(ctx, hipMemcpyAsync(d_dst, src, (which == 3 ? 4 : 16) * fb->N, hipMemcpyDeviceToDevice, ctx->stream));
+    // the slot may take its next frame only after this copy has read its radiance
+    if (which == 0) HIPCHK(ctx, hipEventRecord(fb->slot[fb->cur].free, ctx->stream));
     return MCRT_OK;
 }
 
@@ -1602,81 +1661,6 @@ MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, 
     return MCRT_OK;
 }
 
-// ---------------------------------------------------------------------------
-// host camera helper (RTPrimaryRaysPass::generatePrimaryRays + RTUtil::screenToRay)
-// ---------------------------------------------------------------------------
-MCRT_API mcrt_status mcrt_make_pinhole_camera(const float pos[3], const float forward[3], const float up[3],
-                                              float fov_y_deg, float near_z, float far_z, uint32_t width,
-                                              uint32_t height, const float pixel_offset[2], mcrt_camera* out) {
-    if (!pos || !forward || !up || !out || width == 0 || height == 0 || !(far_z > near_z))
-        return fail(nullptr, MCRT_ERROR_INVALID_ARG, "invalid camera");
-    double f[3] = {forward[0], forward[1], forward[2]};
-    double fl = std::sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
-    for (double& x : f) x /= fl;
-    double u0[3] = {up[0], up[1], up[2]};
-    double s[3] = {u0[1] * f[2] - u0[2] * f[1], u0[2] * f[0] - u0[0] * f[2], u0[0] * f[1] - u0[1] * f[0]};
-    double sl = std::sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
-    for (double& x : s) x /= sl;
-    double u[3] = {f[1] * s[2] - f[2] * s[1], f[2] * s[0] - f[0] * s[2], f[0] * s[1] - f[1] * s[0]};
-    double V[4][4] = {{s[0], s[1], s[2], -(s[0] * pos[0] + s[1] * pos[1] + s[2] * pos[2])},
-                      {u[0], u[1], u[2], -(u[0] * pos[0] + u[1] * pos[1] + u[2] * pos[2])},
-                      {f[0], f[1], f[2], -(f[0] * pos[0] + f[1] * pos[1] + f[2] * pos[2])},
-                      {0, 0, 0, 1}};
-    const double t = std::tan(fov_y_deg * 3.14159265358979323846 / 360.0), aspect = (double)width / height;
-    double P[4][4] = {{1.0 / (aspect * t), 0, 0, 0}, {0, 1.0 / t, 0, 0},
-                      {0, 0, (far_z + near_z) / (far_z - near_z), -(2.0 * far_z * near_z) / (far_z - near_z)},
-                      {0, 0, 1, 0}};
-    double VP[4][4], M[4][4];
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) {
-            VP[i][j] = 0;
-            for (int k = 0; k < 4; ++k) VP[i][j] += P[i][k] * V[k][j];
-        }
-    const double ox = pixel_offset ? pixel_offset[0] / width : 0.0, oy = pixel_offset ? pixel_offset[1] / height : 0.0;
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) M[i][j] = VP[i][j] + (i == 0 ? ox * VP[3][j] : i == 1 ? oy * VP[3][j] : 0.0);
-    // invert M (Gauss-Jordan)
-    double A[4][8];
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 8; ++j) A[i][j] = j < 4 ? M[i][j] : (j - 4 == i ? 1.0 : 0.0);
-    for (int c = 0; c < 4; ++c) {
-        int pr = c;
-        for (int r = c + 1; r < 4; ++r)
-            if (std::fabs(A[r][c]) > std::fabs(A[pr][c])) pr = r;
-        for (int j = 0; j < 8; ++j) std::swap(A[c][j], A[pr][j]);
-        const double d = A[c][c];
-        if (d == 0.0) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "singular camera matrix");
-        for (int j = 0; j < 8; ++j) A[c][j] /= d;
-        for (int r = 0; r < 4; ++r)
-            if (r != c) {
-                const double m = A[r][c];
-                for (int j = 0; j < 8; ++j) A[r][j] -= m * A[c][j];
-            }
-    }
-    auto ray = [&](double sx, double sy, mcrt_float4& o) {
-        const double nx = sx / width * 2.0 - 1.0, ny = sy / height * 2.0 - 1.0;
-        double a[4] = {nx, ny, -1.0, 1.0}, b[4] = {nx, ny, 1.0, 1.0}, ra[4] = {}, rb[4] = {};
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) { ra[i] += A[i][4 + j] * a[j]; rb[i] += A[i][4 + j] * b[j]; }
-        double d[3];
-        for (int i = 0; i < 3; ++i) d[i] = rb[i] / rb[3] - ra[i] / ra[3];
-        const double l = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-        o.x = (float)(d[0] / l); o.y = (float)(d[1] / l); o.z = (float)(d[2] / l); o.w = 0.0f;
-    };
-    std::memset(out, 0, sizeof(*out));
-    float* wc = &out->worldToClip.m0.x;
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) wc[4 * i + j] = (float)VP[i][j];
-    ray(0, 0, out->r00);
-    ray(width, 0, out->r10);
-    ray(width, height, out->r11);
-    ray(0, height, out->r01);
-    out->pos.x = pos[0]; out->pos.y = pos[1]; out->pos.z = pos[2];
-    out->direction.x = (float)f[0]; out->direction.y = (float)f[1]; out->direction.z = (float)f[2];
-    out->width = width;
-    out->height = height;
-    out->area = (float)((2.0 * t * aspect) * (2.0 * t));
-    return MCRT_OK;
-}
+// host camera helpers: mcrt_camera.cpp
 
 }  // extern "C"

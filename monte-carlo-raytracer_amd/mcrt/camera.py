@@ -87,9 +87,11 @@ def sobol_1d(idx, dim, mats, scramble=0):
 
 
 def taa_jitter(frame, radius=(2.0, 2.0), mats=None):
-    """PathTracingApp.cpp:208-215: lerp(-r, r, sobol(frame, dim 0/1, scramble 0))."""
+    """PathTracingApp.cpp:208-215: lerp(-r, r, sobol(frame, dim 0/1, scramble 0)); mats defaults to
+    the Sobol matrices shipped with the package (g_SobolMatrices32)."""
     if mats is None:
-        return (0.0, 0.0)
+        from . import sobol_matrices
+        mats = sobol_matrices()
     u = sobol_1d(frame, 0, mats)
     v = sobol_1d(frame, 1, mats)
     return (-radius[0] + (2 * radius[0]) * float(u), -radius[1] + (2 * radius[1]) * float(v))

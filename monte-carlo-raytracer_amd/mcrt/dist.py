@@ -48,11 +48,14 @@ def frame_split(num_frames, world, rank):
     return np.arange(rank, num_frames, world, dtype=np.int64)
 
 
-def packed_accumulators(num_pixels, device):
+def packed_accumulators(num_pixels, device, base=None):
     """One contiguous float32 buffer holding sum(w*L) (4 per pixel) then sum(w) (1 per pixel), so
-    the end-of-job reduction is a single collective; returns (buf, wsum view, wts view)."""
+    the end-of-job reduction is a single collective; returns (buf, wsum view, wts view).
+    base: an existing packed buffer to view instead of a new one (e.g. the reduced sum)."""
     import torch
-    buf = torch.empty(num_pixels * 5, dtype=torch.float32, device=device)
+    buf = torch.empty(num_pixels * 5, dtype=torch.float32, device=device) if base is None else base
+    if buf.numel() != num_pixels * 5:
+        raise ValueError("packed accumulator buffer has the wrong size")
     return buf, buf[:num_pixels * 4], buf[num_pixels * 4:]
 
 

@@ -63,6 +63,9 @@ SIGNATURES = {
     "mcrt_framebuffer_read_bdpt": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64)]),
     "mcrt_make_pinhole_camera": (_c.c_int, [_vp, _vp, _vp, _c.c_float, _c.c_float, _c.c_float, _c.c_uint32,
                                             _c.c_uint32, _vp, _vp]),
+    "mcrt_make_pinhole_camera_axes": (_c.c_int, [_vp, _vp, _vp, _vp, _c.c_float, _c.c_float, _c.c_float,
+                                                 _c.c_uint32, _c.c_uint32, _vp, _vp]),
+    "mcrt_taa_pixel_offset": (_c.c_int, [_vp, _c.c_uint32, _c.c_float, _c.c_float, _vp]),
 }
 
 
@@ -364,6 +367,23 @@ def make_pinhole_camera(pos, forward, up, fovy, near, far, width, height, pixel_
     _check(lib().mcrt_make_pinhole_camera(_p(a[0]), _p(a[1]), _p(a[2]), fovy, near, far, width, height, _p(a[3]),
                                           _p(cam)))
     return cam
+
+
+def make_pinhole_camera_axes(pos, right, up, look, fovy_rad, near, far, width, height, pixel_offset=(0.0, 0.0)):
+    """mcrt_make_pinhole_camera_axes: the reference host's RTPinholeCamera, bit for bit."""
+    cam = np.zeros(1, T.CAMERA_DTYPE)
+    a = [np.asarray(v, np.float32) for v in (pos, right, up, look, pixel_offset)]
+    _check(lib().mcrt_make_pinhole_camera_axes(_p(a[0]), _p(a[1]), _p(a[2]), _p(a[3]), fovy_rad, near, far, width,
+                                               height, _p(a[4]), _p(cam)))
+    return cam
+
+
+def taa_pixel_offset(sobol_matrices, frame, radius=(2.0, 2.0)):
+    """mcrt_taa_pixel_offset: the reference's per-frame TAA jitter in pixels."""
+    m = np.ascontiguousarray(sobol_matrices, np.uint32)
+    out = np.zeros(2, np.float32)
+    _check(lib().mcrt_taa_pixel_offset(_p(m), frame, radius[0], radius[1], _p(out)))
+    return out
 
 
 def header_symbols():

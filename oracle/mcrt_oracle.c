@@ -643,7 +643,15 @@ struct orc_scene {
     int32_t* tri_shape;
     int32_t* tri_prim;
     int64_t num_tris;
+    /* optional per-node "touched" marks for the bench's compulsory-traffic roofline (bench.py):
+     * [class][node] bytes, class 0 = camera rays, 1 = extension rays, 2 = shadow rays of bounce 0,
+     * 3 = shadow rays of later bounces (k_shadow_extend traces classes 1 + 2 together) */
+    uint8_t* touched;
 };
+
+static inline void markTouched(uint8_t* mark, uint32_t node) {
+    if (mark) __atomic_store_n(&mark[node], (uint8_t)1, __ATOMIC_RELAXED);   /* idempotent; races benign */
+}
 
 /* RR transform_point (RR/include/math/mathutils.h:111-118 with matrix*float4,
  * RR/include/math/matrix.h:182-193): sequential sum, w = 0, then + translation. */
@@ -1062,7 +1070,8 @@ static inline void triBarycentrics(v3 p, const float* v1, const float* v2, const
 typedef struct { uint32_t* data; int cap; } Stack;
 
 /* intersect_bvh2_lds.cl:66-226 (the LDS short stack + global spill is one LIFO) */
-static int traceClosest(const orc_scene* s, const Ray* r, mcrt_intersection* hit, uint32_t* stack, int* visits) {
+static int traceClosest(const orc_scene* s, const Ray* r, mcrt_intersection* hit, uint32_t* stack, int* visits,
+                        uint8_t* mark) {
     const RRNode* nodes = s->nodes;
     v3 inv = safe_invdir(r->d);
     v3 oxinv = V3(-r->o.x * inv.x, -r->o.y * inv.y, -r->o.z * inv.z);
@@ -1073,6 +1082,7 @@ static int traceClosest(const orc_scene* s, const Ray* r, mcrt_intersection* hit
     while (addr != INVALID_ADDR) {
         const RRNode* node = &nodes[addr];
         ++nv;
+        markTouched(mark, addr);
         if (node->addr_left != INVALID_ADDR) {
             float a0, a1, b0, b1;
             bbox2(node->lmin_v0, node->lmax_v1, inv, oxinv, closest_t, &a0, &a1);
@@ -1110,7 +1120,7 @@ static int traceClosest(const orc_scene* s, const Ray* r, mcrt_intersection* hit
     return 0;
 }
 /* intersect_bvh2_lds.cl:229-363 */
-static int traceAny(const orc_scene* s, const Ray* r, uint32_t* stack, int* visits) {
+static int traceAny(const orc_scene* s, const Ray* r, uint32_t* stack, int* visits, uint8_t* mark) {
     const RRNode* nodes = s->nodes;
     v3 inv = safe_invdir(r->d);
     v3 oxinv = V3(-r->o.x * inv.x, -r->o.y * inv.y, -r->o.z * inv.z);
@@ -1121,6 +1131,7 @@ static int traceAny(const orc_scene* s, const Ray* r, uint32_t* stack, int* visi
     while (addr != INVALID_ADDR) {
         const RRNode* node = &nodes[addr];
         ++nv;
+        markTouched(mark, addr);
         if (node->addr_left != INVALID_ADDR) {
             float a0, a1, b0, b1;
             bbox2(node->lmin_v0, node->lmax_v1, inv, oxinv, closest_t, &a0, &a1);
@@ -1180,7 +1191,7 @@ static void closest_one(void* c, int64_t i, uint32_t* stack) {
     Ray r = loadRay(&t->rays[i]);
     if (!r.active) { if (t->visits) t->visits[i] = 0; return; }   /* record untouched (Q12) */
     int nv = 0;
-    traceClosest(t->s, &r, &t->hits[i], stack, &nv);
+    traceClosest(t->s, &r, &t->hits[i], stack, &nv, NULL);
     if (t->visits) t->visits[i] = nv;
 }
 static void any_one(void* c, int64_t i, uint32_t* stack) {
@@ -1188,7 +1199,7 @@ static void any_one(void* c, int64_t i, uint32_t* stack) {
     Ray r = loadRay(&t->rays[i]);
     if (!r.active) { if (t->visits) t->visits[i] = 0; return; }
     int nv = 0;
-    t->ihits[i] = traceAny(t->s, &r, stack, &nv);
+    t->ihits[i] = traceAny(t->s, &r, stack, &nv, NULL);
     if (t->visits) t->visits[i] = nv;
 }
 void orc_trace_closest(orc_scene* s, const mcrt_ray* rays, int n, mcrt_intersection* hits, int32_t* visits, int threads) {
@@ -1486,7 +1497,9 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
     int nv = 0;
     int64_t nprim = 0, vprim = 0, nclosest = 0, nany = 0, vclosest = 0, vany = 0;
     /* RTPrimaryRaysPass: first closest hit */
-    traceClosest(s, &ray, &isect, stack, &nv);
+    uint8_t* const tch = s->touched;
+    const int64_t NN = s->num_nodes;
+    traceClosest(s, &ray, &isect, stack, &nv, tch);
     nprim++; vprim += nv;
     for (int b = 0; b < rc->maxDepth; ++b) {
         v3 temp = V3(0, 0, 0);
@@ -1566,7 +1579,7 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
         int occl = -1;
         if (shadowSet && shadow.active) {
             int anv = 0;
-            occl = traceAny(s, &shadow, stack, &anv);
+            occl = traceAny(s, &shadow, stack, &anv, tch ? tch + (b == 0 ? 2 : 3) * NN : NULL);
             nany++; vany += anv;
         }
         if (!ignoreOcclusion) {
@@ -1575,7 +1588,7 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
         }
         radianceAcc = (b == 0) ? temp : vadd(radianceAcc, temp);
         if (b + 1 < rc->maxDepth && ray.active) {
-            traceClosest(s, &ray, &isect, stack, &nv);
+            traceClosest(s, &ray, &isect, stack, &nv, tch ? tch + NN : NULL);
             nclosest++; vclosest += nv;
         }
     }
@@ -1627,6 +1640,10 @@ void orc_render_frame(orc_scene* s, const mcrt_camera* cam, int frame, int max_d
     }
     render_common(s, cam, frame, max_depth, sampler, NULL, y1 - y0, y0, threads, radiance, stats);
 }
+/* touched: NULL (off) or 4 x num_nodes bytes the renders mark (camera / extension / shadow of
+ * bounce 0 / later shadow rays) */
+void orc_set_touched(orc_scene* s, uint8_t* touched) { s->touched = touched; }
+
 void orc_render_rows(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,
                      const int32_t* rows, int nrows, int threads, float* radiance, int64_t* stats) {
     render_common(s, cam, frame, max_depth, sampler, rows, nrows, 0, threads, radiance, stats);

@@ -62,6 +62,8 @@ void orc_brute_any(orc_scene* s, const mcrt_ray* rays, int n, int32_t* hits);
 void orc_render_frame(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,
                       int y0, int y1, int threads, float* radiance, int64_t* stats);
 /* Same, but only every `stride`-th row starting at y0 (bounded CPU-baseline samples). */
+/* per-node touched marks of later renders: NULL or 4 x num_nodes bytes (bench.py roofline) */
+void orc_set_touched(orc_scene* s, uint8_t* touched);
 void orc_render_rows(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,
                      const int32_t* rows, int nrows, int threads, float* radiance, int64_t* stats);
 

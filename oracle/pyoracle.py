@@ -48,6 +48,7 @@ def lib():
         L.orc_brute_closest.argtypes = [_vp, _vp, _c.c_int, _vp]
         L.orc_brute_any.argtypes = [_vp, _vp, _c.c_int, _vp]
         L.orc_render_frame.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _vp, _vp]
+        L.orc_set_touched.argtypes = [_vp, _vp]
         L.orc_render_rows.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _c.c_int, _c.c_int, _vp, _vp]
         L.orc_accumulate.argtypes = [_c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp, _vp]
         L.orc_denoise.argtypes = [_c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float, _vp, _vp]
@@ -127,6 +128,18 @@ class OracleScene:
         stats = np.zeros(6, np.int64)
         lib().orc_render_frame(self.h, _p(cam), frame, max_depth, sampler, y0, y1, threads, _p(radiance), _p(stats))
         return radiance, stats
+
+    def track_touched(self, on=True):
+        """Marks every BVH node later renders visit, per query class (bench.py's compulsory-traffic
+        roofline): returns the (4, num_nodes) uint8 array -- rows camera, extension, shadow of
+        bounce 0, later shadow rays -- or None when switched off."""
+        if not on:
+            lib().orc_set_touched(self.h, None)
+            self._touched = None
+            return None
+        self._touched = np.zeros((4, self.num_nodes), np.uint8)
+        lib().orc_set_touched(self.h, _p(self._touched))
+        return self._touched
 
     def render_rows(self, cam, rows, frame=0, max_depth=2, sampler=1, threads=8, radiance=None):
         W, H = int(cam["width"][0]), int(cam["height"][0])

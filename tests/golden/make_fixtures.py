@@ -10,7 +10,8 @@ own C++ (oracle/_ref/librrref.so, built from /root/reference by oracle/refbuild)
                         radeon_rays_conformance_test_cl.h:160,552-556) + brute-force golden hits
                         from the reference's UnitTest/utils.cpp TestIntersections/TestOcclusions
   bunny.npz             assets/meshes/bunny.obj
-  sobol_1024x52.npy     the Joe-Kuo Sobol generator matrices uploaded as scene data
+  sobol_1024x52.npy     the Joe-Kuo Sobol generator matrices uploaded as scene data (written to
+                        monte-carlo-raytracer_amd/mcrt/data/, the product's package data)
                         (source/application/PathTracer/raytracing/sampling/sobol.h:34)
   rr_bvh_mixed.npz      node array of the reference Bvh2 (bvh2.cpp) over mcrt.scenes.test_scene()
 
@@ -105,7 +106,8 @@ def sobol():
     body = body[body.index("{") + 1: body.index("};")]
     vals = np.array([int(x, 16) for x in re.findall(r"0x[0-9A-Fa-f]+", body)], np.uint32)
     assert vals.size == 1024 * 52, vals.size
-    np.save(os.path.join(HERE, "sobol_1024x52.npy"), vals)
+    # package data: the product uploads it as scene input (scene_sobolMatrices), like the reference
+    np.save(os.path.join(HERE, "..", "..", "monte-carlo-raytracer_amd", "mcrt", "data", "sobol_1024x52.npy"), vals)
 
 
 def rr_conformance(n=10000):

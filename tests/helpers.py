@@ -30,7 +30,8 @@ def bunny_scene():
 
 
 def sobol():
-    return np.load(os.path.join(GOLDEN, "sobol_1024x52.npy"))
+    from mcrt import sobol_matrices
+    return sobol_matrices()
 
 
 def random_rays(scene, n, seed, tmax=1000.0, inside=True):

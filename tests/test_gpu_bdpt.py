@@ -133,3 +133,48 @@ def test_bdpt_matches_reference(hip_ctx, clref_bdpt, case):
     fb.close()
     ds.close()
     assert not bad, (bad, report)
+
+
+def test_bdpt_frames_in_flight(hip_ctx):
+    """BDPT frames overlapping in 2 and 4 frame slots (per-slot BDPT sets; the shared
+    sampled-light-vertex planes, which the s = 1 strategy reads from the PREVIOUS frame,
+    BDPT.cl:585-586, are kept in frame order by an event between the connect launches), with only
+    mcrt_accumulate between the frames and one read-back at the end, against one slot:
+      * the sampled-light planes after the last frame, both subpaths' vertex counts and the
+        camera vertices: bit-exact (no atomics involved);
+      * the last radiance and the accumulated image: within the splat tolerance (light-tracing
+        splats are float atomics, so their order varies from run to run even with one slot)."""
+    from mcrt import lib
+    name, W, H, D, frames = "mixed", 96, 64, 2, 7
+    ds = lib.DeviceScene(hip_ctx, build_scene(name))
+    cam = scene_camera(name, W, H)
+    filt = T.make_filter(T.BOX)
+    out = {}
+    for fif in (1, 2, 4):
+        fb = lib.FrameBuffer(hip_ctx, W, H)
+        fb.set_frames_in_flight(fif)
+        for f in range(frames):
+            fb.render(ds, cam, frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT)
+            fb.accumulate(filt, f)
+        out[fif] = {"rad": fb.read(0), "img": fb.read(2), "wts": fb.read(1),
+                    **{k: fb.read_bdpt(k) for k in ("sampled_light", "camera_counts", "light_counts",
+                                                    "camera_vertices")}}
+        fb.close()
+    ds.close()
+    ref = out[1]
+    assert ref["img"][..., :3].max() > 0
+    N = W * H
+    live = ref["camera_counts"].view(np.int32)[None, :] > np.arange(D + 2)[:, None]   # (depth, N)
+    for fif in (2, 4):
+        o = out[fif]
+        for k in ("sampled_light", "camera_counts", "light_counts"):
+            np.testing.assert_array_equal(o[k], ref[k], err_msg=f"fif={fif} {k}")
+        # vertices of the last frame (depths past a path's end keep older frames' data in each set)
+        a = our_planes(o["camera_vertices"], D + 2, N).view(np.uint32)[:, :8]
+        b = our_planes(ref["camera_vertices"], D + 2, N).view(np.uint32)[:, :8]
+        ne = (a != b).any(-1).any(1)   # (depth, N)
+        assert not (ne & live).any(), (fif, int((ne & live).sum()))
+        for k in ("rad", "img"):
+            a, b = o[k][..., :3], ref[k][..., :3]
+            close = np.abs(a - b) <= REL_TOL * (np.abs(a) + np.abs(b)) + 1e-30
+            assert close.all(), (fif, k, int((~close).sum()))

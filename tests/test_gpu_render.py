@@ -254,3 +254,113 @@ def test_batched_frames_bit_exact(hip_ctx, mixed, num_bands, band_index, count):
     fb.close()
     ref.close()
     ds.close()
+
+
+def test_sorted_rays_batched_frames_bit_exact(hip_ctx, mixed, monkeypatch):
+    """MCRT_SORT_RAYS=1 (global sort of each extension queue) with batched frames: the sort
+    buffers cover the batch's queue (count x N paths), and reordering the queue changes nothing
+    (each path only touches its own pixel, in launch order), so the accumulators and the
+    first-frame radiance equal the unsorted render bit for bit."""
+    from mcrt import lib
+    sc, _ = mixed
+    W, H, D, count = 96, 72, 3, 4
+    cams = [scene_camera("mixed", W, H, frame=f, jitter=True) for f in range(2 * count)]
+    filt = T.make_filter(T.BOX)
+    monkeypatch.setenv("MCRT_SORT_RAYS", "1")
+    sctx = lib.Context(0)
+    monkeypatch.delenv("MCRT_SORT_RAYS")
+    out = []
+    for ctx in (hip_ctx, sctx):
+        ds = lib.DeviceScene(ctx, sc)
+        fb = lib.FrameBuffer(ctx, W, H)
+        for f0 in (0, count):
+            fb.render_frames(ds, cams[f0:f0 + count], frame=f0, max_depth=D)
+            fb.accumulate(filt, f0)
+        out.append((fb.read(0), fb.read(1), fb.read(2), fb.stats()))
+        fb.close()
+        ds.close()
+    for k in range(3):
+        np.testing.assert_array_equal(out[1][k].view(np.uint32), out[0][k].view(np.uint32))
+    assert out[1][3] == out[0][3]
+    sctx.close()
+
+
+def test_batched_no_lights_after_lit_batch(hip_ctx, mixed):
+    """A batch rendered after the lights are removed accumulates zeros for EVERY frame of the
+    batch (not stale radiance of the slot's previous batch), exactly as single frames do."""
+    from mcrt import lib
+    sc, _ = mixed
+    W, H, D, count = 64, 48, 2, 4
+    cams = [scene_camera("mixed", W, H, frame=f, jitter=True) for f in range(2 * count)]
+    filt = T.make_filter(T.BOX)
+    ds = lib.DeviceScene(hip_ctx, sc)
+    single = lib.FrameBuffer(hip_ctx, W, H)
+    batch = lib.FrameBuffer(hip_ctx, W, H)
+    for f in range(count):
+        single.render(ds, cams[f], frame=f, max_depth=D)
+        single.accumulate(filt, f)
+    batch.render_frames(ds, cams[:count], frame=0, max_depth=D)
+    batch.accumulate(filt, 0)
+    lit = batch.read(1)
+    assert lit[..., :3].max() > 0
+    ds.update_lights(np.zeros(0, T.LIGHT_DTYPE))
+    for f in range(count, 2 * count):
+        single.render(ds, cams[f], frame=f, max_depth=D)
+        single.accumulate(filt, f)
+    batch.render_frames(ds, cams[count:], frame=count, max_depth=D)
+    batch.accumulate(filt, count)
+    for which in (1, 2):
+        np.testing.assert_array_equal(batch.read(which).view(np.uint32), single.read(which).view(np.uint32))
+    np.testing.assert_array_equal(batch.read(1)[..., :3], lit[..., :3])   # + 4 x zero radiance
+    single.close()
+    batch.close()
+    ds.close()
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_multi_gpu_reduce_through_product(hip_ctx, mixed, ranks):
+    """The multi-GPU path of bench.py, every rank emulated by its own frame buffer on this GPU:
+    each renders its 8-row band share of batched frames and accumulates them; the accumulators
+    leave through mcrt_framebuffer_copy_device into torch buffers (the RCCL reduce's input),
+    are summed as the reduce does (bands are disjoint, so every pixel is x + 0 + ... = x) and
+    installed with mcrt_framebuffer_set_accumulation on rank 0.  The accumulators and the image
+    must equal one frame buffer rendering the whole image, bit for bit."""
+    import torch
+    from mcrt import dist as mdist
+    from mcrt import lib
+    sc, _ = mixed
+    W, H, D, frames, batch = 96, 80, 3, 8, 4
+    cams = [scene_camera("mixed", W, H, frame=f, jitter=True) for f in range(frames)]
+    filt = T.make_filter(T.BOX)
+    ds = lib.DeviceScene(hip_ctx, sc)
+    full = lib.FrameBuffer(hip_ctx, W, H)
+    for f0 in range(0, frames, batch):
+        full.render_frames(ds, cams[f0:f0 + batch], frame=f0, max_depth=D)
+        full.accumulate(filt, f0)
+    want = (full.read(1), full.read(2))
+    bufs, fbs = [], []
+    for r in range(ranks):
+        fb = lib.FrameBuffer(hip_ctx, W, H)
+        for f0 in range(0, frames, batch):
+            fb.render_frames(ds, cams[f0:f0 + batch], frame=f0, max_depth=D, band_rows=8, num_bands=ranks,
+                             band_index=r)
+            fb.accumulate(filt, f0)
+        buf, s, w = mdist.packed_accumulators(W * H, "cuda")
+        fb.copy_device(1, s.data_ptr())
+        fb.copy_device(3, w.data_ptr())
+        hip_ctx.sync()
+        bufs.append(buf)
+        fbs.append(fb)
+    total = bufs[0].clone()
+    for b in bufs[1:]:
+        total += b
+    torch.cuda.synchronize()
+    _, s0, w0 = mdist.packed_accumulators(W * H, "cuda", base=total)
+    fbs[0].set_accumulation(s0.data_ptr(), w0.data_ptr())
+    np.testing.assert_array_equal(fbs[0].read(1).view(np.uint32), want[0].view(np.uint32))
+    np.testing.assert_array_equal(fbs[0].read(2).view(np.uint32), want[1].view(np.uint32))
+    assert want[1][..., :3].max() > 0
+    for fb in fbs:
+        fb.close()
+    full.close()
+    ds.close()

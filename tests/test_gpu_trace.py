@@ -113,3 +113,54 @@ def test_empty_query_and_errors(hip_ctx):
     ds.build()
     ds.trace_closest(0, 0, 0)            # n = 0 is a no-op
     ds.close()
+
+
+def _stacked_quads(n):
+    """n parallel unit quads at z = 0..n-1: a ray along +z through the centre intersects every
+    internal node's both children, so a closest-hit traversal keeps ~log2(2n) entries on its
+    stack (more than the 16-entry LDS stack for n = 2^16)."""
+    b = scenes.SceneBuilder("stacked")
+    m = b.add_material()
+    z = np.arange(n, dtype=np.float32)
+    P = np.zeros((4 * n, 3), np.float32)
+    P[0::4] = np.stack([-np.ones(n), -np.ones(n), z], -1)
+    P[1::4] = np.stack([np.ones(n), -np.ones(n), z], -1)
+    P[2::4] = np.stack([np.ones(n), np.ones(n), z], -1)
+    P[3::4] = np.stack([-np.ones(n), np.ones(n), z], -1)
+    k = 4 * np.arange(n)[:, None]
+    T_ = np.concatenate([k + [0, 1, 2], k + [0, 2, 3]], 1).reshape(-1, 3)
+    b.add_mesh(P, np.tile([0, 0, 1], (len(P), 1)), np.zeros((len(P), 2)), T_, m)
+    return b.build()
+
+
+def test_traversal_stack_overflow_is_reported(hip_ctx, monkeypatch):
+    """A traversal that needs more stack entries than its spill column holds drops entries
+    (mcrt_traverse.h); the next synchronisation must report it (MCRT_ERROR_DEVICE), not return
+    silently.  The spill columns are capped at 0 entries by the MCRT_TEST_SPILL_CAP test hook, so
+    the deep stack of a ray along a column of 65536 quads overflows the 16-entry LDS stack."""
+    import torch
+    from mcrt import lib
+    sc = _stacked_quads(1 << 16)
+    rays = np.zeros(64, T.RAY_DTYPE)
+    rays["o"] = (0.1, 0.2, -10.0, 1e6)
+    rays["d"] = (0.0, 0.0, 1.0, 0.0)
+    rays["extra"] = (-1, 1)
+    r = torch.from_numpy(rays.view(np.uint8).copy()).cuda()
+    h = torch.zeros(64 * 32, dtype=torch.uint8, device="cuda")
+    # the default spill capacity covers the tree: correct hit, no error
+    ok = lib.DeviceScene(hip_ctx, sc)
+    assert ok.layout()["depth"] > 16
+    ok.trace_closest(r.data_ptr(), 64, h.data_ptr())
+    hip_ctx.sync()
+    hits = h.cpu().numpy().view(T.ISECT_DTYPE)
+    assert (hits["shapeid"] == 0).all()
+    np.testing.assert_allclose(hits["uvwt"][:, 3], 10.0, rtol=1e-6)
+    ok.close()
+    monkeypatch.setenv("MCRT_TEST_SPILL_CAP", "0")
+    bad = lib.DeviceScene(hip_ctx, sc)
+    monkeypatch.delenv("MCRT_TEST_SPILL_CAP")
+    bad.trace_closest(r.data_ptr(), 64, h.data_ptr())
+    with pytest.raises(lib.MCRTError, match="overflow"):
+        hip_ctx.sync()
+    hip_ctx.sync()   # the flag is cleared once reported
+    bad.close()

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--scene", default="san_miguel_proxy")
     ap.add_argument("--fif", type=int, default=0, help="frames in flight (0 = the library's auto choice)")
     ap.add_argument("--batch", type=int, default=1, help="frames per mcrt_render_frames call (0 = N)")
+    ap.add_argument("--base-ms", type=float, default=None,
+                    help="1-GPU ms/frame (the efficiency base) when --ns does not include 1")
     args = ap.parse_args()
     from mcrt import lib, scenes
     from mcrt import types as T
@@ -61,9 +63,12 @@ def main():
             per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
         out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
                            "min_ms": round(min(per_rank), 4)}
-    base = out["per_n"][min(out["per_n"])]["max_ms"]
+    # efficiency is relative to ONE GPU rendering the whole image: the N = 1 run of this sweep, or
+    # --base-ms from a separate N = 1 run (never the smallest N of the sweep, which may be > 1)
+    base = out["per_n"][1]["max_ms"] if 1 in out["per_n"] else args.base_ms
+    out["base_ms_n1"] = base
     for n, v in out["per_n"].items():
-        v["compute_eff"] = round(base / (n * v["max_ms"]), 4)
+        v["compute_eff"] = round(base / (n * v["max_ms"]), 4) if base else None
     print(json.dumps(out), flush=True)
     fb.close()
     ds.close()
