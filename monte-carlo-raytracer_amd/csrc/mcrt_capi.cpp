@@ -276,31 +276,6 @@ static inline void xformPoint(const mcrt_mat4& m, const mcrt_float4& p, float* o
     }
 }
 
-// filters.cl:12-69 (uniform per frame: the reference evaluates one pixelOffset per frame)
-static float filter_weight(const mcrt_filter& f) {
-    const float px = f.pixelOffset.x, py = f.pixelOffset.y;
-    auto mitchell1D = [](float x, float B, float C) {
-        x = std::fabs(2.0f * x);
-        if (x > 1.0f) return ((-B - 6 * C) * x * x * x + (6 * B + 30 * C) * x * x + (-12 * B - 48 * C) * x + (8 * B + 24 * C)) * (1.f / 6.f);
-        return ((12 - 9 * B - 6 * C) * x * x * x + (-18 + 12 * B + 6 * C) * x * x + (6 - 2 * B)) * (1.f / 6.f);
-    };
-    auto sinc = [](float x) { x = std::fabs(x); return x < 1e-5 ? 1.0f : std::sin(3.14159265359f * x) / (3.14159265359f * x); };
-    auto wsinc = [&](float x, float r, float tau) { x = std::fabs(x); return x > r ? 0.0f : sinc(x) * sinc(x / tau); };
-    switch (f.filterType) {
-    case MCRT_TRIANGLE_FILTER:
-        return std::fmax(0.0f, f.radius.x - std::fabs(px)) * std::fmax(0.0f, f.radius.y - std::fabs(py));
-    case MCRT_GAUSSIAN_FILTER:
-        return std::fmax(0.0f, std::exp(-f.gaussianAlpha * px * px) - f.gaussianExpX) *
-               std::fmax(0.0f, std::exp(-f.gaussianAlpha * py * py) - f.gaussianExpY);
-    case MCRT_MITCHELL_FILTER:
-        return mitchell1D(px / f.radius.x, f.mitchellB, f.mitchellC) * mitchell1D(py / f.radius.y, f.mitchellB, f.mitchellC);
-    case MCRT_LANCZOS_SINC_FILTER:
-        return wsinc(px, f.radius.x, f.lanczosSincTau) * wsinc(py, f.radius.y, f.lanczosSincTau);
-    default:
-        return 1.0f;
-    }
-}
-
 // Per-ray spill columns for `rays` rays (rounded up to whole waves); grown on demand.
 static bool ensure_spill(mcrt_scene s, size_t rays) {
     rays = (rays + 63) / 64 * 64;
@@ -1476,8 +1451,8 @@ static mcrt_status accumulate(mcrt_framebuffer fb, const mcrt_filter* filters, i
     const int batch = fb->lastIntegrator == MCRT_INTEGRATOR_PT ? slot.lastBatch : 1;
     if (nfilters != 1 && nfilters != batch)
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "one filter, or one per frame of the last mcrt_render_frames");
-    BatchWeights w{};
-    for (int k = 0; k < batch; ++k) w.w[k] = filter_weight(filters[nfilters == 1 ? 0 : k]);
+    BatchFilters w{};   // weights are evaluated on the device (k_accumulate, filters.cl)
+    for (int k = 0; k < batch; ++k) w.f[k] = filters[nfilters == 1 ? 0 : k];
     FrameArgs f = fb->bands;
     f.batch = batch;
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, slot.done, 0));   // the frame's render (its slot stream)

@@ -40,7 +40,9 @@ struct FrameArgs {
     int batch;              // frames per launch (mcrt_render_frames): path id = k * W*H + pixel, frame f.frame + k
 };
 #define MCRT_MAX_BATCH_FRAMES 16
-struct BatchWeights { float w[MCRT_MAX_BATCH_FRAMES]; };
+// the reconstruction filter of each frame of a batch (device layout, KRN/kernel_data.h:63-80);
+// k_accumulate evaluates its weight on the device like ReconstructionPass (reconstruction.cl:21-42)
+struct BatchFilters { mcrt_filter f[MCRT_MAX_BATCH_FRAMES]; };
 
 struct QueueArgs {
     int* shadowCount;
@@ -97,7 +99,7 @@ void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int
                    int maxCount, hipStream_t st);
 void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits, int which,
                 float4* out, hipStream_t st);
-void launch_accumulate(const FrameArgs& f, int frame, const BatchWeights& w, const float4* radiance, float4* wsum, float* wts,
+void launch_accumulate(const FrameArgs& f, int frame, const BatchFilters& w, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st);
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st);
 void launch_denoise(int W, int H, int r, float ss, float sr, const float4* in, float4* out, hipStream_t st);

@@ -461,12 +461,56 @@ __global__ __launch_bounds__(256) void k_aov(SceneArgs s, FrameArgs f, const mcr
 }
 
 // ---------------------------------------------------------------------------
-// ReconstructionPass (KRN/reconstruction.cl:6-60); weight precomputed on the host
-// (KRN/filters.cl, uniform per frame).  Band rows only.
+// ReconstructionPass (KRN/reconstruction.cl:6-60) with the filters of KRN/filters.cl:12-69,
+// evaluated on the device as the reference does (same expression shapes, so clang contracts the
+// same products into fma; `/` is the OpenCL-default 2.5-ulp division, cl_div; exp and sin are the
+// device library's, like OpenCL's).  The weight is uniform per frame (one pixelOffset per frame,
+// RTReconstructionPass.cpp:71-123); pinned against the reference's filters.cl run live
+// (oracle/refbuild/clprobe_filters.cl, tests/test_gpu_accumulate.py).  Band rows only.
 // ---------------------------------------------------------------------------
+MCRT_DEV float filterTriangle(f2 p, f2 radius) {   // filters.cl:17-20
+    return fmaxf(0.0f, radius.x - fabsf(p.x)) * fmaxf(0.0f, radius.y - fabsf(p.y));
+}
+MCRT_DEV float filterGaussian1D(float d, float alpha, float expv) {   // filters.cl:22-25
+    return fmaxf(0.0f, expf(-alpha * d * d) - expv);
+}
+MCRT_DEV float filterMitchell1D(float x, float B, float C) {   // filters.cl:32-39
+    x = fabsf(2.0f * x);
+    if (x > 1.0f)
+        return ((-B - 6*C) * x*x*x + (6*B + 30*C) * x*x + (-12*B - 48*C) * x + (8*B + 24*C)) * (1.f/6.f);
+    else
+        return ((12 - 9*B - 6*C) * x*x*x + (-18 + 12*B + 6*C) * x*x + (6 - 2*B)) * (1.f/6.f);
+}
+MCRT_DEV float filterSinc(float x) {   // filters.cl:47-54 (1e-5 is a float literal: no cl_khr_fp64 pragma)
+    x = fabsf(x);
+    if (x < 1e-5f) return 1.0f;
+    return cl_div(sinf(PI_F * x), (PI_F * x));
+}
+MCRT_DEV float filterWindowedSinc(float x, float radius, float tau) {   // filters.cl:56-64
+    x = fabsf(x);
+    if (x > radius) return 0.0f;
+    const float lanczos = filterSinc(cl_div(x, tau));
+    return filterSinc(x) * lanczos;
+}
+// the switch of reconstruction.cl:23-42
+MCRT_DEV float filterWeight(const mcrt_filter& fp) {
+    const f2 p = f2{fp.pixelOffset.x, fp.pixelOffset.y}, radius = f2{fp.radius.x, fp.radius.y};
+    switch (fp.filterType) {
+    case MCRT_TRIANGLE_FILTER: return filterTriangle(p, radius);
+    case MCRT_GAUSSIAN_FILTER:
+        return filterGaussian1D(p.x, fp.gaussianAlpha, fp.gaussianExpX) * filterGaussian1D(p.y, fp.gaussianAlpha, fp.gaussianExpY);
+    case MCRT_MITCHELL_FILTER:
+        return filterMitchell1D(cl_div(p.x, radius.x), fp.mitchellB, fp.mitchellC) *
+               filterMitchell1D(cl_div(p.y, radius.y), fp.mitchellB, fp.mitchellC);
+    case MCRT_LANCZOS_SINC_FILTER:
+        return filterWindowedSinc(p.x, radius.x, fp.lanczosSincTau) * filterWindowedSinc(p.y, radius.y, fp.lanczosSincTau);
+    default: return 1.0f;   // RT_BOX_FILTER
+    }
+}
+
 // A batch of f.batch frames (mcrt_render_frames) is accumulated in frame order, frame + k with
-// weight bw.w[k]: per pixel the same operations as f.batch single-frame launches.
-__global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, BatchWeights bw,
+// filter bf.f[k]: per pixel the same operations as f.batch single-frame launches.
+__global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, BatchFilters bf,
                                                     const float4* __restrict__ radiance, float4* __restrict__ wsum,
                                                     float* __restrict__ wts, float4* __restrict__ image) {
     const int lane = threadIdx.x & 63;
@@ -485,12 +529,12 @@ __global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, Batc
         const float4 r4 = radiance[(size_t)k * f.W * f.H + pix];
         const f4 radiance4 = f4{cl_clamp(r4.x, 0.0f, 1000.0f), cl_clamp(r4.y, 0.0f, 1000.0f),
                                 cl_clamp(r4.z, 0.0f, 1000.0f), cl_clamp(r4.w, 0.0f, 1000.0f)};
-        const float w = bw.w[k];
+        const float w = filterWeight(bf.f[k]);
         if (frame + k == 0) {
             s = radiance4 * w;
             ws = w;
         } else {
-            s += radiance4 * w;
+            s += radiance4 * w;   // contracted to fma, as reconstruction.cl:50
             ws = ws + w;
         }
     }
@@ -645,7 +689,7 @@ void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, 
     const int blocks = (f.numTiles * 64 + 255) / 256;
     hipLaunchKernelGGL(k_aov, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, s, f, cam, hits, which, out);
 }
-void launch_accumulate(const FrameArgs& f, int frame, const BatchWeights& w, const float4* radiance, float4* wsum,
+void launch_accumulate(const FrameArgs& f, int frame, const BatchFilters& w, const float4* radiance, float4* wsum,
                        float* wts, float4* image, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + 255) / 256;
     hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(256), 0, st, f, frame, w, radiance, wsum, wts, image);

@@ -94,7 +94,11 @@ def taa_jitter(frame, radius=(2.0, 2.0), mats=None):
         mats = sobol_matrices()
     u = sobol_1d(frame, 0, mats)
     v = sobol_1d(frame, 1, mats)
-    return (-radius[0] + (2 * radius[0]) * float(u), -radius[1] + (2 * radius[1]) * float(v))
+    f32 = np.float32
+
+    def lerp(s, e, t):   # math::lerp (source/engine/util/math.h:38) in float32
+        return float(f32(f32(1) - t) * f32(s) + t * f32(e))
+    return (lerp(-radius[0], radius[0], u), lerp(-radius[1], radius[1], v))
 
 
 def scene_camera(name, width, height, frame=0, mats=None, jitter=False):

@@ -162,7 +162,7 @@ def ptr(a):
 
 
 def make_filter(kind=BOX, radius=(2.0, 2.0), pixel_offset=(0.0, 0.0), B=1.0 / 3, C=1.0 / 3, tau=3.0,
-                alpha=2.0):
+                alpha=1.0):
     """RTFilterProperties with the device layout (filters.cl); defaults per PathTracingSettings.h."""
     f = np.zeros(1, FILTER_DTYPE)
     f["filterType"] = kind

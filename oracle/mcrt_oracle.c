@@ -1719,9 +1719,11 @@ void orc_tonemap(int W, int H, float Lwhite, const float* in, float* out) {
     }
 }
 
-void orc_accumulate(int W, int H, int frame, const mcrt_filter* f, const float* radiance,
-                    float* wsum, float* wts, float* image) {
-    float w = filterWeight(f);
+/* KRN/reconstruction.cl:20-57 for one frame with filter weight w.  `weighted += radiance * w`
+ * (reconstruction.cl:50) is contracted to an fma by the reference's OpenCL compiler (FP_CONTRACT
+ * ON is the OpenCL default), so it is fmaf here; the final division is IEEE (the reference GPU
+ * build uses the 2.5-ulp OpenCL division, tests allow 3 ulp on the image). */
+void orc_accumulate_w(int W, int H, int frame, float w, const float* radiance, float* wsum, float* wts, float* image) {
     for (int64_t i = 0; i < (int64_t)W * H; ++i) {
         float r[4];
         for (int c = 0; c < 4; ++c) r[c] = clampf(radiance[4 * i + c], 0.0f, 1000.0f);
@@ -1729,9 +1731,13 @@ void orc_accumulate(int W, int H, int frame, const mcrt_filter* f, const float* 
             for (int c = 0; c < 4; ++c) wsum[4 * i + c] = r[c] * w;
             wts[i] = w;
         } else {
-            for (int c = 0; c < 4; ++c) wsum[4 * i + c] += r[c] * w;
+            for (int c = 0; c < 4; ++c) wsum[4 * i + c] = fmaf(r[c], w, wsum[4 * i + c]);
             wts[i] += w;
         }
         for (int c = 0; c < 4; ++c) image[4 * i + c] = wsum[4 * i + c] / wts[i];
     }
+}
+void orc_accumulate(int W, int H, int frame, const mcrt_filter* f, const float* radiance,
+                    float* wsum, float* wts, float* image) {
+    orc_accumulate_w(W, H, frame, filterWeight(f), radiance, wsum, wts, image);
 }

@@ -68,6 +68,8 @@ void orc_render_rows(orc_scene* s, const mcrt_camera* cam, int frame, int max_de
                      const int32_t* rows, int nrows, int threads, float* radiance, int64_t* stats);
 
 /* ReconstructionPass (reconstruction.cl:6-60). */
+/* one frame of ReconstructionPass with an explicit filter weight */
+void orc_accumulate_w(int W, int H, int frame, float w, const float* radiance, float* wsum, float* wts, float* image);
 void orc_accumulate(int W, int H, int frame, const mcrt_filter* f, const float* radiance,
                     float* wsum, float* wts, float* image);
 

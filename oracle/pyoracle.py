@@ -51,6 +51,7 @@ def lib():
         L.orc_set_touched.argtypes = [_vp, _vp]
         L.orc_render_rows.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _c.c_int, _c.c_int, _vp, _vp]
         L.orc_accumulate.argtypes = [_c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp, _vp]
+        L.orc_accumulate_w.argtypes = [_c.c_int, _c.c_int, _c.c_int, _c.c_float, _vp, _vp, _vp, _vp]
         L.orc_denoise.argtypes = [_c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float, _vp, _vp]
         L.orc_tonemap.argtypes = [_c.c_int, _c.c_int, _c.c_float, _vp, _vp]
         L.orc_sample_uber.argtypes = [_vp] * 6 + [_c.c_float, _vp, _vp, _vp]
@@ -159,6 +160,18 @@ def accumulate(radiance, frame, filt, wsum=None, wts=None):
         wts = np.zeros((H, W), np.float32)
     image = np.zeros((H, W, 4), np.float32)
     lib().orc_accumulate(W, H, frame, _p(filt), _p(radiance), _p(wsum), _p(wts), _p(image))
+    return wsum, wts, image
+
+
+def accumulate_w(radiance, frame, w, wsum=None, wts=None):
+    """ReconstructionPass for one frame with an explicit filter weight w (orc_accumulate_w)."""
+    radiance = np.ascontiguousarray(radiance, np.float32)
+    H, W = radiance.shape[:2]
+    if wsum is None:
+        wsum = np.zeros((H, W, 4), np.float32)
+        wts = np.zeros((H, W), np.float32)
+    image = np.zeros((H, W, 4), np.float32)
+    lib().orc_accumulate_w(W, H, frame, float(w), _p(radiance), _p(wsum), _p(wts), _p(image))
     return wsum, wts, image
 
 
@@ -370,6 +383,7 @@ def clref(variant="ieee"):
         L.clref_bdpt_read.restype = _c.c_int64
         L.clref_bdpt_read.argtypes = [_vp, _c.c_int, _vp]
         L.clref_probe_lod.argtypes = [_vp, _c.c_char_p, _vp, _vp, _c.c_int, _c.c_int, _vp]
+        L.clref_probe_filters.argtypes = [_c.c_char_p, _vp, _c.c_int, _vp]
         L.clref_scene_set_two_level.argtypes = [_vp, _vp, _c.c_int64, _vp, _c.c_int64, _vp, _c.c_int64, _vp,
                                                 _c.c_int64, _c.c_int]
         st = L.clref_init(os.path.join(HERE, "_ref").encode(), variant.encode())
@@ -377,6 +391,18 @@ def clref(variant="ieee"):
             raise RuntimeError(f"clref_init({variant}) = {st}: {L.clref_error().decode()}")
         _clref = L
     return _clref
+
+
+def clref_filter_weights(filters, variant="ieee"):
+    """The reference's filter weights (filters.cl via oracle/refbuild/clprobe_filters.cl, run live)
+    for an array of mcrt.types.FILTER_DTYPE records (the 56-B device layout)."""
+    L = clref(variant)
+    f = np.ascontiguousarray(filters)
+    out = np.zeros(len(f), np.float32)
+    st = L.clref_probe_filters(os.path.join(HERE, "_ref", "clref_probe_filters.hsaco").encode(), _p(f), len(f), _p(out))
+    if st != 0:
+        raise RuntimeError(f"clref_probe_filters {st}: {L.clref_error().decode()}")
+    return out
 
 
 class CLRefScene:

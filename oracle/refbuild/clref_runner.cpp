@@ -493,6 +493,35 @@ __attribute__((visibility("default"))) int clref_probe_lod(void* sp, const char*
     return good ? 0 : -5;
 }
 
+// Filter probe (clprobe_filters.cl, test infrastructure): the reference's filter weight for each of
+// n 56-B RTFilterProperties records.
+__attribute__((visibility("default"))) int clref_probe_filters(const char* hsaco, const void* props, int n,
+                                                               float* out) {
+    static cl_program prog = nullptr;
+    static cl_kernel k = nullptr;
+    cl_int e = 0;
+    if (!k) {
+        prog = loadProgram(hsaco);
+        if (!prog) return -1;
+        k = clCreateKernel(prog, "ProbeFilters", &e);
+        if (!ok(e, "kernel ProbeFilters")) return -2;
+    }
+    cl_mem bp = buf(56 * (size_t)n, props);
+    std::vector<float> zero((size_t)n, 0.0f);
+    cl_mem bo = buf(4 * (size_t)n, zero.data());
+    e = 0;
+    e |= arg(k, 0, bp);
+    e |= arg(k, 1, n);
+    e |= arg(k, 2, bo);
+    if (!ok(e, "probe filter args")) return -4;
+    size_t gs = ((size_t)n + 63) / 64 * 64, ls = 64;
+    bool good = ok(clEnqueueNDRangeKernel(R.q, k, 1, nullptr, &gs, &ls, 0, nullptr, nullptr), "probe filter launch") &&
+                ok(clEnqueueReadBuffer(R.q, bo, CL_TRUE, 0, 4 * (size_t)n, out, 0, nullptr, nullptr), "probe filter read");
+    clReleaseMemObject(bp);
+    clReleaseMemObject(bo);
+    return good ? 0 : -5;
+}
+
 // ---------------------------------------------------------------------------
 // BDPT (RTBDPTPass::update, RTBDPTPass.cpp:67-128; kernels BDPT.cl:240-932)
 // ---------------------------------------------------------------------------

@@ -141,6 +141,86 @@ def build_scene(name):
     raise KeyError(name)
 
 
+# BASELINE.json configs at full size against the reference kernels run live
+# (tests/test_gpu_reference_scale.py): (key, scene, W, H, integrator, frames, max_depth).
+# The sampler is the job's variant: "ieee" = random (the reference default), "sobol_ieee" = the
+# reference rebuilt with RT_SAMPLER_SOBOL (oracle/refbuild/Makefile SOBOL_BUILD).
+SCALE_CASES = {
+    "ieee": [
+        ("sm_pt_1080p", "san_miguel_proxy", 1920, 1080, "pt", (0, 1), 2),            # headline / config 4 scene
+        ("sponza_pt_1080p", "sponza_proxy", 1920, 1080, "pt", (0, 1), 2),           # config 3
+        ("sm_bdpt_960x540", "san_miguel_proxy", 960, 540, "bdpt", (0, 1), 2),       # config 4 integrator
+    ],
+    "sobol_ieee": [
+        ("sm_sobol_4k", "san_miguel_proxy", 3840, 2160, "pt", (0, 600), 2),        # config 5; frame 600: Q6 wrap
+        ("mixed_sobol_d5", "mixed", 96, 64, "pt", (0, 3), 5),
+        ("mixed_sobol_bdpt", "mixed", 96, 64, "bdpt", (0, 1), 2),
+    ],
+}
+BDPT_VERTEX_STRIDE = 17   # vertex records kept for every 17th pixel (the full arrays are ~0.5 GB at 960x540)
+
+
+def scale_scene(name):
+    from mcrt import sobol_matrices
+    sc = scenes.san_miguel_proxy() if name == "san_miguel_proxy" else scenes.sponza_proxy() \
+        if name == "sponza_proxy" else build_scene(name)
+    sc.sobol = sobol_matrices()
+    return sc
+
+
+def scale_job(out_path, variant):
+    res = {}
+    cache, nodes = {}, {}
+    for key, name, W, H, integ, frames, D in SCALE_CASES[variant]:
+        if name not in cache:
+            cache.clear()
+            nodes.clear()
+            cache[name] = scale_scene(name)
+        cam = scene_camera(name, W, H)
+        cs = po.CLRefScene(cache[name], variant, nodes=nodes.get(name))   # Bvh2 nodes built once per scene
+        nodes[name] = cs.nodes
+        t0 = time.time()
+        for f in frames:
+            res[f"{key}_f{f}"] = (cs.render_bdpt if integ == "bdpt" else cs.render)(cam, frame=f, max_depth=D)
+        if integ == "bdpt":
+            N = W * H
+            sel = np.arange(0, N, BDPT_VERTEX_STRIDE)
+            for which, depths in (("camera_vertices", D + 2), ("light_vertices", D + 1)):
+                v = cs.read_bdpt(which).view(po.REF_VERTEX_DTYPE).reshape(N, depths)
+                res[f"{key}_{which}"] = np.ascontiguousarray(v[sel])
+            for which in ("camera_counts", "light_counts"):
+                res[f"{key}_{which}"] = cs.read_bdpt(which).view(np.int32)
+        print(f"{key}: {len(frames)} frames in {time.time() - t0:.1f}s", flush=True)
+        del cs
+    np.savez(out_path, **res)
+
+
+def filter_table():
+    """Reconstruction filters for tests/test_gpu_accumulate.py: every filter type at the reference's
+    default settings (PathTracingSettings.h:55-66) and variations, each at TAA pixel offsets of
+    frames 0..11 (PathTracingApp.cpp:208-215) plus hand-picked edge offsets."""
+    from mcrt.camera import taa_jitter
+    rows = []
+    settings = [(T.BOX, {}), (T.TRIANGLE, {}), (T.TRIANGLE, dict(radius=(1.5, 3.0))),
+                (T.GAUSSIAN, {}), (T.GAUSSIAN, dict(alpha=2.5, radius=(1.0, 2.0))),
+                (T.MITCHELL, {}), (T.MITCHELL, dict(B=0.5, C=0.25)), (T.LANCZOS, {}), (T.LANCZOS, dict(tau=2.0))]
+    for kind, kw in settings:
+        r = kw.get("radius", (2.0, 2.0))
+        offs = [taa_jitter(f, radius=r) for f in range(12)]
+        offs += [(0.0, 0.0), (r[0], -r[1]), (0.5 * r[0], 1e-6), (-0.999 * r[0], 0.25)]
+        for o in offs:
+            rows.append(T.make_filter(kind, pixel_offset=o, **kw)[0])
+    out = np.zeros(len(rows), T.FILTER_DTYPE)
+    for i, r in enumerate(rows):
+        out[i] = r
+    return out
+
+
+def filters_job(out_path, variant):
+    f = filter_table()
+    np.savez(out_path, filters=f, weights=po.clref_filter_weights(f, variant))
+
+
 def sm_job(out_path, variant, W, H, tris):
     """Two depth-2 frames of the San-Miguel proxy (test_san_miguel_proxy_bit_exact_vs_reference)."""
     cs = po.CLRefScene(scenes.san_miguel_proxy(tris=tris), variant)
@@ -159,6 +239,12 @@ def main():
         return
     if len(sys.argv) > 3 and sys.argv[3] == "2l":
         tl_job(out_path, variant)
+        return
+    if len(sys.argv) > 3 and sys.argv[3] == "filters":
+        filters_job(out_path, variant)
+        return
+    if len(sys.argv) > 3 and sys.argv[3] == "scale":
+        scale_job(out_path, variant)
         return
     if len(sys.argv) > 3 and sys.argv[3] == "sm":
         sm_job(out_path, variant, int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6]))

@@ -52,6 +52,13 @@ def test_camera_matches_reference_live():
     np.testing.assert_array_equal(_bits(product(c, offs)), _bits(cams_ref))
 
 
+def test_python_taa_restatement_matches_reference():
+    from mcrt.camera import taa_jitter
+    z = np.load(camref.FIXTURE, allow_pickle=False)
+    got = np.array([taa_jitter(int(f)) for f in z["frame"]], np.float32)
+    np.testing.assert_array_equal(_bits(got), _bits(z["taa_offset"]))
+
+
 def test_axes_form_and_errors():
     """mcrt_make_pinhole_camera_axes with the look-at axes equals the look-at form; bad input fails."""
     z = np.load(camref.FIXTURE, allow_pickle=False)

@@ -1,0 +1,101 @@
+"""BASELINE.json configs at FULL size against the REFERENCE's own kernels run live on this MI355X
+(tests/clref_job.py ... scale, one child process per sampler build):
+
+  * headline + config 4's scene: San-Miguel proxy (9,984,786 triangles) 1920x1080, PT, D = 2,
+    frames 0 and 1 -- every radiance value BIT-EXACT (PathTracing.cl + intersect_bvh2_lds.cl);
+  * config 3: Sponza proxy (16 x 1024^2 mip-mapped textures) 1920x1080, PT -- bit-exact;
+  * config 4: San-Miguel proxy BDPT at 960x540, frames 0 and 1 in sequence from fresh buffers
+    (BDPT.cl) -- vertex counts bit-exact, every defined field of the vertices of every 17th pixel
+    bit-exact, radiance within 4e-6 relative (splat atomics, tests/test_gpu_bdpt.py) and
+    bit-exact where no light-tracing splat landed;
+  * config 5: San-Miguel proxy 3840x2160 with the Sobol sampler (the reference rebuilt with
+    RT_SAMPLER_SOBOL, samplers.cl:18), frames 0 and 600 -- frame 600's sample index
+    pix + 600 x W x H exceeds 2^32 and wraps -- bit-exact; plus the mixed
+    scene at depth 5 and Sobol BDPT on the mixed scene."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from clref_job import BDPT_VERTEX_STRIDE, SCALE_CASES, scale_scene
+from mcrt import types as T
+from mcrt.camera import scene_camera
+from oracle import pyoracle as po
+from test_gpu_bdpt import REL_TOL, compare_vertices, our_planes
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+CASES = [(v, c) for v in SCALE_CASES for c in SCALE_CASES[v]]
+
+
+@pytest.fixture(scope="module")
+def clref_scale(tmp_path_factory):
+    if not po.clref_available():
+        pytest.skip("oracle/_ref/clref_runner.so not built")
+    out = {}
+    for variant in SCALE_CASES:
+        path = str(tmp_path_factory.mktemp("clref") / f"scale_{variant}.npz")
+        r = subprocess.run([sys.executable, os.path.join(HERE, "clref_job.py"), path, variant, "scale"],
+                           capture_output=True, text=True, timeout=900)
+        if r.returncode != 0:
+            pytest.fail(f"reference scale job ({variant}) failed:\n" + r.stdout + r.stderr)
+        print(r.stdout)
+        out[variant] = np.load(path, allow_pickle=False)
+    return out
+
+
+_scenes = {}
+
+
+def device_scene(ctx, name):
+    from mcrt import lib
+    if name not in _scenes:
+        for k in list(_scenes):
+            _scenes.pop(k).close()
+        _scenes[name] = lib.DeviceScene(ctx, scale_scene(name))
+    return _scenes[name]
+
+
+@pytest.mark.parametrize("variant,case", CASES, ids=[c[0] for _, c in CASES])
+def test_full_size_config_matches_reference(hip_ctx, clref_scale, variant, case):
+    from mcrt import lib
+    key, name, W, H, integ, frames, D = case
+    ref = clref_scale[variant]
+    sampler = T.SAMPLER_SOBOL if variant.startswith("sobol") else T.SAMPLER_RANDOM
+    ds = device_scene(hip_ctx, name)
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    cam = scene_camera(name, W, H)
+    bad = []
+    for f in frames:
+        fb.render(ds, cam, frame=f, max_depth=D, sampler=sampler,
+                  integrator=T.INTEGRATOR_BDPT if integ == "bdpt" else T.INTEGRATOR_PT)
+        g = fb.read(0)[..., :3]
+        r = ref[f"{key}_f{f}"][..., :3]
+        exact = (g.view(np.uint32) == r.view(np.uint32)) | (np.isnan(g) & np.isnan(r))
+        assert r.max() > 0, (key, f, "empty reference frame")
+        if integ == "pt":
+            if not exact.all():
+                bad.append(f"frame {f}: {int((~exact.all(-1)).sum())} of {W * H} pixels differ")
+            continue
+        close = exact | (np.abs(g - r) <= REL_TOL * (np.abs(g) + np.abs(r)) + 1e-30)
+        nosplat = (fb.read_bdpt("splat").view(np.float32).reshape(H, W, 4)[..., :3] == 0).all(-1)
+        if not close.all():
+            bad.append(f"frame {f}: {int((~close.all(-1)).sum())} pixels outside {REL_TOL}")
+        if not exact.all(-1)[nosplat].all():
+            bad.append(f"frame {f}: {int((~exact.all(-1)[nosplat]).sum())} no-splat pixels not bit-exact")
+    if integ == "bdpt":
+        N = W * H
+        sel = np.arange(0, N, BDPT_VERTEX_STRIDE)
+        cc = fb.read_bdpt("camera_counts").view(np.int32)
+        lc = fb.read_bdpt("light_counts").view(np.int32)
+        for nm, a, b in (("camera", cc, ref[f"{key}_camera_counts"]), ("light", lc, ref[f"{key}_light_counts"])):
+            if (a != b).any():
+                bad.append(f"{nm} counts differ at {int((a != b).sum())} pixels")
+        for which, depths, counts in (("camera_vertices", D + 2, cc), ("light_vertices", D + 1, lc)):
+            ours = our_planes(fb.read_bdpt(which), depths, N)[:, :, sel]
+            theirs = ref[f"{key}_{which}"].view(po.REF_VERTEX_DTYPE).reshape(len(sel), depths)
+            bad += compare_vertices(ours, theirs, counts[sel], depths, len(sel), which)
+    fb.close()
+    assert not bad, (key, bad)

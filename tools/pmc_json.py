@@ -1,18 +1,24 @@
-"""Builds profiles/pmc_latest.json (read by bench.py for roofline.traffic) from two rocprofv3
-PMC passes of `bench.py` (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
+"""Builds profiles/pmc_latest.json (read by bench.py: roofline.traffic and roofline.limiter) from
+rocprofv3 PMC passes of one bench.py command (tools/r2_gpu2.sh runs them, each pass in its own
+process because FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
 
-  rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o f -- python3 bench.py ...
-  rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o w -- python3 bench.py ...
-  python tools/pmc_json.py gpurun_out/pmc_fetch/f_results.db gpurun_out/pmc_write/w_results.db
+  python tools/pmc_json.py DIR_WITH_RESULTS_DBS "bench command" [launches_per_kernel_in_stats_pass]
 
-Correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE counts 128-B memory-side read requests at
-64 B, so it is doubled; WRITE_SIZE is taken as is.  Both are KB in rocprofv3.  Infinity-Cache
-hits are counted as fetches by these L2 memory-side counters (same section), so the figure is
-L2-miss traffic, an upper bound on HBM bytes.  Per kernel: median over its dispatches.
+Per kernel the figures are the MEDIAN over the dispatches of bench.py's untimed one-slot
+kernel-timing pass (its last `--stats-launches` dispatches of that kernel), i.e. the same launches
+whose HIP-event durations price roofline.achieved.
+
+Corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE counts 128-B memory-side read requests at
+64 B, so it is doubled; WRITE_SIZE is taken as is; both are KB.  These L2-to-fabric counters also
+count Infinity-Cache hits, so the figure is L2-miss traffic (an upper bound on HBM bytes).
+Limiter (SQ block, per dispatch; SQ_WAVE_CYCLES / WAIT_* / ACTIVE_INST_* in the same unit, so
+their ratios are unit-free): share of wave time waiting on memory (SQ_WAIT_ANY), stalled at issue
+(SQ_WAIT_INST_ANY) and issuing (SQ_ACTIVE_INST_ANY); VALU pipe busy = SQ_INSTS_VALU x 2 cycles
+(a wave64 VALU op occupies a SIMD32 for 2 cycles) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs).
 """
+import glob
 import json
 import os
-import sqlite3
 import statistics
 import sys
 
@@ -24,31 +30,65 @@ KERNELS = ["k_shadow_extend", "k_primary", "k_extend", "k_shadow", "k_shade0", "
            "k_bdpt_start", "k_bdpt_vertex", "k_bdpt_connect", "k_bdpt_vis", "k_bdpt_gather"]
 
 
-def per_kernel(db, counter):
-    out = {}
-    for d in dispatches(db):
-        name = next((k for k in KERNELS if k in d["kernel"]), None)
-        if name is None or counter not in d["pmc"]:
-            continue
-        out.setdefault(name, []).append(d["pmc"][counter])
-    return {k: statistics.median(v) for k, v in out.items()}
+def collect(dbs, last):
+    """kernel -> counter -> median over the kernel's last `last` dispatches (per pass db)."""
+    out, ms = {}, {}
+    for db in dbs:
+        per = {}
+        for d in dispatches(db):
+            name = next((k for k in KERNELS if "_Z" in d["kernel"] and k in d["kernel"].split("ILb")[0] or
+                         d["kernel"].endswith(k)), None)
+            name = name or next((k for k in KERNELS if k in d["kernel"]), None)
+            if name is None:
+                continue
+            per.setdefault(name, []).append(d)
+        for name, ds in per.items():
+            ds = ds[-last:]
+            for c in ds[0]["pmc"]:
+                out.setdefault(name, {})[c] = statistics.median(x["pmc"][c] for x in ds)
+            ms.setdefault(name, []).extend(x["ms"] for x in ds)
+    return out, {k: statistics.median(v) for k, v in ms.items()}
 
 
 def main():
-    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
-    write = per_kernel(sys.argv[2], "WRITE_SIZE")
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py (San-Miguel proxy 1080p, D=2)",
+    d = sys.argv[1]
+    cmd = sys.argv[2] if len(sys.argv) > 2 else "bench.py"
+    last = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    dbs = sorted(glob.glob(os.path.join(d, "pmc_*", "*_results.db")))
+    pmc, ms = collect(dbs, last)
+    res = {"source": f"rocprofv3 --kernel-trace --pmc passes ({', '.join(os.path.basename(os.path.dirname(x)) for x in dbs)})",
+           "config": f"{cmd}; medians over the last {last} dispatches of each kernel = the untimed one-slot "
+                     "kernel-timing pass (4 frames per launch)",
            "correction": "hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (MI355X_MICROARCH.md HBM section)",
            "kernels": {}}
-    for k in KERNELS:
-        if k in fetch and k in write:
-            fb, wb = 2 * fetch[k] * 1024, write[k] * 1024
-            res["kernels"][k] = {"fetch_bytes_corrected": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
-                                 "fetch_size_kb_raw": fetch[k], "write_size_kb_raw": write[k]}
-    out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                                             "profiles", "pmc_latest.json")
+    for k, c in pmc.items():
+        r = {"dispatch_ms_median": round(ms[k], 4), "counters": {n: v for n, v in sorted(c.items())}}
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            fb, wb = 2 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
+            r.update(fetch_bytes_corrected=fb, write_bytes=wb, hbm_bytes_per_launch=fb + wb)
+        if all(x in c for x in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE")):
+            wc = c["SQ_WAVE_CYCLES"]
+            cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+            lim = {"wave_time_waiting_on_memory": round(c["SQ_WAIT_ANY"] / wc, 3),
+                   "wave_time_issue_stalled": round(c["SQ_WAIT_INST_ANY"] / wc, 3),
+                   "valu_busy": round(c["SQ_INSTS_VALU"] * 2 / (1024 * cyc), 3),
+                   "clock_ghz": round(cyc / (ms[k] * 1e-3) / 1e9, 3)}
+            if "SQ_ACTIVE_INST_ANY" in c:
+                lim["wave_time_issuing"] = round(c["SQ_ACTIVE_INST_ANY"] / wc, 3)
+            if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+                lim["l2_hit_rate"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 3)
+            if "hbm_bytes_per_launch" in r:
+                lim["memory_side_tb_s"] = round(r["hbm_bytes_per_launch"] / (ms[k] * 1e-3) / 1e12, 3)
+            mem, iss = lim["wave_time_waiting_on_memory"], lim["wave_time_issue_stalled"]
+            bw = lim.get("memory_side_tb_s", 0.0)
+            lim["binding"] = ("HBM bandwidth" if bw >= 5.0 else
+                              "memory latency" if mem >= 0.4 and lim["valu_busy"] < 0.6 else
+                              "VALU issue" if lim["valu_busy"] >= 0.6 else "mixed")
+            r["limiter"] = lim
+        res["kernels"][k] = r
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_latest.json")
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps(res, indent=1))
+    print(json.dumps({k: v.get("limiter") for k, v in res["kernels"].items()}, indent=1))
 
 
 if __name__ == "__main__":
