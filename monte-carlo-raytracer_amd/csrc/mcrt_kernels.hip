@@ -19,6 +19,10 @@
 #include "mcrt_traverse.h"
 #include "mcrt_shading.h"
 
+// Occupancy experiments: extra LDS bytes per traversal workgroup (0 = none).
+#ifndef MCRT_LDS_PAD
+#define MCRT_LDS_PAD 0
+#endif
 // Shading workgroup size (threads; one queue atomic per workgroup and queue).
 #ifndef SHADE_BLOCK
 #define SHADE_BLOCK 256
@@ -46,7 +50,7 @@
 template <bool ANY, bool TL>
 __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* __restrict__ rays, int n,
                                                    mcrt_intersection* __restrict__ hits, int* __restrict__ occl) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
     const int lane = threadIdx.x;
     const int i = blockIdx.x * 64 + lane;
     if (i >= n) return;
@@ -113,7 +117,7 @@ __global__ void k_surface_records(const uint32_t* __restrict__ meshStartIdx, con
 template <bool TL>
 __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 float4* __restrict__ hitOut) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
     const int lane = threadIdx.x;
     const int tileAll = xcdRemap(blockIdx.x, gridDim.x);   // batch frame k = tileAll / numTiles
     const int k = tileAll / f.numTiles, tile = tileAll - k * f.numTiles;
@@ -135,7 +139,7 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
 template <bool TL>
 __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ qO,
                                                const float4* __restrict__ qD, float4* __restrict__ hitOut) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
     const int n = *count;
     if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
@@ -158,7 +162,7 @@ template <bool TL>
 __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ sO,
                                                const float4* __restrict__ sD, const float4* __restrict__ sL,
                                                float4* __restrict__ radiance) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
     const int n = *count;
     if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
@@ -189,7 +193,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
                                                       float4* __restrict__ hitOut, const int* __restrict__ shadowCount,
                                                       const float4* __restrict__ sO, const float4* __restrict__ sD,
                                                       const float4* __restrict__ sL, float4* __restrict__ radiance) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
     const int ne = *extCount;
     const int eb = (ne + 63) >> 6;
     const int lane = threadIdx.x;

@@ -52,6 +52,10 @@ MCRT_DEV float triHit(const TraceRay& r, float4 A, float4 E1, float4 E2, float t
 #ifndef MCRT_OCT_TRAV
 #define MCRT_OCT_TRAV 1
 #endif
+// Packed slab tests (v_pk_fma_f32, two box planes per instruction) in the octant loops (1 = on).
+#ifndef MCRT_PK_SLAB
+#define MCRT_PK_SLAB 0
+#endif
 
 // Closest (ANY = false) or any (ANY = true) hit over the unified node array (mcrt_bvh.cpp):
 // the RadeonRays intersect_bvh2_lds.cl:107-178 loop -- one uniform 64-B fetch per step, an
@@ -83,7 +87,23 @@ MCRT_DEV int traverseOct(const float4* __restrict__ nodes, const TraceRay& r, f3
         if (n3.x >= 0) {
             // slab tests of both children (RR intersect_bvh2_lds.cl:54-63, mad -> fma)
             float a0, a1, b0, b1;
-            if constexpr (OCT >= 0) {
+            if constexpr (OCT >= 0 && MCRT_PK_SLAB) {
+                // the same 12 fmas as below, two per v_pk_fma_f32 (bit-identical: each lane of a
+                // packed fma is an IEEE fma)
+                constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
+                const f2 invxy = f2{inv.x, inv.y}, oxixy = f2{oxi.x, oxi.y};
+                const f2 invzz = f2{inv.z, inv.z}, oxizz = f2{oxi.z, oxi.z};
+                const f2 an = __builtin_elementwise_fma(f2{SX ? n0.y : n0.x, SY ? n0.w : n0.z}, invxy, oxixy);
+                const f2 af = __builtin_elementwise_fma(f2{SX ? n0.x : n0.y, SY ? n0.z : n0.w}, invxy, oxixy);
+                const f2 bn = __builtin_elementwise_fma(f2{SX ? n1.y : n1.x, SY ? n1.w : n1.z}, invxy, oxixy);
+                const f2 bf = __builtin_elementwise_fma(f2{SX ? n1.x : n1.y, SY ? n1.z : n1.w}, invxy, oxixy);
+                const f2 zn = __builtin_elementwise_fma(f2{SZ ? n2.y : n2.x, SZ ? n2.w : n2.z}, invzz, oxizz);
+                const f2 zf = __builtin_elementwise_fma(f2{SZ ? n2.x : n2.y, SZ ? n2.z : n2.w}, invzz, oxizz);
+                a0 = fmaxf(fmaxf(an.x, an.y), fmaxf(zn.x, 0.0f));
+                a1 = fminf(fminf(af.x, af.y), fminf(zf.x, t));
+                b0 = fmaxf(fmaxf(bn.x, bn.y), fmaxf(zn.y, 0.0f));
+                b1 = fminf(fminf(bf.x, bf.y), fminf(zf.y, t));
+            } else if constexpr (OCT >= 0) {
                 constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
                 const float axn = fmaf(SX ? n0.y : n0.x, inv.x, oxi.x), axf = fmaf(SX ? n0.x : n0.y, inv.x, oxi.x);
                 const float ayn = fmaf(SY ? n0.w : n0.z, inv.y, oxi.y), ayf = fmaf(SY ? n0.z : n0.w, inv.y, oxi.y);

@@ -228,6 +228,11 @@ class DeviceScene:
         self._mats = np.ascontiguousarray(mats)
         _check(lib().mcrt_scene_update_materials(self.h, _p(self._mats), len(self._mats)), self.ctx.h)
 
+    def update_shapes(self, shapes):
+        """mcrt_scene_update_shapes (same topology; call build() after a transform change)."""
+        self._shapes = np.ascontiguousarray(shapes)
+        _check(lib().mcrt_scene_update_shapes(self.h, _p(self._shapes), len(self._shapes)), self.ctx.h)
+
     def trace_closest(self, rays_dev_ptr, n, hits_dev_ptr):
         _check(lib().mcrt_trace_closest(self.h, rays_dev_ptr, n, hits_dev_ptr), self.ctx.h)
 

@@ -195,6 +195,52 @@ def scale_job(out_path, variant):
     np.savez(out_path, **res)
 
 
+def update_steps(sc):
+    """Dynamic scene updates (RTScene::update, RTScene.cpp:317-391) applied cumulatively to the
+    mixed scene: returns [(kind, new array)] -- materials edited, a shape moved (its transform and
+    inverse transpose; the BVH is rebuilt, as RR's Commit does), lights re-scaled and re-aimed."""
+    steps = []
+    mats = sc.materials.copy()
+    mats["uber_kd"][0, :3] *= 0.5
+    mats["uber_roughness"][1] = (0.31, 0.07)
+    mats["uber_ks"][2, :3] = (0.2, 0.6, 0.1)
+    steps.append(("materials", mats))
+    shapes = sc.shapes.copy()
+    k = len(shapes) // 2
+    M = shapes["toWorldTransform"][k].astype(np.float64)
+    Tm = np.eye(4)
+    Tm[:3, 3] = (0.3, 0.05, -0.2)
+    M2 = (Tm @ M).astype(np.float32)
+    shapes["toWorldTransform"][k] = M2
+    shapes["toWorldInverseTranspose"][k] = np.linalg.inv(M2.astype(np.float64)).T.astype(np.float32)
+    steps.append(("shapes", shapes))
+    lights = sc.lights.copy()
+    lights["intensity"][:, :3] *= np.float32(1.7)
+    d = lights["d"][0, :3].astype(np.float64) + (0.1, -0.05, 0.2)
+    lights["d"][0, :3] = (d / np.linalg.norm(d)).astype(np.float32)   # light 0 re-aimed
+    steps.append(("lights", lights))
+    return steps
+
+
+def apply_step(sc, kind, arr):
+    setattr(sc, kind, arr)
+    sc._desc = None
+
+
+def updates_job(out_path, variant):
+    """The reference renders the mixed scene freshly built with each cumulative update."""
+    res = {}
+    sc = build_scene("mixed")
+    cam = scene_camera("mixed", 96, 64)
+    for i, (kind, arr) in enumerate(update_steps(sc)):
+        apply_step(sc, kind, arr)
+        cs = po.CLRefScene(sc, variant)
+        for f in (0, 1):
+            res[f"update{i}_{kind}_f{f}"] = cs.render(cam, frame=f, max_depth=3)
+        del cs
+    np.savez(out_path, **res)
+
+
 def filter_table():
     """Reconstruction filters for tests/test_gpu_accumulate.py: every filter type at the reference's
     default settings (PathTracingSettings.h:55-66) and variations, each at TAA pixel offsets of
@@ -239,6 +285,9 @@ def main():
         return
     if len(sys.argv) > 3 and sys.argv[3] == "2l":
         tl_job(out_path, variant)
+        return
+    if len(sys.argv) > 3 and sys.argv[3] == "updates":
+        updates_job(out_path, variant)
         return
     if len(sys.argv) > 3 and sys.argv[3] == "filters":
         filters_job(out_path, variant)

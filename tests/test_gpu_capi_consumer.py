@@ -1,0 +1,69 @@
+"""The C ABI from compiled C++: tests/capi_consumer/capi_consumer.cpp replays INTEGRATION.md's
+reference-side code (RTScene::commit -> mcrt_scene_create + mcrt_accel_build; RTPrimaryRaysPass
+with 48-B rays in hipMalloc'd memory through mcrt_trace_closest / mcrt_trace_any;
+RTPathTracingPass + RTReconstructionPass -> mcrt_render_frame + mcrt_accumulate +
+mcrt_framebuffer_read; errors as std::runtime_error via check()).  It runs as its own process on
+the GPU; its outputs must equal the same calls made through the ctypes binding, bit for bit."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from mcrt import scenes, sobol_matrices
+from mcrt import types as T
+from mcrt.camera import scene_camera
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+EXE = os.path.join(HERE, "capi_consumer", "capi_consumer")
+
+
+def write_scene(sc, cam, d):
+    os.makedirs(d, exist_ok=True)
+    arrays = {"shapes": sc.shapes, "indices": sc.indices, "positions": sc.positions, "uvs": sc.uvs,
+              "normals": sc.normals, "tangents": sc.tangents, "binormals": sc.binormals, "textures": sc.textures,
+              "texdata": sc.tex_data, "sobol": sc.sobol, "lights": sc.lights, "materials": sc.materials, "camera": cam}
+    for k, a in arrays.items():
+        np.ascontiguousarray(a).tofile(os.path.join(d, f"{k}.bin"))
+
+
+def test_cpp_consumer_matches_ctypes(hip_ctx, tmp_path):
+    import torch
+    from mcrt import lib
+    if not os.path.exists(EXE):
+        pytest.skip("tests/capi_consumer/capi_consumer not built (make -C tests/capi_consumer)")
+    sc = scenes.test_scene()
+    sc.sobol = sobol_matrices()
+    W, H, frames, D = 96, 64, 4, 3
+    cam = scene_camera("mixed", W, H)
+    write_scene(sc, cam, str(tmp_path / "scene"))
+    os.makedirs(tmp_path / "out")
+    r = subprocess.run([EXE, str(tmp_path / "scene"), str(tmp_path / "out"), str(frames), str(D)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["pixels"] == W * H and info["error_caught"] == 1 and info["closest_hits"] > 0, info
+    out = lambda n, dt: np.fromfile(str(tmp_path / "out" / f"{n}.bin"), dt)   # noqa: E731
+    # the same through ctypes
+    ds = lib.DeviceScene(hip_ctx, sc)
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    for f in range(frames):
+        fb.render(ds, cam, frame=f, max_depth=D)
+        fb.accumulate(T.make_filter(T.BOX), f)
+    np.testing.assert_array_equal(out("radiance", np.uint32).reshape(H, W, 4), fb.read(0).view(np.uint32))
+    np.testing.assert_array_equal(out("image", np.uint32).reshape(H, W, 4), fb.read(2).view(np.uint32))
+    rays = out("rays", T.RAY_DTYPE)
+    rd = torch.from_numpy(rays.view(np.uint8).copy()).cuda()
+    h = torch.full((len(rays) * 32,), 0xff, dtype=torch.uint8, device="cuda")
+    o = torch.full((len(rays),), 0x7f7f7f7f, dtype=torch.int32, device="cuda")
+    ds.trace_closest(rd.data_ptr(), len(rays), h.data_ptr())
+    ds.trace_any(rd.data_ptr(), len(rays), o.data_ptr())
+    hip_ctx.sync()
+    np.testing.assert_array_equal(out("hits", np.uint8), h.cpu().numpy())
+    np.testing.assert_array_equal(out("occl", np.int32), o.cpu().numpy())
+    inactive = rays["extra"][:, 1] == 0
+    assert inactive.any() and (out("occl", np.int32)[inactive] == 0x7f7f7f7f).all()   # untouched (Q12)
+    fb.close()
+    ds.close()

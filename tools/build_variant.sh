@@ -11,5 +11,5 @@ mkdir -p "$C/build_$V"
 FLAGS="-O3 -std=c++17 -fPIC -I$ROOT/include -I/opt/rocm/include --offload-arch=gfx950 -munsafe-fp-atomics -ffp-contract=on -fno-hip-fp32-correctly-rounded-divide-sqrt"
 /opt/rocm/bin/hipcc $FLAGS $DEFS -c "$C/mcrt_kernels.hip" -o "$C/build_$V/mcrt_kernels.o"
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/monte-carlo-raytracer_amd/libmcrt_$V.so" \
-  "$C/build_$V/mcrt_kernels.o" "$C/build/mcrt_bdpt.o" "$C/build/mcrt_gpubuild.o" "$C/build/mcrt_raysort.o" "$C/build/mcrt_capi.o" "$C/build/mcrt_bvh.o" "$C/build/mcrt_bvh2l.o" -lpthread
+  "$C/build_$V/mcrt_kernels.o" $(ls "$C"/build/*.o | grep -v mcrt_kernels.o) -lpthread
 echo "built libmcrt_$V.so ($DEFS)"
