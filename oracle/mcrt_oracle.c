@@ -1741,3 +1741,721 @@ void orc_accumulate(int W, int H, int frame, const mcrt_filter* f, const float* 
                     float* wsum, float* wts, float* image) {
     orc_accumulate_w(W, H, frame, filterWeight(f), radiance, wsum, wts, image);
 }
+
+/* ======================================================================= */
+/* BDPT: KRN/BDPT.cl (GenerateStartVertices :240-312, GenerateSecondaryVertices :317-458,  */
+/* PrepareConnections :460-646, ConnectVertices :671-913, CopyBuffer :916-931) in the host */
+/* pass order of RTBDPTPass::update (RTBDPTPass.cpp:67-128), one pixel per work item.      */
+/* Camera model KRN/cameras.cl; light emission sampling KRN/lights.cl:148-252.             */
+/* IEEE fp32 without contraction, like the PT restatement above.                           */
+/* ======================================================================= */
+enum { BV_CAMERA = 0, BV_LIGHT = 1, BV_SURFACE = 2 };                 /* kernel_data.h:202-207 */
+enum { BVF_CONNECTIBLE = 1, BVF_DELTA_LIGHT = 2, BVF_DELTA = 4, BVF_INFINITE_LIGHT = 8 };   /* :209-218 */
+#define TRANSPORT_MODE_IMPORTANCE_ 1
+
+typedef struct {            /* RTBDPTVertex (kernel_data.h:220-244) */
+    v3 throughput;
+    Interaction in;
+    int type, flags, lightIdx, materialIdx;
+    float pdfFwd, pdfRev, pdfPos;
+    int radianceBufferIdx;
+} BVert;
+
+static inline int bvOnSurface(const BVert* v) {   /* BDPT.cl:40-43 */
+    return isNotNearZero(v->in.gn.x) || isNotNearZero(v->in.gn.y) || isNotNearZero(v->in.gn.z);
+}
+static inline int bvLight(const BVert* v) { return v->type == BV_LIGHT || v->lightIdx != -1; }   /* kernel_data.h:457-460 */
+
+/* KRN/matrix.cl:62-70 (transformVector4): row dots */
+static inline float dot4(const mcrt_float4* r, const float v[4]) { return r->x * v[0] + r->y * v[1] + r->z * v[2] + r->w * v[3]; }
+
+/* cameras.cl:8-32 */
+static v3 evalPinholeCameraWe(const mcrt_camera* c, v3 ro, v3 rd, v2* nip) {
+    float cosTheta = vdot(rd, load3(&c->direction));
+    if (cosTheta <= 0.0f) return V3(0, 0, 0);
+    v3 pf = vadd(ro, vdivs(rd, cosTheta));
+    float p4[4] = {pf.x, pf.y, pf.z, 1.0f};
+    float ic[4] = {dot4(&c->worldToClip.m0, p4), dot4(&c->worldToClip.m1, p4), dot4(&c->worldToClip.m2, p4),
+                   dot4(&c->worldToClip.m3, p4)};
+    if (ic[0] < -ic[3] || ic[0] > ic[3] || ic[1] < -ic[3] || ic[1] > ic[3]) return V3(0, 0, 0);
+    if (nip) { nip->x = (ic[0] / ic[3] + 1.0f) * 0.5f; nip->y = (ic[1] / ic[3] + 1.0f) * 0.5f; }
+    float w = 1.0f / (c->area * cosTheta * cosTheta * cosTheta);
+    return V3(w, w, w);
+}
+/* cameras.cl:34-57 */
+static void evalPinholeCameraPdfWe(const mcrt_camera* c, v3 ro, v3 rd, float* pdfPos, float* pdfDir) {
+    float cosTheta = vdot(rd, load3(&c->direction));
+    if (cosTheta <= 0.0f) { *pdfPos = 0.0f; *pdfDir = 0.0f; return; }
+    v3 pf = vadd(ro, vs(rd, 1.0f / cosTheta));
+    float p4[4] = {pf.x, pf.y, pf.z, 1.0f};
+    float ic[4] = {dot4(&c->worldToClip.m0, p4), dot4(&c->worldToClip.m1, p4), dot4(&c->worldToClip.m2, p4),
+                   dot4(&c->worldToClip.m3, p4)};
+    if (ic[0] < -ic[3] || ic[0] > ic[3] || ic[1] < -ic[3] || ic[1] > ic[3]) { *pdfPos = 0.0f; *pdfDir = 0.0f; return; }
+    *pdfPos = 1.0f;
+    *pdfDir = 1.0f / (c->area * cosTheta * cosTheta * cosTheta);
+}
+/* cameras.cl:59-69 */
+static v3 samplePinholeCameraWi(const mcrt_camera* c, const Interaction* si, v3* wi, float* pdf, v2* nip) {
+    *wi = vsub(load3(&c->pos), si->p);
+    float dist = vlength(*wi);
+    *wi = vdivs(*wi, dist);
+    *pdf = (dist * dist) / absDot(load3(&c->direction), *wi);
+    return evalPinholeCameraWe(c, load3(&c->pos), vneg(*wi), nip);
+}
+
+/* samplers.cl:143-149, 200-203 */
+static v3 uniformSampleSphere(v2 u) {
+    float y = 1.0f - 2.0f * u.x;
+    float r = sqrtf(fmaxf(0.0f, 1.0f - y * y));
+    float phi = 2.0f * PI * u.y;
+    return V3(r * cosf(phi), y, r * sinf(phi));
+}
+static inline float cosineHemispherePdf(float cosTheta) { return cosTheta * PI_INV; }
+
+/* lights.cl:148-225 */
+static v3 sampleLightLe(const orc_scene* s, int li, v2 u1, v2 u2, v3* ro, v3* rd, v3* ln, float* pdfPos, float* pdfDir) {
+    const mcrt_light* L = &s->d.lights[li];
+    switch (L->type) {
+    case MCRT_DIRECTIONAL_LIGHT: {
+        ShapeSample si = sampleDisk(load3(&L->p), load3(&L->d), L->radius, u1, pdfPos);
+        *ln = load3(&L->d);
+        *pdfDir = 1.0f;
+        *ro = si.p;
+        *rd = load3(&L->d);
+        return load3(&L->intensity);
+    }
+    case MCRT_POINT_LIGHT:
+        *rd = uniformSampleSphere(u1);
+        *ro = load3(&L->p);
+        *ln = *rd;
+        *pdfPos = 1.0f;
+        *pdfDir = PI4_INV;
+        return load3(&L->intensity);
+    case MCRT_DISK_AREA_LIGHT: {
+        ShapeSample si = sampleDisk(load3(&L->p), load3(&L->d), L->radius, u1, pdfPos);
+        *ln = si.gn;
+        v3 w = cosineSampleHemisphere(u2);
+        *pdfDir = cosineHemispherePdf(w.y);
+        v3 v0 = computeOrthogonalVector(si.gn);
+        v3 v1 = vcross(v0, si.gn);
+        *rd = vadd(vadd(sv(w.x, v0), sv(w.y, si.gn)), sv(w.z, v1));
+        *ro = vadd(si.p, vs(si.gn, RT_TRACE_OFFSET));
+        return load3(&L->intensity);
+    }
+    case MCRT_TRIANGLE_MESH_AREA_LIGHT: {
+        const mcrt_shape* sh = &s->d.shapes[L->shapeId];
+        int tri = ((int)floorf(u1.x * (float)sh->numTriangles)) % (int)sh->numTriangles;
+        u1.x = u1.x * (float)sh->numTriangles - (float)tri;
+        const uint32_t* I = s->d.indices;
+        uint32_t i0 = I[sh->startIdx + 3 * tri], i1 = I[sh->startIdx + 3 * tri + 1], i2 = I[sh->startIdx + 3 * tri + 2];
+        v3 p0 = transformPoint3(&sh->toWorldTransform, load3(&s->d.positions[sh->startVertex + i0]));
+        v3 p1 = transformPoint3(&sh->toWorldTransform, load3(&s->d.positions[sh->startVertex + i1]));
+        v3 p2 = transformPoint3(&sh->toWorldTransform, load3(&s->d.positions[sh->startVertex + i2]));
+        ShapeSample si = sampleTriangle(p0, p1, p2, u1, pdfPos);
+        *pdfPos = 1.0f / L->area;
+        *ln = si.gn;
+        v3 w = cosineSampleHemisphere(u2);
+        *pdfDir = cosineHemispherePdf(w.y);
+        v3 v0 = computeOrthogonalVector(si.gn);
+        v3 v1 = vcross(v0, si.gn);
+        *rd = vadd(vadd(sv(w.x, v0), sv(w.y, si.gn)), sv(w.z, v1));
+        *ro = vadd(si.p, vs(si.gn, RT_TRACE_OFFSET));
+        return load3(&L->intensity);
+    }
+    }
+    return V3(0, 0, 0);
+}
+/* lights.cl:227-252 (the output pdfs are left unset for unknown types, as the reference) */
+static void evalLightPdfLe(const orc_scene* s, int li, v3 rd, v3 ln, float* pdfPos, float* pdfDir) {
+    const mcrt_light* L = &s->d.lights[li];
+    switch (L->type) {
+    case MCRT_DIRECTIONAL_LIGHT: *pdfPos = 1.0f / L->area; *pdfDir = 0.0f; break;
+    case MCRT_POINT_LIGHT: *pdfPos = 0.0f; *pdfDir = PI4_INV; break;
+    case MCRT_DISK_AREA_LIGHT:
+    case MCRT_TRIANGLE_MESH_AREA_LIGHT: *pdfPos = 1.0f / L->area; *pdfDir = cosineHemispherePdf(vdot(ln, rd)); break;
+    }
+}
+/* lights.cl:45-146 with the light position / normal outputs the BDPT s = 1 strategy uses */
+static v3 sampleLightLiPos(const orc_scene* s, int li, const Interaction* it, v2 u, v3* lpos, v3* lnrm, v3* wi,
+                           float* pdf, Ray* shadow, int* shadowSet) {
+    const mcrt_light* L = &s->d.lights[li];
+    *shadowSet = 0;
+    switch (L->type) {
+    case MCRT_DIRECTIONAL_LIGHT:
+        *wi = vneg(load3(&L->d));
+        *lnrm = V3(0, 0, 0);
+        *lpos = vadd(it->p, vs(vs(*wi, L->radius), 2.0f));
+        *pdf = 1.0f;
+        shadow->o = vadd(it->p, vs(it->gn, it->traceErrorOffset));
+        shadow->tmax = 1000.0f; shadow->d = *wi; shadow->mask = -1; shadow->active = -1;
+        *shadowSet = 1;
+        return load3(&L->intensity);
+    case MCRT_POINT_LIGHT: {
+        *wi = vsub(load3(&L->p), it->p);
+        float distSq = vdot(*wi, *wi);
+        if (isNearZero(distSq)) return V3(0, 0, 0);   /* Q13: pdf, position and ray unset */
+        float dist = sqrtf(distSq);
+        *wi = vdivs(*wi, dist);
+        *lnrm = V3(0, 0, 0);
+        *pdf = 1.0f;
+        shadow->o = vadd(it->p, vs(it->gn, it->traceErrorOffset));
+        *lpos = load3(&L->p);
+        shadow->tmax = dist; shadow->d = *wi; shadow->mask = -1; shadow->active = -1;
+        *shadowSet = 1;
+        return vdivs(load3(&L->intensity), distSq);
+    }
+    case MCRT_DISK_AREA_LIGHT: {
+        ShapeSample si = sampleDisk(load3(&L->p), load3(&L->d), L->radius, u, pdf);
+        *lnrm = si.gn;
+        *lpos = si.p;
+        v3 ro = vadd(it->p, vs(it->gn, it->traceErrorOffset));
+        v3 rt = vadd(si.p, vs(si.gn, RT_TRACE_OFFSET));
+        *wi = vnormalize(vsub(rt, ro));
+        float distSq = distanceSquared(si.p, it->p);
+        float c = absDot(si.gn, vneg(*wi));
+        if (isNearZero(c)) { *pdf = 0.0f; return V3(0, 0, 0); }
+        *pdf *= distSq / c;
+        shadow->o = ro; shadow->tmax = vlength(vsub(ro, rt)); shadow->d = *wi; shadow->mask = -1; shadow->active = -1;
+        *shadowSet = 1;
+        return vdot(si.gn, vneg(*wi)) > 0.0f ? load3(&L->intensity) : V3(0, 0, 0);
+    }
+    case MCRT_TRIANGLE_MESH_AREA_LIGHT: {
+        const mcrt_shape* sh = &s->d.shapes[L->shapeId];
+        int tri = ((int)floorf(u.x * (float)sh->numTriangles)) % (int)sh->numTriangles;
+        u.x = u.x * (float)sh->numTriangles - (float)tri;
+        const uint32_t* I = s->d.indices;
+        uint32_t i0 = I[sh->startIdx + 3 * tri], i1 = I[sh->startIdx + 3 * tri + 1], i2 = I[sh->startIdx + 3 * tri + 2];
+        v3 p0 = transformPoint3(&sh->toWorldTransform, load3(&s->d.positions[sh->startVertex + i0]));
+        v3 p1 = transformPoint3(&sh->toWorldTransform, load3(&s->d.positions[sh->startVertex + i1]));
+        v3 p2 = transformPoint3(&sh->toWorldTransform, load3(&s->d.positions[sh->startVertex + i2]));
+        ShapeSample si = sampleTriangle(p0, p1, p2, u, pdf);
+        *lnrm = si.gn;
+        *lpos = si.p;
+        *pdf = 1.0f / L->area;
+        v3 ro = vadd(it->p, vs(it->gn, it->traceErrorOffset));
+        v3 rt = vadd(si.p, vs(si.gn, RT_TRACE_OFFSET));
+        *wi = vnormalize(vsub(si.p, it->p));
+        float distSq = distanceSquared(si.p, it->p);
+        float c = absDot(si.gn, vneg(*wi));
+        if (isNearZero(c)) { *pdf = 0.0f; return V3(0, 0, 0); }
+        *pdf *= distSq / c;
+        shadow->o = ro; shadow->tmax = vlength(vsub(ro, rt)); shadow->d = *wi; shadow->mask = -1; shadow->active = -1;
+        *shadowSet = 1;
+        return vdot(si.gn, vneg(*wi)) > 0.0f ? load3(&L->intensity) : V3(0, 0, 0);
+    }
+    }
+    return V3(0, 0, 0);
+}
+
+/* materials.cl:93-179 (uber only; other material types evaluate to zero) */
+static int isUberMat(const orc_scene* s, int mi) { return s->d.materials[mi].type == 0; }
+static float evaluateMaterialPdf(const orc_scene* s, int mi, v3 wo, v3 wi, const Interaction* si) {
+    if (!isUberMat(s, mi)) return 0.0f;
+    UberProps um;
+    getUberProps(s, mi, si, &um);
+    return evaluateUberBSDF_Pdf(&um, si, wo, wi, BSDF_ALL);
+}
+static v3 evaluateMaterial(const orc_scene* s, int mi, v3 wo, v3 wi, const Interaction* si, int mode) {
+    if (!isUberMat(s, mi)) return V3(0, 0, 0);
+    UberProps um;
+    getUberProps(s, mi, si, &um);
+    return evaluateUberBSDF(&um, si, wo, wi, mode);
+}
+static int hasMaterialNonDeltaComponents(const orc_scene* s, int mi, const Interaction* si) {
+    const mcrt_material* m = &s->d.materials[mi];
+    if (m->type != 0) return 0;
+    v3 Kd = load3(&m->uber_kd), Ks = load3(&m->uber_ks), op = load3(&m->uber_opacity);
+    if (m->uber_diffuseTexId != -1) { f4 t = readTex(s, m->uber_diffuseTexId, si->uv); Kd = V3(t.x, t.y, t.z); }
+    if (m->uber_glossyTexId != -1) { f4 t = readTex(s, m->uber_glossyTexId, si->uv); Ks = V3(t.x, t.y, t.z); }
+    if (m->uber_opacityTexId != -1) { f4 t = readTex(s, m->uber_opacityTexId, si->uv); op = V3(t.x, t.y, t.z); }
+    return !isBlack(vmul(Kd, op)) || !isBlack(vmul(Ks, op));
+}
+
+/* BDPT.cl:22-35 */
+static float computeShadingNormalCorrection(const Interaction* in, v3 wo, v3 wi, int mode) {
+    if (mode == TRANSPORT_MODE_IMPORTANCE_) {
+        float denom = absDot(wo, in->gn) * absDot(wi, in->sn);
+        if (isNearZero(denom)) return 0.0f;
+        return (absDot(wo, in->sn) * absDot(wi, in->gn)) / denom;
+    }
+    return 1.0f;
+}
+/* BDPT.cl:45-60 */
+static float convertVertexDensity(float pdf, const BVert* th, const BVert* nx) {
+    if (nx->flags & BVF_INFINITE_LIGHT) return pdf;
+    v3 w = vsub(nx->in.p, th->in.p);
+    float lenSq = vdot(w, w);
+    if (isNearZero(lenSq)) return 0.0f;
+    float invDistSq = 1.0f / lenSq;
+    if (bvOnSurface(nx)) pdf *= absDot(nx->in.gn, vs(w, sqrtf(invDistSq)));
+    return pdf * invDistSq;
+}
+/* BDPT.cl:62-91 */
+static float evalVertexPdfLight(const orc_scene* s, const BVert* th, const BVert* v) {
+    v3 w = vsub(v->in.p, th->in.p);
+    float lenSq = vdot(w, w);
+    if (isNearZero(lenSq)) return 0.0f;
+    float invDistSq = 1.0f / lenSq;
+    w = vs(w, sqrtf(invDistSq));
+    float pdf;
+    if (th->flags & BVF_INFINITE_LIGHT) {
+        float radius = s->d.lights[th->lightIdx].radius;
+        pdf = 1.0f / (PI * radius * radius);
+    } else {
+        float pdfPos = 0.0f, pdfDir = 0.0f;
+        evalLightPdfLe(s, th->lightIdx, w, th->in.gn, &pdfPos, &pdfDir);
+        pdf = pdfDir * invDistSq;
+    }
+    if (bvOnSurface(v)) pdf *= absDot(v->in.gn, w);
+    return pdf;
+}
+/* BDPT.cl:93-132 */
+static float evalVertexPdf(const orc_scene* s, const mcrt_camera* cam, const BVert* th, const BVert* prev, const BVert* next) {
+    if (th->type == BV_LIGHT) return evalVertexPdfLight(s, th, next);
+    v3 wn = vsub(next->in.p, th->in.p);
+    float lenSq = vdot(wn, wn);
+    if (isNearZero(lenSq)) return 0.0f;
+    wn = vdivs(wn, sqrtf(lenSq));
+    float pdf = 0.0f, unused;
+    if (th->type == BV_CAMERA) {
+        evalPinholeCameraPdfWe(cam, th->in.p, wn, &unused, &pdf);
+    } else if (th->type == BV_SURFACE) {
+        v3 wp = V3(0, 0, 0);
+        if (prev) {
+            wp = vsub(prev->in.p, th->in.p);
+            lenSq = vdot(wp, wp);
+            if (isNearZero(lenSq)) return 0.0f;
+            wp = vdivs(wp, sqrtf(lenSq));
+        }
+        Interaction in = th->in;
+        pdf = evaluateMaterialPdf(s, th->materialIdx, wp, wn, &in);
+    }
+    return convertVertexDensity(pdf, th, next);
+}
+/* BDPT.cl:135-152 */
+static float evalVertexPdfLightOrigin(const orc_scene* s, const BVert* th, v3 nextPos) {
+    v3 w = vsub(nextPos, th->in.p);
+    float lenSq = vdot(w, w);
+    if (isNearZero(lenSq)) return 0.0f;
+    w = vs(w, sqrtf(1.0f / lenSq));
+    if (th->flags & BVF_INFINITE_LIGHT) return 0.0f;
+    float pdfPos = 0.0f, pdfDir = 0.0f;
+    evalLightPdfLe(s, th->lightIdx, w, th->in.gn, &pdfPos, &pdfDir);
+    return pdfPos * s->d.lights[th->lightIdx].choicePdf;
+}
+/* BDPT.cl:157-174 */
+static BVert createCameraVertex(v3 p, v3 throughput) {
+    BVert v;
+    memset(&v, 0, sizeof(v));
+    v.throughput = throughput;
+    v.in.p = p;
+    v.in.gn = V3(0, 0, 0);
+    v.type = BV_CAMERA;
+    v.flags = BVF_CONNECTIBLE;
+    v.lightIdx = -1;
+    return v;
+}
+/* BDPT.cl:176-203 */
+static BVert createLightVertex(int li, v3 p, v3 ln, v3 throughput, float pdfFwd, int lightFlags) {
+    BVert v;
+    memset(&v, 0, sizeof(v));
+    v.throughput = throughput;
+    v.in.p = p;
+    v.in.gn = ln;
+    v.in.sn = ln;
+    v.in.traceErrorOffset = RT_TRACE_OFFSET;
+    v.type = BV_LIGHT;
+    v.lightIdx = li;
+    v.pdfFwd = pdfFwd;
+    if (lightFlags & MCRT_LIGHT_FLAG_DELTA_DIRECTION) v.flags = BVF_DELTA_LIGHT | BVF_INFINITE_LIGHT;
+    else {
+        v.flags = BVF_CONNECTIBLE;
+        if (lightFlags & MCRT_LIGHT_FLAG_DELTA_POSITION) v.flags |= BVF_DELTA_LIGHT;
+    }
+    return v;
+}
+/* BDPT.cl:214-234 */
+static v3 evalVertex_f(const orc_scene* s, const BVert* th, const BVert* nx, int mode) {
+    v3 wi = vsub(nx->in.p, th->in.p);
+    float lenSq = vdot(wi, wi);
+    if (isNearZero(lenSq)) return V3(0, 0, 0);
+    wi = vdivs(wi, sqrtf(lenSq));
+    if (th->type == BV_SURFACE) {
+        Interaction si = th->in;
+        v3 f = evaluateMaterial(s, th->materialIdx, si.wo, wi, &si, mode);
+        return vs(f, computeShadingNormalCorrection(&si, si.wo, wi, mode));
+    }
+    return V3(1.0f, 0.0784f, 0.5765f);
+}
+static inline float remap0(float f) { return f == 0.0f ? 1.0f : f; }   /* BDPT.cl:650-653 */
+
+/* atomicAdd_f (BDPT.cl:655-669): CAS loop on the float bits */
+static void atomicAddF(float* addr, float val) {
+    _Atomic uint32_t* a = (_Atomic uint32_t*)addr;
+    uint32_t cur = atomic_load_explicit(a, memory_order_relaxed);
+    for (;;) {
+        float f;
+        memcpy(&f, &cur, 4);
+        f += val;
+        uint32_t nx;
+        memcpy(&nx, &f, 4);
+        if (atomic_compare_exchange_weak_explicit(a, &cur, nx, memory_order_relaxed, memory_order_relaxed)) return;
+    }
+}
+
+struct orc_bdpt {
+    int W, H, D;
+    BVert* sampledLight;   /* W*H*D, persistent across frames (read before it is overwritten, BDPT.cl:585-586) */
+    float* final3;         /* finalRadianceBuffer, 3 floats per pixel */
+    int32_t* camCount;
+    int32_t* lightCount;
+};
+orc_bdpt* orc_bdpt_create(int W, int H, int D) {
+    orc_bdpt* b = (orc_bdpt*)calloc(1, sizeof(orc_bdpt));
+    b->W = W; b->H = H; b->D = D;
+    const size_t N = (size_t)W * H;
+    b->sampledLight = (BVert*)calloc(N * (size_t)D, sizeof(BVert));   /* zero-filled like the clref runner */
+    b->final3 = (float*)calloc(3 * N, sizeof(float));
+    b->camCount = (int32_t*)calloc(N, sizeof(int32_t));
+    b->lightCount = (int32_t*)calloc(N, sizeof(int32_t));
+    return b;
+}
+void orc_bdpt_destroy(orc_bdpt* b) {
+    if (!b) return;
+    free(b->sampledLight); free(b->final3); free(b->camCount); free(b->lightCount);
+    free(b);
+}
+
+typedef struct {
+    const orc_scene* s; orc_bdpt* b; const mcrt_camera* cam;
+    int frame, sampler;
+    const int32_t* rows;
+    atomic_llong stats[4];   /* subpath rays traced, their node visits, connection rays traced, their visits */
+} BdptCtx;
+
+/* GenerateSecondaryVertices (BDPT.cl:317-458) for one pixel and depth */
+static void bdptSecondary(BdptCtx* c, uint32_t bufferIdx, int isCam, int curDepth, BVert* verts, int* count, Ray* ray,
+                          const mcrt_intersection* isect, v3* throughput, float* fwdPdf) {
+    const orc_scene* s = c->s;
+    const int D = c->b->D, W = c->b->W, H = c->b->H;
+    Sampler smp;
+    makeSampler(&smp, c->sampler, bufferIdx, c->frame, curDepth + (D + 1) * isCam, W, H, s->d.sobol_matrices);
+    const int shapeIdx = isect->shapeid, prim = isect->primid;
+    if (!ray->active || shapeIdx == -1 || prim == -1 || s->d.shapes[shapeIdx].materialId == -1) { ray->active = 0; return; }
+    (*count)++;
+    Interaction si;
+    computeSurfaceInteraction(s, shapeIdx, prim, isect->uvwt.x, isect->uvwt.y, &si);
+    si.wo = vneg(ray->d);
+    si.traceErrorOffset = vdot(si.gn, si.wo) < 0.0f ? -RT_TRACE_OFFSET : RT_TRACE_OFFSET;
+    const int mi = s->d.shapes[shapeIdx].materialId;
+    applyNormalMapping(s, mi, &si);
+    BVert* cur = &verts[curDepth];
+    BVert* prev = &verts[curDepth - 1];
+    const int mode = isCam ? TRANSPORT_MODE_RADIANCE : TRANSPORT_MODE_IMPORTANCE_;
+    float pdfFwd = *fwdPdf;
+    /* setSurfaceVertex (BDPT.cl:205-212) */
+    cur->throughput = *throughput;
+    cur->in = si;
+    cur->type = BV_SURFACE;
+    cur->materialIdx = mi;
+    cur->flags = 0;
+    cur->pdfRev = 0.0f;
+    cur->pdfFwd = convertVertexDensity(pdfFwd, prev, cur);
+    cur->lightIdx = s->d.shapes[shapeIdx].lightID;
+    if (!isCam && curDepth == 1 && (prev->flags & BVF_INFINITE_LIGHT)) {
+        cur->pdfFwd = prev->pdfPos;
+        if (bvOnSurface(cur)) cur->pdfFwd *= absDot(ray->d, si.gn);
+        prev->pdfFwd = 0.0f;
+    }
+    if (curDepth == D + isCam) {
+        if (hasMaterialNonDeltaComponents(s, mi, &si)) cur->flags |= BVF_CONNECTIBLE;
+        ray->active = 0;
+        return;
+    }
+    v3 wi = V3(0, 0, 0), wo = si.wo;
+    int sampledType = 0, numNonDelta = 0;
+    v2 bs = getSample2D(&smp);
+    v3 f = V3(0, 0, 0);
+    if (isUberMat(s, mi)) {
+        UberProps um;
+        getUberProps(s, mi, &si, &um);
+        f = sampleUberBSDF(&um, &si, bs, mode, BSDF_ALL, wo, &wi, &pdfFwd, &numNonDelta, &sampledType);
+    }
+    cur->in = si;
+    if (numNonDelta > 0) cur->flags |= BVF_CONNECTIBLE;
+    if (isBlack(f) || isNearZero(pdfFwd)) { ray->active = 0; return; }
+    *throughput = vmul(*throughput, vdivs(vs(f, absDot(wi, si.sn)), pdfFwd));
+    float pdfRev;
+    if (sampledType & BSDF_SPECULAR) {
+        cur->flags |= BVF_DELTA;
+        pdfFwd = 0.0f;
+        pdfRev = 0.0f;
+    } else {
+        pdfRev = evaluateMaterialPdf(s, mi, wi, wo, &si);
+    }
+    float off = si.traceErrorOffset;
+    if ((sampledType & BSDF_TRANSMISSION) != 0 && vdot(si.gn, wi) * signf(off) < 0.0f) off *= -1.0f;
+    ray->o = vadd(si.p, vs(si.gn, off));
+    ray->tmax = RT_MAX_TRACE_DISTANCE;
+    ray->d = wi;
+    ray->mask = -1;
+    ray->active = -1;
+    *throughput = vs(*throughput, computeShadingNormalCorrection(&si, wo, wi, mode));
+    prev->pdfRev = convertVertexDensity(pdfRev, cur, prev);
+    *fwdPdf = pdfFwd;
+}
+
+static void bdptPixel(void* vc, int64_t i, uint32_t* stack) {
+    BdptCtx* c = (BdptCtx*)vc;
+    const orc_scene* s = c->s;
+    orc_bdpt* b = c->b;
+    const mcrt_camera* cam = c->cam;
+    const int W = b->W, H = b->H, D = b->D;
+    const int y = c->rows ? c->rows[i / W] : (int)(i / W), x = (int)(i % W);
+    const uint32_t bufferIdx = (uint32_t)(x + y * W);
+    const int maxCam = D + 2, maxLight = D + 1;
+    const int C = maxCam * (maxCam + 1) / 2 - 2;
+    BVert cv[34], lv[33];
+    int64_t nSub = 0, vSub = 0, nConn = 0, vConn = 0;
+    uint8_t* const tch = s->touched;
+    const int64_t NN = s->num_nodes;
+    /* ---- GenerateStartVertices (BDPT.cl:240-312) ---- */
+    Sampler smp;
+    makeSampler(&smp, c->sampler, bufferIdx, c->frame, 0, W, H, s->d.sobol_matrices);
+    int camCount = 1, lightCount = 1;
+    float rx = 1.0f / (float)W, ry = 1.0f / (float)H;
+    Ray cray;
+    cray.o = load3(&cam->pos); cray.tmax = RT_MAX_TRACE_DISTANCE;
+    cray.d = lerpDirection(load3(&cam->r00), load3(&cam->r10), load3(&cam->r11), load3(&cam->r01), (float)x * rx, (float)y * ry);
+    cray.mask = -1; cray.active = -1;
+    cv[0] = createCameraVertex(load3(&cam->pos), V3(1, 1, 1));
+    v3 camT = cv[0].throughput;
+    float pdfPos = 0.0f, pdfDir = 0.0f;
+    evalPinholeCameraPdfWe(cam, load3(&cam->pos), cray.d, &pdfPos, &pdfDir);
+    float camFwd = pdfDir;
+    const int nl = (int)s->d.num_lights;
+    int chosen = (int)((uint32_t)floorf(getSample1D(&smp) * (float)nl) % (uint32_t)nl);
+    float lightPdf = s->d.lights[chosen].choicePdf;
+    v2 u1 = getSample2D(&smp);
+    v2 u2 = getSample2D(&smp);
+    v3 ro = V3(0, 0, 0), rd = V3(0, 0, 0), ln = V3(0, 0, 0);
+    v3 Le = sampleLightLe(s, chosen, u1, u2, &ro, &rd, &ln, &pdfPos, &pdfDir);
+    Ray lray;
+    lray.o = ro; lray.tmax = RT_MAX_TRACE_DISTANCE; lray.d = rd; lray.mask = -1; lray.active = -1;
+    lv[0] = createLightVertex(chosen, ro, ln, Le, pdfPos * lightPdf, s->d.lights[chosen].flags);
+    lv[0].pdfPos = pdfPos;
+    v3 lightT = vdivs(vs(Le, absDot(ln, rd)), lightPdf * pdfPos * pdfDir);
+    float lightFwd = pdfDir;
+    /* ---- camera subpath, then light subpath: RR QueryIntersection + GenerateSecondaryVertices ---- */
+    mcrt_intersection isect;
+    isect.shapeid = isect.primid = -1;
+    for (int d = 1; d <= D + 1; ++d) {
+        if (cray.active) {
+            int nv = 0;
+            traceClosest(s, &cray, &isect, stack, &nv, tch ? tch + NN : NULL);
+            nSub++; vSub += nv;
+        }
+        bdptSecondary(c, bufferIdx, 1, d, cv, &camCount, &cray, &isect, &camT, &camFwd);
+    }
+    isect.shapeid = isect.primid = -1;
+    for (int d = 1; d <= D; ++d) {
+        if (lray.active) {
+            int nv = 0;
+            traceClosest(s, &lray, &isect, stack, &nv, tch ? tch + NN : NULL);
+            nSub++; vSub += nv;
+        }
+        bdptSecondary(c, bufferIdx, 0, d, lv, &lightCount, &lray, &isect, &lightT, &lightFwd);
+    }
+    b->camCount[bufferIdx] = camCount;
+    b->lightCount[bufferIdx] = lightCount;
+    /* ---- PrepareConnections (BDPT.cl:460-646) ---- */
+    makeSampler(&smp, c->sampler, bufferIdx, c->frame, maxLight + maxCam, W, H, s->d.sobol_matrices);
+    v3 rad[40];
+    Ray conn[40];
+    BVert sampledCam[32];
+    int slot = 0;
+    for (int t = 1; t <= camCount; ++t)
+        for (int sI = 0; sI <= lightCount; ++sI) {
+            const int depth = t + sI - 2;
+            if ((t == 1 && sI == 1) || depth < 0 || depth > D) continue;
+            BVert* cvx = &cv[t - 1];
+            rad[slot] = V3(0, 0, 0);
+            conn[slot].active = 0;
+            if (sI == 0) {
+                /* nothing: the connection ray keeps what the buffer held (inactive in ConnectVertices' use) */
+            } else if (t == 1) {
+                BVert* lvx = &lv[sI - 1];
+                if (lvx->flags & BVF_CONNECTIBLE) {
+                    Interaction li = lvx->in;
+                    v3 wi;
+                    float pdf;
+                    v2 nip = {(float)x / (float)W, (float)y / (float)H};
+                    v3 imp = samplePinholeCameraWi(cam, &li, &wi, &pdf, &nip);
+                    if (pdf > 0.0f && isNotBlack(imp)) {
+                        BVert* sc = &sampledCam[sI - 2];
+                        *sc = createCameraVertex(load3(&cam->pos), vdivs(imp, pdf));
+                        int ix = (int)floorf(nip.x * (float)W + 0.5f), iy = (int)floorf(nip.y * (float)H + 0.5f);
+                        ix = ix < 0 ? 0 : (ix > W - 1 ? W - 1 : ix);
+                        iy = iy < 0 ? 0 : (iy > H - 1 ? H - 1 : iy);
+                        sc->radianceBufferIdx = ix + iy * W;
+                        rad[slot] = vmul(vmul(lvx->throughput, sc->throughput), evalVertex_f(s, lvx, sc, TRANSPORT_MODE_IMPORTANCE_));
+                        if (bvOnSurface(lvx)) rad[slot] = vs(rad[slot], absDot(wi, li.sn));
+                        v3 o = vadd(li.p, vs(li.gn, lvx->in.traceErrorOffset));
+                        float dist = vlength(vsub(o, load3(&cam->pos)));
+                        conn[slot].o = o; conn[slot].tmax = dist; conn[slot].d = vdivs(vsub(load3(&cam->pos), o), dist);
+                        conn[slot].mask = -1; conn[slot].active = -1;
+                    }
+                }
+            } else if (sI == 1) {
+                if (cvx->flags & BVF_CONNECTIBLE) {
+                    v3 wi = V3(0, 0, 0), lpos = V3(0, 0, 0), lnrm = V3(0, 0, 0);
+                    float pdf = 0.0f;
+                    int ch = (int)floorf(getSample1D(&smp) * (float)nl);
+                    if (ch > nl - 1) ch = nl - 1;
+                    float lp = s->d.lights[ch].choicePdf;
+                    Interaction ci = cvx->in;
+                    Ray shadow;
+                    shadow.active = 0;
+                    int shadowSet = 0;
+                    v2 u = getSample2D(&smp);
+                    v3 Li = sampleLightLiPos(s, ch, &ci, u, &lpos, &lnrm, &wi, &pdf, &shadow, &shadowSet);
+                    if (shadowSet) conn[slot] = shadow;
+                    if (isNotNearZero(pdf) && isNotBlack(Li)) {
+                        BVert* sl = &b->sampledLight[(size_t)bufferIdx * D + t - 2];
+                        float pf = evalVertexPdfLightOrigin(s, sl, cvx->in.p);   /* the previous content (BDPT.cl:585) */
+                        *sl = createLightVertex(ch, lpos, lnrm, vdivs(Li, lp * pdf), pf, s->d.lights[ch].flags);
+                        v3 f = evaluateMaterial(s, cvx->materialIdx, ci.wo, wi, &ci, TRANSPORT_MODE_RADIANCE);
+                        rad[slot] = vmul(vmul(cvx->throughput, sl->throughput), f);
+                        if (bvOnSurface(cvx)) rad[slot] = vs(rad[slot], absDot(wi, ci.sn));
+                    } else {
+                        conn[slot].active = 0;
+                    }
+                }
+            } else {
+                BVert* lvx = &lv[sI - 1];
+                if ((cvx->flags & BVF_CONNECTIBLE) && (lvx->flags & BVF_CONNECTIBLE)) {
+                    v3 lvf = evalVertex_f(s, lvx, cvx, TRANSPORT_MODE_IMPORTANCE_);
+                    v3 cvf = evalVertex_f(s, cvx, lvx, TRANSPORT_MODE_RADIANCE);
+                    v3 lp = vadd(lvx->in.p, vs(lvx->in.gn, lvx->in.traceErrorOffset));
+                    v3 cp = vadd(cvx->in.p, vs(cvx->in.gn, cvx->in.traceErrorOffset));
+                    v3 w = vsub(cp, lp);
+                    float sqDist = vdot(w, w);
+                    float dist = sqrtf(sqDist);
+                    w = vdivs(w, dist);
+                    if (isNotNearZero(sqDist)) {
+                        float g = absDot(cvx->in.sn, w) * absDot(lvx->in.sn, w) / sqDist;
+                        rad[slot] = vs(vmul(vmul(vmul(lvx->throughput, cvx->throughput), lvf), cvf), g);
+                    }
+                    if (isNotBlack(rad[slot])) {
+                        conn[slot].o = lp; conn[slot].tmax = dist; conn[slot].d = w; conn[slot].mask = -1; conn[slot].active = -1;
+                    }
+                }
+            }
+            ++slot;
+        }
+    (void)C;
+    /* ---- RR QueryOcclusion over the connection rays + ConnectVertices (BDPT.cl:671-913) ---- */
+    float* out = b->final3;
+    slot = 0;
+    for (int t = 1; t <= camCount; ++t)
+        for (int sI = 0; sI <= lightCount; ++sI) {
+            const int depth = t + sI - 2;
+            if ((t == 1 && sI == 1) || depth < 0 || depth > D) continue;
+            BVert* pt0 = &cv[t - 1];
+            if (sI == 0) {
+                if (bvLight(pt0)) rad[slot] = vmul(evalLightLe(&s->d.lights[pt0->lightIdx], pt0->in.gn, pt0->in.wo), pt0->throughput);
+            } else {
+                float vis = 0.0f;
+                if (conn[slot].active) {
+                    int anv = 0;
+                    int occ = traceAny(s, &conn[slot], stack, &anv, tch ? tch + 2 * NN : NULL);
+                    nConn++; vConn += anv;
+                    vis = occ != -1 ? 0.0f : 1.0f;
+                }
+                rad[slot] = vs(rad[slot], vis);
+            }
+            float mis = 1.0f;
+            if (isBlack(rad[slot])) mis = 0.0f;
+            else if (sI + t == 2) mis = 1.0f;
+            else {
+                float sumRi = 0.0f;
+                BVert* qs = sI > 0 ? &lv[sI - 1] : NULL;
+                BVert* pt = t > 0 ? &cv[t - 1] : NULL;
+                BVert* qsPrev = sI > 1 ? &lv[sI - 2] : NULL;
+                BVert* ptPrev = t > 1 ? &cv[t - 2] : NULL;
+                BVert backup;
+                if (sI == 1) { backup = *qs; *qs = b->sampledLight[(size_t)bufferIdx * D + t - 2]; }
+                else if (t == 1) { backup = *pt; *pt = sampledCam[sI - 2]; }
+                int ptFlags = 0, qsFlags = 0;
+                float ptRev = 0, qsRev = 0, ptPrevRev = 0, qsPrevRev = 0;
+                if (pt) { ptFlags = pt->flags; pt->flags &= ~BVF_DELTA; }
+                if (qs) { qsFlags = qs->flags; qs->flags &= ~BVF_DELTA; }
+                if (pt) { ptRev = pt->pdfRev; pt->pdfRev = sI > 0 ? evalVertexPdf(s, cam, qs, qsPrev, pt) : evalVertexPdfLightOrigin(s, pt, ptPrev->in.p); }
+                if (ptPrev) { ptPrevRev = ptPrev->pdfRev; ptPrev->pdfRev = sI > 0 ? evalVertexPdf(s, cam, pt, qs, ptPrev) : evalVertexPdfLight(s, pt, ptPrev); }
+                if (qs) { qsRev = qs->pdfRev; qs->pdfRev = evalVertexPdf(s, cam, pt, ptPrev, qs); }
+                if (qsPrev) { qsPrevRev = qsPrev->pdfRev; qsPrev->pdfRev = evalVertexPdf(s, cam, qs, pt, qsPrev); }
+                float ri = 1.0f;
+                for (int k = t - 1; k > 0; --k) {
+                    ri *= remap0(cv[k].pdfRev) / remap0(cv[k].pdfFwd);
+                    if (!(cv[k].flags & BVF_DELTA) && !(cv[k - 1].flags & BVF_DELTA)) sumRi += ri;
+                }
+                ri = 1.0f;
+                for (int k = sI - 1; k >= 0; --k) {
+                    ri *= remap0(lv[k].pdfRev) / remap0(lv[k].pdfFwd);
+                    int deltaLight = k > 0 ? (lv[k - 1].flags & BVF_DELTA) != 0 : (lv[0].flags & BVF_DELTA_LIGHT) != 0;
+                    if (!(lv[k].flags & BVF_DELTA) && !deltaLight) sumRi += ri;
+                }
+                if (pt) { pt->flags = ptFlags; pt->pdfRev = ptRev; }
+                if (qs) { qs->flags = qsFlags; qs->pdfRev = qsRev; }
+                if (ptPrev) ptPrev->pdfRev = ptPrevRev;
+                if (qsPrev) qsPrev->pdfRev = qsPrevRev;
+                if (sI == 1) *qs = backup;
+                else if (t == 1) *pt = backup;
+                mis = 1.0f / (1.0f + sumRi);
+            }
+            if (t == 1) {
+                if (isNotBlack(rad[slot])) {
+                    const size_t ri3 = (size_t)sampledCam[sI - 2].radianceBufferIdx * 3;
+                    atomicAddF(out + ri3, rad[slot].x * mis);
+                    atomicAddF(out + ri3 + 1, rad[slot].y * mis);
+                    atomicAddF(out + ri3 + 2, rad[slot].z * mis);
+                }
+            } else {
+                const size_t ri3 = (size_t)bufferIdx * 3;
+                atomicAddF(out + ri3, rad[slot].x * mis);
+                atomicAddF(out + ri3 + 1, rad[slot].y * mis);
+                atomicAddF(out + ri3 + 2, rad[slot].z * mis);
+            }
+            ++slot;
+        }
+    atomic_fetch_add(&c->stats[0], nSub);
+    atomic_fetch_add(&c->stats[1], vSub);
+    atomic_fetch_add(&c->stats[2], nConn);
+    atomic_fetch_add(&c->stats[3], vConn);
+}
+
+/* One RTBDPTPass::update frame over `rows` (NULL = all rows); radiance = CopyBuffer output
+ * (float4 per pixel, W*H*4) -- splats from the rendered rows land in any row.  stats[4]:
+ * subpath rays traced, their node visits, connection rays traced, their node visits. */
+void orc_bdpt_render(orc_scene* s, orc_bdpt* b, const mcrt_camera* cam, int frame, int sampler, const int32_t* rows,
+                     int nrows, int threads, float* radiance, int32_t* camCounts, int32_t* lightCounts, int64_t* stats) {
+    const size_t N = (size_t)b->W * b->H;
+    if (stats) memset(stats, 0, 4 * sizeof(int64_t));
+    memset(b->final3, 0, 3 * N * sizeof(float));   /* GenerateStartVertices clears the pixel (BDPT.cl:264-267) */
+    if (s->nodes && s->d.num_lights > 0) {          /* RTBDPTPass.cpp:69: no lights -> pass skipped */
+        BdptCtx c;
+        c.s = s; c.b = b; c.cam = cam; c.frame = frame; c.sampler = sampler; c.rows = rows;
+        for (int k = 0; k < 4; ++k) atomic_init(&c.stats[k], 0);
+        const int64_t n = rows ? (int64_t)nrows * b->W : (int64_t)N;
+        parallel_for(n, threads, b->W, bdptPixel, &c);
+        if (stats) for (int k = 0; k < 4; ++k) stats[k] = atomic_load(&c.stats[k]);
+    }
+    for (size_t i = 0; i < N; ++i) {   /* CopyBuffer (BDPT.cl:916-931) */
+        radiance[4 * i] = b->final3[3 * i];
+        radiance[4 * i + 1] = b->final3[3 * i + 1];
+        radiance[4 * i + 2] = b->final3[3 * i + 2];
+        radiance[4 * i + 3] = 0.0f;
+    }
+    if (camCounts) memcpy(camCounts, b->camCount, N * sizeof(int32_t));
+    if (lightCounts) memcpy(lightCounts, b->lightCount, N * sizeof(int32_t));
+}

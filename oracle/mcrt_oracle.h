@@ -62,6 +62,13 @@ void orc_brute_any(orc_scene* s, const mcrt_ray* rays, int n, int32_t* hits);
 void orc_render_frame(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,
                       int y0, int y1, int threads, float* radiance, int64_t* stats);
 /* Same, but only every `stride`-th row starting at y0 (bounded CPU-baseline samples). */
+/* BDPT (KRN/BDPT.cl, RTBDPTPass order): persistent per-frame-buffer state (the sampled light
+ * vertices the s = 1 strategy reads from the previous frame) + one frame over rows (NULL = all) */
+typedef struct orc_bdpt orc_bdpt;
+orc_bdpt* orc_bdpt_create(int W, int H, int D);
+void orc_bdpt_destroy(orc_bdpt* b);
+void orc_bdpt_render(orc_scene* s, orc_bdpt* b, const mcrt_camera* cam, int frame, int sampler, const int32_t* rows,
+                     int nrows, int threads, float* radiance, int32_t* camCounts, int32_t* lightCounts, int64_t* stats);
 /* per-node touched marks of later renders: NULL or 4 x num_nodes bytes (bench.py roofline) */
 void orc_set_touched(orc_scene* s, uint8_t* touched);
 void orc_render_rows(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,

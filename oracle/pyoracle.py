@@ -49,6 +49,10 @@ def lib():
         L.orc_brute_any.argtypes = [_vp, _vp, _c.c_int, _vp]
         L.orc_render_frame.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _vp, _vp]
         L.orc_set_touched.argtypes = [_vp, _vp]
+        L.orc_bdpt_create.restype = _vp
+        L.orc_bdpt_create.argtypes = [_c.c_int, _c.c_int, _c.c_int]
+        L.orc_bdpt_destroy.argtypes = [_vp]
+        L.orc_bdpt_render.argtypes = [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp]
         L.orc_render_rows.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _c.c_int, _c.c_int, _vp, _vp]
         L.orc_accumulate.argtypes = [_c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp, _vp]
         L.orc_accumulate_w.argtypes = [_c.c_int, _c.c_int, _c.c_int, _c.c_float, _vp, _vp, _vp, _vp]
@@ -151,6 +155,37 @@ class OracleScene:
         lib().orc_render_rows(self.h, _p(cam), frame, max_depth, sampler, _p(rows), len(rows), threads,
                               _p(radiance), _p(stats))
         return radiance, stats
+
+
+class OracleBDPT:
+    """The oracle's BDPT (KRN/BDPT.cl restated in oracle/mcrt_oracle.c) on an OracleScene: keeps
+    the per-pixel sampled-light-vertex state the s = 1 strategy carries from frame to frame
+    (BDPT.cl:585-586), zero-filled at creation like the reference runner's buffers."""
+
+    def __init__(self, oscene, W, H, max_depth=2):
+        self.o, self.W, self.H, self.D = oscene, W, H, max_depth
+        self.h = lib().orc_bdpt_create(W, H, max_depth)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().orc_bdpt_destroy(self.h)
+        except Exception:
+            pass
+
+    def render(self, cam, frame=0, sampler=1, rows=None, threads=8):
+        """One frame -> (radiance (H, W, 4), camera counts, light counts, stats[4] = subpath rays,
+        their node visits, connection rays, their node visits).  rows: render only these rows'
+        subpaths (their light-tracing splats still land anywhere)."""
+        assert int(cam["width"][0]) == self.W and int(cam["height"][0]) == self.H
+        rad = np.zeros((self.H, self.W, 4), np.float32)
+        cc = np.zeros(self.W * self.H, np.int32)
+        lc = np.zeros(self.W * self.H, np.int32)
+        st = np.zeros(4, np.int64)
+        r = None if rows is None else np.ascontiguousarray(rows, np.int32)
+        lib().orc_bdpt_render(self.o.h, self.h, _p(cam), frame, sampler, _p(r), 0 if r is None else len(r), threads,
+                              _p(rad), _p(cc), _p(lc), _p(st))
+        return rad, cc, lc, st
 
 
 def accumulate(radiance, frame, filt, wsum=None, wts=None):
