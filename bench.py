@@ -16,7 +16,10 @@ Also reported (one JSON line on rank 0):
                 duration in an untimed one-slot pass, vs the 8 TB/s HBM peak; traffic = rocprofv3
                 memory-side bytes per launch from the committed counter summary (profiles/)
   cpu_baseline  the oracle (C restatement of the reference kernels) on a bounded sample of rows of
-                the same frame, all host cores (rank 0, N = 1 only)
+                the same frames, all host cores (rank 0, N = 1 only)
+  bdpt          SURVEY config 4's integrator (BDPT) on the same scene: Mpaths/s (frame split over
+                the ranks), per-kernel times, roofline of its dominant kernel (k_extend) and a CPU
+                baseline of the oracle's BDPT restatement
 """
 import argparse
 import json
@@ -155,6 +158,123 @@ def pmc_traffic(kernel):
         return None
 
 
+def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing):
+    """Config 4's integrator on the same scene and GPU(s): BDPT (RTBDPTPass::update), 1 spp per
+    step, frame split over the ranks (rank r renders frames r, r + N, ...; light-tracing splats land
+    anywhere in the image) and the same single reduce of the accumulators.  Returns the measured
+    numbers plus an untimed one-slot per-kernel timing pass."""
+    import torch
+    import torch.distributed as dist
+    from mcrt import dist as mdist
+    from mcrt import lib
+    from mcrt import types as T
+    fb = lib.FrameBuffer(ctx, W, H)
+    filt = T.make_filter(T.BOX)
+    first = [True]
+
+    def run(i0, count):
+        for i in range(i0, i0 + count):
+            f = rank + world * i
+            fb.render(ds, cam_of(f), frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT)
+            fb.accumulate(filt, 0 if first[0] else f)
+            first[0] = False
+
+    run(0, max(warmup, 2))
+    ctx.sync()
+    f0 = max(warmup, 2)
+    if world > 1:
+        acc_buf, acc_s, acc_w = mdist.packed_accumulators(W * H, "cuda")
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(f0, steps)
+    if world > 1:
+        fb.copy_device(1, acc_s.data_ptr())
+        fb.copy_device(3, acc_w.data_ptr())
+        ctx.sync()
+        mdist.reduce_packed(acc_buf, dst=0)
+        if rank == 0:
+            torch.cuda.synchronize()
+            fb.set_accumulation(acc_s.data_ptr(), acc_w.data_ptr())
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    st = fb.stats()
+    out = {"value": round(W * H * steps * world / el / 1e6, 3), "unit": "Mpaths/s", "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 4), "scaling": "weak",
+           "workload": f"same scene {W}x{H}, BDPT, maxDepth {D}, 1 spp per step (SURVEY config 4's integrator), "
+                       f"frame split x {world} + 1 RCCL reduce",
+           "rays_per_path": {"subpath": round(st["closest_rays"] / (W * H), 4),
+                             "connection": round(st["any_rays"] / (W * H), 4)}}
+    if kernel_timing:
+        fb.set_frames_in_flight(1)
+        run(f0 + steps, 1)
+        ctx.sync()
+        ctx.set_profiling(True)
+        ctx.reset_stats()
+        run(f0 + steps + 1, 2)
+        ctx.sync()
+        ks = ctx.kernel_stats()
+        ctx.set_profiling(False)
+        out["kernels"] = {k: {"avg_ms": round(v["ms"] / max(v["launches"], 1), 4), "launches": v["launches"],
+                              "ms_per_frame": round(v["ms"] / 2, 4)} for k, v in ks.items()}
+    out["_fb"] = fb
+    return out
+
+
+def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s):
+    """BDPT's dominant kernel is k_extend (the closest-hit launches over both subpaths' rays, D + 1
+    per frame).  Compulsory bytes per frame: 48 B per subpath ray (read o, d; write the hit) + 64 B
+    per DISTINCT BVH node the frame's subpath rays visit (counted by the oracle's BDPT on frame 0),
+    over k_extend's time per frame in the one-slot pass.  CPU baseline: the oracle's BDPT on whole
+    frames (its splats land anywhere) of the same cameras, ~target_s of CPU work."""
+    from oracle import pyoracle as po
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    o = oracle
+    if o is None:
+        o = po.OracleScene(scene)
+        o.build()
+    out = {}
+    b = po.OracleBDPT(o, W, H, D)
+    touched = o.track_touched(True)
+    t0 = time.perf_counter()
+    _, _, _, st0 = b.render(cam_of(0), frame=0, threads=threads)
+    first_s = time.perf_counter() - t0
+    o.track_touched(False)
+    n_nodes = int((touched[1] != 0).sum())
+    ks = res.get("kernels", {}).get("k_extend")
+    if ks:
+        ms_frame = ks["ms_per_frame"]
+        rays = res["rays_per_path"]["subpath"] * W * H
+        alg = rays * 48 + 64 * n_nodes
+        ach = alg / (ms_frame * 1e-3) / 1e9
+        out["roofline"] = {"bound": "hbm", "kernel": "k_extend (BDPT, D+1 launches per frame)", "achieved": round(ach, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                           "alg_bytes_per_frame": int(alg), "kernel_ms_per_frame": ms_frame,
+                           "distinct_nodes_per_frame": n_nodes,
+                           "model": "compulsory bytes per frame: 48 B per subpath ray + 64 B per DISTINCT BVH node the "
+                                    "frame's subpath rays visit (oracle BDPT, frame 0)"}
+    # CPU baseline: whole frames 1, 2, ... until ~target_s (frame 0 above carried the node marks)
+    el, frames = 0.0, 0
+    while frames == 0 or el + el / frames <= target_s:
+        t0 = time.perf_counter()
+        b.render(cam_of(1 + frames), frame=1 + frames, threads=threads)
+        el += time.perf_counter() - t0
+        frames += 1
+    out["cpu_baseline"] = {"value": round(W * H * frames / el / 1e6, 4), "unit": "Mpaths/s", "cores": threads,
+                           "kind": "port",
+                           "sample": f"{frames} whole {W}x{H} frames (1..{frames}), D={D}; oracle = C restatement of "
+                                     f"BDPT.cl (RTBDPTPass order) + RR Bvh2/LDS traversal, {threads} threads, {el:.1f}s "
+                                     f"(frame 0, {first_s:.1f}s with node marking, not timed)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -176,6 +296,8 @@ def main():
     ap.add_argument("--stats-launches", type=int, default=4,
                     help="launch sequences of the untimed per-kernel timing pass (one frame slot)")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
+    ap.add_argument("--no-bdpt", action="store_true", help="skip the BDPT object (config 4) of the PT run")
+    ap.add_argument("--bdpt-steps", type=int, default=8, help="timed BDPT frames of the BDPT object")
     ap.add_argument("--save-image", default=None, help="rank 0 saves the final accumulated image (.npy)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the product path); gloo only rehearses N ranks on one GPU")
@@ -324,6 +446,11 @@ def main():
         ctx.set_profiling(False)
         fb.set_frames_in_flight(0)
 
+    bd = None
+    if not bdpt and not args.no_bdpt and not two_level:   # config 4's integrator beside the PT headline
+        bd = bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, args.bdpt_steps, args.warmup,
+                          not args.no_kernel_timing)
+
     paths = W * H * args.steps * (world if bdpt else 1)
     value = paths / elapsed / 1e6
     out = {
@@ -378,7 +505,15 @@ def main():
                 avg_ms = kstats[dom]["ms"] / max(kstats[dom]["launches"], 1)
                 out["roofline"] = roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx,
                                                          cpu["_oracle"] if cpu else None)
+        if bd is not None:
+            bdo = {k: v for k, v in bd.items() if not k.startswith("_")}
+            if oracle_ok and sampler == T.SAMPLER_RANDOM and not args.no_cpu_baseline:
+                bdo.update(bdpt_roofline_and_cpu(scene, cpu["_oracle"] if cpu else None, cam_of, W, H, D, bdo,
+                                                 args.cpu_seconds))
+            out["bdpt"] = bdo
         print(json.dumps(out), flush=True)
+    if bd is not None:
+        bd["_fb"].close()
     fb.close()
     ds.close()
     ctx.close()
