@@ -10,7 +10,7 @@ echo "pytest rc=$rc"; grep -E "PASS|FAIL|Error|assert" gpurun_out/pytest2.log | 
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -s KILL 60 rocprofv3 -L > gpurun_out/counters.txt 2>&1
 echo "counters rc=$?"
-B="python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-roofline-model"
+B="python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-roofline-model --no-bdpt"
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o f -- $B > gpurun_out/pmc_fetch.log 2>&1 || { echo "fetch pass failed"; tail -5 gpurun_out/pmc_fetch.log; exit 5; }
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o w -- $B > gpurun_out/pmc_write.log 2>&1 || { echo "write pass failed"; tail -5 gpurun_out/pmc_write.log; exit 5; }
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY -d gpurun_out/pmc_sq1 -o s -- $B > gpurun_out/pmc_sq1.log 2>&1 || { echo "sq1 pass failed"; tail -5 gpurun_out/pmc_sq1.log; exit 5; }
