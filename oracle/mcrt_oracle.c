@@ -647,6 +647,10 @@ struct orc_scene {
      * [class][node] bytes, class 0 = camera rays, 1 = extension rays, 2 = shadow rays of bounce 0,
      * 3 = shadow rays of later bounces (k_shadow_extend traces classes 1 + 2 together) */
     uint8_t* touched;
+    /* optional per-pixel path log (tools/oracle_divergence.py): pathlog_depth records of
+     * ORC_PATHLOG_FLOATS floats per pixel, layout in mcrt_oracle.h */
+    float* pathlog;
+    int pathlog_depth;
 };
 
 static inline void markTouched(uint8_t* mark, uint32_t node) {
@@ -1501,7 +1505,19 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
     const int64_t NN = s->num_nodes;
     traceClosest(s, &ray, &isect, stack, &nv, tch);
     nprim++; vprim += nv;
+    float* plog = s->pathlog ? s->pathlog + (size_t)bufferIdx * s->pathlog_depth * ORC_PATHLOG_FLOATS : NULL;
     for (int b = 0; b < rc->maxDepth; ++b) {
+        float* L = (plog && b < s->pathlog_depth) ? plog + (size_t)b * ORC_PATHLOG_FLOATS : NULL;
+        if (L) {
+            int32_t iv[2] = {ray.active ? isect.shapeid : -2, isect.primid};
+            memcpy(&L[0], iv, 8);
+            L[2] = isect.uvwt.x; L[3] = isect.uvwt.y; L[4] = isect.uvwt.w;
+            L[24] = ray.o.x; L[25] = ray.o.y; L[26] = ray.o.z;
+            L[27] = ray.d.x; L[28] = ray.d.y; L[29] = ray.d.z; L[30] = ray.tmax; L[31] = 0.0f;
+            int32_t none[3] = {-1, -1, -2};
+            memcpy(&L[5], none, 12);
+            L[21] = 0.0f;
+        }
         v3 temp = V3(0, 0, 0);
         int ignoreOcclusion = 0;
         Ray shadow; shadow.active = 0; int shadowSet = 0;
@@ -1533,6 +1549,7 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
                     v3 wi = V3(0, 0, 0);
                     v2 uL = getSample2D(&smp);
                     v3 Li = sampleLightLi(s, (int)lightIdx, &si, uL, &wi, &lightPdf, &shadow, &shadowSet);
+                    if (L) { int32_t li = (int32_t)lightIdx; memcpy(&L[6], &li, 4); }
                     lightPdf *= s->d.lights[lightIdx].choicePdf;
                     v3 L = V3(0, 0, 0);
                     int mid = sh->materialId;
@@ -1555,6 +1572,7 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
                         getUberProps(s, sh->materialId, &si, &um);
                         v3 f = sampleUberBSDF(&um, &si, bs, TRANSPORT_MODE_RADIANCE, BSDF_ALL, si.wo, &wi, &pdf, &unused, &sampledType);
                         prevBsdfFlags = sampledType;
+                        if (L) { int32_t st = sampledType; memcpy(&L[5], &st, 4); L[22] = bs.x; L[23] = bs.y; }
                         if (isNearZero(pdf) || isBlack(f)) {
                             ray.active = 0;
                         } else {
@@ -1566,6 +1584,10 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
                             ray.o = vadd(si.p, vs(si.gn, off));
                             ray.tmax = RT_MAX_TRACE_DISTANCE;
                             ray.d = wi; ray.mask = -1; ray.active = -1;
+                            if (L) {
+                                L[15] = ray.o.x; L[16] = ray.o.y; L[17] = ray.o.z;
+                                L[18] = ray.d.x; L[19] = ray.d.y; L[20] = ray.d.z; L[21] = 1.0f;
+                            }
                         }
                     } else {
                         ray.active = 0;
@@ -1581,6 +1603,11 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
             int anv = 0;
             occl = traceAny(s, &shadow, stack, &anv, tch ? tch + (b == 0 ? 2 : 3) * NN : NULL);
             nany++; vany += anv;
+            if (L) {
+                int32_t oc = occl; memcpy(&L[7], &oc, 4);
+                L[8] = shadow.o.x; L[9] = shadow.o.y; L[10] = shadow.o.z;
+                L[11] = shadow.d.x; L[12] = shadow.d.y; L[13] = shadow.d.z; L[14] = shadow.tmax;
+            }
         }
         if (!ignoreOcclusion) {
             float V = (!shadowSet || occl != -1) ? 0.0f : 1.0f;
@@ -1643,6 +1670,7 @@ void orc_render_frame(orc_scene* s, const mcrt_camera* cam, int frame, int max_d
 /* touched: NULL (off) or 4 x num_nodes bytes the renders mark (camera / extension / shadow of
  * bounce 0 / later shadow rays) */
 void orc_set_touched(orc_scene* s, uint8_t* touched) { s->touched = touched; }
+void orc_set_pathlog(orc_scene* s, float* log, int depth) { s->pathlog = log; s->pathlog_depth = log ? depth : 0; }
 
 void orc_render_rows(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,
                      const int32_t* rows, int nrows, int threads, float* radiance, int64_t* stats) {

@@ -71,6 +71,15 @@ void orc_bdpt_render(orc_scene* s, orc_bdpt* b, const mcrt_camera* cam, int fram
                      int nrows, int threads, float* radiance, int32_t* camCounts, int32_t* lightCounts, int64_t* stats);
 /* per-node touched marks of later renders: NULL or 4 x num_nodes bytes (bench.py roofline) */
 void orc_set_touched(orc_scene* s, uint8_t* touched);
+/* per-pixel path log of later PT renders (divergence diagnostics, tools/oracle_divergence.py):
+ * NULL (off) or W*H*depth records of ORC_PATHLOG_FLOATS floats, one per bounce b:
+ *   [0] shapeid (int32 bits; -2 = no ray this bounce) [1] primid [2] u [3] v [4] t   (hit of bounce b)
+ *   [5] sampled BxDF type (int32; -1 = none) [6] light index (int32; -1 = none)
+ *   [7] occlusion result (int32; -2 = no shadow query) [8..10] shadow o [11..13] shadow d [14] tmax
+ *   [15..17] next ray o [18..20] next ray d [21] next ray active (1/0) [22..23] BSDF sample u
+ *   [24..26] o [27..29] d [30] tmax of the ray traced for bounce b's hit [31] unused */
+#define ORC_PATHLOG_FLOATS 32
+void orc_set_pathlog(orc_scene* s, float* log, int depth);
 void orc_render_rows(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,
                      const int32_t* rows, int nrows, int threads, float* radiance, int64_t* stats);
 

@@ -49,6 +49,7 @@ def lib():
         L.orc_brute_any.argtypes = [_vp, _vp, _c.c_int, _vp]
         L.orc_render_frame.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _vp, _vp]
         L.orc_set_touched.argtypes = [_vp, _vp]
+        L.orc_set_pathlog.argtypes = [_vp, _vp, _c.c_int]
         L.orc_bdpt_create.restype = _vp
         L.orc_bdpt_create.argtypes = [_c.c_int, _c.c_int, _c.c_int]
         L.orc_bdpt_destroy.argtypes = [_vp]
@@ -145,6 +146,20 @@ class OracleScene:
         self._touched = np.zeros((4, self.num_nodes), np.uint8)
         lib().orc_set_touched(self.h, _p(self._touched))
         return self._touched
+
+    PATHLOG_FLOATS = 32   # ORC_PATHLOG_FLOATS (mcrt_oracle.h)
+
+    def path_log(self, W=None, H=None, depth=2):
+        """Per-pixel path records of later PT renders (divergence diagnostics): returns the
+        (H*W, depth, 32) float32 array the renders fill (layout in mcrt_oracle.h), or switches the
+        log off when W is None."""
+        if W is None:
+            lib().orc_set_pathlog(self.h, None, 0)
+            self._pathlog = None
+            return None
+        self._pathlog = np.zeros((H * W, depth, self.PATHLOG_FLOATS), np.float32)
+        lib().orc_set_pathlog(self.h, _p(self._pathlog), depth)
+        return self._pathlog
 
     def render_rows(self, cam, rows, frame=0, max_depth=2, sampler=1, threads=8, radiance=None):
         W, H = int(cam["width"][0]), int(cam["height"][0])
