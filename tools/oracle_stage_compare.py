@@ -1,0 +1,89 @@
+"""CPU side of the stage-by-stage oracle check (tools/oracle_stage_dump.py makes the reference dump
+on the GPU box): renders the same rows of the headline frame with the oracle under its path log
+and reports, per stage, how often the oracle's float values are bit-identical to the reference
+pipeline's (= the product's) and how the bounce-0 radiance error depends on the barycentrics.
+
+usage: python tools/oracle_stage_compare.py DUMP.npz OUT.json
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "monte-carlo-raytracer_amd"))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def within(a, b):
+    d = np.abs(a[:, :3].astype(np.float64) - b[:, :3])
+    return (d <= 1e-4 * np.maximum(1, np.abs(b[:, :3]))).all(1)
+
+
+def main():
+    from mcrt import types as T
+    from mcrt.camera import scene_camera
+    from oracle import pyoracle as po
+    from clref_job import scale_scene
+    z = np.load(sys.argv[1])
+    rows = z["rows"]
+    W, H = 1920, 1080
+    sc = scale_scene("san_miguel_proxy")
+    cam = scene_camera("san_miguel_proxy", W, H, frame=0, jitter=True)
+    o = po.OracleScene(sc)
+    o.build()
+    rad, logs = {}, {}
+    for D in (1, 2):
+        log = o.path_log(W, H, 2)
+        r, _ = o.render_rows(cam, rows, frame=0, max_depth=D, threads=8)
+        rad[D] = r[rows].reshape(-1, 4)
+        logs[D] = log.reshape(H, W, 2, 32)[rows].reshape(-1, 2, 32).copy()
+    o.path_log(None)
+    res = {"rows": int(len(rows)), "pixels": int(len(rows) * W)}
+    for D in (1, 2):
+        res[f"radiance_within_1e-4_d{D}"] = float(within(rad[D], z[f"radiance_d{D}"].reshape(-1, 4)).mean())
+    L = logs[1]
+    iv = L.view(np.int32)
+    hit = z["isect_d1"].reshape(-1).view(np.uint8).reshape(-1, 32).view(T.ISECT_DTYPE).reshape(-1)
+    same = (iv[:, 0, 0] == hit["shapeid"]) & (iv[:, 0, 1] == hit["primid"]) & (hit["shapeid"] >= 0)
+    res["primary_hit_same_triangle"] = float(same[hit["shapeid"] >= 0].mean())
+    uv = hit["uvwt"]
+    st = {}
+    for k, nm, col in ((2, "u", 0), (3, "v", 1), (4, "t", 3)):
+        st[nm] = float((L[same, 0, k] == uv[same, col]).mean())
+    res["primary_hit_bit_identical"] = st
+    sh = z["shadow_rays_d1"].reshape(-1).view(np.uint8).reshape(-1, 48).view(T.RAY_DTYPE).reshape(-1)
+    m = same & (iv[:, 0, 7] != -2)
+    res["shadow_ray0_bit_identical"] = {
+        "o": float((L[m, 0, 8:11] == sh["o"][m, :3]).all(1).mean()),
+        "d": float((L[m, 0, 11:14] == sh["d"][m, :3]).all(1).mean()),
+        "tmax": float((L[m, 0, 14] == sh["o"][m, 3]).mean())}
+    r1 = z["radiance_d1"].reshape(-1, 4)
+    occ = z["occlusion_d1"].reshape(-1).view(np.int32)
+    m2 = m & ((iv[:, 0, 7] != -1) == (occ != -1))
+    rel = (np.abs(rad[1][m2, :3] - r1[m2, :3]) / np.maximum(1, np.abs(r1[m2, :3]))).max(1)
+    uvsame = ((L[:, 0, 2] == uv[:, 0]) & (L[:, 0, 3] == uv[:, 1]) & (L[:, 0, 4] == uv[:, 3]))[m2]
+    res["bounce0_same_hit_and_visibility"] = {
+        "pixels": int(m2.sum()), "outside_1e-4": float((rel > 1e-4).mean()),
+        "outside_1e-4_when_uvt_bit_identical": float((rel[uvsame] > 1e-4).mean()) if uvsame.any() else None,
+        "pixels_uvt_bit_identical": int(uvsame.sum()),
+        "outside_1e-4_when_uvt_differ": float((rel[~uvsame] > 1e-4).mean()),
+        "by_light": {str(int(li)): float((rel[iv[m2, 0, 6] == li] > 1e-4).mean()) for li in np.unique(iv[m2, 0, 6])}}
+    res["reading"] = (
+        "the oracle's first differing values are the RR hit barycentrics/t: the reference's compiled "
+        "intersect_bvh2_lds.cl computes them with native_recip (v_rcp_f32, 1 ulp) and device-library fma "
+        "chains (dot, cross), the oracle with IEEE 1/x and unfused products (-ffp-contract=off). Wherever "
+        "(u, v, t) come out bit-identical the bounce-0 radiance is inside the 1e-4 band. The ulp offsets "
+        "reach the radiance through the texture coordinate: the proxy's materials tile 1024^2 textures "
+        "4-8x (uv up to 8), so 1 ulp of uv (~1e-6) is ~1e-3 texel after the wrap, and the bilinear fetch "
+        "(textures.cl:103-124) of a high-contrast texel pair moves by that fraction of the contrast. Only "
+        "the sun (light 0, intensity 40, radiance > 1 so the band is relative) carries it past 1e-4; the "
+        "dim mesh light's pixels (light 1) stay inside the absolute 1e-4 band.")
+    json.dump(res, open(sys.argv[2], "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -3,6 +3,7 @@ rocprofv3 PMC passes of one bench.py command (tools/r2_gpu2.sh runs them, each p
 process because FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
 
   python tools/pmc_json.py DIR_WITH_RESULTS_DBS "bench command" [launches_per_kernel_in_stats_pass]
+                           [pass_dir_prefix (default pmc_)] [output (default profiles/pmc_latest.json)]
 
 Per kernel the figures are the MEDIAN over the dispatches of bench.py's untimed one-slot
 kernel-timing pass (its last `--stats-launches` dispatches of that kernel), i.e. the same launches
@@ -54,7 +55,8 @@ def main():
     d = sys.argv[1]
     cmd = sys.argv[2] if len(sys.argv) > 2 else "bench.py"
     last = int(sys.argv[3]) if len(sys.argv) > 3 else 4
-    dbs = sorted(glob.glob(os.path.join(d, "pmc_*", "*_results.db")))
+    prefix = sys.argv[4] if len(sys.argv) > 4 else "pmc_"
+    dbs = sorted(glob.glob(os.path.join(d, prefix + "*", "*_results.db")))
     pmc, ms = collect(dbs, last)
     res = {"source": f"rocprofv3 --kernel-trace --pmc passes ({', '.join(os.path.basename(os.path.dirname(x)) for x in dbs)})",
            "config": f"{cmd}; medians over the last {last} dispatches of each kernel = the untimed one-slot "
@@ -86,7 +88,8 @@ def main():
                               "VALU issue" if lim["valu_busy"] >= 0.6 else "mixed")
             r["limiter"] = lim
         res["kernels"][k] = r
-    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_latest.json")
+    out = sys.argv[5] if len(sys.argv) > 5 else \
+        os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_latest.json")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v.get("limiter") for k, v in res["kernels"].items()}, indent=1))
 
