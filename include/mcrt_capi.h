@@ -193,7 +193,10 @@ typedef struct {
     /* 0 (default): host build that reproduces RadeonRays' Bvh2 node for node (bit-exact parity,
      * seconds for 10 M triangles).  1: on-device linear BVH (Morton order, rocPRIM radix sort;
      * tens of ms), same record format and triangle data, different tree (equal-t hit ties may
-     * resolve differently from the reference).  Ignores the three SAH fields. */
+     * resolve differently from the reference); ignores the three SAH fields.  2: on-device SAH
+     * build that reproduces the same RadeonRays Bvh2 node for node (mcrt_sahbuild.hip: the
+     * reference's split arithmetic incl. this host's _mm_rcp_ps, its partition order in closed
+     * form); byte-identical records to 0; takes the host path for num_bins > 64. */
     int   device_build;
     /* Two-level (instanced) structure: RadeonRays' IntersectorTwoLevel, which RR selects when a
      * shape is an instance (RTScene::attachMesh -> CreateInstance for every further entity that
@@ -293,6 +296,12 @@ MCRT_API mcrt_status mcrt_accel_info(mcrt_scene scene, uint64_t* num_nodes, uint
  * meshes and instances of the two-level one, deepest traversal path. */
 MCRT_API mcrt_status mcrt_accel_layout(mcrt_scene scene, int32_t* two_level, uint32_t* num_meshes,
                                        uint32_t* num_instances, int32_t* depth);
+/* Copy of the device records (64 B each, the mcrt_accel_build_host_records layout) into out
+ * (up to max_records; out may be NULL to query *num_records). */
+MCRT_API mcrt_status mcrt_accel_read_records(mcrt_scene scene, float* out, uint64_t max_records,
+                                             uint64_t* num_records);
+/* Which builder made the flat structure: 0 host (or two-level), 1 device LBVH, 2 device SAH. */
+MCRT_API mcrt_status mcrt_accel_builder(mcrt_scene scene, int32_t* builder);
 /* Host-only build of the structure mcrt_accel_build would upload (no device needed): 64-B
  * records (mcrt_bvh.cpp / mcrt_bvh2l.cpp layouts) into out_records (up to max_records; may be
  * NULL to query *num_records); info[4] = {two_level, top-level records, depth, meshes}.

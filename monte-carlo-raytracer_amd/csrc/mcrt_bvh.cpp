@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "mcrt_internal.h"
+#include "mcrt_sah.h"
 
 namespace mcrt {
 namespace {
@@ -193,6 +194,63 @@ struct Builder {
 };
 
 }  // namespace
+
+// The running host's _mm_rcp_ps, tabulated once per process for the device SAH build
+// (mcrt_sahbuild.hip): R(m) for x = 1.m over the leading mantissa bits the instruction reads,
+// then the device rule (mcrt_sah.h rcp_ps) and the _mm_dp_ps order (sa4) checked against the
+// instructions over every exponent and sign.  ok = false -> the device build is refused.
+const HostRcp& host_rcp_table() {
+    static HostRcp R;
+    static std::once_flag once;
+    std::call_once(once, []() {
+        std::vector<uint32_t> full(1u << 23);
+        for (uint32_t m = 0; m < (1u << 23); m += 4) {
+            alignas(16) uint32_t in[4] = {(127u << 23) | m, (127u << 23) | (m + 1), (127u << 23) | (m + 2),
+                                          (127u << 23) | (m + 3)};
+            const __m128 r = _mm_rcp_ps(_mm_castsi128_ps(_mm_load_si128((const __m128i*)in)));
+            _mm_storeu_si128((__m128i*)&full[m], _mm_castps_si128(r));
+        }
+        int bits = 23;
+        for (int k = 8; k < 23; ++k) {
+            bool same = true;
+            const uint32_t low = (1u << (23 - k)) - 1;
+            for (uint32_t m = 0; m < (1u << 23) && same; ++m) same = full[m] == full[m & ~low];
+            if (same) {
+                bits = k;
+                break;
+            }
+        }
+        R.bits = bits;
+        R.t.resize((size_t)1 << bits);
+        for (uint32_t m = 0; m < (1u << bits); ++m) R.t[m] = full[(size_t)m << (23 - bits)];
+        bool ok = true;
+        uint32_t x = 0x12345u;
+        for (uint32_t e = 0; e < 256 && ok; ++e)
+            for (int t = 0; t < 512 && ok; ++t) {
+                x = x * 1664525u + 1013904223u;
+                const uint32_t b = (x & 0x807fffffu) | (e << 23);
+                float f;
+                std::memcpy(&f, &b, 4);
+                const float want = _mm_cvtss_f32(_mm_rcp_ss(_mm_set_ss(f)));
+                const float got = sah::rcp_ps(f, R.t.data(), bits);
+                if (std::memcmp(&want, &got, 4) != 0 && !(std::isnan(want) && std::isnan(got))) ok = false;
+            }
+        for (int t = 0; t < 4096 && ok; ++t) {
+            alignas(16) float a[4], c[4];
+            for (int k = 0; k < 4; ++k) {
+                x = x * 1664525u + 1013904223u;
+                a[k] = (float)(x >> 8) * 5.9604645e-8f * 2000.0f - 1000.0f;
+                x = x * 1664525u + 1013904223u;
+                c[k] = (float)(x >> 8) * 5.9604645e-8f * 2000.0f - 1000.0f;
+            }
+            const float want = lane(sa4(_mm_load_ps(a), _mm_load_ps(c)), 0);
+            const float got = sah::sa4(sah::V4{a[0], a[1], a[2], a[3]}, sah::V4{c[0], c[1], c[2], c[3]});
+            if (std::memcmp(&want, &got, 4) != 0) ok = false;
+        }
+        R.ok = ok;
+    });
+    return R;
+}
 
 bool build_bvh(const float* tri, const int32_t* shapeOf, const int32_t* primOf, std::size_t n, float cost, int bins,
                bool sah, int threads, BvhOut& out) {

@@ -94,6 +94,7 @@ struct mcrt_scene_s {
     uint64_t numNodes = 0;
     uint32_t numTris = 0;
     double buildMs = 0.0;
+    int builder = 0;   // which builder made the flat structure: 0 host, 1 device LBVH, 2 device SAH
     int bvhDepth = 0;
     bool twoLevel = false;          // instanced scene: two-level records (mcrt_bvh2l.cpp)
     int numMeshes = 0, numInstances = 0;
@@ -678,7 +679,37 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     }
     s->twoLevel = false;
     s->numMeshes = s->numInstances = 0;
-    if (opts && opts->device_build) {   // on-device linear BVH (mcrt_gpubuild.hip)
+    if (opts && opts->device_build == 2) {   // on-device SAH, node-identical to the host build
+        hipSetDevice(ctx->device);
+        std::vector<uint32_t> first(s->shapes.size());
+        uint32_t acc = 0;
+        for (size_t si = 0; si < s->shapes.size(); ++si) { first[si] = acc; acc += s->shapes[si].numTriangles; }
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        float4* nodes = nullptr;
+        int depth = 0;
+        const char* why = nullptr;
+        const hipError_t e = mcrt::gpu_build_sah((const mcrt_shape*)s->dShapes, first, (const uint32_t*)s->dIndices,
+                                                 (const float4*)s->dPositions, n, cost, bins, sah, ctx->stream, &nodes,
+                                                 &depth, &why);
+        if (e == hipSuccess) {
+            if (s->dNodes) hipFree(s->dNodes);
+            if (s->dTris) hipFree(s->dTris);
+            s->dTris = nullptr;
+            s->dNodes = nodes;
+            s->numNodes = 2 * n - 1;
+            s->numTris = (uint32_t)n;
+            s->bvhDepth = depth;
+            s->builder = 2;
+            return finish_accel(s, t0, nullptr);
+        }
+        // configurations the device path does not reproduce (> 64 bins, a host whose rcpps the
+        // table cannot model, pathological level counts) take the host build: same tree
+        if (e != hipErrorNotSupported && e != hipErrorInvalidValue)
+            return fail(ctx, MCRT_ERROR_DEVICE, std::string("device SAH build: ") + (why ? why : hipGetErrorString(e)));
+        (void)hipGetLastError();
+    }
+    s->builder = 0;
+    if (opts && opts->device_build == 1) {   // on-device linear BVH (mcrt_gpubuild.hip)
         hipSetDevice(ctx->device);
         std::vector<uint32_t> first(s->shapes.size());
         uint32_t acc = 0;
@@ -695,6 +726,7 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
         s->numNodes = 2 * n - 1;
         s->numTris = (uint32_t)n;
         s->bvhDepth = depth;
+        s->builder = 1;
         return finish_accel(s, t0, nullptr);
     }
     std::vector<float> tri(9 * n);
@@ -788,6 +820,24 @@ MCRT_API mcrt_status mcrt_accel_layout(mcrt_scene s, int32_t* two_level, uint32_
     if (num_meshes) *num_meshes = (uint32_t)s->numMeshes;
     if (num_instances) *num_instances = (uint32_t)s->numInstances;
     if (depth) *depth = s->bvhDepth;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_accel_read_records(mcrt_scene s, float* out, uint64_t max_records, uint64_t* num_records) {
+    if (!s || !num_records) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    if (!s->dNodes) return fail(s->ctx, MCRT_ERROR_INVALID_ARG, "scene has no acceleration structure");
+    *num_records = s->numNodes;
+    if (!out) return MCRT_OK;
+    mcrt_ctx ctx = s->ctx;
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpy(out, s->dNodes, 64 * std::min<uint64_t>(max_records, s->numNodes), hipMemcpyDeviceToHost));
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_accel_builder(mcrt_scene s, int32_t* builder) {
+    if (!s || !builder) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    *builder = s->twoLevel ? 0 : s->builder;
     return MCRT_OK;
 }
 

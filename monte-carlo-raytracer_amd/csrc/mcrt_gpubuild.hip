@@ -296,4 +296,17 @@ hipError_t gpu_build_bvh(const mcrt_shape* dShapes, const std::vector<uint32_t>&
     return hipSuccess;
 }
 
+// world-space triangles, shape/primitive ids, boxes and centroids (k_prims) for the device SAH
+// build (mcrt_sahbuild.hip); cbounds: 16 ints of scratch
+hipError_t launch_build_prims(int n, const mcrt_shape* dShapes, const uint32_t* dShapeFirst, int numShapes,
+                              const uint32_t* dIndices, const float4* dPositions, float* tri, int* shapeOf, int* primOf,
+                              float4* amin, float4* amax, float4* cen, int* cbounds, hipStream_t st) {
+    const int init[8] = {0x7fffffff, 0x7fffffff, 0x7fffffff, (int)0x80000000, (int)0x80000000, (int)0x80000000, 0, 0};
+    hipError_t e = hipMemcpyAsync(cbounds, init, sizeof(init), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_prims, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, n, dShapes, dShapeFirst,
+                       numShapes, dIndices, dPositions, tri, shapeOf, primOf, amin, amax, cen, cbounds);
+    return hipGetLastError();
+}
+
 }  // namespace mcrt

@@ -121,6 +121,22 @@ void launch_bdpt_clear_splat(int n, float4* splat, hipStream_t st);
 namespace mcrt {
 hipError_t gpu_build_bvh(const mcrt_shape* dShapes, const std::vector<uint32_t>& shapeFirst, const uint32_t* dIndices,
                          const float4* dPositions, size_t n, hipStream_t st, float4** nodesOut, int* depthOut);
+hipError_t launch_build_prims(int n, const mcrt_shape* dShapes, const uint32_t* dShapeFirst, int numShapes,
+                              const uint32_t* dIndices, const float4* dPositions, float* tri, int* shapeOf, int* primOf,
+                              float4* amin, float4* amax, float4* cen, int* cbounds, hipStream_t st);
+// Device SAH build node-identical to the host / RadeonRays Bvh2 build (mcrt_sahbuild.hip); on
+// failure *why names the reason (the caller falls back to the host build)
+hipError_t gpu_build_sah(const mcrt_shape* dShapes, const std::vector<uint32_t>& shapeFirst, const uint32_t* dIndices,
+                         const float4* dPositions, size_t n, float cost, int bins, bool sah, hipStream_t st,
+                         float4** nodesOut, int* depthOut, const char** why);
+// The running host's _mm_rcp_ps over the mantissa bits it reads (exponent 127), and whether the
+// device rule mcrt_sah.h rcp_ps / sa4 reproduces _mm_rcp_ps / _mm_dp_ps here (mcrt_bvh.cpp)
+struct HostRcp {
+    std::vector<uint32_t> t;
+    int bits = 0;
+    bool ok = false;
+};
+const HostRcp& host_rcp_table();
 }
 // Optional extension-queue sort (mcrt_raysort.hip)
 namespace mcrt {

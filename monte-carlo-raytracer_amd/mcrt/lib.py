@@ -41,6 +41,8 @@ SIGNATURES = {
     "mcrt_accel_build": (_c.c_int, [_vp, _vp]),
     "mcrt_accel_info": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_accel_layout": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "mcrt_accel_builder": (_c.c_int, [_vp, _vp]),
+    "mcrt_accel_read_records": (_c.c_int, [_vp, _vp, _c.c_uint64, _vp]),
     "mcrt_accel_build_host_records": (_c.c_int, [_vp, _vp, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64), _vp]),
     "mcrt_trace_closest": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
     "mcrt_trace_any": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
@@ -167,10 +169,11 @@ class Context:
 
 def accel_opts(cost=10.0, bins=64, sah=True, device_build=False, force_2level=False, force_flat=False,
                world_to_local=None):
-    """mcrt_accel_opts; world_to_local: optional (num_shapes, 4, 4) float32 array (kept alive by
+    """mcrt_accel_opts; device_build: 0/False host, 1/True device LBVH, 2 device SAH (node-identical
+    to the host build); world_to_local: optional (num_shapes, 4, 4) float32 array (kept alive by
     the caller until the build returns)."""
     w2l = None if world_to_local is None else world_to_local.ctypes.data
-    return T.AccelOpts(cost, bins, 1 if sah else 0, 1 if device_build else 0, 1 if force_2level else 0,
+    return T.AccelOpts(cost, bins, 1 if sah else 0, int(device_build), 1 if force_2level else 0,
                        1 if force_flat else 0, w2l)
 
 
@@ -214,6 +217,20 @@ class DeviceScene:
         tl, nm, ni, dp = _c.c_int32(), _c.c_uint32(), _c.c_uint32(), _c.c_int32()
         _check(lib().mcrt_accel_layout(self.h, _c.byref(tl), _c.byref(nm), _c.byref(ni), _c.byref(dp)), self.ctx.h)
         return {"two_level": tl.value, "meshes": nm.value, "instances": ni.value, "depth": dp.value}
+
+    def records(self):
+        """The device's BVH records, float32 (n, 16) (mcrt_accel_read_records)."""
+        n = _c.c_uint64()
+        _check(lib().mcrt_accel_read_records(self.h, None, 0, _c.byref(n)), self.ctx.h)
+        rec = np.zeros((n.value, 16), np.float32)
+        _check(lib().mcrt_accel_read_records(self.h, _p(rec), n.value, _c.byref(n)), self.ctx.h)
+        return rec
+
+    def builder(self):
+        """0 host build (or two-level), 1 device LBVH, 2 device SAH (mcrt_accel_builder)."""
+        b = _c.c_int32()
+        _check(lib().mcrt_accel_builder(self.h, _c.byref(b)), self.ctx.h)
+        return b.value
 
     def info(self):
         nn, nb, ms, nt = _c.c_uint64(), _c.c_uint64(), _c.c_double(), _c.c_uint32()
