@@ -301,7 +301,9 @@ def main():
     ap.add_argument("--save-image", default=None, help="rank 0 saves the final accumulated image (.npy)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the product path); gloo only rehearses N ranks on one GPU")
-    ap.add_argument("--device-build", action="store_true", help="on-device linear BVH instead of the RR-identical host build")
+    ap.add_argument("--device-build", action="store_true", help="on-device linear BVH instead of the RR-identical tree")
+    ap.add_argument("--host-build", action="store_true",
+                    help="build the RR-identical tree on the host (mcrt_bvh.cpp) instead of the device (mcrt_sahbuild.hip)")
     ap.add_argument("--force-flat", action="store_true",
                     help="flat BVH even for instanced scenes (RR bvh.forceflat); default: RR's auto selection")
     ap.add_argument("--russian-roulette", action="store_true",
@@ -357,7 +359,8 @@ def main():
 
     ctx = lib.Context(local)
     t0 = time.perf_counter()
-    ds = lib.DeviceScene(ctx, scene, device_build=args.device_build, force_flat=args.force_flat)
+    ds = lib.DeviceScene(ctx, scene, device_build=1 if args.device_build else 3 if args.host_build else 2,
+                         force_flat=args.force_flat)
     info = ds.info()
     two_level = ds.layout()["two_level"] == 1
     log(f"[bench] upload+BVH {time.perf_counter() - t0:.1f}s (build {info['build_ms'] / 1e3:.1f}s, "
@@ -464,7 +467,8 @@ def main():
                                   if args.russian_roulette and not bdpt else ""), "width": W, "height": H,
                    "triangles": scene.num_triangles, "max_depth": D, "spp_per_step": 1,
                    "bvh": ("two-level (instanced), RadeonRays-identical Bvh trees" if two_level else
-                           "device LBVH" if args.device_build else "host RadeonRays-identical SAH"),
+                           "device LBVH" if args.device_build else
+                           "RadeonRays-identical SAH, " + ("host build" if args.host_build else "device build")),
                    "bvh_build_ms": round(info["build_ms"], 1),
                    "parallelism": (f"frame split x {world} + 1 RCCL reduce" if bdpt else
                                    f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce"),

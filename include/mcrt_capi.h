@@ -190,13 +190,13 @@ typedef struct {
     float traversal_cost;   /* "bvh.sah.traversal_cost", default 10 */
     int   num_bins;         /* "bvh.sah.num_bins", default 64 */
     int   use_sah;          /* "bvh.builder" == "sah", default 1 */
-    /* 0 (default): host build that reproduces RadeonRays' Bvh2 node for node (bit-exact parity,
-     * seconds for 10 M triangles).  1: on-device linear BVH (Morton order, rocPRIM radix sort;
-     * tens of ms), same record format and triangle data, different tree (equal-t hit ties may
-     * resolve differently from the reference); ignores the three SAH fields.  2: on-device SAH
-     * build that reproduces the same RadeonRays Bvh2 node for node (mcrt_sahbuild.hip: the
-     * reference's split arithmetic incl. this host's _mm_rcp_ps, its partition order in closed
-     * form); byte-identical records to 0; takes the host path for num_bins > 64. */
+    /* Which builder makes the flat structure.  0 (default) / 2: RadeonRays' Bvh2 node for node
+     * (bit-exact parity), built on the device (mcrt_sahbuild.hip: the reference's split
+     * arithmetic incl. this host's _mm_rcp_ps, its partition order in closed form; ~0.2 s for
+     * 10 M triangles); falls back to 3 for num_bins > 64.  3: the same tree built on the host
+     * (mcrt_bvh.cpp; ~2 s for 10 M triangles).  1: on-device linear BVH (Morton order, rocPRIM
+     * radix sort), same record format and triangle data, different tree (equal-t hit ties may
+     * resolve differently from the reference); ignores the three SAH fields. */
     int   device_build;
     /* Two-level (instanced) structure: RadeonRays' IntersectorTwoLevel, which RR selects when a
      * shape is an instance (RTScene::attachMesh -> CreateInstance for every further entity that
@@ -300,7 +300,8 @@ MCRT_API mcrt_status mcrt_accel_layout(mcrt_scene scene, int32_t* two_level, uin
  * (up to max_records; out may be NULL to query *num_records). */
 MCRT_API mcrt_status mcrt_accel_read_records(mcrt_scene scene, float* out, uint64_t max_records,
                                              uint64_t* num_records);
-/* Which builder made the flat structure: 0 host (or two-level), 1 device LBVH, 2 device SAH. */
+/* Which builder made the flat structure: 0 host (or two-level), 1 device LBVH, 2 device SAH
+ * (mcrt_accel_opts.device_build 0 and 2). */
 MCRT_API mcrt_status mcrt_accel_builder(mcrt_scene scene, int32_t* builder);
 /* Host-only build of the structure mcrt_accel_build would upload (no device needed): 64-B
  * records (mcrt_bvh.cpp / mcrt_bvh2l.cpp layouts) into out_records (up to max_records; may be

@@ -679,7 +679,8 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     }
     s->twoLevel = false;
     s->numMeshes = s->numInstances = 0;
-    if (opts && opts->device_build == 2) {   // on-device SAH, node-identical to the host build
+    const int buildMode = opts ? opts->device_build : 0;
+    if (buildMode == 0 || buildMode == 2) {   // on-device SAH, node-identical to the host build
         hipSetDevice(ctx->device);
         std::vector<uint32_t> first(s->shapes.size());
         uint32_t acc = 0;
@@ -709,7 +710,7 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
         (void)hipGetLastError();
     }
     s->builder = 0;
-    if (opts && opts->device_build == 1) {   // on-device linear BVH (mcrt_gpubuild.hip)
+    if (buildMode == 1) {   // on-device linear BVH (mcrt_gpubuild.hip)
         hipSetDevice(ctx->device);
         std::vector<uint32_t> first(s->shapes.size());
         uint32_t acc = 0;

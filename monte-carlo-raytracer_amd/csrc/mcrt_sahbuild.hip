@@ -26,6 +26,7 @@
 // build (tests/test_gpu_build.py compares them).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -37,7 +38,10 @@ namespace {
 using namespace mcrt::sah;
 
 constexpr int MAXB = 64;      // bins supported on the device path
-constexpr int SMALL = 1024;   // requests up to this many references finish in one wave
+#ifndef SAH_SMALL
+#define SAH_SMALL 256
+#endif
+constexpr int SMALL = SAH_SMALL;   // requests up to this many references finish in one wave (LDS)
 constexpr int CHUNK = 4096;   // references per workgroup in the level passes
 constexpr int LT = 256;       // threads per level-pass workgroup
 constexpr int PER = CHUNK / LT;
@@ -46,6 +50,7 @@ constexpr int MAX_LEVELS = 4096;
 struct Seg {   // one request (bvh2.cpp SplitRequest)
     V4 bmin, bmax, cmin, cmax;
     uint32_t start, num, index, level;
+    uint32_t chunk0, pad[3];   // its first chunk in the level's chunk list (contiguous, in order)
 };
 struct SegState {
     uint32_t axis, sahNode, mode, nL;   // mode 0: partition at `split`; 1: median of the current order
@@ -133,34 +138,40 @@ __device__ __forceinline__ void addSide(float* b, bool L, float4 mn, float4 mx, 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_bounds(int n, const float4* __restrict__ amin, const float4* __restrict__ amax,
                                                 const float4* __restrict__ cen, int* __restrict__ out) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
     int v[12];
     for (int a = 0; a < 3; ++a) {
         v[a] = v[6 + a] = 0x7fffffff;
         v[3 + a] = v[9 + a] = (int)0x80000000;
     }
-    if (i < n) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const float4 mn = amin[i], mx = amax[i], c = cen[i];
         const float m[3] = {mn.x, mn.y, mn.z}, M[3] = {mx.x, mx.y, mx.z}, C[3] = {c.x, c.y, c.z};
         for (int a = 0; a < 3; ++a) {
-            v[a] = oi(m[a]);
-            v[3 + a] = oi(M[a]);
-            v[6 + a] = oi(C[a]);
-            v[9 + a] = oi(C[a]);
+            v[a] = min(v[a], oi(m[a]));
+            v[3 + a] = max(v[3 + a], oi(M[a]));
+            v[6 + a] = min(v[6 + a], oi(C[a]));
+            v[9 + a] = max(v[9 + a], oi(C[a]));
         }
     }
+    __shared__ int red[12];
+    if (threadIdx.x < 12) red[threadIdx.x] = ((threadIdx.x % 6) >= 3) ? (int)0x80000000 : 0x7fffffff;
+    __syncthreads();
     for (int k = 0; k < 12; ++k) {
         const bool isMax = (k % 6) >= 3;
         for (int off = 32; off > 0; off >>= 1) {
             const int o = __shfl_xor(v[k], off);
             v[k] = isMax ? max(v[k], o) : min(v[k], o);
         }
-    }
-    if ((threadIdx.x & 63) == 0)
-        for (int k = 0; k < 12; ++k) {
-            if ((k % 6) >= 3) atomicMax(&out[k], v[k]);
-            else atomicMin(&out[k], v[k]);
+        if ((threadIdx.x & 63) == 0) {
+            if (isMax) atomicMax(&red[k], v[k]);
+            else atomicMin(&red[k], v[k]);
         }
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        if ((threadIdx.x % 6) >= 3) atomicMax(&out[threadIdx.x], red[threadIdx.x]);
+        else atomicMin(&out[threadIdx.x], red[threadIdx.x]);
+    }
 }
 
 __global__ void k_root(int n, const int* __restrict__ b, Seg* __restrict__ big, Chunk* __restrict__ chunks,
@@ -174,6 +185,7 @@ __global__ void k_root(int n, const int* __restrict__ b, Seg* __restrict__ big, 
     s.num = (uint32_t)n;
     s.index = 0;
     s.level = 0;
+    s.chunk0 = 0;
     if (n == 1) {   // a single triangle: the root is a leaf (k_single_leaf)
         ctr->segs = ctr->chunks = ctr->small = 0;
     } else if (n > SMALL) {
@@ -203,8 +215,7 @@ __global__ __launch_bounds__(256) void k_iota(int n, uint32_t* __restrict__ refs
 // level passes over the large requests
 // ---------------------------------------------------------------------------
 // K0: split axis, midpoint, SAH constants (bvh2.cpp:339-348, 505-520); clear bins and bounds
-__global__ __launch_bounds__(64) void k_prepare(Params P, const Seg* __restrict__ segs, SegState* __restrict__ st,
-                                                const Chunk* __restrict__ chunks, uint32_t numChunks) {
+__global__ __launch_bounds__(64) void k_prepare(Params P, const Seg* __restrict__ segs, SegState* __restrict__ st) {
     const Seg g = segs[blockIdx.x];
     SegState& S = st[blockIdx.x];
     for (uint32_t k = threadIdx.x; k < P.nb; k += 64) {
@@ -227,13 +238,7 @@ __global__ __launch_bounds__(64) void k_prepare(Params P, const Seg* __restrict_
     S.cinv = rcp_ps(ext, P.rcpTable, P.rcpBits);
     S.areaInv = rcp_ps(sa4(g.bmin, g.bmax), P.rcpTable, P.rcpBits);
     S.nL = 0;
-    // this request's chunks are contiguous in the level's chunk list (k_emit appends them so)
-    uint32_t lo = 0, hi = numChunks;   // first chunk with seg >= blockIdx.x
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (chunks[mid].seg < blockIdx.x) lo = mid + 1; else hi = mid;
-    }
-    S.chunk0 = lo;
+    S.chunk0 = g.chunk0;
     S.nchunks = ((g.num + CHUNK - 1) / CHUNK);
 }
 
@@ -536,7 +541,7 @@ __global__ __launch_bounds__(64) void k_emit(Params P, const Seg* __restrict__ s
                 atomicOr(&P.ctr->error, 1u);
                 continue;
             }
-            next[slot] = Seg{cb[k][0], cb[k][1], cb[k][2], cb[k][3], cs[k], cn[k], ci[k], g.level + 1};
+            next[slot] = Seg{cb[k][0], cb[k][1], cb[k][2], cb[k][3], cs[k], cn[k], ci[k], g.level + 1, c0, {0, 0, 0}};
             for (uint32_t q = 0; q < nc; ++q)
                 nextChunks[c0 + q] = Chunk{slot, q * CHUNK, min((q + 1) * CHUNK, cn[k]), 0};
         } else {
@@ -547,24 +552,6 @@ __global__ __launch_bounds__(64) void k_emit(Params P, const Seg* __restrict__ s
             }
             small[slot] = make_uint4(cs[k], cn[k], ci[k], g.level + 1);
         }
-    }
-}
-
-// chunks of one level are appended by concurrent k_emit threads: sort them by request so each
-// request's chunks are contiguous (k_prepare finds them by binary search)
-__global__ __launch_bounds__(256) void k_sort_chunks(const Chunk* __restrict__ in, Chunk* __restrict__ out, uint32_t n,
-                                                     const uint32_t* __restrict__ segChunk0) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const Chunk c = in[i];
-    out[segChunk0[c.seg] + c.begin / CHUNK] = c;
-}
-__global__ void k_seg_chunk0(const Seg* __restrict__ segs, uint32_t n, uint32_t* __restrict__ segChunk0) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint32_t run = 0;
-    for (uint32_t s = 0; s < n; ++s) {
-        segChunk0[s] = run;
-        run += (segs[s].num + CHUNK - 1) / CHUNK;
     }
 }
 
@@ -585,6 +572,69 @@ __device__ __forceinline__ float wmax(float v) {
     return v;
 }
 
+// one lane builds a whole subtree of <= LANE_T references (no SAH below 9, bvh2.cpp:509): the
+// reference's own two-pointer loop on its slice of perm, serially
+constexpr uint32_t LANE_T = 8;
+__device__ __forceinline__ void laneSubtree(const Params& P, const SNode& root, float (*C)[SMALL], float (*MN)[SMALL],
+                                            float (*MX)[SMALL], const uint32_t* gid, uint16_t* perm,
+                                            uint32_t& maxLevel) {
+    SNode st[4];
+    int sp = 0;
+    st[sp++] = root;
+    while (sp > 0) {
+        const SNode nd = st[--sp];
+        const uint32_t ax = maxAxis(nd.cmin, nd.cmax);
+        const float ext = lane(vsub(nd.cmax, nd.cmin), ax);
+        const float split = 0.5f * (lane(nd.cmax, ax) + lane(nd.cmin, ax));
+        const float* CA = C[ax > 2 ? 0 : ax];
+        const uint32_t s0 = nd.s0, num = nd.num;
+        uint32_t nl = 0;
+        bool median = !(ext > 0.0f);
+        if (!median) {
+            uint32_t first = s0, last = s0 + num;
+            for (;;) {
+                while (first != last && CA[perm[first]] < split) ++first;
+                if (first == last--) break;
+                while (first != last && CA[perm[last]] >= split) --last;
+                if (first == last) break;
+                const uint16_t t = perm[first];
+                perm[first] = perm[last];
+                perm[last] = t;
+                ++first;
+            }
+            nl = first - s0;
+            median = nl == 0 || nl == num;
+        }
+        if (median) nl = num >> 1;
+        const uint32_t nr = num - nl;
+        float b[24];
+        for (int k = 0; k < 24; ++k) b[k] = ((k / 3) & 1) ? -INFINITY : INFINITY;
+        for (uint32_t j = 0; j < num; ++j) {
+            const uint32_t e = perm[s0 + j];
+            addSide(b, j < nl, make_float4(MN[0][e], MN[1][e], MN[2][e], 0.0f),
+                    make_float4(MX[0][e], MX[1][e], MX[2][e], 0.0f), make_float4(C[0][e], C[1][e], C[2][e], 0.0f));
+        }
+        const V4 lmn{b[0], b[1], b[2], 0.0f}, lmx{b[3], b[4], b[5], 0.0f}, lcmn{b[6], b[7], b[8], 0.0f},
+            lcmx{b[9], b[10], b[11], 0.0f};
+        const V4 rmn{b[12], b[13], b[14], 0.0f}, rmx{b[15], b[16], b[17], 0.0f}, rcmn{b[18], b[19], b[20], 0.0f},
+            rcmx{b[21], b[22], b[23], 0.0f};
+        const uint32_t li = nd.index + 1, ri = nd.index + nl * 2;
+        const uint32_t lref = gid[perm[s0]], rref = gid[perm[s0 + nl]];
+        float b0[6], b1[6];
+        childBox(P, nl, lref, lmn, lmx, b0);
+        childBox(P, nr, rref, rmn, rmx, b1);
+        writeInternal(P, nd.index, b0, b1, li, ri);
+        if (nl == 1) writeLeaf(P, li, lref);
+        if (nr == 1) writeLeaf(P, ri, rref);
+        maxLevel = max(maxLevel, nd.level + 1);
+        const SNode L{lmn, lmx, lcmn, lcmx, s0, nl, li, nd.level + 1};
+        const SNode R{rmn, rmx, rcmn, rcmx, s0 + nl, nr, ri, nd.level + 1};
+        const bool leftFirst = nl >= nr;
+        if ((leftFirst ? L : R).num > 1) st[sp++] = leftFirst ? L : R;
+        if ((leftFirst ? R : L).num > 1) st[sp++] = leftFirst ? R : L;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_small(Params P, const uint4* __restrict__ list) {
     __shared__ float C[3][SMALL], MN[3][SMALL], MX[3][SMALL];
     __shared__ uint32_t gid[SMALL];
@@ -593,6 +643,7 @@ __global__ __launch_bounds__(64) void k_small(Params P, const uint4* __restrict_
     __shared__ uint16_t slot[SMALL / 2];
     __shared__ int bins[MAXB * 7];
     __shared__ SNode stack[24];
+    __shared__ SNode laneList[64];
     const int ln = threadIdx.x;
     const uint4 item = list[blockIdx.x];
     const uint32_t start = item.x, num0 = item.y;
@@ -611,14 +662,26 @@ __global__ __launch_bounds__(64) void k_small(Params P, const uint4* __restrict_
         for (int k = 0; k < 12; ++k) r[k] = ((k / 3) & 1) ? fmaxf(r[k], v[k]) : fminf(r[k], v[k]);
     }
     for (int k = 0; k < 12; ++k) r[k] = ((k / 3) & 1) ? wmax(r[k]) : wmin(r[k]);
-    int sp = 0;   // wave-uniform
-    if (ln == 0)
-        stack[0] = SNode{V4{r[0], r[1], r[2], 0.0f}, V4{r[3], r[4], r[5], 0.0f}, V4{r[6], r[7], r[8], 0.0f},
-                         V4{r[9], r[10], r[11], 0.0f}, 0u, num0, item.z, item.w};
-    sp = 1;
+    // nodes of > LANE_T references: the whole wave, one at a time (stack, wave-uniform sp);
+    // subtrees of <= LANE_T: collected in laneList and built one per lane
+    int sp = 0, nLane = 0;
+    const SNode root{V4{r[0], r[1], r[2], 0.0f}, V4{r[3], r[4], r[5], 0.0f}, V4{r[6], r[7], r[8], 0.0f},
+                     V4{r[9], r[10], r[11], 0.0f}, 0u, num0, item.z, item.w};
+    if (ln == 0) {
+        if (num0 <= LANE_T) laneList[0] = root;
+        else stack[0] = root;
+    }
+    if (num0 <= LANE_T) nLane = 1;
+    else sp = 1;
     __syncthreads();
     uint32_t maxLevel = item.w;
-    while (sp > 0) {
+    while (sp > 0 || nLane > 0) {
+        if (sp == 0 || nLane >= 63) {
+            if (ln < nLane) laneSubtree(P, laneList[ln], C, MN, MX, gid, perm, maxLevel);
+            nLane = 0;
+            __syncthreads();
+            continue;
+        }
         const SNode nd = stack[--sp];
         __syncthreads();
         const uint32_t s0 = nd.s0, num = nd.num;
@@ -794,20 +857,23 @@ __global__ __launch_bounds__(64) void k_small(Params P, const uint4* __restrict_
         const bool leftFirst = nl >= nr;
         const SNode& A = leftFirst ? L : R;
         const SNode& B2 = leftFirst ? R : L;
-        if (A.num > 1) {
-            if (ln == 0) stack[sp] = A;
-            ++sp;
-        }
-        if (B2.num > 1) {
-            if (ln == 0) stack[sp] = B2;
-            ++sp;
-        }
-        if (sp > 24) {
+        if (sp + 2 > 24) {   // not reached: depth O(log SMALL) with the smaller child first
             if (ln == 0) atomicOr(&P.ctr->error, 4u);
             return;
         }
+        for (const SNode* c : {&A, &B2}) {
+            if (c->num <= 1) continue;
+            if (c->num <= LANE_T) {
+                if (ln == 0) laneList[nLane] = *c;
+                ++nLane;
+            } else {
+                if (ln == 0) stack[sp] = *c;
+                ++sp;
+            }
+        }
         __syncthreads();
     }
+    for (int off = 32; off > 0; off >>= 1) maxLevel = max(maxLevel, (uint32_t)__shfl_xor((int)maxLevel, off));
     if (ln == 0) atomicMax(&P.ctr->depth, maxLevel);
 }
 
@@ -840,8 +906,8 @@ hipError_t gpu_build_sah(const mcrt_shape* dShapes, const std::vector<uint32_t>&
     float* tri = nullptr;
     int *shapeOf = nullptr, *primOf = nullptr, *cb = nullptr;
     float4 *amin = nullptr, *amax = nullptr, *cen = nullptr, *nodes = nullptr;
-    uint32_t *refs = nullptr, *slots = nullptr, *chunkL = nullptr, *chunkLb = nullptr, *segChunk0 = nullptr,
-             *rtab = nullptr, *dShapeFirst = nullptr;
+    uint32_t *refs = nullptr, *slots = nullptr, *chunkL = nullptr, *chunkLb = nullptr, *rtab = nullptr,
+             *dShapeFirst = nullptr;
     Seg *segA = nullptr, *segB = nullptr;
     SegState* state = nullptr;
     Chunk *chA = nullptr, *chB = nullptr;
@@ -863,7 +929,6 @@ hipError_t gpu_build_sah(const mcrt_shape* dShapes, const std::vector<uint32_t>&
     A((void**)&slots, sizeof(uint32_t) * n);
     A((void**)&chunkL, sizeof(uint32_t) * capChunks);
     A((void**)&chunkLb, sizeof(uint32_t) * capChunks);
-    A((void**)&segChunk0, sizeof(uint32_t) * capSegs);
     A((void**)&rtab, sizeof(uint32_t) * R.t.size());
     A((void**)&dShapeFirst, sizeof(uint32_t) * shapeFirst.size());
     A((void**)&segA, sizeof(Seg) * capSegs);
@@ -887,7 +952,7 @@ hipError_t gpu_build_sah(const mcrt_shape* dShapes, const std::vector<uint32_t>&
         Params P{cen, amin, amax, tri, shapeOf, primOf, refs, slots, nodes, rtab, R.bits, (uint32_t)bins,
                  (float)bins, cost, sah ? 1 : 0, ctr};
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_bounds, dim3(g), dim3(256), 0, st, (int)n, amin, amax, cen, cb);
+            hipLaunchKernelGGL(k_bounds, dim3(std::min(g, 2048)), dim3(256), 0, st, (int)n, amin, amax, cen, cb);
             hipLaunchKernelGGL(k_iota, dim3(g), dim3(256), 0, st, (int)n, refs);
             e = hipMemsetAsync(ctr, 0, sizeof(Counters), st);
         }
@@ -907,7 +972,7 @@ hipError_t gpu_build_sah(const mcrt_shape* dShapes, const std::vector<uint32_t>&
                 break;
             }
             const dim3 S(numSegs), Cg(numChunks), S64((numSegs + 63) / 64);
-            hipLaunchKernelGGL(k_prepare, S, dim3(64), 0, st, P, segA, state, chA, numChunks);
+            hipLaunchKernelGGL(k_prepare, S, dim3(64), 0, st, P, segA, state);
             hipLaunchKernelGGL(k_bin, Cg, dim3(LT), 0, st, P, segA, state, chA);
             hipLaunchKernelGGL(k_sweep, S64, dim3(64), 0, st, P, segA, state, numSegs);
             hipLaunchKernelGGL(k_count, Cg, dim3(LT), 0, st, P, segA, state, chA, chunkL);
@@ -928,12 +993,8 @@ hipError_t gpu_build_sah(const mcrt_shape* dShapes, const std::vector<uint32_t>&
             }
             numSegs = hc.segs;
             numChunks = hc.chunks;
-            if (numSegs > 0) {   // group the next level's chunks by request
-                hipLaunchKernelGGL(k_seg_chunk0, dim3(1), dim3(1), 0, st, segB, numSegs, segChunk0);
-                hipLaunchKernelGGL(k_sort_chunks, dim3((numChunks + 255) / 256), dim3(256), 0, st, chB, chA, numChunks,
-                                   segChunk0);
-            }
             std::swap(segA, segB);
+            std::swap(chA, chB);
         }
         if (e == hipSuccess && hc.small > 0) {
             hipLaunchKernelGGL(k_small, dim3(hc.small), dim3(64), 0, st, P, small);
@@ -952,7 +1013,7 @@ hipError_t gpu_build_sah(const mcrt_shape* dShapes, const std::vector<uint32_t>&
         depth = (int)hc.depth;
     }
     for (void* p : {(void*)tri, (void*)shapeOf, (void*)primOf, (void*)amin, (void*)amax, (void*)cen, (void*)cb,
-                    (void*)refs, (void*)slots, (void*)chunkL, (void*)chunkLb, (void*)segChunk0, (void*)rtab,
+                    (void*)refs, (void*)slots, (void*)chunkL, (void*)chunkLb, (void*)rtab,
                     (void*)dShapeFirst, (void*)segA, (void*)segB, (void*)state, (void*)chA, (void*)chB, (void*)small,
                     (void*)ctr})
         if (p) (void)hipFree(p);

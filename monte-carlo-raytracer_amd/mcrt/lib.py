@@ -169,8 +169,8 @@ class Context:
 
 def accel_opts(cost=10.0, bins=64, sah=True, device_build=False, force_2level=False, force_flat=False,
                world_to_local=None):
-    """mcrt_accel_opts; device_build: 0/False host, 1/True device LBVH, 2 device SAH (node-identical
-    to the host build); world_to_local: optional (num_shapes, 4, 4) float32 array (kept alive by
+    """mcrt_accel_opts; device_build: 0/False (default) or 2 the RadeonRays-identical tree built on
+    the device, 3 the same tree built on the host, 1/True device LBVH; world_to_local: optional (num_shapes, 4, 4) float32 array (kept alive by
     the caller until the build returns)."""
     w2l = None if world_to_local is None else world_to_local.ctypes.data
     return T.AccelOpts(cost, bins, 1 if sah else 0, int(device_build), 1 if force_2level else 0,

@@ -76,9 +76,12 @@ def _scene(name):
 def test_device_sah_records_identical_to_host_build(hip_ctx, name):
     from mcrt import lib
     sc = _scene(name)
-    host = lib.DeviceScene(hip_ctx, sc)
+    host = lib.DeviceScene(hip_ctx, sc, device_build=3)
     dev = lib.DeviceScene(hip_ctx, sc, device_build=2)
     assert dev.builder() == 2 and host.builder() == 0
+    default = lib.DeviceScene(hip_ctx, sc)
+    assert default.builder() == 2   # the default build is the device one
+    default.close()
     assert dev.layout()["depth"] == host.layout()["depth"]
     a, b = host.records(), dev.records()
     assert _same_records(a, b), np.nonzero((a.view(np.uint32) != b.view(np.uint32)).any(1))[0][:10]
@@ -91,7 +94,7 @@ def test_device_sah_san_miguel_identical_and_fast(hip_ctx):
     < 200 ms; the host build takes ~2 s)."""
     from mcrt import lib
     sc = scenes.san_miguel_proxy()
-    host = lib.DeviceScene(hip_ctx, sc)
+    host = lib.DeviceScene(hip_ctx, sc, device_build=3)
     a = host.records()
     host.close()
     dev = lib.DeviceScene(hip_ctx, sc, build=False)
@@ -114,7 +117,7 @@ def test_device_sah_frames_bit_identical(hip_ctx):
     W, H = 96, 64
     cam = scene_camera("mixed", W, H)
     out = []
-    for device in (0, 2):
+    for device in (3, 2):
         ds = lib.DeviceScene(hip_ctx, sc, device_build=device)
         fb = lib.FrameBuffer(hip_ctx, W, H)
         fb.render(ds, cam, frame=1, max_depth=3)
