@@ -300,6 +300,28 @@ MCRT_API mcrt_status mcrt_accel_layout(mcrt_scene scene, int32_t* two_level, uin
  * (up to max_records; out may be NULL to query *num_records). */
 MCRT_API mcrt_status mcrt_accel_read_records(mcrt_scene scene, float* out, uint64_t max_records,
                                              uint64_t* num_records);
+/* ------------------------------------------------------------------------ */
+/* Scene ingestion for C/C++ hosts (mcrt_objload.cpp): OBJ + MTL + PNG into the
+ * SCENE_PARAMS arrays, replacing the reference's assimp import + RTScene mesh,
+ * material and texture conversion (source/engine/resource/AssetImporter.cpp:40,
+ * APP/raytracing/scene/RTScene.cpp:564-766, 826-880).  Left-handed (z negated,
+ * winding flipped), fan triangulation, face normals where vn is missing,
+ * uber materials from Kd/Ks/Ns + map_Kd/map_bump/map_d/map_Ks, RGBA8 textures.  */
+/* ------------------------------------------------------------------------ */
+typedef struct mcrt_obj_scene_s* mcrt_obj_scene;
+#define MCRT_OBJ_MIPS            1   /* store each texture's glGenerateMipmap chain (uploadTextures) */
+#define MCRT_OBJ_EMISSIVE_LIGHTS 2   /* materials with Ke > 0 become triangle-mesh area lights */
+MCRT_API mcrt_status mcrt_obj_load(const char* path, uint32_t flags, mcrt_obj_scene* out);
+/* Extra lights (the demo's sun: PathTracingApp.cpp:395-401).  Directional lights are placed on
+ * the scene's bounding sphere like RTScene::setLight (RTScene.cpp:482-494). */
+MCRT_API mcrt_status mcrt_obj_add_directional_light(mcrt_obj_scene s, const float dir[3], const float intensity[3]);
+MCRT_API mcrt_status mcrt_obj_add_point_light(mcrt_obj_scene s, const float pos[3], const float intensity[3]);
+/* The arrays as a mcrt_scene_desc for mcrt_scene_create (pointers owned by s, valid until the
+ * next add_* call or mcrt_obj_free; sobol_matrices left NULL for the caller to set). */
+MCRT_API mcrt_status mcrt_obj_scene_desc(mcrt_obj_scene s, mcrt_scene_desc* desc);
+MCRT_API const char* mcrt_obj_warnings(mcrt_obj_scene s);   /* missing MTL / skipped textures */
+MCRT_API void mcrt_obj_free(mcrt_obj_scene s);
+
 /* Which builder made the flat structure: 0 host (or two-level), 1 device LBVH, 2 device SAH
  * (mcrt_accel_opts.device_build 0 and 2). */
 MCRT_API mcrt_status mcrt_accel_builder(mcrt_scene scene, int32_t* builder);

@@ -42,6 +42,12 @@ SIGNATURES = {
     "mcrt_accel_info": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_accel_layout": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_accel_builder": (_c.c_int, [_vp, _vp]),
+    "mcrt_obj_load": (_c.c_int, [_c.c_char_p, _c.c_uint32, _vp]),
+    "mcrt_obj_add_directional_light": (_c.c_int, [_vp, _vp, _vp]),
+    "mcrt_obj_add_point_light": (_c.c_int, [_vp, _vp, _vp]),
+    "mcrt_obj_scene_desc": (_c.c_int, [_vp, _vp]),
+    "mcrt_obj_warnings": (_c.c_char_p, [_vp]),
+    "mcrt_obj_free": (None, [_vp]),
     "mcrt_accel_read_records": (_c.c_int, [_vp, _vp, _c.c_uint64, _vp]),
     "mcrt_accel_build_host_records": (_c.c_int, [_vp, _vp, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64), _vp]),
     "mcrt_trace_closest": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
@@ -381,6 +387,44 @@ class FrameBuffer:
             self.close()
         except Exception:
             pass
+
+
+def load_obj(path, mips=True, emissive_lights=True, directional_lights=(), point_lights=()):
+    """Scene ingestion through the C ABI (mcrt_obj_load, csrc/mcrt_objload.cpp): returns a
+    mcrt.scenes.Scene holding copies of the loader's arrays and the loader's warnings.
+    directional_lights / point_lights: [(direction or position, intensity)] added after the
+    emissive-material lights, as a host adds the demo sun."""
+    from .scenes import Scene
+    h = _vp()
+    flags = (T.OBJ_MIPS if mips else 0) | (T.OBJ_EMISSIVE_LIGHTS if emissive_lights else 0)
+    _check(lib().mcrt_obj_load(os.fsencode(path), flags, _c.byref(h)))
+    try:
+        f3 = lambda v: (_c.c_float * 3)(*[float(x) for x in v])   # noqa: E731
+        for d, it in directional_lights:
+            _check(lib().mcrt_obj_add_directional_light(h, f3(d), f3(it)))
+        for p, it in point_lights:
+            _check(lib().mcrt_obj_add_point_light(h, f3(p), f3(it)))
+        d = T.SceneDesc()
+        _check(lib().mcrt_obj_scene_desc(h, _c.byref(d)))
+
+        def arr(ptr, n, dtype, shape=None):
+            dtype = np.dtype(dtype)
+            if not n or not ptr:
+                return np.zeros((0,) + (shape or ()), dtype)
+            a = np.frombuffer(_c.string_at(ptr, n * dtype.itemsize), dtype).copy()
+            return a.reshape((n,) + shape) if shape else a
+        nv = d.num_vertices
+        sc = Scene(arr(d.shapes, d.num_shapes, T.SHAPE_DTYPE), arr(d.indices, d.num_indices, np.uint32),
+                   arr(d.positions, nv * 4, np.float32).reshape(-1, 4), arr(d.uvs, nv * 2, np.float32).reshape(-1, 2),
+                   arr(d.normals, nv * 4, np.float32).reshape(-1, 4), arr(d.tangents, nv * 4, np.float32).reshape(-1, 4),
+                   arr(d.binormals, nv * 4, np.float32).reshape(-1, 4), None,
+                   arr(d.textures, d.num_textures, T.TEXDESC_DTYPE), arr(d.tex_data, d.tex_data_bytes, np.uint8),
+                   arr(d.lights, d.num_lights, T.LIGHT_DTYPE), arr(d.materials, d.num_materials, T.MATERIAL_DTYPE),
+                   name=os.path.splitext(os.path.basename(path))[0])
+        sc.warnings = lib().mcrt_obj_warnings(h).decode()
+        return sc
+    finally:
+        lib().mcrt_obj_free(h)
 
 
 def make_pinhole_camera(pos, forward, up, fovy, near, far, width, height, pixel_offset=(0.0, 0.0)):

@@ -177,3 +177,7 @@ def make_filter(kind=BOX, radius=(2.0, 2.0), pixel_offset=(0.0, 0.0), B=1.0 / 3,
 
 AOV_ALBEDO = 0        # MCRT_AOV_ALBEDO
 AOV_TEXTURE_LOD = 1   # MCRT_AOV_TEXTURE_LOD
+
+# mcrt_obj_load flags (include/mcrt_capi.h)
+OBJ_MIPS = 1
+OBJ_EMISSIVE_LIGHTS = 2

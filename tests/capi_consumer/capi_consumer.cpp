@@ -74,7 +74,7 @@ void perspectiveRays(const mcrt_camera& cam, std::vector<mcrt_ray>& rays) {
 
 int main(int argc, char** argv) {
     if (argc < 5) {
-        std::fprintf(stderr, "usage: %s SCENE_DIR OUT_DIR frames max_depth\n", argv[0]);
+        std::fprintf(stderr, "usage: %s SCENE_DIR OUT_DIR frames max_depth [OBJ_FILE]\n", argv[0]);
         return 2;
     }
     const std::string in = argv[1], out = argv[2];
@@ -83,6 +83,13 @@ int main(int argc, char** argv) {
     int caught = 0;
     try {
         check(mcrt_ctx_create(0, &ctx), nullptr);
+        // ---- AssetImporter + RTScene (optional): an OBJ file through mcrt_obj_load ------------
+        mcrt_obj_scene objScene = nullptr;
+        if (argc > 5) {
+            check(mcrt_obj_load(argv[5], MCRT_OBJ_MIPS | MCRT_OBJ_EMISSIVE_LIGHTS, &objScene), ctx);
+            auto sun = load<float>(in + "/sun.bin");   // direction xyz, intensity rgb
+            if (sun.size() == 6) check(mcrt_obj_add_directional_light(objScene, &sun[0], &sun[3]), ctx);
+        }
         // ---- RTScene::commit ------------------------------------------------------------------
         auto shapes = load<mcrt_shape>(in + "/shapes.bin");
         auto indices = load<uint32_t>(in + "/indices.bin");
@@ -97,7 +104,7 @@ int main(int argc, char** argv) {
         auto lights = load<mcrt_light>(in + "/lights.bin");
         auto materials = load<mcrt_material>(in + "/materials.bin");
         auto camv = load<mcrt_camera>(in + "/camera.bin");
-        if (camv.size() != 1 || shapes.empty()) throw std::runtime_error("bad scene directory");
+        if (camv.size() != 1 || (shapes.empty() && !objScene)) throw std::runtime_error("bad scene directory");
         mcrt_scene_desc d = {};
         d.shapes = shapes.data();                 d.num_shapes = (uint32_t)shapes.size();
         d.indices = indices.data();               d.num_indices = (uint32_t)indices.size();
@@ -111,8 +118,14 @@ int main(int argc, char** argv) {
         d.sobol_matrices = sobol.data();          d.num_sobol_words = (uint32_t)sobol.size();
         d.lights = lights.data();                 d.num_lights = (uint32_t)lights.size();
         d.materials = materials.data();           d.num_materials = (uint32_t)materials.size();
+        if (objScene) {
+            check(mcrt_obj_scene_desc(objScene, &d), ctx);
+            d.sobol_matrices = sobol.empty() ? nullptr : sobol.data();
+            d.num_sobol_words = (uint32_t)sobol.size();
+        }
         mcrt_scene scene = nullptr;
         check(mcrt_scene_create(ctx, &d, &scene), ctx);
+        if (objScene) mcrt_obj_free(objScene);   // the scene holds device copies
         mcrt_accel_opts o = {10.0f, 64, 1};       // RTScene::commit: SAH, 64 bins, cost 10 (rest zero)
         check(mcrt_accel_build(scene, &o), ctx);
         const mcrt_camera cam = camv[0];

@@ -67,3 +67,39 @@ def test_cpp_consumer_matches_ctypes(hip_ctx, tmp_path):
     assert inactive.any() and (out("occl", np.int32)[inactive] == 0x7f7f7f7f).all()   # untouched (Q12)
     fb.close()
     ds.close()
+
+
+def test_cpp_consumer_obj_scene(hip_ctx, tmp_path):
+    """A C++ host loading an OBJ/MTL/PNG scene through mcrt_obj_load (the reference's
+    AssetImporter + RTScene step) renders the same frames as the ctypes path over lib.load_obj."""
+    from mcrt import lib
+    from mcrt.camera import make_camera
+    from test_objload_cpu import _write_scene
+    if not os.path.exists(EXE):
+        pytest.skip("tests/capi_consumer/capi_consumer not built (make -C tests/capi_consumer)")
+    _write_scene(str(tmp_path))
+    obj = str(tmp_path / "s.obj")
+    W, H, frames, D = 48, 40, 3, 3
+    cam = make_camera((0.5, 0.5, -3.0), (0.5, 0.5, 0.0), W, H)
+    sun = (scenes.euler_forward(45.0, 20.0), (4.0, 4.0, 4.0))
+    d = tmp_path / "scene"
+    os.makedirs(d)
+    np.ascontiguousarray(cam).tofile(str(d / "camera.bin"))
+    np.array(list(sun[0]) + list(sun[1]), np.float32).tofile(str(d / "sun.bin"))
+    os.makedirs(tmp_path / "out")
+    r = subprocess.run([EXE, str(d), str(tmp_path / "out"), str(frames), str(D), obj], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = lambda n, dt: np.fromfile(str(tmp_path / "out" / f"{n}.bin"), dt)   # noqa: E731
+    sc = lib.load_obj(obj, directional_lights=[sun])
+    ds = lib.DeviceScene(hip_ctx, sc)
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    for f in range(frames):
+        fb.render(ds, cam, frame=f, max_depth=D)
+        fb.accumulate(T.make_filter(T.BOX), f)
+    img = fb.read(2)
+    assert img[..., :3].max() > 0
+    np.testing.assert_array_equal(out("radiance", np.uint32).reshape(H, W, 4), fb.read(0).view(np.uint32))
+    np.testing.assert_array_equal(out("image", np.uint32).reshape(H, W, 4), img.view(np.uint32))
+    fb.close()
+    ds.close()
