@@ -138,10 +138,11 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
     return out
 
 
-def pmc_traffic(kernel):
-    """Memory-side bytes per launch of `kernel` (and the SQ limiter summary, if measured) from the
-    committed rocprofv3 counter summary profiles/pmc_latest.json (tools/pmc_json.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
+    """Memory-side bytes per launch of `kernel` (and the SQ limiter summary, if measured) from a
+    committed rocprofv3 counter summary under profiles/ (tools/pmc_json.py).  last_launches > 0:
+    also the summed bytes of the kernel's last `last_launches` dispatches (one BDPT frame)."""
+    path = os.path.join(ROOT, "profiles", summary)
     if not os.path.exists(path):
         return None
     try:
@@ -150,7 +151,12 @@ def pmc_traffic(kernel):
         if k is None:
             return None
         r = {"bytes_per_launch": float(k["hbm_bytes_per_launch"]),
-             "source": f"profiles/pmc_latest.json ({d.get('config', 'config not recorded')})"}
+             "source": f"profiles/{summary} ({d.get('config', 'config not recorded')})"}
+        raw = k.get("last_dispatches", {})
+        if last_launches and len(raw.get("FETCH_SIZE", [])) >= last_launches and \
+                len(raw.get("WRITE_SIZE", [])) >= last_launches:
+            r["bytes_last"] = sum(2 * f * 1024 for f in raw["FETCH_SIZE"][-last_launches:]) + \
+                sum(w * 1024 for w in raw["WRITE_SIZE"][-last_launches:])
         if "limiter" in k:
             r["limiter"] = k["limiter"]
         return r
@@ -260,6 +266,12 @@ def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s):
                            "distinct_nodes_per_frame": n_nodes,
                            "model": "compulsory bytes per frame: 48 B per subpath ray + 64 B per DISTINCT BVH node the "
                                     "frame's subpath rays visit (oracle BDPT, frame 0)"}
+        pm = pmc_traffic("k_extend", "pmc_bdpt.json", last_launches=D + 1)
+        if pm and "bytes_last" in pm:   # the last frame's D + 1 k_extend dispatches of the counter run
+            out["roofline"].update(traffic=int(pm["bytes_last"]), traffic_source=pm["source"],
+                                   traffic_over_alg=round(pm["bytes_last"] / alg, 2))
+        if pm and "limiter" in pm:
+            out["roofline"]["limiter"] = pm["limiter"]
     # CPU baseline: whole frames 1, 2, ... until ~target_s (frame 0 above carried the node marks)
     el, frames = 0.0, 0
     while frames == 0 or el + el / frames <= target_s:

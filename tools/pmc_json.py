@@ -31,9 +31,10 @@ KERNELS = ["k_shadow_extend", "k_primary", "k_extend", "k_shadow", "k_shade0", "
            "k_bdpt_start", "k_bdpt_vertex", "k_bdpt_connect", "k_bdpt_vis", "k_bdpt_gather"]
 
 
-def collect(dbs, last):
-    """kernel -> counter -> median over the kernel's last `last` dispatches (per pass db)."""
-    out, ms = {}, {}
+def collect(dbs, last, keep=12):
+    """kernel -> counter -> median over the kernel's last `last` dispatches (per pass db); also the
+    raw values of the last `keep` dispatches per counter (consumers that sum a frame's launches)."""
+    out, ms, raw = {}, {}, {}
     for db in dbs:
         per = {}
         for d in dispatches(db):
@@ -44,11 +45,13 @@ def collect(dbs, last):
                 continue
             per.setdefault(name, []).append(d)
         for name, ds in per.items():
+            for c in ds[0]["pmc"]:
+                raw.setdefault(name, {})[c] = [x["pmc"][c] for x in ds[-keep:]]
             ds = ds[-last:]
             for c in ds[0]["pmc"]:
                 out.setdefault(name, {})[c] = statistics.median(x["pmc"][c] for x in ds)
             ms.setdefault(name, []).extend(x["ms"] for x in ds)
-    return out, {k: statistics.median(v) for k, v in ms.items()}
+    return out, {k: statistics.median(v) for k, v in ms.items()}, raw
 
 
 def main():
@@ -57,14 +60,15 @@ def main():
     last = int(sys.argv[3]) if len(sys.argv) > 3 else 4
     prefix = sys.argv[4] if len(sys.argv) > 4 else "pmc_"
     dbs = sorted(glob.glob(os.path.join(d, prefix + "*", "*_results.db")))
-    pmc, ms = collect(dbs, last)
+    pmc, ms, raw = collect(dbs, last)
     res = {"source": f"rocprofv3 --kernel-trace --pmc passes ({', '.join(os.path.basename(os.path.dirname(x)) for x in dbs)})",
            "config": f"{cmd}; medians over the last {last} dispatches of each kernel = the untimed one-slot "
                      "kernel-timing pass (4 frames per launch)",
            "correction": "hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (MI355X_MICROARCH.md HBM section)",
            "kernels": {}}
     for k, c in pmc.items():
-        r = {"dispatch_ms_median": round(ms[k], 4), "counters": {n: v for n, v in sorted(c.items())}}
+        r = {"dispatch_ms_median": round(ms[k], 4), "counters": {n: v for n, v in sorted(c.items())},
+             "last_dispatches": {n: raw[k][n] for n in ("FETCH_SIZE", "WRITE_SIZE") if n in raw.get(k, {})}}
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             fb, wb = 2 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
             r.update(fetch_bytes_corrected=fb, write_bytes=wb, hbm_bytes_per_launch=fb + wb)
