@@ -164,11 +164,12 @@ def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
         return None
 
 
-def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing):
+def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing, split="frame"):
     """Config 4's integrator on the same scene and GPU(s): BDPT (RTBDPTPass::update), 1 spp per
-    step, frame split over the ranks (rank r renders frames r, r + N, ...; light-tracing splats land
-    anywhere in the image) and the same single reduce of the accumulators.  Returns the measured
-    numbers plus an untimed one-slot per-kernel timing pass."""
+    step, split over the ranks by frames (rank r renders frames r, r + N, ...; light-tracing splats
+    land anywhere in the image) or by 8-row bands (one splat all-reduce per frame,
+    mcrt.dist.exchange_splats), and the same single reduce of the accumulators.  Returns the
+    measured numbers plus an untimed one-slot per-kernel timing pass."""
     import torch
     import torch.distributed as dist
     from mcrt import dist as mdist
@@ -177,11 +178,19 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     fb = lib.FrameBuffer(ctx, W, H)
     filt = T.make_filter(T.BOX)
     first = [True]
+    band = split == "band" and world > 1
+    splat_buf = torch.zeros(4 * W * H, dtype=torch.float32, device="cuda") if band else None
 
     def run(i0, count):
         for i in range(i0, i0 + count):
-            f = rank + world * i
-            fb.render(ds, cam_of(f), frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT)
+            if band:
+                f = i
+                fb.render(ds, cam_of(f), frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT,
+                          band_rows=8, num_bands=world, band_index=rank)
+                mdist.exchange_splats(fb, splat_buf)
+            else:
+                f = rank + world * i
+                fb.render(ds, cam_of(f), frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT)
             fb.accumulate(filt, 0 if first[0] else f)
             first[0] = False
 
@@ -212,10 +221,11 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     st = fb.stats()
-    out = {"value": round(W * H * steps * world / el / 1e6, 3), "unit": "Mpaths/s", "steps": steps,
-           "ms_per_step": round(el / steps * 1e3, 4), "scaling": "weak",
+    out = {"value": round(W * H * steps * (1 if band else world) / el / 1e6, 3), "unit": "Mpaths/s", "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong" if band else "weak",
            "workload": f"same scene {W}x{H}, BDPT, maxDepth {D}, 1 spp per step (SURVEY config 4's integrator), "
-                       f"frame split x {world} + 1 RCCL reduce",
+                       + (f"band split x {world} + 1 splat all-reduce per frame + 1 RCCL reduce" if band else
+                          f"frame split x {world} + 1 RCCL reduce"),
            "rays_per_path": {"subpath": round(st["closest_rays"] / (W * H), 4),
                              "connection": round(st["any_rays"] / (W * H), 4)}}
     if kernel_timing:
@@ -310,6 +320,10 @@ def main():
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     ap.add_argument("--no-bdpt", action="store_true", help="skip the BDPT object (config 4) of the PT run")
     ap.add_argument("--bdpt-steps", type=int, default=8, help="timed BDPT frames of the BDPT object")
+    ap.add_argument("--bdpt-split", default="frame", choices=["frame", "band"],
+                    help="multi-GPU BDPT: whole frames per rank (no per-frame exchange; each rank's sampled-light "
+                         "history differs, BDPT.cl:585) or 8-row bands per rank with one splat all-reduce per frame "
+                         "(the 1-GPU image up to splat summation order; mcrt.dist.exchange_splats)")
     ap.add_argument("--save-image", default=None, help="rank 0 saves the final accumulated image (.npy)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the product path); gloo only rehearses N ranks on one GPU")
@@ -380,7 +394,13 @@ def main():
     fb = lib.FrameBuffer(ctx, W, H)
     filt = T.make_filter(T.BOX)
     bdpt = args.integrator == "bdpt"
-    if bdpt:   # frame split: whole frames per rank
+    band_bdpt = bdpt and args.bdpt_split == "band" and world > 1
+    splat_buf = None
+    if band_bdpt:   # band split: every rank renders every frame's rows of its bands
+        band = dict(band_rows=8, num_bands=world, band_index=rank, integrator=T.INTEGRATOR_BDPT)
+        import torch
+        splat_buf = torch.zeros(4 * W * H, dtype=torch.float32, device="cuda")
+    elif bdpt:   # frame split: whole frames per rank
         band = dict(band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_BDPT)
     else:
         band = dict(band_rows=args.band_rows, num_bands=world, band_index=rank)
@@ -391,10 +411,12 @@ def main():
 
     def step(i, n=1):
         """frames i .. i+n-1 (one mcrt_render_frames call when n > 1)"""
-        frame = rank + world * i if bdpt else i
+        frame = rank + world * i if bdpt and not band_bdpt else i
         kw = dict(max_depth=D, sampler=sampler, rr=args.russian_roulette, rr_start=args.rr_start, **band)
         if n == 1:
             fb.render(ds, cam_of(frame), frame=frame, **kw)
+            if band_bdpt:
+                mdist.exchange_splats(fb, splat_buf)
         else:
             fb.render_frames(ds, [cam_of(frame + k) for k in range(n)], frame=frame, **kw)
         fb.accumulate(filt, 0 if first[0] else frame)   # 0: the first accumulation overwrites
@@ -464,14 +486,14 @@ def main():
     bd = None
     if not bdpt and not args.no_bdpt and not two_level:   # config 4's integrator beside the PT headline
         bd = bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, args.bdpt_steps, args.warmup,
-                          not args.no_kernel_timing)
+                          not args.no_kernel_timing, args.bdpt_split)
 
-    paths = W * H * args.steps * (world if bdpt else 1)
+    paths = W * H * args.steps * (world if bdpt and not band_bdpt else 1)
     value = paths / elapsed / 1e6
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak" if bdpt else "strong", "vs_baseline": None, "dtype": "f32",
+        "scaling": "weak" if bdpt and not band_bdpt else "strong", "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic: deterministic {args.scene} ({scene.num_triangles} tris, seeded generator mcrt/scenes.py)",
         "config": {"workload": f"{args.scene} {W}x{H}, {'BDPT' if bdpt else 'unidirectional PT'}, maxDepth {D}, "
                                f"{args.sampler} sampler, 1 spp per step, box-filter accumulate"
@@ -482,7 +504,8 @@ def main():
                            "device LBVH" if args.device_build else
                            "RadeonRays-identical SAH, " + ("host build" if args.host_build else "device build")),
                    "bvh_build_ms": round(info["build_ms"], 1),
-                   "parallelism": (f"frame split x {world} + 1 RCCL reduce" if bdpt else
+                   "parallelism": (f"band split x {world}, 1 splat all-reduce per frame + 1 RCCL reduce" if band_bdpt
+                                   else f"frame split x {world} + 1 RCCL reduce" if bdpt else
                                    f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce"),
                    "frames_per_launch": batch},
     }

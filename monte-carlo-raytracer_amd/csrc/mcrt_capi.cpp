@@ -187,6 +187,7 @@ struct mcrt_framebuffer_s {
     float4 *cO = nullptr, *cD = nullptr, *cL = nullptr;   // connection queue
     int lastIntegrator = MCRT_INTEGRATOR_PT;
     bool bdptOneSet = false;     // a second BDPT set did not fit in HBM: BDPT frames use slot 0 only
+    bool bdptPendingGather = false;   // band-split BDPT frame waiting for the ranks' summed splats
 };
 
 static int bdpt_max_connections(int D) { const int t = D + 2; return t * (t + 1) / 2 - 2; }   // RTBDPTPass.cpp:404-408
@@ -1234,6 +1235,9 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         q.t = fb->bqT[d & 1];
         return q;
     };
+    const bool bandSplit = f.numBands > 1;
+    if (bandSplit)   // splats of this rank's light paths land in any pixel: clear the whole buffer
+        mcrt::launch_bdpt_clear_splat((int)N, fb->splat, st);
     {
         Timed t(ctx, K_BDPT_START, nullptr, (int64_t)f.numTiles * 64, st);
         mcrt::launch_bdpt_start(sa, f, b, dCam, queue(0), st);
@@ -1262,7 +1266,9 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         Timed t(ctx, K_BDPT_VIS, cq.count, 0, st);
         mcrt::launch_bdpt_vis(tcs, b, cq, (int)(C * N), st);
     }
-    {
+    if (bandSplit) {   // completed by mcrt_bdpt_gather once the ranks' splats are summed
+        fb->bdptPendingGather = true;
+    } else {
         Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)f.numTiles * 64, st);
         mcrt::launch_bdpt_gather(f, b, fb->radiance, st);
     }
@@ -1293,8 +1299,8 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "Sobol sampler requires the 1024x52 Sobol matrices in the scene");
     if (p->integrator != MCRT_INTEGRATOR_PT && p->integrator != MCRT_INTEGRATOR_BDPT)
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "unknown integrator");
-    if (p->integrator == MCRT_INTEGRATOR_BDPT && p->num_bands > 1)
-        return fail(ctx, MCRT_ERROR_INVALID_ARG, "BDPT renders whole frames (num_bands must be 1)");
+    if (fb->bdptPendingGather)
+        return fail(ctx, MCRT_ERROR_NOT_READY, "band-split BDPT frame not completed (mcrt_bdpt_gather)");
     FrameArgs f;
     std::string err;
     if (!frame_args(fb, p, f, err)) return fail(ctx, MCRT_ERROR_INVALID_ARG, err);
@@ -1489,6 +1495,8 @@ MCRT_API mcrt_status mcrt_render_aov(mcrt_scene s, mcrt_framebuffer fb, const mc
 static mcrt_status accumulate(mcrt_framebuffer fb, const mcrt_filter* filters, int nfilters, int32_t frame_index) {
     if (!fb || !filters) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
     mcrt_ctx ctx = fb->ctx;
+    if (fb->bdptPendingGather)
+        return fail(ctx, MCRT_ERROR_NOT_READY, "band-split BDPT frame not completed (mcrt_bdpt_gather)");
     if (!fb->haveBands) {   // no frame rendered yet: whole image
         mcrt_frame_params p{};
         std::memset(&p, 0, sizeof(p));
@@ -1658,6 +1666,43 @@ MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which,
     for (int k = 0; k < 3; ++k)
         HIPCHK(ctx, hipMemcpy(static_cast<char*>(host_dst) + (size_t)k * 16 * max_records, src[k], 16 * (size_t)m,
                               hipMemcpyDeviceToHost));
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst) {
+    if (!fb || !d_dst) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    if (!fb->bdptPendingGather) {   // e.g. a scene without lights: the frame is complete, no splats
+        HIPCHK(ctx, hipMemset(d_dst, 0, 16 * fb->N));
+        return MCRT_OK;
+    }
+    FrameSlot& slot = fb->slot[fb->cur];
+    HIPCHK(ctx, hipStreamSynchronize(slot.stream));
+    HIPCHK(ctx, hipMemcpy(d_dst, fb->splat, 16 * fb->N, hipMemcpyDeviceToDevice));
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_splat_sum) {
+    if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
+    mcrt_ctx ctx = fb->ctx;
+    if (!fb->bdptPendingGather) return MCRT_OK;   // nothing deferred (whole-image or light-less frame)
+    hipSetDevice(ctx->device);
+    FrameSlot& slot = fb->slot[fb->cur];
+    hipStream_t st = slot.stream;
+    if (d_splat_sum && d_splat_sum != fb->splat)
+        HIPCHK(ctx, hipMemcpyAsync(fb->splat, d_splat_sum, 16 * fb->N, hipMemcpyDeviceToDevice, st));
+    BdptArgs b{};
+    b.slots = fb->slots;
+    b.splat = fb->splat;
+    b.ownSlots = bdpt_max_connections(fb->bdptDepth) - fb->bdptDepth;
+    {
+        Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)fb->bands.numTiles * 64, st);
+        mcrt::launch_bdpt_gather(fb->bands, b, fb->radiance, st);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(slot.done, st));
+    fb->bdptPendingGather = false;
     return MCRT_OK;
 }
 

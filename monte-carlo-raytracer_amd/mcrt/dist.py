@@ -40,6 +40,28 @@ def band_rows_of(height, band_rows, num_bands, band_index):
     return rows[rows < height]
 
 
+def exchange_splats(fb, buf, group=None):
+    """Band-split BDPT (mcrt_frame_params.num_bands > 1): the frame's light-tracing strategies
+    splat into any pixel of the image, so after each rank rendered its bands the ranks' splat
+    buffers (float4 x W*H) are summed with ONE all-reduce and every rank completes its bands
+    with the sum (mcrt_bdpt_splats_copy / mcrt_bdpt_gather).  Each pixel's camera subpath, light
+    subpath and persistent sampled-light vertex (BDPT.cl:585-586) stay on the rank that owns the
+    pixel, so the N-rank frame equals the 1-GPU frame up to the order of the splat sums (which
+    the reference's own CAS atomics leave open).  buf: a float32 tensor of 4 * W * H on the GPU."""
+    import torch
+    import torch.distributed as dist
+    fb.bdpt_splats_copy(buf.data_ptr())
+    if buf.is_cuda and dist.get_backend(group) == "gloo":   # gloo rehearsal: via a host copy
+        h = buf.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        buf.copy_(h)
+    else:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    if buf.is_cuda:
+        torch.cuda.current_stream(buf.device).synchronize()
+    fb.bdpt_gather(buf.data_ptr())
+
+
 def frame_split(num_frames, world, rank):
     """Frame split (BDPT, whose light-tracing splats land anywhere in the image): rank r renders
     whole frames r, r + N, r + 2N, ... of the sequence 0 .. num_frames-1."""

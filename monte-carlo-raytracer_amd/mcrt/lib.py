@@ -42,6 +42,8 @@ SIGNATURES = {
     "mcrt_accel_info": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_accel_layout": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_accel_builder": (_c.c_int, [_vp, _vp]),
+    "mcrt_bdpt_splats_copy": (_c.c_int, [_vp, _vp]),
+    "mcrt_bdpt_gather": (_c.c_int, [_vp, _vp]),
     "mcrt_obj_load": (_c.c_int, [_c.c_char_p, _c.c_uint32, _vp]),
     "mcrt_obj_add_directional_light": (_c.c_int, [_vp, _vp, _vp]),
     "mcrt_obj_add_point_light": (_c.c_int, [_vp, _vp, _vp]),
@@ -340,6 +342,14 @@ class FrameBuffer:
 
     def copy_device(self, which, dst_ptr):
         _check(lib().mcrt_framebuffer_copy_device(self.h, which, dst_ptr), self.ctx.h)
+
+    def bdpt_splats_copy(self, dst_ptr):
+        """Band-split BDPT: this rank's light-tracing splats (float4 x W*H) into device memory."""
+        _check(lib().mcrt_bdpt_splats_copy(self.h, dst_ptr), self.ctx.h)
+
+    def bdpt_gather(self, splat_sum_ptr=None):
+        """Completes a band-split BDPT frame with the ranks' summed splats (None: own splats)."""
+        _check(lib().mcrt_bdpt_gather(self.h, splat_sum_ptr), self.ctx.h)
 
     def set_accumulation(self, wsum_ptr, wts_ptr):
         _check(lib().mcrt_framebuffer_set_accumulation(self.h, wsum_ptr, wts_ptr), self.ctx.h)

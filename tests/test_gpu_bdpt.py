@@ -178,3 +178,71 @@ def test_bdpt_frames_in_flight(hip_ctx):
             a, b = o[k][..., :3], ref[k][..., :3]
             close = np.abs(a - b) <= REL_TOL * (np.abs(a) + np.abs(b)) + 1e-30
             assert close.all(), (fif, k, int((~close).sum()))
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_bdpt_band_split_matches_whole_frames(hip_ctx, ranks):
+    """Band-split BDPT (multi-GPU, emulated on one GPU with one framebuffer per rank): rank r
+    renders the camera and light subpaths of its 8-row bands; the ranks' splat buffers are summed
+    (the all-reduce of mcrt.dist.exchange_splats, in rank order here) and every rank completes its
+    bands with mcrt_bdpt_gather; the accumulators are summed at the end.  Against whole frames in
+    one framebuffer, over 5 frames (the sampled-light state, BDPT.cl:585-586, persists on the
+    pixel's owner):
+      * camera / light vertex counts and the sampled-light planes of every pixel: bit-exact;
+      * each frame's radiance and the reduced accumulation: within the splat tolerance (sums of
+        the same splats in another order)."""
+    import torch
+    from mcrt import lib
+    from mcrt import dist as mdist
+    name, W, H, D, frames = "mixed", 96, 64, 2, 5
+    ds = lib.DeviceScene(hip_ctx, build_scene(name))
+    cam = scene_camera(name, W, H)
+    filt = T.make_filter(T.BOX)
+    full = lib.FrameBuffer(hip_ctx, W, H)
+    fbs = [lib.FrameBuffer(hip_ctx, W, H) for _ in range(ranks)]
+    rows = [mdist.band_rows_of(H, 8, ranks, r) for r in range(ranks)]
+    bufs = [torch.zeros(4 * W * H, dtype=torch.float32, device="cuda") for _ in range(ranks)]
+    N = W * H
+    for f in range(frames):
+        full.render(ds, cam, frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT)
+        full.accumulate(filt, f)
+        for r, fb in enumerate(fbs):
+            fb.render(ds, cam, frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT, band_rows=8, num_bands=ranks,
+                      band_index=r)
+            with pytest.raises(lib.MCRTError):   # the frame is not complete before the exchange
+                fb.accumulate(filt, f)
+            fb.bdpt_splats_copy(bufs[r].data_ptr())
+        total = bufs[0].clone()
+        for r in range(1, ranks):
+            total += bufs[r]
+        torch.cuda.synchronize()
+        for fb in fbs:
+            fb.bdpt_gather(total.data_ptr())
+            fb.accumulate(filt, f)
+        ref = full.read(0)
+        for r, fb in enumerate(fbs):
+            a, b = fb.read(0)[rows[r], :, :3], ref[rows[r], :, :3]
+            close = np.abs(a - b) <= REL_TOL * (np.abs(a) + np.abs(b)) + 1e-30
+            assert close.all(), (ranks, f, r, int((~close).sum()))
+        want = {k: full.read_bdpt(k) for k in ("camera_counts", "light_counts", "sampled_light")}
+        for k, w in want.items():
+            got = np.zeros_like(w)
+            per = w.size // N   # bytes per pixel in this array (planes x pixel layout for sampled_light)
+            for r, fb in enumerate(fbs):
+                pix = (rows[r][:, None] * W + np.arange(W)[None, :]).ravel()
+                g = fb.read_bdpt(k)
+                if k == "sampled_light":   # D planes of float4 x N
+                    gv, wv = g.view(np.uint32).reshape(D, N, 4), got.view(np.uint32).reshape(D, N, 4)
+                    wv[:, pix] = gv[:, pix]
+                else:
+                    got.view(np.int32)[pix] = g.view(np.int32)[pix]
+            assert per > 0
+            np.testing.assert_array_equal(got, w, err_msg=f"frame {f} {k}")
+    # end of job: ONE sum of the per-rank accumulators (zero outside each rank's bands)
+    acc = sum(fb.read(1).astype(np.float64) for fb in fbs)
+    ref_acc = full.read(1)
+    close = np.abs(acc - ref_acc) <= 2 * REL_TOL * np.abs(ref_acc) + 1e-30
+    assert close.all(), int((~close).sum())
+    for fb in fbs + [full]:
+        fb.close()
+    ds.close()
