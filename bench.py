@@ -337,7 +337,7 @@ def main():
     ap.add_argument("--rr-start", type=int, default=1, help="first bounce whose extension rays RR may cut")
     ap.add_argument("--batch", type=int, default=0,
                     help="PT frames per mcrt_render_frames call (one launch sequence for all of them); "
-                         "0 = auto (min(16, 4 x ranks))")
+                         "0 = auto (16)")
     args = ap.parse_args()
 
     import torch
@@ -405,9 +405,13 @@ def main():
     else:
         band = dict(band_rows=args.band_rows, num_bands=world, band_index=rank)
     first = [True]
-    # auto: 4 frames per launch on one GPU, 16 from 4 GPUs on (a 1/N band share x 16 frames keeps
-    # every launch at >= 4 whole images of paths; tools/scale_emulate.py sweeps)
-    batch = 1 if bdpt else (args.batch if args.batch > 0 else min(16, 4 * world))
+    # auto: 16 frames per launch (MCRT_MAX_BATCH_FRAMES); at N = 1 the sweep tools/r2_gpu12.sh
+    # measured 1120 / 1140 / 1145 / 1147 Mpaths/s for 2 / 4 / 8 / 16 frames per launch, and a 1/N
+    # band share x 16 frames keeps every multi-GPU launch at >= 2 whole images of paths
+    batch = 1 if bdpt else (args.batch if args.batch > 0 else 16)
+    # the untimed per-kernel pass and the roofline price launches of (at most) 4 frames, which
+    # keeps the oracle's distinct-node count of one launch to ~10 s of CPU
+    stats_batch = min(batch, 4)
 
     def step(i, n=1):
         """frames i .. i+n-1 (one mcrt_render_frames call when n > 1)"""
@@ -422,10 +426,11 @@ def main():
         fb.accumulate(filt, 0 if first[0] else frame)   # 0: the first accumulation overwrites
         first[0] = False
 
-    def run(i0, count):
+    def run(i0, count, per=None):
         i = 0
+        per = per or batch
         while i < count:
-            n = min(batch, count - i)
+            n = min(per, count - i)
             step(i0 + i, n)
             i += n
 
@@ -470,14 +475,14 @@ def main():
     kstats = {}
     if not args.no_kernel_timing:
         # per-kernel HIP-event durations in a separate, untimed pass: one frame slot (kernels do not
-        # share the GPU with another frame's launches, so each duration is the kernel's own), the
-        # same frames per launch as the timed region
+        # share the GPU with another frame's launches, so each duration is the kernel's own), at
+        # most 4 frames per launch (stats_batch)
         fb.set_frames_in_flight(1)
-        run(frame0 + args.steps, batch)   # the slot re-binds outside the profiled launches
+        run(frame0 + args.steps, stats_batch, stats_batch)   # the slot re-binds outside the profiled launches
         ctx.sync()
         ctx.set_profiling(True)
         ctx.reset_stats()
-        run(frame0 + args.steps + batch, args.stats_launches * batch)
+        run(frame0 + args.steps + stats_batch, args.stats_launches * stats_batch, stats_batch)
         ctx.sync()
         kstats = ctx.kernel_stats()
         ctx.set_profiling(False)
@@ -538,11 +543,11 @@ def main():
                                   "items_per_launch": round(v["items"] / max(v["launches"], 1), 1)}
                               for k, v in kstats.items()}
             out["kernels_note"] = ("HIP-event durations from an untimed pass after the timed region: one frame slot "
-                                   f"(no overlap with another frame's launches), {batch} frames per launch")
+                                   f"(no overlap with another frame's launches), {stats_batch} frames per launch (the timed region uses {batch})")
             dom = max(kstats, key=lambda k: kstats[k]["ms"])
             if oracle_ok and dom == "k_shadow_extend" and not args.no_roofline_model:
                 avg_ms = kstats[dom]["ms"] / max(kstats[dom]["launches"], 1)
-                out["roofline"] = roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx,
+                out["roofline"] = roofline_shadow_extend(scene, cam_of, W, H, D, stats_batch, avg_ms, qcounts, ctx,
                                                          cpu["_oracle"] if cpu else None)
         if bd is not None:
             bdo = {k: v for k, v in bd.items() if not k.startswith("_")}
