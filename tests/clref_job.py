@@ -149,6 +149,7 @@ SCALE_CASES = {
     "ieee": [
         ("sm_pt_1080p", "san_miguel_proxy", 1920, 1080, "pt", (0, 1), 2),            # headline / config 4 scene
         ("sponza_pt_1080p", "sponza_proxy", 1920, 1080, "pt", (0, 1), 2),           # config 3
+        ("dragon_pt_1080p", "dragon_proxy", 1920, 1080, "pt", (0, 1), 2),           # config 2
         ("sm_bdpt_960x540", "san_miguel_proxy", 960, 540, "bdpt", (0, 1), 2),       # config 4 integrator
     ],
     "sobol_ieee": [
@@ -162,8 +163,9 @@ BDPT_VERTEX_STRIDE = 17   # vertex records kept for every 17th pixel (the full a
 
 def scale_scene(name):
     from mcrt import sobol_matrices
-    sc = scenes.san_miguel_proxy() if name == "san_miguel_proxy" else scenes.sponza_proxy() \
-        if name == "sponza_proxy" else build_scene(name)
+    full = {"san_miguel_proxy": scenes.san_miguel_proxy, "sponza_proxy": scenes.sponza_proxy,
+            "dragon_proxy": scenes.dragon_proxy}
+    sc = full[name]() if name in full else build_scene(name)
     sc.sobol = sobol_matrices()
     return sc
 

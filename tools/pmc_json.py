@@ -63,7 +63,7 @@ def main():
     pmc, ms, raw = collect(dbs, last)
     res = {"source": f"rocprofv3 --kernel-trace --pmc passes ({', '.join(os.path.basename(os.path.dirname(x)) for x in dbs)})",
            "config": f"{cmd}; medians over the last {last} dispatches of each kernel = the untimed one-slot "
-                     "kernel-timing pass (4 frames per launch)",
+                     "kernel-timing pass " + ("(1 frame per launch)" if "bdpt" in cmd else "(4 frames per launch)"),
            "correction": "hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (MI355X_MICROARCH.md HBM section)",
            "kernels": {}}
     for k, c in pmc.items():
