@@ -826,7 +826,7 @@ __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const i
     r.d = ld3(d);
     r.tmax = o.w;
     r.mask = -1;
-    const bool occluded = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow);
+    const bool occluded = traceAny<TL>(c, r, lds + lane, raySpill(c, blockIdx.x, lane));
     const int code = __float_as_int(d.w);
     if (code >= 0) {
         if (occluded) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);

@@ -73,6 +73,8 @@ struct TraceCtx {
     const float4* nodes;   // 4 float4 per node (mcrt_bvh.cpp): internal = child boxes + indices, leaf = triangle
                            // two-level (mcrt_bvh2l.cpp): + instance records (world->object rows, bottom root)
     int twoLevel;          // selects the kernels' two-level instantiation (launch-time, not per lane)
+    int compact;           // flat tree in the descent-compact records (mcrt_traverse.h traverseOct2)
+    uint32_t rootWord;     // compact records: the root's child word (index | leaf bit)
     uint32_t* spill;
     int spillCap;           // spill entries per ray (a multiple of STACK_LDS)
     int* overflow;
@@ -105,6 +107,9 @@ void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts
 void launch_denoise(int W, int H, int r, float ss, float sr, const float4* in, float4* out, hipStream_t st);
 void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStream_t st);
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st);
+// descent-compact traversal records (mcrt_traverse.h traverseOct2); *bad = 1 if the tree lacks
+// the exact-union property or an index does not fit the 27-bit child word
+void launch_pack_compact(const float4* in, float4* out, uint32_t n, int* bad, hipStream_t st);
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& q, hipStream_t st);
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,

@@ -62,11 +62,11 @@ __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* _
     r.tmax = rr.o.w;
     r.mask = rr.extra[0];
     if (ANY) {
-        occl[i] = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow) ? 1 : -1;
+        occl[i] = traceAny<TL>(c, r, lds + lane, raySpill(c, blockIdx.x, lane)) ? 1 : -1;
         return;
     }
     float t;
-    const float4 h4 = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow, t);
+    const float4 h4 = traceClosest<TL>(c, r, lds + lane, raySpill(c, blockIdx.x, lane), t);
     if (__float_as_int(h4.z) >= 0) {
         mcrt_intersection h;
         h.shapeid = __float_as_int(h4.z);
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
     r.mask = -1;
     float t;
     hitOut[(size_t)k * f.W * f.H + (size_t)y * f.W + x] =
-        traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, tileAll, lane), c.spillCap, c.overflow, t);
+        traceClosest<TL>(c, r, lds + lane, raySpill(c, tileAll, lane), t);
 }
 
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict
     r.tmax = RT_MAX_TRACE_F;
     r.mask = -1;
     float t;
-    hitOut[i] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blk, lane), c.spillCap, c.overflow, t);
+    hitOut[i] = traceClosest<TL>(c, r, lds + lane, raySpill(c, blk, lane), t);
 }
 
 // Any hit over the shadow queue + ShadowPass (PathTracing.cl:186-217):
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     r.d = ld3(d);
     r.tmax = o.w;
     r.mask = -1;
-    const float V = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blk, lane), c.spillCap, c.overflow) ? 0.0f : 1.0f;
+    const float V = traceAny<TL>(c, r, lds + lane, raySpill(c, blk, lane)) ? 0.0f : 1.0f;
     const int pix = __float_as_int(d.w);
     float4 acc = radiance[pix];
     acc.x += L.x * V;
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.tmax = RT_MAX_TRACE_F;
         r.mask = -1;
         float t;
-        hitOut[i] = traceClosest<TL>(c.nodes, r, lds + lane, raySpill(c, blk, lane), c.spillCap, c.overflow, t);
+        hitOut[i] = traceClosest<TL>(c, r, lds + lane, raySpill(c, blk, lane), t);
     } else {
         const int ns = *shadowCount;
         const int sb = (ns + 63) >> 6;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.d = ld3(d);
         r.tmax = o.w;
         r.mask = -1;
-        const float V = traceAny<TL>(c.nodes, r, lds + lane, raySpill(c, blockIdx.x, lane), c.spillCap, c.overflow) ? 0.0f : 1.0f;
+        const float V = traceAny<TL>(c, r, lds + lane, raySpill(c, blockIdx.x, lane)) ? 0.0f : 1.0f;
         const int pix = __float_as_int(d.w);
         float4 acc = radiance[pix];
         acc.x += L.x * V;
@@ -633,6 +633,64 @@ __global__ __launch_bounds__(256) void k_stream_copy(const f4* __restrict__ src,
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
+// Descent-compact records (mcrt_traverse.h traverseOct2) from the mcrt_bvh.cpp records, one
+// thread per node.  Internal node i: per coordinate slot the union value X_s (the node's own box,
+// which its parent record holds as a child box), the other child's value S_s and the owner bit.
+// Each thread also checks, for each internal child, that the box its own record carries for
+// that child equals the union of the child's two boxes -- the property the compact decode rests
+// on (RR pulls bounds into parents); a mismatch sets *bad and the host keeps the plain layout.
+__global__ void k_pack_compact(const float4* __restrict__ in, float4* __restrict__ out, uint32_t n, int* bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int4* in4 = reinterpret_cast<const int4*>(in);
+    const float4 n0 = in[4 * (size_t)i], n1 = in[4 * (size_t)i + 1], n2 = in[4 * (size_t)i + 2];
+    const int4 n3 = in4[4 * (size_t)i + 3];
+    float4* o = out + 4 * (size_t)i;
+    if (n3.x < 0) {   // leaf: unchanged
+        o[0] = n0;
+        o[1] = n1;
+        o[2] = n2;
+        reinterpret_cast<int4*>(o)[3] = n3;
+        return;
+    }
+    const float A[6] = {n0.x, n0.y, n0.z, n0.w, n2.x, n2.y};
+    const float B[6] = {n1.x, n1.y, n1.z, n1.w, n2.z, n2.w};
+    float X[6], S[6];
+    uint32_t own = 0;
+    for (int k = 0; k < 6; ++k) {
+        X[k] = (k & 1) ? fmaxf(A[k], B[k]) : fminf(A[k], B[k]);
+        const bool a = A[k] == X[k];
+        own |= (a ? 1u : 0u) << k;
+        S[k] = a ? B[k] : A[k];
+    }
+    const uint32_t l = (uint32_t)n3.x, r = (uint32_t)n3.y;
+    bool leaf[2];
+    for (int c = 0; c < 2; ++c) {
+        const uint32_t ch = c ? r : l;
+        if (ch >= n) {
+            *bad = 1;
+            leaf[c] = false;
+            continue;
+        }
+        const int4 m = in4[4 * (size_t)ch + 3];
+        leaf[c] = m.x < 0;
+        if (leaf[c]) continue;
+        const float4 c0 = in[4 * (size_t)ch], c1 = in[4 * (size_t)ch + 1], c2 = in[4 * (size_t)ch + 2];
+        const float* P = c ? B : A;
+        const float U[6] = {fminf(c0.x, c1.x), fmaxf(c0.y, c1.y), fminf(c0.z, c1.z),
+                            fmaxf(c0.w, c1.w), fminf(c2.x, c2.z), fmaxf(c2.y, c2.w)};
+        for (int k = 0; k < 6; ++k)
+            if (!(U[k] == P[k])) *bad = 1;
+    }
+    if (l > CW_IDX || r > CW_IDX) *bad = 1;
+    const uint32_t wA = (l & CW_IDX) | (leaf[0] ? CW_LEAF : 0u) | ((own & 7u) << 28);
+    const uint32_t wB = (r & CW_IDX) | (leaf[1] ? CW_LEAF : 0u) | ((own >> 3) << 28);
+    o[0] = make_float4(S[0], S[1], S[2], S[3]);
+    o[1] = make_float4(S[4], S[5], __uint_as_float(wA), __uint_as_float(wB));
+    o[2] = make_float4(X[0], X[1], X[2], X[3]);
+    o[3] = make_float4(X[4], X[5], 0.0f, 0.0f);
+}
+
 namespace mcrt {
 
 void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, mcrt_intersection* hits, int* occl,
@@ -711,6 +769,10 @@ void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, h
     const size_t blocks = std::min(need, (size_t)std::max(numCUs, 1) * 8);
     hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const f4*>(src),
                        reinterpret_cast<f4*>(dst), n4);
+}
+
+void launch_pack_compact(const float4* in, float4* out, uint32_t n, int* bad, hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_compact, dim3((n + 255) / 256), dim3(256), 0, st, in, out, n, bad);
 }
 
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st) {

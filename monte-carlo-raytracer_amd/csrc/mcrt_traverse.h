@@ -170,26 +170,176 @@ MCRT_DEV int traverseOct(const float4* __restrict__ nodes, const TraceRay& r, f3
     return hit;
 }
 
+// ---------------------------------------------------------------------------
+// Descent-compact records (mcrt_kernels.hip k_pack_compact), used by the camera-ray launch.
+//
+// A coherent launch is bound by the vector-memory path, not the ALUs: every step gathers four
+// 16-B pieces per lane from a record (measured on k_primary: TA busy 92 % of its cycles, L2 hit
+// 94 %).  The records are re-laid out to need fewer loads per step without changing a single box
+// value the slab tests see:
+//   * a parent's two child boxes are exact float min/max unions (RR bvh2.cpp pulls bounds into
+//     parents), so per coordinate slot s (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z) one child holds
+//     the node's own value X_s and only the OTHER child's value S_s must be stored, plus a bit
+//     saying which child owns X_s;
+//   * 80 % of internal steps descend into a child whose box the previous step just tested, so
+//     X's slab distances are already in registers (dX_s = fma(X_s, 1/d, -o/d), the same floats).
+// Record of internal node i (children A = left, B = right):
+//   q0 = (S0, S1, S2, S3), q1 = (S4, S5, wA, wB),      <- a descent reads only these 32 B
+//   q2 = (X.lo.x, X.hi.x, X.lo.y, X.hi.y), q3 = (X.lo.z, X.hi.z, 0, 0)   <- + these after a pop
+//   child word w = index (bits 0-26) | leaf (bit 27) | owner bits of 3 slots (28-30)
+// Leaf record: (v0, shapeId), (v1 - v0, primId), (v2 - v0, 0), (-1, -1, 0, 0) as before: 48 B,
+// and the leaf bit in the parent's word says so before the fetch.  A step loads 2, 3 (leaf) or
+// 4 (after a pop) pieces instead of 4; the decode reproduces both child boxes exactly (the
+// owner's value is X_s bit for bit up to the sign of a zero, which no slab decision can see),
+// so the visit order, every box test and every triangle test are those of traverseOct.
+// Measured (SM proxy 1080p): k_primary -9 %; the incoherent extension / shadow launches are
+// bound by L2 misses instead and ran 2-5 % slower with it, so they keep the plain records.
+// ---------------------------------------------------------------------------
+#define CW_IDX 0x07FFFFFFu
+#define CW_LEAF 0x08000000u
+#define CW_NODE 0x0FFFFFFFu   // index | leaf, the part the stack keeps
+#define CW_DONE 0x80000000u
+
+template <bool ANY, int OCT>
+MCRT_DEV int traverseOct2(const float4* __restrict__ nodes, uint32_t rootWord, const TraceRay& r, f3 inv,
+                          uint32_t* stk, uint32_t* spill, int spillCap, int* overflowFlag, float& tHit) {
+    const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
+    float t = r.tmax;
+    int hit = -1;
+    uint32_t word = rootWord;
+    bool popped = true;   // the root's own box comes from its record
+    // slab distances of the node's own box per slot (valid after a descent)
+    float dx0 = 0.f, dx1 = 0.f, dx2 = 0.f, dx3 = 0.f, dx4 = 0.f, dx5 = 0.f;
+    stk[0] = CW_DONE;
+    int sp = 1, spillTop = 0;
+    while (word != CW_DONE) {
+        const uint32_t idx = word & CW_IDX;
+        const bool leaf = (word & CW_LEAF) != 0;
+        const float4* q = nodes + 4 * (size_t)idx;
+        const float4 q0 = q[0], q1 = q[1];
+        float4 q2 = make_float4(0.f, 0.f, 0.f, 0.f), q3 = q2;
+        if (leaf || popped) q2 = q[2];
+        if (popped && !leaf) q3 = q[3];
+        bool pop = true;
+        uint32_t next = CW_DONE;
+        if (!leaf) {
+            if (popped) {
+                dx0 = fmaf(q2.x, inv.x, oxi.x); dx1 = fmaf(q2.y, inv.x, oxi.x);
+                dx2 = fmaf(q2.z, inv.y, oxi.y); dx3 = fmaf(q2.w, inv.y, oxi.y);
+                dx4 = fmaf(q3.x, inv.z, oxi.z); dx5 = fmaf(q3.y, inv.z, oxi.z);
+            }
+            const uint32_t wA = __float_as_uint(q1.z), wB = __float_as_uint(q1.w);
+            const float ds0 = fmaf(q0.x, inv.x, oxi.x), ds1 = fmaf(q0.y, inv.x, oxi.x);
+            const float ds2 = fmaf(q0.z, inv.y, oxi.y), ds3 = fmaf(q0.w, inv.y, oxi.y);
+            const float ds4 = fmaf(q1.x, inv.z, oxi.z), ds5 = fmaf(q1.y, inv.z, oxi.z);
+            // owner masks (all ones: A holds X_s) and the two children's slot distances
+            const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)wA, 28, 1);
+            const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)wA, 29, 1);
+            const uint32_t m2 = (uint32_t)__builtin_amdgcn_sbfe((int)wA, 30, 1);
+            const uint32_t m3 = (uint32_t)__builtin_amdgcn_sbfe((int)wB, 28, 1);
+            const uint32_t m4 = (uint32_t)__builtin_amdgcn_sbfe((int)wB, 29, 1);
+            const uint32_t m5 = (uint32_t)__builtin_amdgcn_sbfe((int)wB, 30, 1);
+#define MCRT_SEL(m, a, b) __uint_as_float(((m) & __float_as_uint(a)) | (~(m) & __float_as_uint(b)))
+            const float A0 = MCRT_SEL(m0, dx0, ds0), B0 = MCRT_SEL(m0, ds0, dx0);
+            const float A1 = MCRT_SEL(m1, dx1, ds1), B1 = MCRT_SEL(m1, ds1, dx1);
+            const float A2 = MCRT_SEL(m2, dx2, ds2), B2 = MCRT_SEL(m2, ds2, dx2);
+            const float A3 = MCRT_SEL(m3, dx3, ds3), B3 = MCRT_SEL(m3, ds3, dx3);
+            const float A4 = MCRT_SEL(m4, dx4, ds4), B4 = MCRT_SEL(m4, ds4, dx4);
+            const float A5 = MCRT_SEL(m5, dx5, ds5), B5 = MCRT_SEL(m5, ds5, dx5);
+#undef MCRT_SEL
+            float a0, a1, b0, b1;
+            if constexpr (OCT >= 0) {
+                // per axis the entry plane is lo for 1/d > 0 and hi otherwise (fma is monotone)
+                constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
+                a0 = fmaxf(fmaxf(SX ? A1 : A0, SY ? A3 : A2), fmaxf(SZ ? A5 : A4, 0.0f));
+                a1 = fminf(fminf(SX ? A0 : A1, SY ? A2 : A3), fminf(SZ ? A4 : A5, t));
+                b0 = fmaxf(fmaxf(SX ? B1 : B0, SY ? B3 : B2), fmaxf(SZ ? B5 : B4, 0.0f));
+                b1 = fminf(fminf(SX ? B0 : B1, SY ? B2 : B3), fminf(SZ ? B4 : B5, t));
+            } else {   // RR intersect_bvh2_lds.cl:54-63 (fast_intersect_bbox2)
+                a0 = fmaxf(fmaxf(fmaxf(fminf(A0, A1), fminf(A2, A3)), fminf(A4, A5)), 0.0f);
+                a1 = fminf(fminf(fminf(fmaxf(A0, A1), fmaxf(A2, A3)), fmaxf(A4, A5)), t);
+                b0 = fmaxf(fmaxf(fmaxf(fminf(B0, B1), fminf(B2, B3)), fminf(B4, B5)), 0.0f);
+                b1 = fminf(fminf(fminf(fmaxf(B0, B1), fmaxf(B2, B3)), fmaxf(B4, B5)), t);
+            }
+            const bool h0 = a0 <= a1, h1 = b0 <= b1;
+            const bool c1first = h1 && (a0 > b0);   // intersect_bvh2_lds.cl:128-141
+            if (h0 && h1) {   // defer the far child
+                if (sp == STACK_LDS) {   // spill entries 1..15 (RR: intersect_bvh2_lds.cl:146-155)
+                    if (spillTop + STACK_LDS - 1 <= spillCap) {
+                        for (int k = 1; k < STACK_LDS; ++k) spill[(size_t)(spillTop + k - 1) * 64] = stk[k * 64];
+                        spillTop += STACK_LDS - 1;
+                    } else {
+                        *overflowFlag = 1;   // depth beyond capacity: drop (reported by the host)
+                    }
+                    sp = 1;
+                }
+                stk[sp * 64] = (c1first ? wA : wB) & CW_NODE;
+                ++sp;
+            }
+            if (h0 || h1) {
+                const bool toB = c1first || !h0;
+                next = (toB ? wB : wA) & CW_NODE;
+                dx0 = toB ? B0 : A0; dx1 = toB ? B1 : A1; dx2 = toB ? B2 : A2;
+                dx3 = toB ? B3 : A3; dx4 = toB ? B4 : A4; dx5 = toB ? B5 : A5;
+                pop = false;
+            }
+        } else if (r.mask != __float_as_int(q0.w)) {   // RR_RAY_MASK
+            const float th = triHit(r, q0, q1, q2, t);
+            if (th < t) {
+                t = th;
+                hit = (int)idx;
+                if (ANY) pop = false;   // next = DONE
+            }
+        }
+        if (pop) {
+            --sp;
+            next = stk[sp * 64];
+            if (next == CW_DONE && spillTop > 0) {   // refill (intersect_bvh2_lds.cl:182-191)
+                spillTop -= STACK_LDS - 1;
+                for (int k = 1; k < STACK_LDS; ++k) stk[k * 64] = spill[(size_t)(spillTop + k - 1) * 64];
+                sp = STACK_LDS - 1;
+                next = stk[sp * 64];
+            }
+        }
+        popped = pop;
+        word = next;
+    }
+    tHit = t;
+    return hit;
+}
+
 template <bool ANY>
-MCRT_DEV int traverse(const float4* __restrict__ nodes, const TraceRay& r, uint32_t* stk, uint32_t* spill, int spillCap,
-                      int* overflowFlag, float& tHit) {
+MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, float& tHit) {
     const f3 inv = safeInvDir(r.d);
 #if MCRT_OCT_TRAV
     const int oct = (int)(__float_as_uint(inv.x) >> 31) | (int)((__float_as_uint(inv.y) >> 31) << 1) |
                     (int)((__float_as_uint(inv.z) >> 31) << 2);
     const int oct0 = __builtin_amdgcn_readfirstlane(oct);
     if (__all(oct == oct0)) {
-        switch (oct0) {
-#define MCRT_OCT_CASE(k) \
-    case k: return traverseOct<ANY, k>(nodes, r, inv, stk, spill, spillCap, overflowFlag, tHit);
-            MCRT_OCT_CASE(0) MCRT_OCT_CASE(1) MCRT_OCT_CASE(2) MCRT_OCT_CASE(3)
-            MCRT_OCT_CASE(4) MCRT_OCT_CASE(5) MCRT_OCT_CASE(6) MCRT_OCT_CASE(7)
+        if (c.compact) {
+            switch (oct0) {
+#define MCRT_OCT_CASE(k)                                                                                       \
+    case k:                                                                                                    \
+        return traverseOct2<ANY, k>(c.nodes, c.rootWord, r, inv, stk, spill, c.spillCap, c.overflow, tHit);
+                MCRT_OCT_CASE(0) MCRT_OCT_CASE(1) MCRT_OCT_CASE(2) MCRT_OCT_CASE(3)
+                MCRT_OCT_CASE(4) MCRT_OCT_CASE(5) MCRT_OCT_CASE(6) MCRT_OCT_CASE(7)
 #undef MCRT_OCT_CASE
-            default: break;
+                default: break;
+            }
+        } else {
+            switch (oct0) {
+#define MCRT_OCT_CASE(k) \
+    case k: return traverseOct<ANY, k>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit);
+                MCRT_OCT_CASE(0) MCRT_OCT_CASE(1) MCRT_OCT_CASE(2) MCRT_OCT_CASE(3)
+                MCRT_OCT_CASE(4) MCRT_OCT_CASE(5) MCRT_OCT_CASE(6) MCRT_OCT_CASE(7)
+#undef MCRT_OCT_CASE
+                default: break;
+            }
         }
     }
 #endif
-    return traverseOct<ANY, -1>(nodes, r, inv, stk, spill, spillCap, overflowFlag, tHit);
+    if (c.compact) return traverseOct2<ANY, -1>(c.nodes, c.rootWord, r, inv, stk, spill, c.spillCap, c.overflow, tHit);
+    return traverseOct<ANY, -1>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit);
 }
 
 // RR common.cl:249-277 (triangle_calculate_barycentrics)
@@ -362,25 +512,23 @@ MCRT_DEV float4 closestRecord2L(const float4* __restrict__ nodes, const TraceRay
 
 // Closest / any hit over either layout; TL selects the two-level instantiation.
 template <bool TL>
-MCRT_DEV float4 traceClosest(const float4* __restrict__ nodes, const TraceRay& r, uint32_t* stk, uint32_t* spill,
-                             int spillCap, int* overflowFlag, float& t) {
+MCRT_DEV float4 traceClosest(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, float& t) {
     if (TL) {
         int inst;
-        const int tri = traverse2L<false>(nodes, r, stk, spill, spillCap, overflowFlag, t, inst);
-        return closestRecord2L(nodes, r, tri, inst, t);
+        const int tri = traverse2L<false>(c.nodes, r, stk, spill, c.spillCap, c.overflow, t, inst);
+        return closestRecord2L(c.nodes, r, tri, inst, t);
     }
-    const int tri = traverse<false>(nodes, r, stk, spill, spillCap, overflowFlag, t);
-    return closestRecord(nodes, r, tri, t);
+    const int tri = traverse<false>(c, r, stk, spill, t);
+    return closestRecord(c.nodes, r, tri, t);   // leaf records are the same in both flat layouts
 }
 template <bool TL>
-MCRT_DEV bool traceAny(const float4* __restrict__ nodes, const TraceRay& r, uint32_t* stk, uint32_t* spill,
-                       int spillCap, int* overflowFlag) {
+MCRT_DEV bool traceAny(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill) {
     float t;
     if (TL) {
         int inst;
-        return traverse2L<true>(nodes, r, stk, spill, spillCap, overflowFlag, t, inst) >= 0;
+        return traverse2L<true>(c.nodes, r, stk, spill, c.spillCap, c.overflow, t, inst) >= 0;
     }
-    return traverse<true>(nodes, r, stk, spill, spillCap, overflowFlag, t) >= 0;
+    return traverse<true>(c, r, stk, spill, t) >= 0;
 }
 
 // XCD-aware workgroup order for the traversal launches.  Workgroups are dealt round-robin to the

@@ -1,0 +1,116 @@
+/* trav_sim.c -- CPU model of the GPU traversal's dependent-fetch structure (analysis tool).
+ *
+ * Replays the Bvh2 closest/any traversal (intersect_bvh2_lds.cl:66-363, same node order as
+ * the oracle) and counts, per ray, the node records visited and the number of dependent
+ * fetch rounds under schemes that fetch several records in one round:
+ *   K = 1  one record per round (the current kernel);
+ *   K = k  a round fetches the current record plus, while the records already chosen are
+ *          leaves, the next stack entries (the nodes a leaf's pop will reach), up to k records.
+ * A leaf never changes which node comes next (closest-hit pops after every leaf), so the
+ * k-record rounds visit exactly the reference's sequence.  Waves = 64 consecutive rays;
+ * a wave's rounds = the max over its lanes.
+ * Build: gcc -O2 -shared -fPIC tools/trav_sim.c -o /tmp/trav_sim.so -lm
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+typedef struct { float lmin[3]; uint32_t left; float lmax[3]; uint32_t mesh; float rmin[3]; uint32_t right; float rmax[3]; uint32_t prim; } Node;
+typedef struct { float o[4]; float d[4]; int32_t extra[2]; int32_t bf; int32_t pad; } Ray;
+#define INV 0xffffffffu
+#define KMAX 4
+
+static inline float sinv(float d) { return 1.0f / (fabsf(d) > 1e-8f ? d : copysignf(1e-8f, d)); }
+
+static void bbox(const float* lo, const float* hi, const float* inv, const float* oxi, float tmax, float* t0, float* t1) {
+    float f[3], n[3];
+    for (int k = 0; k < 3; ++k) { f[k] = fmaf(hi[k], inv[k], oxi[k]); n[k] = fmaf(lo[k], inv[k], oxi[k]); }
+    *t1 = fminf(fminf(fminf(fmaxf(f[0], n[0]), fmaxf(f[1], n[1])), fmaxf(f[2], n[2])), tmax);
+    *t0 = fmaxf(fmaxf(fmaxf(fminf(f[0], n[0]), fminf(f[1], n[1])), fminf(f[2], n[2])), 0.f);
+}
+static float tri(const Ray* r, const Node* n, float tmax) {
+    float e1[3], e2[3], s1[3], d[3], s2[3];
+    for (int k = 0; k < 3; ++k) { e1[k] = n->lmax[k] - n->lmin[k]; e2[k] = n->rmin[k] - n->lmin[k]; }
+    s1[0] = r->d[1] * e2[2] - r->d[2] * e2[1]; s1[1] = r->d[2] * e2[0] - r->d[0] * e2[2]; s1[2] = r->d[0] * e2[1] - r->d[1] * e2[0];
+    float den = s1[0] * e1[0] + s1[1] * e1[1] + s1[2] * e1[2];
+    if (den == 0.f) return tmax;
+    float id = 1.0f / den;
+    for (int k = 0; k < 3; ++k) d[k] = r->o[k] - n->lmin[k];
+    float b1 = (d[0] * s1[0] + d[1] * s1[1] + d[2] * s1[2]) * id;
+    s2[0] = d[1] * e1[2] - d[2] * e1[1]; s2[1] = d[2] * e1[0] - d[0] * e1[2]; s2[2] = d[0] * e1[1] - d[1] * e1[0];
+    float b2 = (r->d[0] * s2[0] + r->d[1] * s2[1] + r->d[2] * s2[2]) * id;
+    float t = (e2[0] * s2[0] + e2[1] * s2[1] + e2[2] * s2[2]) * id;
+    if (b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || t < 0.f || t > tmax) return tmax;
+    return t;
+}
+
+/* out per ray: [0] visits, [1] leaf visits, [2..2+KMAX-1] rounds for K=1..KMAX,
+ * [2+KMAX] internal visits reached by descent (not by a pop); hit_t/hit_node */
+void sim(const Node* nodes, const Ray* rays, int n, int any, int32_t* out, float* hit_t, int32_t* hit_node) {
+    static uint32_t stack[1 << 16];
+    static uint32_t seq[1 << 20];
+    static uint8_t leaf[1 << 20];
+    static uint32_t stk_at[1 << 20]; /* stack depth when the record was chosen (for the K>1 rule) */
+    (void)stk_at;
+    for (int i = 0; i < n; ++i) {
+        const Ray* r = &rays[i];
+        int32_t* o = out + (size_t)i * (3 + KMAX);
+        memset(o, 0, sizeof(int32_t) * (3 + KMAX));
+        if (r->extra[1] == 0) { hit_t[i] = -1; hit_node[i] = -1; continue; }
+        float inv[3], oxi[3];
+        for (int k = 0; k < 3; ++k) { inv[k] = sinv(r->d[k]); oxi[k] = -r->o[k] * inv[k]; }
+        float ct = r->o[3];
+        uint32_t addr = 0, best = INV;
+        int sp = 0, nv = 0, desc = 1, ndesc = 0;
+        stack[sp++] = INV;
+        /* The K>1 rule needs, at each round start, whether the chosen records are leaves: we
+         * record the visit sequence and the leaf flags, then group afterwards. A round that
+         * starts at visit j takes visits j..j+m-1 while visits j..j+m-2 are leaves and each
+         * next visit is a POP target (true after any leaf). */
+        while (addr != INV) {
+            const Node* nd = &nodes[addr];
+            int isleaf = nd->left == INV;
+            if (nv < (1 << 20)) { seq[nv] = addr; leaf[nv] = (uint8_t)isleaf; }
+            ++nv;
+            if (!isleaf && desc) ++ndesc;
+            if (!isleaf) {
+                float a0, a1, b0, b1;
+                bbox(nd->lmin, nd->lmax, inv, oxi, ct, &a0, &a1);
+                bbox(nd->rmin, nd->rmax, inv, oxi, ct, &b0, &b1);
+                int h0 = a0 <= a1, h1 = b0 <= b1, c1 = h1 && (a0 > b0);
+                if (h0 || h1) {
+                    uint32_t def;
+                    if (c1 || !h0) { addr = nd->right; def = nd->left; } else { addr = nd->left; def = nd->right; }
+                    if (h0 && h1) stack[sp++] = def;
+                    desc = 1;
+                    continue;
+                }
+            } else if (r->extra[0] != (int)nd->mesh) {
+                float t = tri(r, nd, ct);
+                if (t < ct) {
+                    ct = t; best = addr;
+                    if (any) break;
+                }
+            }
+            addr = stack[--sp];
+            desc = 0;
+        }
+        o[0] = nv;
+        o[2 + KMAX] = ndesc;
+        int lv = 0;
+        for (int j = 0; j < nv && j < (1 << 20); ++j) lv += leaf[j];
+        o[1] = lv;
+        for (int K = 1; K <= KMAX; ++K) {
+            int rounds = 0, j = 0;
+            while (j < nv) {
+                int m = 1;
+                while (m < K && j + m - 1 < nv && leaf[j + m - 1] && j + m < nv) ++m;
+                j += m;
+                ++rounds;
+            }
+            o[1 + K] = rounds;
+        }
+        hit_t[i] = ct;
+        hit_node[i] = best == INV ? -1 : (int32_t)best;
+    }
+}

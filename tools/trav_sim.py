@@ -1,0 +1,126 @@
+"""Dependent-fetch rounds of the Bvh2 traversal under multi-record rounds (analysis tool).
+
+Builds the San-Miguel proxy's tree with the oracle (test infrastructure, CPU), traces camera
+rays in 8x8 tile order and one diffuse bounce from their hits, and reports per query class
+the node visits, leaf visits, and dependent rounds per ray and per wave for K = 1..4 records
+per round (tools/trav_sim.c).  Usage: python tools/trav_sim.py [tris] [W] [H]
+"""
+import ctypes
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "monte-carlo-raytracer_amd")]
+from mcrt import scenes, types as T  # noqa: E402
+from mcrt.camera import scene_camera  # noqa: E402
+from oracle import pyoracle as po  # noqa: E402
+
+KMAX = 4
+
+
+def lib():
+    so = "/tmp/trav_sim.so"
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", os.path.join(ROOT, "tools", "trav_sim.c"), "-o", so, "-lm"],
+                   check=True)
+    L = ctypes.CDLL(so)
+    L.sim.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 3
+    return L
+
+
+def camera_rays(cam, W, H):
+    r00, r10, r11, r01 = (cam[k][0, :3].astype(np.float32) for k in ("r00", "r10", "r11", "r01"))
+    ys, xs = np.mgrid[0:H, 0:W]
+    # 8x8 tile order (one wave per tile, as k_primary)
+    tx, ty = xs // 8, ys // 8
+    key = (ty * (W // 8) + tx) * 64 + (ys % 8) * 8 + (xs % 8)
+    order = np.argsort(key.ravel(), kind="stable")
+    u = (xs.ravel()[order] / W).astype(np.float32)[:, None]
+    v = (ys.ravel()[order] / H).astype(np.float32)[:, None]
+    d = (r00 * (1 - u) + r10 * u) * (1 - v) + (r01 * (1 - u) + r11 * u) * v
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros(len(d), T.RAY_DTYPE)
+    rays["o"][:, :3] = cam["pos"][0, :3]
+    rays["o"][:, 3] = 1000.0
+    rays["d"][:, :3] = d
+    rays["extra"][:, 0] = -1
+    rays["extra"][:, 1] = 1
+    return rays
+
+
+def bounce_rays(nodes, rays, hit_t, hit_node, rng):
+    ok = hit_node >= 0
+    out = np.zeros(len(rays), T.RAY_DTYPE)
+    nd = nodes[np.maximum(hit_node, 0)]
+    v0, v1, v2 = nd["lmin_v0"], nd["lmax_v1"], nd["rmin_v2"]
+    n = np.cross(v1 - v0, v2 - v0)
+    n /= np.maximum(np.linalg.norm(n, axis=1, keepdims=True), 1e-20)
+    d = rays["d"][:, :3]
+    n = np.where((n * d).sum(1, keepdims=True) > 0, -n, n)
+    # cosine hemisphere about n
+    a = np.where(np.abs(n[:, :1]) > 0.9, np.array([[0, 1, 0]], np.float32), np.array([[1, 0, 0]], np.float32))
+    t1 = np.cross(a, n)
+    t1 /= np.linalg.norm(t1, axis=1, keepdims=True)
+    t2 = np.cross(n, t1)
+    u1, u2 = rng.random(len(rays)), rng.random(len(rays))
+    r, ph = np.sqrt(u1), 2 * np.pi * u2
+    w = (t1 * (r * np.cos(ph))[:, None] + t2 * (r * np.sin(ph))[:, None] + n * np.sqrt(1 - u1)[:, None])
+    p = rays["o"][:, :3] + hit_t[:, None] * d + n * 1e-5
+    out["o"][:, :3] = p
+    out["o"][:, 3] = 1000.0
+    out["d"][:, :3] = w
+    out["extra"][:, 0] = -1
+    out["extra"][:, 1] = ok.astype(np.int32)
+    return out
+
+
+def report(name, out, active):
+    o = out[active]
+    nv, lv = o[:, 0].mean(), o[:, 1].mean()
+    nd = o[:, 2 + KMAX].mean()
+    line = f"{name:10s} rays {active.sum():8d} visits {nv:6.2f} leaves {lv:6.2f} ({lv / nv:.2f}) internal-by-descent {nd:6.2f} ({nd / (nv - lv):.2f})"
+    n = (len(out) // 64) * 64
+    for K in range(1, KMAX + 1):
+        per_ray = o[:, 1 + K].mean()
+        waves = out[:n, 1 + K].reshape(-1, 64).max(1)
+        line += f" | K={K} {per_ray:6.2f}/ray wave {waves.mean():6.1f}"
+    print(line, flush=True)
+
+
+def main():
+    tris = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+    W = int(sys.argv[2]) if len(sys.argv) > 2 else 480
+    H = int(sys.argv[3]) if len(sys.argv) > 3 else 272
+    t0 = time.time()
+    sc = scenes.san_miguel_proxy(tris=tris)
+    o = po.OracleScene(sc)
+    o.build()
+    nodes = o.nodes()
+    print(f"scene {sc.num_triangles} tris, {len(nodes)} nodes, {time.time() - t0:.1f}s", flush=True)
+    L = lib()
+    cam = scene_camera("san_miguel_proxy", W, H)
+    rng = np.random.default_rng(1)
+    rays = camera_rays(cam, W, H)
+    for name, any_ in (("camera", 0), ("bounce", 0), ("shadow", 1)):
+        out = np.zeros((len(rays), 3 + KMAX), np.int32)
+        ht = np.zeros(len(rays), np.float32)
+        hn = np.zeros(len(rays), np.int32)
+        L.sim(nodes.ctypes.data, rays.ctypes.data, len(rays), any_, out.ctypes.data, ht.ctypes.data, hn.ctypes.data)
+        report(name, out, rays["extra"][:, 1] != 0)
+        if name == "camera":
+            cam_t, cam_n, cam_rays = ht, hn, rays
+            rays = bounce_rays(nodes, rays, ht, hn, rng)
+        elif name == "bounce":
+            # shadow rays toward the directional light from the camera hits
+            ld = -np.asarray(sc.lights["d"][0, :3], np.float32)
+            ld /= np.linalg.norm(ld)
+            rays = bounce_rays(nodes, cam_rays, cam_t, cam_n, rng)
+            rays["d"][:, :3] = ld
+            rays["o"][:, 3] = 1000.0
+
+
+if __name__ == "__main__":
+    main()
