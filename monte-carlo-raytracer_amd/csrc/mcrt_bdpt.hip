@@ -810,7 +810,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
 
 // Any hit over the connection queue (RR occluded_main semantics): occluded own strategies are
 // zeroed in their slot, unoccluded light-tracing strategies splatted (BDPT.cl:888-899).
-template <bool TL>
+template <int LAY>
 __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const int* __restrict__ count,
                                                  const float4* __restrict__ sO, const float4* __restrict__ sD,
                                                  const float4* __restrict__ sL) {
@@ -826,7 +826,7 @@ __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const i
     r.d = ld3(d);
     r.tmax = o.w;
     r.mask = -1;
-    const bool occluded = traceAny<TL>(c, r, lds + lane, raySpill(c, blockIdx.x, lane));
+    const bool occluded = traceAny<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane));
     const int code = __float_as_int(d.w);
     if (code >= 0) {
         if (occluded) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -885,7 +885,7 @@ void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
 }
 void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st) {
     const int blocks = (maxCount + 63) / 64 > 0 ? (maxCount + 63) / 64 : 1;
-    hipLaunchKernelGGL(c.twoLevel ? k_bdpt_vis<true> : k_bdpt_vis<false>, dim3(blocks), dim3(64), 0, st, c, b, q.count,
+    hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_COMPACT>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks), dim3(64), 0, st, c, b, q.count,
                        q.o, q.d, q.t);
 }
 void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, hipStream_t st) {

@@ -309,10 +309,8 @@ static TraceCtx trace_ctx(mcrt_scene s) {
 // the camera-ray launch's view: descent-compact records when the scene has them
 static TraceCtx compact_ctx(mcrt_scene s) {
     TraceCtx c = trace_ctx(s);
-    if (s->compact) {
-        c.nodes = (const float4*)s->dNodesC;
-        c.compact = 1;
-    }
+    c.nodes = (const float4*)(s->compact ? s->dNodesC : s->dNodes);
+    c.compact = s->compact ? 1 : 0;
     return c;
 }
 

@@ -73,7 +73,7 @@ struct TraceCtx {
     const float4* nodes;   // 4 float4 per node (mcrt_bvh.cpp): internal = child boxes + indices, leaf = triangle
                            // two-level (mcrt_bvh2l.cpp): + instance records (world->object rows, bottom root)
     int twoLevel;          // selects the kernels' two-level instantiation (launch-time, not per lane)
-    int compact;           // flat tree in the descent-compact records (mcrt_traverse.h traverseOct2)
+    int compact;           // flat-tree record layout: 0 plain (traverseOct), 1 descent-compact (traverseOct2)
     uint32_t rootWord;     // compact records: the root's child word (index | leaf bit)
     uint32_t* spill;
     int spillCap;           // spill entries per ray (a multiple of STACK_LDS)

@@ -47,7 +47,7 @@
 // 8 waves per SIMD resident and refills them as they finish -- measured faster on MI355X
 // than a persistent grid pulling work from an atomic queue.
 // ---------------------------------------------------------------------------
-template <bool ANY, bool TL>
+template <bool ANY, int LAY>
 __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* __restrict__ rays, int n,
                                                    mcrt_intersection* __restrict__ hits, int* __restrict__ occl) {
     __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
@@ -62,11 +62,11 @@ __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* _
     r.tmax = rr.o.w;
     r.mask = rr.extra[0];
     if (ANY) {
-        occl[i] = traceAny<TL>(c, r, lds + lane, raySpill(c, blockIdx.x, lane)) ? 1 : -1;
+        occl[i] = traceAny<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane)) ? 1 : -1;
         return;
     }
     float t;
-    const float4 h4 = traceClosest<TL>(c, r, lds + lane, raySpill(c, blockIdx.x, lane), t);
+    const float4 h4 = traceClosest<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane), t);
     if (__float_as_int(h4.z) >= 0) {
         mcrt_intersection h;
         h.shapeid = __float_as_int(h4.z);
@@ -114,7 +114,7 @@ __global__ void k_surface_records(const uint32_t* __restrict__ meshStartIdx, con
 
 // Camera ray generation fused with the first closest-hit query (RTPrimaryRaysPass):
 // one workgroup = one wave = one 8x8 pixel tile of the rank's bands.
-template <bool TL>
+template <int LAY>
 __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 float4* __restrict__ hitOut) {
     __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
@@ -131,12 +131,12 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
     r.mask = -1;
     float t;
     hitOut[(size_t)k * f.W * f.H + (size_t)y * f.W + x] =
-        traceClosest<TL>(c, r, lds + lane, raySpill(c, tileAll, lane), t);
+        traceClosest<LAY>(c, r, lds + lane, raySpill(c, tileAll, lane), t);
 }
 
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
 // The grid covers the queue's capacity; workgroups past the device-side count exit at once.
-template <bool TL>
+template <int LAY>
 __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ qO,
                                                const float4* __restrict__ qD, float4* __restrict__ hitOut) {
     __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
@@ -153,12 +153,12 @@ __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict
     r.tmax = RT_MAX_TRACE_F;
     r.mask = -1;
     float t;
-    hitOut[i] = traceClosest<TL>(c, r, lds + lane, raySpill(c, blk, lane), t);
+    hitOut[i] = traceClosest<LAY>(c, r, lds + lane, raySpill(c, blk, lane), t);
 }
 
 // Any hit over the shadow queue + ShadowPass (PathTracing.cl:186-217):
 // sO = (o.xyz, tmax), sD = (d.xyz, pix), sL = throughput * L; radiance[pix] += L * V.
-template <bool TL>
+template <int LAY>
 __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ sO,
                                                const float4* __restrict__ sD, const float4* __restrict__ sL,
                                                float4* __restrict__ radiance) {
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     r.d = ld3(d);
     r.tmax = o.w;
     r.mask = -1;
-    const float V = traceAny<TL>(c, r, lds + lane, raySpill(c, blk, lane)) ? 0.0f : 1.0f;
+    const float V = traceAny<LAY>(c, r, lds + lane, raySpill(c, blk, lane)) ? 0.0f : 1.0f;
     const int pix = __float_as_int(d.w);
     float4 acc = radiance[pix];
     acc.x += L.x * V;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
 // Shadow rays of bounce b and extension rays of bounce b+1 in ONE launch: both only depend on
 // the shading of bounce b.  Extension workgroups come first (their rays are the longer ones),
 // shadow workgroups fill the extension launch's divergent tail instead of waiting for it.
-template <bool TL>
+template <int LAY>
 __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __restrict__ extCount,
                                                       const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                       float4* __restrict__ hitOut, const int* __restrict__ shadowCount,
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.tmax = RT_MAX_TRACE_F;
         r.mask = -1;
         float t;
-        hitOut[i] = traceClosest<TL>(c, r, lds + lane, raySpill(c, blk, lane), t);
+        hitOut[i] = traceClosest<LAY>(c, r, lds + lane, raySpill(c, blk, lane), t);
     } else {
         const int ns = *shadowCount;
         const int sb = (ns + 63) >> 6;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.d = ld3(d);
         r.tmax = o.w;
         r.mask = -1;
-        const float V = traceAny<TL>(c, r, lds + lane, raySpill(c, blockIdx.x, lane)) ? 0.0f : 1.0f;
+        const float V = traceAny<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane)) ? 0.0f : 1.0f;
         const int pix = __float_as_int(d.w);
         float4 acc = radiance[pix];
         acc.x += L.x * V;
@@ -696,12 +696,15 @@ namespace mcrt {
 void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, mcrt_intersection* hits, int* occl,
                        hipStream_t st) {
     const dim3 g((n + 63) / 64), b(64);
-    if (c.twoLevel) {
-        if (any) hipLaunchKernelGGL((k_trace_rays<true, true>), g, b, 0, st, c, rays, n, hits, occl);
-        else hipLaunchKernelGGL((k_trace_rays<false, true>), g, b, 0, st, c, rays, n, hits, occl);
-    } else {
-        if (any) hipLaunchKernelGGL((k_trace_rays<true, false>), g, b, 0, st, c, rays, n, hits, occl);
-        else hipLaunchKernelGGL((k_trace_rays<false, false>), g, b, 0, st, c, rays, n, hits, occl);
+    {
+        if (any)
+            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<true, LAY_TWO_LEVEL>,
+                                          k_trace_rays<true, LAY_COMPACT>, k_trace_rays<true, LAY_PLAIN>),
+                               g, b, 0, st, c, rays, n, hits, occl);
+        else
+            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<false, LAY_TWO_LEVEL>,
+                                          k_trace_rays<false, LAY_COMPACT>, k_trace_rays<false, LAY_PLAIN>),
+                               g, b, 0, st, c, rays, n, hits, occl);
     }
 }
 void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshStartVertex, const uint32_t* meshBase,
@@ -713,24 +716,24 @@ void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshSt
 }
 
 void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st) {
-    hipLaunchKernelGGL(c.twoLevel ? k_primary<true> : k_primary<false>, dim3(f.numTiles * f.batch), dim3(64), 0, st, c, f, cam,
+    hipLaunchKernelGGL(pickLayout(c, k_primary<LAY_TWO_LEVEL>, k_primary<LAY_COMPACT>, k_primary<LAY_PLAIN>), dim3(f.numTiles * f.batch), dim3(64), 0, st, c, f, cam,
                        hits);
 }
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
                    hipStream_t st) {
-    hipLaunchKernelGGL(c.twoLevel ? k_extend<true> : k_extend<false>, dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+    hipLaunchKernelGGL(pickLayout(c, k_extend<LAY_TWO_LEVEL>, k_extend<LAY_COMPACT>, k_extend<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, qO, qD, hits);
 }
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st) {
-    hipLaunchKernelGGL(c.twoLevel ? k_shadow<true> : k_shadow<false>, dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+    hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_COMPACT>, k_shadow<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, sO, sD, sL, radiance);
 }
 void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
                           const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
                           float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
     const int blocks = (maxExt + 63) / 64 + (maxShadow + 63) / 64;
-    hipLaunchKernelGGL(c.twoLevel ? k_shadow_extend<true> : k_shadow_extend<false>, dim3(blocks > 0 ? blocks : 1),
+    hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_COMPACT>, k_shadow_extend<LAY_PLAIN>), dim3(blocks > 0 ? blocks : 1),
                        dim3(64), 0, st, c, extCount, qO, qD, hits, shadowCount, sO, sD, sL, radiance);
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,

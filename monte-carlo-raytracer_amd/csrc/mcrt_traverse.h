@@ -9,6 +9,17 @@
 // ---------------------------------------------------------------------------
 #define STACK_LDS 16
 
+// Node-record layouts of the traversal kernels' template parameter LAY (TraceCtx::compact,
+// TraceCtx::twoLevel): each layout gets its own kernel instantiation, so a kernel's register
+// budget is that of the one loop it runs.
+#define LAY_PLAIN 0       // mcrt_bvh.cpp records, traverseOct
+#define LAY_COMPACT 1     // descent-compact records, traverseOct2
+#define LAY_TWO_LEVEL 3   // mcrt_bvh2l.cpp records, traverse2L
+template <typename K>
+inline K pickLayout(const TraceCtx& c, K twoLevel, K compact, K plain) {
+    return c.twoLevel ? twoLevel : c.compact ? compact : plain;
+}
+
 struct TraceRay {
     f3 o, d;
     float tmax;
@@ -308,38 +319,36 @@ MCRT_DEV int traverseOct2(const float4* __restrict__ nodes, uint32_t rootWord, c
     return hit;
 }
 
-template <bool ANY>
+template <bool ANY, int LAY>
 MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, float& tHit) {
     const f3 inv = safeInvDir(r.d);
+#define MCRT_TRAV_CALL(OCT)                                                                                       \
+    do {                                                                                                          \
+        if constexpr (LAY == LAY_COMPACT)                                                                         \
+            return traverseOct2<ANY, OCT>(c.nodes, c.rootWord, r, inv, stk, spill, c.spillCap, c.overflow, tHit); \
+        else                                                                                                      \
+            return traverseOct<ANY, OCT>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit);             \
+    } while (0)
 #if MCRT_OCT_TRAV
     const int oct = (int)(__float_as_uint(inv.x) >> 31) | (int)((__float_as_uint(inv.y) >> 31) << 1) |
                     (int)((__float_as_uint(inv.z) >> 31) << 2);
     const int oct0 = __builtin_amdgcn_readfirstlane(oct);
     if (__all(oct == oct0)) {
-        if (c.compact) {
-            switch (oct0) {
-#define MCRT_OCT_CASE(k)                                                                                       \
-    case k:                                                                                                    \
-        return traverseOct2<ANY, k>(c.nodes, c.rootWord, r, inv, stk, spill, c.spillCap, c.overflow, tHit);
-                MCRT_OCT_CASE(0) MCRT_OCT_CASE(1) MCRT_OCT_CASE(2) MCRT_OCT_CASE(3)
-                MCRT_OCT_CASE(4) MCRT_OCT_CASE(5) MCRT_OCT_CASE(6) MCRT_OCT_CASE(7)
-#undef MCRT_OCT_CASE
-                default: break;
-            }
-        } else {
-            switch (oct0) {
-#define MCRT_OCT_CASE(k) \
-    case k: return traverseOct<ANY, k>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit);
-                MCRT_OCT_CASE(0) MCRT_OCT_CASE(1) MCRT_OCT_CASE(2) MCRT_OCT_CASE(3)
-                MCRT_OCT_CASE(4) MCRT_OCT_CASE(5) MCRT_OCT_CASE(6) MCRT_OCT_CASE(7)
-#undef MCRT_OCT_CASE
-                default: break;
-            }
+        switch (oct0) {
+            case 0: MCRT_TRAV_CALL(0);
+            case 1: MCRT_TRAV_CALL(1);
+            case 2: MCRT_TRAV_CALL(2);
+            case 3: MCRT_TRAV_CALL(3);
+            case 4: MCRT_TRAV_CALL(4);
+            case 5: MCRT_TRAV_CALL(5);
+            case 6: MCRT_TRAV_CALL(6);
+            case 7: MCRT_TRAV_CALL(7);
+            default: break;
         }
     }
 #endif
-    if (c.compact) return traverseOct2<ANY, -1>(c.nodes, c.rootWord, r, inv, stk, spill, c.spillCap, c.overflow, tHit);
-    return traverseOct<ANY, -1>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit);
+    MCRT_TRAV_CALL(-1);
+#undef MCRT_TRAV_CALL
 }
 
 // RR common.cl:249-277 (triangle_calculate_barycentrics)
@@ -510,25 +519,27 @@ MCRT_DEV float4 closestRecord2L(const float4* __restrict__ nodes, const TraceRay
     return make_float4(uv.x, uv.y, __int_as_float(shape), E1.w);
 }
 
-// Closest / any hit over either layout; TL selects the two-level instantiation.
-template <bool TL>
+// Closest / any hit over the scene's record layout (LAY; LAY_TWO_LEVEL: RR's IntersectorTwoLevel).
+template <int LAY>
 MCRT_DEV float4 traceClosest(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, float& t) {
-    if (TL) {
+    if constexpr (LAY == LAY_TWO_LEVEL) {
         int inst;
         const int tri = traverse2L<false>(c.nodes, r, stk, spill, c.spillCap, c.overflow, t, inst);
         return closestRecord2L(c.nodes, r, tri, inst, t);
+    } else {
+        const int tri = traverse<false, LAY>(c, r, stk, spill, t);
+        return closestRecord(c.nodes, r, tri, t);   // leaf slots are the same in both flat layouts
     }
-    const int tri = traverse<false>(c, r, stk, spill, t);
-    return closestRecord(c.nodes, r, tri, t);   // leaf records are the same in both flat layouts
 }
-template <bool TL>
+template <int LAY>
 MCRT_DEV bool traceAny(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill) {
     float t;
-    if (TL) {
+    if constexpr (LAY == LAY_TWO_LEVEL) {
         int inst;
         return traverse2L<true>(c.nodes, r, stk, spill, c.spillCap, c.overflow, t, inst) >= 0;
+    } else {
+        return traverse<true, LAY>(c, r, stk, spill, t) >= 0;
     }
-    return traverse<true>(c, r, stk, spill, t) >= 0;
 }
 
 // XCD-aware workgroup order for the traversal launches.  Workgroups are dealt round-robin to the
