@@ -138,6 +138,29 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
     return out
 
 
+def gather_ceiling(ctx, rl, vq, avg_ms):
+    """The latency roofline of the traversal launch: its node-visit rate (the launch's rays x the
+    oracle's visits per query, over its HIP-event time) against the rate of a pure dependent-gather
+    probe with the same access pattern (mcrt_ctx_gather_chase: chains of 64-B records fetched as
+    four 16-B loads, links read from the record just fetched, 32 waves per CU) with its records
+    resident in L2, in the Infinity Cache, or (the tree's own size) in HBM.  A node visit also
+    does the slab / triangle arithmetic and stack work the probe leaves out."""
+    rays = rl["rays_per_launch"]
+    visits = rays["extension"] * vq["k_extend"] + rays["shadow"] * vq["k_shadow"]
+    rate = visits / (avg_ms * 1e-3) / 1e9
+    out = {"unit": "G dependent 64-B record fetches / s", "node_visits_per_launch": int(visits),
+           "node_visits_per_s": round(rate, 1), "ceilings": {}}
+    try:
+        for name, recs in (("l2_resident_2MiB", 32768), ("infinity_cache_resident_122MiB", 2_000_000),
+                           ("hbm_tree_size", int(rl["nodes_total"]))):
+            out["ceilings"][name] = round(ctx.gather_chase_gsteps(recs, 256, 3), 1)
+        out["frac_of_l2_resident"] = round(rate / out["ceilings"]["l2_resident_2MiB"], 4)
+        out["frac_of_infinity_cache_resident"] = round(rate / out["ceilings"]["infinity_cache_resident_122MiB"], 4)
+    except Exception as e:   # noqa: BLE001 -- reported, not fatal
+        log(f"[bench] gather-chase probe failed: {e}")
+    return out
+
+
 def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
     """Memory-side bytes per launch of `kernel` (and the SQ limiter summary, if measured) from a
     committed rocprofv3 counter summary under profiles/ (tools/pmc_json.py).  last_launches > 0:
@@ -549,6 +572,9 @@ def main():
                 avg_ms = kstats[dom]["ms"] / max(kstats[dom]["launches"], 1)
                 out["roofline"] = roofline_shadow_extend(scene, cam_of, W, H, D, stats_batch, avg_ms, qcounts, ctx,
                                                          cpu["_oracle"] if cpu else None)
+                if "visits_per_query" in out:
+                    out["roofline"]["gather_ceiling"] = gather_ceiling(ctx, out["roofline"], out["visits_per_query"],
+                                                                       avg_ms)
         if bd is not None:
             bdo = {k: v for k, v in bd.items() if not k.startswith("_")}
             if oracle_ok and sampler == T.SAMPLER_RANDOM and not args.no_cpu_baseline:

@@ -273,6 +273,13 @@ MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx);
  * well above the 256 MB Infinity Cache), best of `iters` launches; *gbps = (read + write)
  * bytes / time.  The roofline's "attainable" figure next to the 8 TB/s spec peak. */
 MCRT_API mcrt_status mcrt_ctx_stream_copy(mcrt_ctx ctx, uint64_t bytes, int iters, double* gbps);
+/* Dependent-gather ceiling of the traversal's access pattern: every lane of 32 waves per CU
+ * follows a chain of 64-B records over an array of `records` records (uniformly random links
+ * read from the record just fetched, four 16-B loads per step), `steps` steps, best of `iters`
+ * launches; *gsteps = dependent record fetches per second / 1e9.  The roofline's reference for
+ * the node-visit rate of the latency-bound traversal kernels (records ~ the tree's node count:
+ * served from HBM; ~2 M: Infinity Cache; ~32 K: L2). */
+MCRT_API mcrt_status mcrt_ctx_gather_chase(mcrt_ctx ctx, uint64_t records, int steps, int iters, double* gsteps);
 
 /* ------------------------------------------------------------------------ */
 /* Scene (replaces RTScene upload + RadeonRays CreateMesh/AttachShape/SetId/

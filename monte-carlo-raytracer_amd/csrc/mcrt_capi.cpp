@@ -463,6 +463,38 @@ MCRT_API mcrt_status mcrt_ctx_stream_copy(mcrt_ctx ctx, uint64_t bytes, int iter
     return MCRT_OK;
 }
 
+MCRT_API mcrt_status mcrt_ctx_gather_chase(mcrt_ctx ctx, uint64_t records, int steps, int iters, double* gsteps) {
+    if (!ctx || !gsteps || records < 64 || records > 0xffffffffull || steps < 1 || iters < 1)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "bad gather-chase args");
+    hipSetDevice(ctx->device);
+    void* rec = nullptr;
+    uint32_t* sink = nullptr;
+    HIPCHK(ctx, hipMalloc(&rec, 64 * records));
+    if (hipMalloc(&sink, 4) != hipSuccess) { hipFree(rec); return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "gather chase"); }
+    mcrt::launch_chase_init(rec, (uint32_t)records, ctx->stream);
+    const int waves = ctx->numCUs * 32;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    float best = 1e30f;
+    for (int i = 0; i < iters + 1; ++i) {
+        hipEventRecord(e0, ctx->stream);
+        mcrt::launch_chase(rec, (uint32_t)records, i == 0 ? std::max(1, steps / 4) : steps, waves, sink, ctx->stream);
+        hipEventRecord(e1, ctx->stream);
+        hipEventSynchronize(e1);
+        float ms = 0.0f;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (i > 0 && ms < best) best = ms;   // launch 0 warms caches and translations
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipFree(rec);
+    hipFree(sink);
+    HIPCHK(ctx, hipGetLastError());
+    *gsteps = (double)waves * 64.0 * steps / (best * 1e-3) / 1e9;
+    return MCRT_OK;
+}
+
 MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx) {
     if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
     drain_pending(ctx);

@@ -107,6 +107,8 @@ void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts
 void launch_denoise(int W, int H, int r, float ss, float sr, const float4* in, float4* out, hipStream_t st);
 void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStream_t st);
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st);
+void launch_chase_init(void* rec, uint32_t n, hipStream_t st);
+void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* sink, hipStream_t st);
 // descent-compact traversal records (mcrt_traverse.h traverseOct2); *bad = 1 if the tree lacks
 // the exact-union property or an index does not fit the 27-bit child word
 void launch_pack_compact(const float4* in, float4* out, uint32_t n, int* bad, hipStream_t st);

@@ -615,6 +615,34 @@ __global__ __launch_bounds__(256) void k_tonemap(int n, float Lwhite, const floa
     out[i] = make_float4(p.x * s, p.y * s, p.z * s, p.w);
 }
 
+// Dependent-gather ceiling probe (mcrt_ctx_gather_chase): every lane follows a chain of 64-B
+// records whose links are read from the record just fetched, fetched as four 16-B pieces -- the
+// traversal's access pattern with none of its arithmetic.  The array size decides where the
+// records come from (L2, Infinity Cache, HBM), so the traversal's node-visit rate can be set
+// against the ceiling of its own access pattern (tools/probe/chase_probe.hip has more variants).
+__global__ void k_chase_init(int4* rec, uint32_t n, uint32_t seed) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    const uint32_t nxt = h % n;
+    for (int q = 0; q < 4; ++q) rec[4 * i + q] = make_int4((int)nxt, (int)(nxt ^ 1u), (int)(nxt ^ 2u), (int)nxt);
+}
+__global__ __launch_bounds__(64) void k_chase(const int4* __restrict__ rec, uint32_t n, int steps, uint32_t* sink) {
+    const uint32_t chain = blockIdx.x * 64 + threadIdx.x;
+    uint32_t h = chain * 0x9E3779B9u + 12345u;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13;
+    uint32_t idx = h % n, acc = 0;
+    for (int s = 0; s < steps; ++s) {
+        const int4 a = rec[4 * (size_t)idx], b = rec[4 * (size_t)idx + 1];
+        const int4 c = rec[4 * (size_t)idx + 2], d = rec[4 * (size_t)idx + 3];
+        asm volatile("" ::"v"(a.y), "v"(b.y), "v"(c.y));
+        acc += (uint32_t)(a.z ^ b.z ^ c.z);
+        idx = (uint32_t)d.w;
+    }
+    if (acc == 0xdeadbeefu) sink[0] = idx;   // never true: keeps the loads live
+}
+
 // Attainable-bandwidth probe (mcrt_ctx_stream_copy): a persistent grid (8 workgroups per CU)
 // strides over the array; each lane keeps 4 independent 16-B nontemporal loads in flight.
 __global__ __launch_bounds__(256) void k_stream_copy(const f4* __restrict__ src, f4* __restrict__ dst, size_t n) {
@@ -767,6 +795,13 @@ void launch_denoise(int W, int H, int r, float ss, float sr, const float4* in, f
 void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStream_t st) {
     hipLaunchKernelGGL(k_tonemap, dim3((n + 255) / 256), dim3(256), 0, st, n, Lwhite, in, out);
 }
+void launch_chase_init(void* rec, uint32_t n, hipStream_t st) {
+    hipLaunchKernelGGL(k_chase_init, dim3((n + 255) / 256), dim3(256), 0, st, reinterpret_cast<int4*>(rec), n, 777u);
+}
+void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* sink, hipStream_t st) {
+    hipLaunchKernelGGL(k_chase, dim3(waves), dim3(64), 0, st, reinterpret_cast<const int4*>(rec), n, steps, sink);
+}
+
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st) {
     const size_t need = (n4 + 1023) / 1024;
     const size_t blocks = std::min(need, (size_t)std::max(numCUs, 1) * 8);

@@ -33,6 +33,7 @@ SIGNATURES = {
     "mcrt_ctx_kernel_stats": (_c.c_int, [_vp, _c.c_int, _vp, _vp, _vp, _vp, _c.POINTER(_c.c_int)]),
     "mcrt_ctx_reset_stats": (_c.c_int, [_vp]),
     "mcrt_ctx_stream_copy": (_c.c_int, [_vp, _c.c_uint64, _c.c_int, _c.POINTER(_c.c_double)]),
+    "mcrt_ctx_gather_chase": (_c.c_int, [_vp, _c.c_uint64, _c.c_int, _c.c_int, _c.POINTER(_c.c_double)]),
     "mcrt_scene_create": (_c.c_int, [_vp, _vp, _c.POINTER(_vp)]),
     "mcrt_scene_destroy": (_c.c_int, [_vp]),
     "mcrt_scene_update_lights": (_c.c_int, [_vp, _vp, _c.c_uint32]),
@@ -156,6 +157,12 @@ class Context:
 
     def reset_stats(self):
         _check(lib().mcrt_ctx_reset_stats(self.h), self.h)
+
+    def gather_chase_gsteps(self, records, steps=256, iters=3):
+        """Dependent 64-B gather ceiling, G steps/s (mcrt_ctx_gather_chase)."""
+        g = _c.c_double()
+        _check(lib().mcrt_ctx_gather_chase(self.h, records, steps, iters, _c.byref(g)), self.h)
+        return g.value
 
     def stream_copy_gbps(self, nbytes=2 << 30, iters=5):
         """Attainable HBM GB/s of a stream copy (mcrt_ctx_stream_copy)."""

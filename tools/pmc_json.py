@@ -85,9 +85,18 @@ def main():
                 lim["l2_hit_rate"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 3)
             if "hbm_bytes_per_launch" in r:
                 lim["memory_side_tb_s"] = round(r["hbm_bytes_per_launch"] / (ms[k] * 1e-3) / 1e12, 3)
+            if "TA_TA_BUSY_sum" in c:   # vector-memory address path, per CU (256 CUs)
+                lim["ta_busy"] = round(c["TA_TA_BUSY_sum"] / (256 * cyc), 3)
+                if "TA_ADDR_STALLED_BY_TC_CYCLES_sum" in c:
+                    lim["ta_stalled_by_tcp"] = round(c["TA_ADDR_STALLED_BY_TC_CYCLES_sum"] / (256 * cyc), 3)
+            if "TCP_TCC_READ_REQ_sum" in c and c["TCP_TCC_READ_REQ_sum"] > 0:
+                lim["l1_miss_latency_cycles"] = round(c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"], 1)
+                lim["l1_hit_rate"] = round(1 - c["TCP_TCC_READ_REQ_sum"] / max(c["TCP_TOTAL_CACHE_ACCESSES_sum"], 1), 3)
             mem, iss = lim["wave_time_waiting_on_memory"], lim["wave_time_issue_stalled"]
             bw = lim.get("memory_side_tb_s", 0.0)
             lim["binding"] = ("HBM bandwidth" if bw >= 5.0 else
+                              "vector-memory pipeline (TA busy) + memory latency"
+                              if lim.get("ta_busy", 0.0) >= 0.85 and mem >= 0.4 else
                               "memory latency" if mem >= 0.4 and lim["valu_busy"] < 0.6 else
                               "VALU issue" if lim["valu_busy"] >= 0.6 else "mixed")
             r["limiter"] = lim
