@@ -7,7 +7,8 @@ renders whole frames f = rank + N*i, "scaling": "weak"), since light-tracing spl
 One step = one 1-spp frame of the whole image (mcrt_render_frame + mcrt_accumulate).
 N GPUs: one process per GPU (torch.distributed.run), the image is tile-split into 8-row bands
 dealt round-robin to the ranks (north star), each rank accumulates its bands, and one RCCL
-reduce of the accumulators (sum) to rank 0 ends the job (inside the timed region).
+collective ends the job (inside the timed region): a gather of every rank's own band rows to
+rank 0 (--end-collective reduce: the full-frame sum-reduce instead; the same bits).
 Total work per step is fixed -> "scaling": "strong".
 
 Also reported (one JSON line on rank 0):
@@ -333,6 +334,8 @@ def main():
                                                                    "instanced_proxy"])
     ap.add_argument("--sampler", default="random", choices=["random", "sobol"])
     ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--end-collective", default="gather", choices=["gather", "reduce"],
+                    help="tile split: gather each rank's band rows to rank 0, or sum-reduce the full frames")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline-model", action="store_true",
@@ -476,11 +479,18 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     run(frame0, args.steps)
-    if world > 1:   # single RCCL reduce of the tile accumulators (north star)
+    if world > 1:   # one collective: each rank's own band rows gathered to rank 0 (north star)
         fb.copy_device(1, acc_s.data_ptr())
         fb.copy_device(3, acc_w.data_ptr())
         ctx.sync()
-        mdist.reduce_packed(acc_buf, dst=0)
+        if args.end_collective == "gather":
+            try:
+                mdist.gather_bands(acc_s, acc_w, H, W, args.band_rows, dst=0)
+            except (RuntimeError, NotImplementedError) as e:   # a backend without gather: every rank raises
+                log(f"[bench] band gather failed ({e}); full-frame reduce instead")
+                args.end_collective = "reduce"
+        if args.end_collective == "reduce":
+            mdist.reduce_packed(acc_buf, dst=0)
         if rank == 0:
             torch.cuda.synchronize()
             fb.set_accumulation(acc_s.data_ptr(), acc_w.data_ptr())
@@ -534,7 +544,8 @@ def main():
                    "bvh_build_ms": round(info["build_ms"], 1),
                    "parallelism": (f"band split x {world}, 1 splat all-reduce per frame + 1 RCCL reduce" if band_bdpt
                                    else f"frame split x {world} + 1 RCCL reduce" if bdpt else
-                                   f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL reduce"),
+                                   f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL "
+                                   + ("band gather" if args.end_collective == "gather" else "reduce")),
                    "frames_per_launch": batch},
     }
     if rank == 0:

@@ -3,10 +3,12 @@
 Tile split: the image is cut into 8-row blocks; bands of `band_rows` rows (a multiple of 8)
 are dealt round-robin to the ranks (interleaved for balance against sky/foliage skew).  The
 kernels enumerate a rank's pixels with the same formula (mcrt_kernels.hip tilePixel), every
-rank keeps full-frame accumulators that are zero outside its rows, and ONE sum-reduce of the
-accumulators to rank 0 (RCCL over xGMI on the GPU, gloo in the CPU tests) ends the job --
-paths are independent and the RNG is keyed by the global pixel index, so the reduced image
-equals the single-GPU image bit for bit (each pixel has exactly one non-zero contribution).
+rank keeps full-frame accumulators that are zero outside its rows, and ONE collective ends the
+job -- paths are independent and the RNG is keyed by the global pixel index, so the combined
+image equals the single-GPU image bit for bit (each pixel has exactly one non-zero contribution).
+The collective is a gather of each rank's own rows to rank 0 (gather_bands: each xGMI link
+carries one rank's 1/N share once, in parallel) rather than a sum-reduce of the full frames
+(reduce_packed: a ring moves ~2x the whole frame through every link); both give the same bits.
 """
 import numpy as np
 
@@ -90,6 +92,41 @@ def reduce_packed(buf, dst=0, group=None):
         buf.copy_(h)
         return
     dist.reduce(buf, dst=dst, op=dist.ReduceOp.SUM, group=group)
+
+
+def gather_bands(wsum, wts, height, width, band_rows, dst=0, group=None):
+    """The end-of-job collective of the tile split: every rank sends only its own rows of the
+    accumulators (sum(w*L) float4 and sum(w) per pixel, packed into one row-major buffer padded
+    to the largest share) and rank `dst` writes them into its full-frame accumulators in place.
+    Bit-identical to reduce_packed (the other ranks' accumulators are zero in those rows) with
+    1/N of the frame per link instead of a ring's ~2 frames.  wsum: float32 (H*W*4,), wts:
+    (H*W,), contiguous, on the GPU (RCCL) or the CPU (gloo; a GPU tensor under gloo goes via
+    the host)."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    rows_all = [band_rows_of(height, band_rows, world, r) for r in range(world)]
+    maxr = max(len(r) for r in rows_all)
+    host = wsum.is_cuda and dist.get_backend(group) == "gloo"
+    dev = torch.device("cpu") if host else wsum.device
+    s = (wsum.cpu() if host else wsum).view(height, width * 4)
+    w = (wts.cpu() if host else wts).view(height, width)
+    own = torch.as_tensor(rows_all[rank], device=dev)
+    send = torch.zeros(maxr, width * 5, dtype=torch.float32, device=dev)
+    send[:len(own), :width * 4] = s[own]
+    send[:len(own), width * 4:] = w[own]
+    recv = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, recv, dst=dst, group=group)
+    if rank == dst:
+        for r, rows in enumerate(rows_all):
+            if r == rank or len(rows) == 0:
+                continue
+            idx = torch.as_tensor(rows, device=dev)
+            s[idx] = recv[r][:len(rows), :width * 4]
+            w[idx] = recv[r][:len(rows), width * 4:]
+        if host:
+            wsum.copy_(s.reshape(-1))
+            wts.copy_(w.reshape(-1))
 
 
 def reduce_accumulators(wsum, wts, dst=0, group=None):

@@ -71,6 +71,45 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
+def _gather_worker(rank, world, port, out_path, height, width, band_rows):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # synthetic accumulators, zero outside the rank's rows (as every rank's framebuffer is)
+    rng = np.random.default_rng(7)
+    full_s = rng.random((height, width, 4), dtype=np.float32) * 3.0
+    full_w = rng.random((height, width), dtype=np.float32) + 0.5
+    rows = mdist.band_rows_of(height, band_rows, world, rank)
+    s = np.zeros_like(full_s)
+    w = np.zeros_like(full_w)
+    s[rows], w[rows] = full_s[rows], full_w[rows]
+    ts = torch.from_numpy(s.reshape(-1).copy())
+    tw = torch.from_numpy(w.reshape(-1).copy())
+    mdist.gather_bands(ts, tw, height, width, band_rows, dst=0)
+    buf, rs, rw = mdist.packed_accumulators(height * width, "cpu")
+    rs.copy_(torch.from_numpy(s.reshape(-1)))
+    rw.copy_(torch.from_numpy(w.reshape(-1)))
+    mdist.reduce_packed(buf, dst=0)
+    if rank == 0:
+        np.savez(out_path, gs=ts.numpy(), gw=tw.numpy(), rs=rs.numpy(), rw=rw.numpy(),
+                 fs=full_s.reshape(-1), fw=full_w.reshape(-1))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,height,band_rows", [(2, 36, 8), (3, 1080 // 8, 16), (4, 40, 8)])
+def test_band_gather_equals_reduce(tmp_path, world, height, band_rows):
+    """bench.py's end-of-job collective: gathering each rank's own band rows to rank 0 gives the
+    sum-reduce of the full-frame accumulators bit for bit (and the whole image)."""
+    out = str(tmp_path / "g.npz")
+    mp.start_processes(_gather_worker, args=(world, _free_port(), out, height, 24, band_rows), nprocs=world,
+                       join=True, start_method="spawn")
+    z = np.load(out)
+    assert np.array_equal(z["gs"].view(np.uint32), z["rs"].view(np.uint32))
+    assert np.array_equal(z["gw"].view(np.uint32), z["rw"].view(np.uint32))
+    assert np.array_equal(z["gs"], z["fs"]) and np.array_equal(z["gw"], z["fw"])
+
+
 def test_two_rank_reduce_matches_single_process(tmp_path):
     out = str(tmp_path / "reduced.npz")
     mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
