@@ -46,6 +46,12 @@ static float tri(const Ray* r, const Node* n, float tmax) {
 
 /* out per ray: [0] visits, [1] leaf visits, [2..2+KMAX-1] rounds for K=1..KMAX,
  * [2+KMAX] internal visits reached by descent (not by a pop); hit_t/hit_node */
+static int g_order = 0;   /* any-hit child order: 0 near first (RR), 1 far first, 2 larger box first, 3 leaf first */
+void set_order(int o) { g_order = o; }
+static float area(const float* lo, const float* hi) {
+    float d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
+    return d0 * d1 + d1 * d2 + d0 * d2;
+}
 void sim(const Node* nodes, const Ray* rays, int n, int any, int32_t* out, float* hit_t, int32_t* hit_node) {
     static uint32_t stack[1 << 16];
     static uint32_t seq[1 << 20];
@@ -78,6 +84,12 @@ void sim(const Node* nodes, const Ray* rays, int n, int any, int32_t* out, float
                 bbox(nd->lmin, nd->lmax, inv, oxi, ct, &a0, &a1);
                 bbox(nd->rmin, nd->rmax, inv, oxi, ct, &b0, &b1);
                 int h0 = a0 <= a1, h1 = b0 <= b1, c1 = h1 && (a0 > b0);
+                if (any && g_order == 1) c1 = h1 && !(a0 > b0);
+                if (any && g_order == 2) c1 = h1 && (area(nd->rmin, nd->rmax) > area(nd->lmin, nd->lmax));
+                if (any && g_order == 3) {
+                    int lL = nodes[nd->left].left == INV, lR = nodes[nd->right].left == INV;
+                    c1 = h1 && ((lR && !lL) || (lR == lL && a0 > b0));
+                }
                 if (h0 || h1) {
                     uint32_t def;
                     if (c1 || !h0) { addr = nd->right; def = nd->left; } else { addr = nd->left; def = nd->right; }

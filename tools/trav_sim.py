@@ -28,6 +28,7 @@ def lib():
                    check=True)
     L = ctypes.CDLL(so)
     L.sim.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 3
+    L.set_order.argtypes = [ctypes.c_int]
     return L
 
 
@@ -104,7 +105,9 @@ def main():
     cam = scene_camera("san_miguel_proxy", W, H)
     rng = np.random.default_rng(1)
     rays = camera_rays(cam, W, H)
-    for name, any_ in (("camera", 0), ("bounce", 0), ("shadow", 1)):
+    for name, any_ in (("camera", 0), ("bounce", 0), ("shadow", 1), ("shadow_far", 1), ("shadow_area", 1),
+                       ("shadow_leaf", 1)):
+        L.set_order({"shadow_far": 1, "shadow_area": 2, "shadow_leaf": 3}.get(name, 0))
         out = np.zeros((len(rays), 3 + KMAX), np.int32)
         ht = np.zeros(len(rays), np.float32)
         hn = np.zeros(len(rays), np.int32)
@@ -113,6 +116,8 @@ def main():
         if name == "camera":
             cam_t, cam_n, cam_rays = ht, hn, rays
             rays = bounce_rays(nodes, rays, ht, hn, rng)
+        elif name.startswith("shadow"):
+            print(f"   occluded {(hn >= 0).mean():.3f}", flush=True)
         elif name == "bounce":
             # shadow rays toward the directional light from the camera hits
             ld = -np.asarray(sc.lights["d"][0, :3], np.float32)
