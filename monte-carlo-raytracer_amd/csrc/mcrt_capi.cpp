@@ -1225,6 +1225,14 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
     f.russianRoulette = p->russian_roulette;
     f.rrStartDepth = p->rr_start_depth;
     f.textureLod = p->texture_lod ? 1 : 0;
+    // batched frames: workgroups of the camera / first-bounce launches walk (tile, frame) with the
+    // frames of a tile adjacent, so one XCD traces a tile's batch of jittered frames back to back
+    // (MCRT_TILE_MAJOR=0: frame-major order, the A/B baseline); the order changes no result
+    static const int tileMajor = [] {
+        const char* e = std::getenv("MCRT_TILE_MAJOR");
+        return e ? std::atoi(e) : 1;
+    }();
+    f.tileMajor = tileMajor;
     f.batch = 1;
     f.numBands = p->num_bands <= 0 ? 1 : p->num_bands;
     f.bandIndex = p->band_index;

@@ -119,10 +119,11 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
                                                 float4* __restrict__ hitOut) {
     __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
     const int lane = threadIdx.x;
-    const int tileAll = xcdRemap(blockIdx.x, gridDim.x);   // batch frame k = tileAll / numTiles
-    const int k = tileAll / f.numTiles, tile = tileAll - k * f.numTiles;
+    const int tileAll = xcdRemap(blockIdx.x, gridDim.x);
+    int k, tile;
+    splitTileFrame(f, tileAll, k, tile);
     int x, y;
-    if (!tilePixel(f, tile, lane, x, y)) return;
+    if (tile >= f.numTiles || k >= f.batch || !tilePixel(f, tile, lane, x, y)) return;
     const mcrt_camera& cam = camp[k];
     TraceRay r;
     r.o = ld3(cam.pos);
@@ -350,9 +351,10 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
                                                 QueueArgs q) {
     const int lane = threadIdx.x & 63;
     const int tileAll = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int k = tileAll / f.numTiles, tile = tileAll - k * f.numTiles;   // batch frame k
+    int k, tile;   // batch frame k
+    splitTileFrame(f, tileAll, k, tile);
     int x = 0, y = 0;
-    bool valid = k < f.batch && tilePixel(f, tile, lane, x, y);
+    bool valid = k < f.batch && tile < f.numTiles && tilePixel(f, tile, lane, x, y);
     __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
 #if MCRT_SORT_OCTANT
     __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];

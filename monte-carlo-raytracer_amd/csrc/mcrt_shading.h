@@ -16,6 +16,17 @@ MCRT_DEV bool tilePixel(const FrameArgs& f, int tile, int lane, int& x, int& y) 
     return x < (int)f.W && y < (int)f.H;
 }
 
+// Launch index of the batched camera / first-bounce launches -> (batch frame k, 8x8 tile).
+MCRT_DEV void splitTileFrame(const FrameArgs& f, int tileAll, int& k, int& tile) {
+    if (f.tileMajor) {
+        tile = tileAll / f.batch;
+        k = tileAll - tile * f.batch;
+    } else {
+        k = tileAll / f.numTiles;
+        tile = tileAll - k * f.numTiles;
+    }
+}
+
 MCRT_DEV f3 cameraDir(const mcrt_camera& cam, int x, int y) {   // PathTracing.cl:13-27
     const f2 r = f2{cl_div(1.0f, (float)cam.width), cl_div(1.0f, (float)cam.height)};
     const f2 uv = f2{(float)x * r.x, (float)y * r.y};
