@@ -384,7 +384,7 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene scene, mcrt_framebuffer fb, co
  * After mcrt_render_frames it accumulates every frame of that batch in frame order
  * (frame_index = the batch's first frame), all with this filter. */
 MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* filter, int32_t frame_index);
-/* Batched frames (PT): renders the `count` (1..16) consecutive 1-spp frames
+/* Batched frames (PT): renders the `count` (1..32) consecutive 1-spp frames
  * params->frame_index + k, k < count, with cameras[k] (per-frame TAA jitter), in ONE pass --
  * every launch (camera rays, shading, shadow + extension rays) covers all count frames' paths,
  * so a small per-rank band share (tile split over N GPUs) still fills the 256 CUs and the

@@ -135,7 +135,7 @@ struct FrameSlot {
     int frames = 1;              // radiance / primary-hit planes of W*H allocated (batch capacity)
     size_t queueCap = 0;         // entries of each ray-queue buffer
 };
-#define SLOT_COUNTER_BYTES 4096
+#define SLOT_COUNTER_BYTES (512 + 176 * MCRT_MAX_BATCH_FRAMES + 1536)
 
 // Per-frame BDPT arrays (RTBDPTPass::createBuffers, RTBDPTPass.cpp:442-479), one set per frame
 // slot so BDPT frames overlap like PT frames; layouts in mcrt_bdpt.hip.
@@ -146,7 +146,7 @@ struct BdptSet {
     float4 *cO = nullptr, *cD = nullptr, *cL = nullptr;
     uint32_t* spill = nullptr;   // traversal spill columns of this set's launches
     size_t spillWords = 0;
-};   // [0..127] ints: counters; cameras (176 B each, <= 16) from byte 512
+};   // [0..127] ints: counters; cameras (176 B each, <= MCRT_MAX_BATCH_FRAMES) from byte 512
 
 struct mcrt_framebuffer_s {
     mcrt_ctx ctx = nullptr;

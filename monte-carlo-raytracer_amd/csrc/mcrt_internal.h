@@ -40,7 +40,7 @@ struct FrameArgs {
     int batch;              // frames per launch (mcrt_render_frames): path id = k * W*H + pixel, frame f.frame + k
     int tileMajor;          // launch order of (tile, frame k): 1 = a tile's frames adjacent, 0 = frame-major
 };
-#define MCRT_MAX_BATCH_FRAMES 16
+#define MCRT_MAX_BATCH_FRAMES 32
 // the reconstruction filter of each frame of a batch (device layout, KRN/kernel_data.h:63-80);
 // k_accumulate evaluates its weight on the device like ReconstructionPass (reconstruction.cl:21-42)
 struct BatchFilters { mcrt_filter f[MCRT_MAX_BATCH_FRAMES]; };

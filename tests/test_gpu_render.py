@@ -250,7 +250,7 @@ def test_batched_frames_bit_exact(hip_ctx, mixed, num_bands, band_index, count):
     with pytest.raises(lib.MCRTError):
         fb.accumulate_frames(filts[:2] if count != 2 else filts[:3], 0)   # neither 1 nor count filters
     with pytest.raises(lib.MCRTError):
-        fb.render_frames(ds, [cams[0]] * 17, frame=0, max_depth=D)
+        fb.render_frames(ds, [cams[0]] * 33, frame=0, max_depth=D)
     fb.close()
     ref.close()
     ds.close()
