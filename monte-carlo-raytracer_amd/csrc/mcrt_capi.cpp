@@ -1233,6 +1233,11 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
         return e ? std::atoi(e) : 1;
     }();
     f.tileMajor = tileMajor;
+    static const int primaryPack = [] {   // MCRT_PRIMARY_PACK=0: one frame's 8x8 tile per wave
+        const char* e = std::getenv("MCRT_PRIMARY_PACK");
+        return e ? std::atoi(e) : 1;
+    }();
+    f.primaryPack = primaryPack;
     f.batch = 1;
     f.numBands = p->num_bands <= 0 ? 1 : p->num_bands;
     f.bandIndex = p->band_index;

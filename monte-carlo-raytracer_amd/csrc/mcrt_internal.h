@@ -39,6 +39,7 @@ struct FrameArgs {
     int textureLod;         // mip-mapped texture reads at camera-ray hits (PT)
     int batch;              // frames per launch (mcrt_render_frames): path id = k * W*H + pixel, frame f.frame + k
     int tileMajor;          // launch order of (tile, frame k): 1 = a tile's frames adjacent, 0 = frame-major
+    int primaryPack;        // camera launch: 1 = a wave holds a few pixels x all batch frames
 };
 #define MCRT_MAX_BATCH_FRAMES 32
 // the reconstruction filter of each frame of a batch (device layout, KRN/kernel_data.h:63-80);

@@ -120,10 +120,18 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
     __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
     const int lane = threadIdx.x;
     const int tileAll = xcdRemap(blockIdx.x, gridDim.x);
-    int k, tile;
-    splitTileFrame(f, tileAll, k, tile);
+    int k, tile, pi = lane;
+    if (f.primaryPack && f.batch > 1 && (64 % f.batch) == 0) {
+        // a wave = 64 / batch pixels of one tile x every frame of the batch: the same pixel's
+        // TAA-jittered rays walk nearly the same nodes, so the lanes' loads coalesce
+        tile = tileAll / f.batch;
+        k = lane % f.batch;
+        pi = (tileAll - tile * f.batch) * (64 / f.batch) + lane / f.batch;
+    } else {
+        splitTileFrame(f, tileAll, k, tile);
+    }
     int x, y;
-    if (tile >= f.numTiles || k >= f.batch || !tilePixel(f, tile, lane, x, y)) return;
+    if (tile >= f.numTiles || k >= f.batch || !tilePixel(f, tile, pi, x, y)) return;
     const mcrt_camera& cam = camp[k];
     TraceRay r;
     r.o = ld3(cam.pos);
