@@ -1238,6 +1238,11 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
         return e ? std::atoi(e) : 1;
     }();
     f.primaryPack = primaryPack;
+    static const int shadePack = [] {   // MCRT_SHADE_PACK=0: one frame's pixels per shading wave
+        const char* e = std::getenv("MCRT_SHADE_PACK");
+        return e ? std::atoi(e) : 1;
+    }();
+    f.shadePack = shadePack;
     f.batch = 1;
     f.numBands = p->num_bands <= 0 ? 1 : p->num_bands;
     f.bandIndex = p->band_index;

@@ -40,6 +40,7 @@ struct FrameArgs {
     int batch;              // frames per launch (mcrt_render_frames): path id = k * W*H + pixel, frame f.frame + k
     int tileMajor;          // launch order of (tile, frame k): 1 = a tile's frames adjacent, 0 = frame-major
     int primaryPack;        // camera launch: 1 = a wave holds a few pixels x all batch frames
+    int shadePack;          // first shading launch: the same packing (its ray queues inherit the order)
 };
 #define MCRT_MAX_BATCH_FRAMES 32
 // the reconstruction filter of each frame of a batch (device layout, KRN/kernel_data.h:63-80);

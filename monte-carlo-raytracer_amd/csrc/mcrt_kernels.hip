@@ -359,10 +359,18 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
                                                 QueueArgs q) {
     const int lane = threadIdx.x & 63;
     const int tileAll = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    int k, tile;   // batch frame k
-    splitTileFrame(f, tileAll, k, tile);
+    int k, tile, pi = lane;   // batch frame k
+    if (f.shadePack && f.batch > 1 && (64 % f.batch) == 0) {
+        // as k_primary's packed waves: 64/batch pixels x every frame; the bounce-0 shadow rays of
+        // a wave (one light direction, nearly one origin) and its extension rays stay together
+        tile = tileAll / f.batch;
+        k = lane % f.batch;
+        pi = (tileAll - tile * f.batch) * (64 / f.batch) + lane / f.batch;
+    } else {
+        splitTileFrame(f, tileAll, k, tile);
+    }
     int x = 0, y = 0;
-    bool valid = k < f.batch && tile < f.numTiles && tilePixel(f, tile, lane, x, y);
+    bool valid = k < f.batch && tile < f.numTiles && tilePixel(f, tile, pi, x, y);
     __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
 #if MCRT_SORT_OCTANT
     __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];
