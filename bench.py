@@ -431,10 +431,11 @@ def main():
     else:
         band = dict(band_rows=args.band_rows, num_bands=world, band_index=rank)
     first = [True]
-    # auto: 16 frames per launch (MCRT_MAX_BATCH_FRAMES); at N = 1 the sweep tools/r2_gpu12.sh
-    # measured 1120 / 1140 / 1145 / 1147 Mpaths/s for 2 / 4 / 8 / 16 frames per launch, and a 1/N
-    # band share x 16 frames keeps every multi-GPU launch at >= 2 whole images of paths
-    batch = 1 if bdpt else (args.batch if args.batch > 0 else 16)
+    # auto: 32 frames per launch (MCRT_MAX_BATCH_FRAMES) up to 1080p, 16 above (slot memory).  The
+    # camera and first-shading waves then hold 2 pixels x 32 jittered frames (packed waves); the
+    # sweep tools/r2_gpu27.sh measured 1297 / 1315 Mpaths/s at 16 / 32 frames per launch, and a
+    # 1/N band share x 32 frames keeps every multi-GPU launch at >= 4 whole images of paths
+    batch = 1 if bdpt else (args.batch if args.batch > 0 else (32 if W * H <= 2_100_000 else 16))
     # the untimed per-kernel pass and the roofline price launches of (at most) 4 frames, which
     # keeps the oracle's distinct-node count of one launch to ~10 s of CPU
     stats_batch = min(batch, 4)
