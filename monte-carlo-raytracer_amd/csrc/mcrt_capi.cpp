@@ -1377,7 +1377,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     if (fb->ctx != ctx) return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame buffer belongs to another context");
     if (!s->dNodes) return fail(ctx, MCRT_ERROR_NOT_READY, "mcrt_accel_build has not been called");
     if (count < 1 || count > MCRT_MAX_BATCH_FRAMES)
-        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame count must be 1 .. 16");
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame count must be 1 .. MCRT_MAX_BATCH_FRAMES (32)");
     for (int k = 0; k < count; ++k)
         if (cam[k].width != fb->W || cam[k].height != fb->H)
             return fail(ctx, MCRT_ERROR_INVALID_ARG, "camera size differs from the frame buffer");

@@ -4,6 +4,7 @@
 // the sorted order.  Queue order never changes results (paths are independent).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -23,7 +24,8 @@ __device__ __forceinline__ uint32_t spread9(uint32_t v) {   // 9 bits -> every t
 
 __global__ __launch_bounds__(256) void k_ray_keys(const int* __restrict__ count, const float4* __restrict__ o,
                                                   const float4* __restrict__ d, float4 lo, float4 inv,
-                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                  int octOnly) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= *count) return;
     const float4 p = o[i], v = d[i];
@@ -31,7 +33,7 @@ __global__ __launch_bounds__(256) void k_ray_keys(const int* __restrict__ count,
     const uint32_t qy = (uint32_t)fminf(fmaxf((p.y - lo.y) * inv.y, 0.0f), 511.0f);
     const uint32_t qz = (uint32_t)fminf(fmaxf((p.z - lo.z) * inv.z, 0.0f), 511.0f);
     const uint32_t oct = (v.x < 0.0f ? 1u : 0u) | (v.y < 0.0f ? 2u : 0u) | (v.z < 0.0f ? 4u : 0u);
-    keys[i] = (oct << 27) | (spread9(qx) << 2) | (spread9(qy) << 1) | spread9(qz);
+    keys[i] = octOnly ? oct : (oct << 27) | (spread9(qx) << 2) | (spread9(qy) << 1) | spread9(qz);
     vals[i] = (uint32_t)i;
 }
 
@@ -75,8 +77,15 @@ hipError_t sort_ray_queue(const int* count, const float4* o, const float4* d, co
     const float4 lo = make_float4(sceneLo.x, sceneLo.y, sceneLo.z, 0.0f);
     const float4 inv = make_float4(512.0f / ex, 512.0f / ey, 512.0f / ez, 0.0f);
     const dim3 g((unsigned)((maxCount + 255) / 256)), b(256);
-    hipLaunchKernelGGL(k_ray_keys, g, b, 0, st, count, o, d, lo, inv, keys, vals);
-    hipError_t e = rocprim::radix_sort_pairs(tmp, tempBytes, keys, keys2, vals, vals2, (size_t)maxCount, 0, 30, st);
+    // MCRT_SORT_KEY=octant: the direction octant alone (a stable 3-bit sort keeps the queue's own
+    // origin order inside each octant)
+    static const int octOnly = [] {
+        const char* k = std::getenv("MCRT_SORT_KEY");
+        return k && std::strcmp(k, "octant") == 0 ? 1 : 0;
+    }();
+    hipLaunchKernelGGL(k_ray_keys, g, b, 0, st, count, o, d, lo, inv, keys, vals, octOnly);
+    hipError_t e = rocprim::radix_sort_pairs(tmp, tempBytes, keys, keys2, vals, vals2, (size_t)maxCount, 0,
+                                             octOnly ? 4 : 30, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_gather3, g, b, 0, st, count, vals2, o, d, t, o2, d2, t2);
     return hipGetLastError();
