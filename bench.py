@@ -361,6 +361,8 @@ def main():
     ap.add_argument("--russian-roulette", action="store_true",
                     help="opt-in RR on extension rays (perf mode; the reference has none, so not a parity run)")
     ap.add_argument("--rr-start", type=int, default=1, help="first bounce whose extension rays RR may cut")
+    ap.add_argument("--chunks", default="",
+                    help="A/B only: comma-separated frames per call of the timed region, cycled (e.g. 4,16)")
     ap.add_argument("--batch", type=int, default=0,
                     help="PT frames per mcrt_render_frames call (one launch sequence for all of them); "
                          "0 = auto (32 up to 1080p, 16 above); each call renders a power-of-two frame count")
@@ -459,9 +461,12 @@ def main():
         # 16 + 4: 1264 Mpaths/s against 1212 for one 20-frame call, tools/r2_gpu32.sh)
         i = 0
         per = per or batch
+        plan = [int(c) for c in args.chunks.split(",")] if args.chunks and per == batch else [per]
+        calls = 0
         while i < count:
-            n = min(per, count - i)
+            n = min(plan[calls % len(plan)], count - i)
             n = 1 << (n.bit_length() - 1)
+            calls += 1
             step(i0 + i, n)
             i += n
 

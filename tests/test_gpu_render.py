@@ -217,7 +217,7 @@ def test_russian_roulette_unbiased(hip_ctx, mixed):
     ds.close()
 
 
-@pytest.mark.parametrize("num_bands,band_index,count", [(1, 0, 2), (1, 0, 5), (4, 3, 8)])
+@pytest.mark.parametrize("num_bands,band_index,count", [(1, 0, 2), (1, 0, 4), (1, 0, 5), (4, 3, 8), (2, 1, 16), (1, 0, 32)])
 def test_batched_frames_bit_exact(hip_ctx, mixed, num_bands, band_index, count):
     """mcrt_render_frames + mcrt_accumulate_frames over `count` frames (per-frame jittered
     cameras, per-frame filter weights) give the accumulators of `count` single-frame renders
