@@ -1,0 +1,144 @@
+// Sanitizer run of the host-side code (no GPU): OBJ/MTL ingestion (mcrt_objload.cpp), the host camera
+// (mcrt_camera.cpp), the host Bvh2 restatement (mcrt_bvh.cpp) and the oracle (oracle/mcrt_oracle.c:
+// BVH build, closest / any-hit traversal against brute force, one PT and one BDPT frame, accumulate,
+// denoise, tone map), all built with -fsanitize=address,undefined (tests/asan/Makefile).  Exit 0 =
+// every check held and the sanitizers reported nothing (they abort on the first finding).
+#include <unistd.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../monte-carlo-raytracer_amd/csrc/mcrt_internal.h"
+extern "C" {
+#include "../../oracle/mcrt_oracle.h"
+}
+
+#define CHECK(c)                                                        \
+    do {                                                                \
+        if (!(c)) {                                                     \
+            std::fprintf(stderr, "check failed: %s (line %d)\n", #c, __LINE__); \
+            return 1;                                                   \
+        }                                                               \
+    } while (0)
+
+static void write_file(const std::string& p, const char* text) {
+    FILE* f = std::fopen(p.c_str(), "w");
+    std::fputs(text, f);
+    std::fclose(f);
+}
+
+int main() {
+    // a room (floor, back wall), a box, an emissive quad and a quad fan, with an MTL
+    char tmpl[] = "/tmp/mcrt_asan_XXXXXX";
+    const char* dir = mkdtemp(tmpl);
+    CHECK(dir != nullptr);
+    const std::string d(dir);
+    write_file(d + "/s.mtl",
+               "newmtl white\nKd 0.7 0.7 0.7\nNs 10\n"
+               "newmtl shiny\nKd 0.1 0.1 0.1\nKs 0.8 0.8 0.8\nNs 200\n"
+               "newmtl glass\nKd 0 0 0\nKs 0.1 0.1 0.1\nTf 0.9 0.9 0.9\nNi 1.5\nd 0.8\n"
+               "newmtl lamp\nKd 0 0 0\nKe 8 8 8\n");
+    write_file(d + "/s.obj",
+               "mtllib s.mtl\n"
+               "v -2 0 -2\nv 2 0 -2\nv 2 0 2\nv -2 0 2\n"          // floor 1-4
+               "v -2 0 2\nv 2 0 2\nv 2 3 2\nv -2 3 2\n"            // back wall 5-8
+               "v -0.5 0 -0.5\nv 0.5 0 -0.5\nv 0.5 1 -0.5\nv -0.5 1 -0.5\n"   // box 9-16
+               "v -0.5 0 0.5\nv 0.5 0 0.5\nv 0.5 1 0.5\nv -0.5 1 0.5\n"
+               "v -0.4 2.9 -0.4\nv 0.4 2.9 -0.4\nv 0.4 2.9 0.4\nv -0.4 2.9 0.4\n"   // lamp 17-20
+               "vt 0 0\nvt 1 0\nvt 1 1\nvt 0 1\nvn 0 1 0\n"
+               "o floor\nusemtl white\nf 1/1/1 2/2/1 3/3/1 4/4/1\n"
+               "o wall\nusemtl shiny\nf 5 6 7 8\n"
+               "o box\nusemtl glass\nf 9 10 11 12\nf 13 16 15 14\nf 9 13 14 10\nf 12 11 15 16\nf 9 12 16 13\nf 10 14 15 11\n"
+               "o lamp\nusemtl lamp\nf 17 20 19 18\n");
+    mcrt_obj_scene os = nullptr;
+    CHECK(mcrt_obj_load((d + "/s.obj").c_str(), MCRT_OBJ_MIPS | MCRT_OBJ_EMISSIVE_LIGHTS, &os) == MCRT_OK);
+    const float sun[3] = {-0.3f, -1.0f, 0.2f}, sunI[3] = {4.0f, 4.0f, 4.0f};
+    CHECK(mcrt_obj_add_directional_light(os, sun, sunI) == MCRT_OK);
+    mcrt_scene_desc desc;
+    CHECK(mcrt_obj_scene_desc(os, &desc) == MCRT_OK);
+    CHECK(desc.num_shapes >= 4 && desc.num_lights >= 2);
+    // a missing file is an error, not a crash
+    mcrt_obj_scene bad = nullptr;
+    CHECK(mcrt_obj_load((d + "/missing.obj").c_str(), 0, &bad) != MCRT_OK);
+
+    // oracle: BVH, traversal vs brute force, PT + BDPT frames, accumulate, post-process
+    orc_scene* s = orc_scene_create(&desc);
+    CHECK(s != nullptr);
+    CHECK(orc_bvh_build(s, 10.0f, 64, 1) > 0);
+    std::mt19937 rng(7);
+    std::uniform_real_distribution<float> U(-1.0f, 1.0f);
+    const int n = 2000;
+    std::vector<mcrt_ray> rays(n);
+    for (auto& r : rays) {
+        std::memset(&r, 0, sizeof(r));
+        r.o = {U(rng) * 1.5f, 1.5f + U(rng), U(rng) * 1.5f, 1000.0f};
+        r.d = {U(rng), U(rng), U(rng), 0.0f};
+        r.extra[0] = -1;
+        r.extra[1] = -1;
+    }
+    std::vector<mcrt_intersection> h1(n), h2(n);
+    std::vector<int32_t> visits(n), a1(n), a2(n);
+    orc_trace_closest(s, rays.data(), n, h1.data(), visits.data(), 4);
+    orc_brute_closest(s, rays.data(), n, h2.data());
+    int same = 0;
+    for (int i = 0; i < n; ++i) same += h1[i].shapeid == h2[i].shapeid;
+    CHECK(same >= n - 2);   // RR conformance: equal-t ties aside
+    orc_trace_any(s, rays.data(), n, a1.data(), visits.data(), 4);
+    orc_brute_any(s, rays.data(), n, a2.data());
+    for (int i = 0; i < n; ++i) CHECK(a1[i] == a2[i]);
+
+    const int W = 48, H = 32;
+    mcrt_camera cam;
+    const float pos[3] = {0.0f, 1.5f, -4.5f}, fwd[3] = {0.0f, -0.1f, 1.0f}, up[3] = {0.0f, 1.0f, 0.0f},
+                off[2] = {0.1f, -0.2f};
+    CHECK(mcrt_make_pinhole_camera(pos, fwd, up, 45.0f, 0.3f, 100.0f, W, H, off, &cam) == MCRT_OK);
+    std::vector<float> rad(4 * W * H), wsum(4 * W * H), wts(W * H), img(4 * W * H), den(4 * W * H), tm(4 * W * H);
+    int64_t st[8] = {};
+    mcrt_filter f;
+    std::memset(&f, 0, sizeof(f));
+    f.filterType = MCRT_BOX_FILTER;
+    f.radius.x = f.radius.y = 0.5f;
+    for (int frame = 0; frame < 3; ++frame) {
+        orc_render_frame(s, &cam, frame, 5, 1, 0, H, 4, rad.data(), st);
+        for (float v : rad) CHECK(std::isfinite(v));
+        orc_accumulate(W, H, frame, &f, rad.data(), wsum.data(), wts.data(), img.data());
+    }
+    double sum = 0;
+    for (int i = 0; i < W * H; ++i) sum += img[4 * i] + img[4 * i + 1] + img[4 * i + 2];
+    CHECK(sum > 0.0);
+    orc_denoise(W, H, 2, 2.0f, 0.2f, img.data(), den.data());
+    orc_tonemap(W, H, 1.0f, den.data(), tm.data());
+    orc_bdpt* b = orc_bdpt_create(W, H, 3);
+    std::vector<int32_t> cc(W * H), lc(W * H);
+    for (int frame = 0; frame < 2; ++frame)
+        orc_bdpt_render(s, b, &cam, frame, 1, nullptr, 0, 4, rad.data(), cc.data(), lc.data(), st);
+    for (float v : rad) CHECK(std::isfinite(v));
+    orc_bdpt_destroy(b);
+    orc_scene_destroy(s);
+
+    // the host Bvh2 restatement (mcrt_bvh.cpp) over a random soup, several threads
+    const size_t nt = 30000;
+    std::vector<float> tri(9 * nt);
+    std::vector<int32_t> shapeOf(nt, 0), primOf(nt);
+    for (size_t i = 0; i < nt; ++i) {
+        const float cx = 50.0f * U(rng), cy = 50.0f * U(rng), cz = 50.0f * U(rng);
+        for (int k = 0; k < 9; ++k) tri[9 * i + k] = (k % 3 == 0 ? cx : k % 3 == 1 ? cy : cz) + 0.5f * U(rng);
+        primOf[i] = (int32_t)i;
+    }
+    mcrt::BvhOut out;
+    CHECK(mcrt::build_bvh(tri.data(), shapeOf.data(), primOf.data(), nt, 10.0f, 64, true, 4, out));
+    CHECK(out.numNodes == 2 * nt - 1);
+    mcrt::free_bvh(out);
+
+    mcrt_obj_free(os);
+    std::string cmd = "rm -rf " + d;
+    (void)std::system(cmd.c_str());
+    std::printf("host asan ok: OBJ -> %u shapes, %u lights; %d/%d closest hits equal brute force; BVH %zu nodes\n",
+                desc.num_shapes, desc.num_lights, same, n, 2 * nt - 1);
+    return 0;
+}
