@@ -50,6 +50,7 @@ struct mcrt_ctx_s {
     bool profiling = false;
     bool fuseShadowExtend = true;   // MCRT_NO_FUSE=1 launches k_shadow and k_extend separately (A/B)
     bool sortRays = false;          // MCRT_SORT_RAYS=1: global sort of the extension queue (mcrt_raysort.hip)
+    bool shadowCompact = false;     // MCRT_SHADOW_COMPACT=1: bounce-0 shadow rays on the descent-compact records
     int envFramesInFlight = 0;      // MCRT_FRAMES_IN_FLIGHT=n overrides the frame buffers' setting (A/B)
     int* dFlags = nullptr;          // device flags: [0] traversal-stack overflow (mcrt_traverse.h), set by any launch
     std::string error;
@@ -354,6 +355,7 @@ MCRT_API mcrt_status mcrt_ctx_create(int device, mcrt_ctx* out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
     if (const char* nf = std::getenv("MCRT_NO_FUSE")) c->fuseShadowExtend = nf[0] != '1';
     if (const char* sr = std::getenv("MCRT_SORT_RAYS")) c->sortRays = sr[0] == '1';
+    if (const char* sc = std::getenv("MCRT_SHADOW_COMPACT")) c->shadowCompact = sc[0] == '1';
     if (const char* fi = std::getenv("MCRT_FRAMES_IN_FLIGHT")) c->envFramesInFlight = std::atoi(fi);
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -1530,8 +1532,11 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
         if (ctx->fuseShadowExtend && b + 1 < p->max_depth) {
             // shadow rays of bounce b + extension rays for bounce b+1 (both from this shading pass)
             Timed t(ctx, K_SHADOW_EXTEND, extCnt + b, 0, st, shadowCnt + b);   // items: extension + shadow rays
-            mcrt::launch_shadow_extend(tcs, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b, fb->sO,
-                                       fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
+            // bounce 0's shadow rays come out of the packed first shading launch coherent: compact records
+            TraceCtx tss = (b == 0 && ctx->shadowCompact) ? compact_ctx(s) : tcs;
+            tss.spill = slot.spill;
+            mcrt::launch_shadow_extend(tcs, tss, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
+                                       fb->sO, fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
             Timed t(ctx, K_SHADOW, shadowCnt + b, 0, st);
             mcrt::launch_shadow(tcs, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, qCap, st);

@@ -196,8 +196,11 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
 // Shadow rays of bounce b and extension rays of bounce b+1 in ONE launch: both only depend on
 // the shading of bounce b.  Extension workgroups come first (their rays are the longer ones),
 // shadow workgroups fill the extension launch's divergent tail instead of waiting for it.
-template <int LAY>
-__global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __restrict__ extCount,
+// SLAY: the shadow rays' record layout (cs).  The bounce-0 shadow rays leave the packed first
+// shading launch coherent (a wave's rays share the light sample's direction and nearly one origin),
+// so they take the descent-compact records like the camera rays; the extension rays keep LAY.
+template <int LAY, int SLAY>
+__global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, TraceCtx cs, const int* __restrict__ extCount,
                                                       const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                       float4* __restrict__ hitOut, const int* __restrict__ shadowCount,
                                                       const float4* __restrict__ sO, const float4* __restrict__ sD,
@@ -230,7 +233,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.d = ld3(d);
         r.tmax = o.w;
         r.mask = -1;
-        const float V = traceAny<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane)) ? 0.0f : 1.0f;
+        const float V = traceAny<SLAY>(cs, r, lds + lane, raySpill(cs, blockIdx.x, lane)) ? 0.0f : 1.0f;
         const int pix = __float_as_int(d.w);
         float4 acc = radiance[pix];
         acc.x += L.x * V;
@@ -775,12 +778,18 @@ void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const 
     hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_COMPACT>, k_shadow<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, sO, sD, sL, radiance);
 }
-void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
-                          const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
-                          float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
+void launch_shadow_extend(const TraceCtx& c, const TraceCtx& cs, const int* extCount, const float4* qO,
+                          const float4* qD, float4* hits, const int* shadowCount, const float4* sO, const float4* sD,
+                          const float4* sL, float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
     const int blocks = (maxExt + 63) / 64 + (maxShadow + 63) / 64;
-    hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_COMPACT>, k_shadow_extend<LAY_PLAIN>), dim3(blocks > 0 ? blocks : 1),
-                       dim3(64), 0, st, c, extCount, qO, qD, hits, shadowCount, sO, sD, sL, radiance);
+    // shadow rays on compact records only beside plain extension records (the two flat layouts)
+    const bool sc = !c.twoLevel && !c.compact && cs.compact;
+    auto k = c.twoLevel ? k_shadow_extend<LAY_TWO_LEVEL, LAY_TWO_LEVEL>
+             : c.compact ? k_shadow_extend<LAY_COMPACT, LAY_COMPACT>
+             : sc        ? k_shadow_extend<LAY_PLAIN, LAY_COMPACT>
+                         : k_shadow_extend<LAY_PLAIN, LAY_PLAIN>;
+    hipLaunchKernelGGL(k, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, sc ? cs : c, extCount, qO, qD, hits,
+                       shadowCount, sO, sD, sL, radiance);
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {
