@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--scene", default="san_miguel_proxy")
     ap.add_argument("--fif", type=int, default=0, help="frames in flight (0 = the library's auto choice)")
     ap.add_argument("--batch", type=int, default=1, help="frames per mcrt_render_frames call (0 = N)")
+    ap.add_argument("--chunks", default="", help="frames per call, cycled, each rounded down to a power of two "
+                                                 "(bench.py's plan; overrides --batch)")
     ap.add_argument("--base-ms", type=float, default=None,
                     help="1-GPU ms/frame (the efficiency base) when --ns does not include 1")
     args = ap.parse_args()
@@ -32,30 +34,36 @@ def main():
     from mcrt.camera import scene_camera
     W, H = 1920, 1080
     scene = scenes.san_miguel_proxy() if args.scene == "san_miguel_proxy" else scenes.dragon_proxy()
-    cam = scene_camera(args.scene, W, H)
+    cams = [scene_camera(args.scene, W, H, frame=f, jitter=True) for f in range(64)]   # TAA as bench.py
     ctx = lib.Context(0)
     ds = lib.DeviceScene(ctx, scene)
     fb = lib.FrameBuffer(ctx, W, H)
     filt = T.make_filter(T.BOX)
     fb.set_frames_in_flight(args.fif)
-    out = {"fif": args.fif, "batch": args.batch, "scene": args.scene, "steps": args.steps, "band_rows": args.band_rows, "per_n": {}}
+    out = {"fif": args.fif, "batch": args.batch, "chunks": args.chunks, "scene": args.scene, "steps": args.steps, "band_rows": args.band_rows, "per_n": {}}
     for n in [int(x) for x in args.ns.split(",")]:
         per_rank = []
         for r in range(n):
             band = dict(band_rows=args.band_rows, num_bands=n, band_index=r)
             B = args.batch if args.batch > 0 else n
 
+            plan = [int(c) for c in args.chunks.split(",")] if args.chunks else [B]
+
             def run(f0, count):
-                i = 0
+                i = calls = 0
                 while i < count:
-                    k = min(B, count - i)
+                    k = min(plan[calls % len(plan)], count - i)
+                    if args.chunks:
+                        k = 1 << (k.bit_length() - 1)
+                    calls += 1
                     if k == 1:
-                        fb.render(ds, cam, frame=f0 + i, max_depth=2, **band)
+                        fb.render(ds, cams[(f0 + i) % 64], frame=f0 + i, max_depth=2, **band)
                     else:
-                        fb.render_frames(ds, [cam] * k, frame=f0 + i, max_depth=2, **band)
+                        fb.render_frames(ds, [cams[(f0 + i + j) % 64] for j in range(k)], frame=f0 + i, max_depth=2,
+                                         **band)
                     fb.accumulate(filt, f0 + i)
                     i += k
-            run(0, max(3, 4 * B))   # every frame slot allocated before timing
+            run(0, max(3, 4 * max(plan)))   # every frame slot allocated before timing
             ctx.sync()
             t0 = time.perf_counter()
             run(16, args.steps)
