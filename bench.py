@@ -361,11 +361,13 @@ def main():
     ap.add_argument("--russian-roulette", action="store_true",
                     help="opt-in RR on extension rays (perf mode; the reference has none, so not a parity run)")
     ap.add_argument("--rr-start", type=int, default=1, help="first bounce whose extension rays RR may cut")
+    ap.add_argument("--pow2-calls", action="store_true",
+                    help="A/B only: round every call's frame count down to a power of two (16 + 4 for 20 steps)")
     ap.add_argument("--chunks", default="",
                     help="A/B only: comma-separated frames per call of the timed region, cycled (e.g. 4,16)")
     ap.add_argument("--batch", type=int, default=0,
                     help="PT frames per mcrt_render_frames call (one launch sequence for all of them); "
-                         "0 = auto (32 up to 1080p, 16 above); each call renders a power-of-two frame count")
+                         "0 = auto (32 up to 1080p, 16 above)")
     args = ap.parse_args()
 
     import torch
@@ -456,16 +458,18 @@ def main():
         first[0] = False
 
     def run(i0, count, per=None):
-        # calls of power-of-two frame counts: the camera and first-shading waves pack 64/n pixels x n
-        # frames only when n divides 64, so a remainder is split too (20 steps at 32 per launch ->
-        # 16 + 4: 1264 Mpaths/s against 1212 for one 20-frame call, tools/r2_gpu32.sh)
+        # calls of min(batch, remaining) frames: the camera and first-shading waves pack 64 consecutive
+        # (pixel, frame) paths for any frame count, so the driver's 20 steps are ONE 20-frame call
+        # (1293 / 1282 Mpaths/s against 1264 / 1267 for 16 + 4, tools/r2_gpu41.sh); --pow2-calls
+        # restores the earlier power-of-two split for A/B
         i = 0
         per = per or batch
         plan = [int(c) for c in args.chunks.split(",")] if args.chunks and per == batch else [per]
         calls = 0
         while i < count:
             n = min(plan[calls % len(plan)], count - i)
-            n = 1 << (n.bit_length() - 1)
+            if args.pow2_calls:
+                n = 1 << (n.bit_length() - 1)
             calls += 1
             step(i0 + i, n)
             i += n

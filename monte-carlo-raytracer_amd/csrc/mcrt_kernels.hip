@@ -112,6 +112,16 @@ __global__ void k_surface_records(const uint32_t* __restrict__ meshStartIdx, con
     R[7] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// Packed waves of a batch of n frames: the n waves of tile t (tileAll = t*n .. t*n + n-1) hold the
+// tile's 64 x n paths (pixel pi, frame k) in pixel-major order, q = 64 * (tileAll - t*n) + lane =
+// pi * n + k.  Each (pi, k) is covered once for any n; for n | 64 a wave is 64/n whole pixels.
+MCRT_DEV void packedPath(const FrameArgs& f, int tileAll, int lane, int& k, int& tile, int& pi) {
+    tile = tileAll / f.batch;
+    const int q = (tileAll - tile * f.batch) * 64 + lane;
+    pi = q / f.batch;
+    k = q - pi * f.batch;
+}
+
 // Camera ray generation fused with the first closest-hit query (RTPrimaryRaysPass):
 // one workgroup = one wave = one 8x8 pixel tile of the rank's bands.
 template <int LAY>
@@ -121,12 +131,10 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
     const int lane = threadIdx.x;
     const int tileAll = xcdRemap(blockIdx.x, gridDim.x);
     int k, tile, pi = lane;
-    if (f.primaryPack && f.batch > 1 && (64 % f.batch) == 0) {
-        // a wave = 64 / batch pixels of one tile x every frame of the batch: the same pixel's
-        // TAA-jittered rays walk nearly the same nodes, so the lanes' loads coalesce
-        tile = tileAll / f.batch;
-        k = lane % f.batch;
-        pi = (tileAll - tile * f.batch) * (64 / f.batch) + lane / f.batch;
+    if (f.primaryPack && f.batch > 1) {
+        // a wave = 64 consecutive (pixel, frame) paths of one tile, frames fastest: the same
+        // pixel's TAA-jittered rays walk nearly the same nodes, so the lanes' loads coalesce
+        packedPath(f, tileAll, lane, k, tile, pi);
     } else {
         splitTileFrame(f, tileAll, k, tile);
     }
@@ -363,12 +371,10 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
     const int lane = threadIdx.x & 63;
     const int tileAll = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     int k, tile, pi = lane;   // batch frame k
-    if (f.shadePack && f.batch > 1 && (64 % f.batch) == 0) {
-        // as k_primary's packed waves: 64/batch pixels x every frame; the bounce-0 shadow rays of
-        // a wave (one light direction, nearly one origin) and its extension rays stay together
-        tile = tileAll / f.batch;
-        k = lane % f.batch;
-        pi = (tileAll - tile * f.batch) * (64 / f.batch) + lane / f.batch;
+    if (f.shadePack && f.batch > 1) {
+        // as k_primary's packed waves; the bounce-0 shadow rays of a wave (one light direction,
+        // nearly one origin) and its extension rays stay together
+        packedPath(f, tileAll, lane, k, tile, pi);
     } else {
         splitTileFrame(f, tileAll, k, tile);
     }
