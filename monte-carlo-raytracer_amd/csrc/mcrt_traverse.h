@@ -63,6 +63,10 @@ MCRT_DEV float triHit(const TraceRay& r, float4 A, float4 E1, float4 E2, float t
 #ifndef MCRT_OCT_TRAV
 #define MCRT_OCT_TRAV 1
 #endif
+// Wave-uniform compact-record fetches through the scalar cache (1 = on; A/B, tools/r2_gpu45.sh).
+#ifndef MCRT_UNIFORM_SLOAD
+#define MCRT_UNIFORM_SLOAD 0
+#endif
 // Packed slab tests (v_pk_fma_f32, two box planes per instruction) in the octant loops (1 = on).
 #ifndef MCRT_PK_SLAB
 #define MCRT_PK_SLAB 0
@@ -227,10 +231,28 @@ MCRT_DEV int traverseOct2(const float4* __restrict__ nodes, uint32_t rootWord, c
         const uint32_t idx = word & CW_IDX;
         const bool leaf = (word & CW_LEAF) != 0;
         const float4* q = nodes + 4 * (size_t)idx;
-        const float4 q0 = q[0], q1 = q[1];
-        float4 q2 = make_float4(0.f, 0.f, 0.f, 0.f), q3 = q2;
-        if (leaf || popped) q2 = q[2];
-        if (popped && !leaf) q3 = q[3];
+        float4 q0, q1, q2 = make_float4(0.f, 0.f, 0.f, 0.f), q3 = q2;
+#if MCRT_UNIFORM_SLOAD
+        // packed camera waves: when every active lane is at the same node, fetch the record once
+        // through the scalar cache (one s_load_dwordx16) instead of 64 lanes' vector loads
+        const uint32_t w0 = __builtin_amdgcn_readfirstlane(word);
+        if (__builtin_amdgcn_ballot_w64(word != w0) == 0) {
+            typedef float v4 __attribute__((ext_vector_type(4)));
+            typedef const __attribute__((address_space(4))) v4* cptr;
+            const cptr cq = (cptr)(uintptr_t)(nodes + 4 * (size_t)(w0 & CW_IDX));
+            const v4 a0 = cq[0], a1 = cq[1], a2 = cq[2], a3 = cq[3];
+            q0 = make_float4(a0.x, a0.y, a0.z, a0.w);
+            q1 = make_float4(a1.x, a1.y, a1.z, a1.w);
+            q2 = make_float4(a2.x, a2.y, a2.z, a2.w);
+            q3 = make_float4(a3.x, a3.y, a3.z, a3.w);
+        } else
+#endif
+        {
+            q0 = q[0];
+            q1 = q[1];
+            if (leaf || popped) q2 = q[2];
+            if (popped && !leaf) q3 = q[3];
+        }
         bool pop = true;
         uint32_t next = CW_DONE;
         if (!leaf) {
