@@ -434,6 +434,10 @@ MCRT_API mcrt_status mcrt_render_aov(mcrt_scene scene, mcrt_framebuffer fb, cons
 /* Copies device -> host (RGBA32F, W*H*4 floats).  which: 0 radiance, 1 weighted sum, 2 image,
  * 3 display image (mcrt_postprocess). */
 MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float* host_rgba);
+/* Radiance of frame k (0 <= k < count) of the last mcrt_render_frames call (k = 0: the same as
+ * mcrt_framebuffer_read 0): the reference's RadianceBufferCL of that frame
+ * (RTPathTracingPass.cpp:106), RGBA32F, W*H*4 floats. */
+MCRT_API mcrt_status mcrt_framebuffer_read_frame(mcrt_framebuffer fb, int32_t k, float* host_rgba);
 /* Device-to-device copy of one frame-buffer array into caller memory (e.g. a torch/RCCL
  * buffer for the multi-GPU reduce): which 0 radiance (float4), 1 weighted sum (float4),
  * 2 image (float4), 3 weight sum (float).  Enqueued on the context stream, ordered after the

@@ -1677,6 +1677,18 @@ MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float
     return check_device_flags(ctx);
 }
 
+MCRT_API mcrt_status mcrt_framebuffer_read_frame(mcrt_framebuffer fb, int32_t k, float* host_rgba) {
+    if (!fb || !host_rgba) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    mcrt_ctx ctx = fb->ctx;
+    const int batch = fb->lastIntegrator == MCRT_INTEGRATOR_PT ? fb->slot[fb->cur].lastBatch : 1;
+    if (k < 0 || k >= std::max(batch, 1))
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame index outside the last mcrt_render_frames batch");
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, fb_sync(fb));
+    HIPCHK(ctx, hipMemcpy(host_rgba, fb->radiance + (size_t)k * fb->N, 16 * fb->N, hipMemcpyDeviceToHost));
+    return check_device_flags(ctx);
+}
+
 MCRT_API mcrt_status mcrt_framebuffer_copy_device(mcrt_framebuffer fb, int which, void* d_dst) {
     if (!fb || !d_dst || which < 0 || which > 3) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
     mcrt_ctx ctx = fb->ctx;

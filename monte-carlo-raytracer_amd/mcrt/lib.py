@@ -64,6 +64,7 @@ SIGNATURES = {
     "mcrt_accumulate_frames": (_c.c_int, [_vp, _vp, _c.c_int32, _c.c_int32]),
     "mcrt_framebuffer_device_ptrs": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_framebuffer_read": (_c.c_int, [_vp, _c.c_int, _vp]),
+    "mcrt_framebuffer_read_frame": (_c.c_int, [_vp, _c.c_int32, _vp]),
     "mcrt_framebuffer_stats": (_c.c_int, [_vp, _vp, _vp, _vp]),
     "mcrt_framebuffer_copy_device": (_c.c_int, [_vp, _c.c_int, _vp]),
     "mcrt_framebuffer_set_accumulation": (_c.c_int, [_vp, _vp, _vp]),
@@ -339,6 +340,12 @@ class FrameBuffer:
     def read(self, which=0):
         out = np.zeros((self.H, self.W, 4), np.float32)
         _check(lib().mcrt_framebuffer_read(self.h, which, _p(out)), self.ctx.h)
+        return out
+
+    def read_frame(self, k):
+        """Radiance of frame k of the last render_frames batch (mcrt_framebuffer_read_frame)."""
+        out = np.zeros((self.H, self.W, 4), np.float32)
+        _check(lib().mcrt_framebuffer_read_frame(self.h, k, _p(out)), self.ctx.h)
         return out
 
     def device_ptrs(self):

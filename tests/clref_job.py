@@ -141,6 +141,17 @@ def build_scene(name):
     raise KeyError(name)
 
 
+# bench.py's timed region at its defaults (--steps 20 --warmup 3): warmup = 4 x 32 frames, one
+# untimed statistics frame, then ONE mcrt_render_frames call of frames 129 .. 148
+TIMED_F0, TIMED_STEPS = 129, 20
+TIMED_CHECK_FRAMES = tuple(TIMED_F0 + k for k in (1, 7, 19))
+
+
+def taa_camera(name, W, H, f):
+    """bench.py's camera of frame f: 64 precomputed TAA-jittered cameras, camera f % 64."""
+    return scene_camera(name, W, H, frame=f % 64, jitter=True)
+
+
 # BASELINE.json configs at full size against the reference kernels run live
 # (tests/test_gpu_reference_scale.py): (key, scene, W, H, integrator, frames, max_depth).
 # The sampler is the job's variant: "ieee" = random (the reference default), "sobol_ieee" = the
@@ -148,9 +159,12 @@ def build_scene(name):
 SCALE_CASES = {
     "ieee": [
         ("sm_pt_1080p", "san_miguel_proxy", 1920, 1080, "pt", (0, 1), 2),            # headline / config 4 scene
+        # the bench's timed call: frames TIMED_F0 .. TIMED_F0 + 19 with TAA-jittered cameras
+        # (camera of frame f = jitter of f % 64, bench.py cam_of); frames 1, 7, 19 of the batch
+        ("sm_pt_1080p_taa", "san_miguel_proxy", 1920, 1080, "pt_taa", TIMED_CHECK_FRAMES, 2),
         ("sponza_pt_1080p", "sponza_proxy", 1920, 1080, "pt", (0, 1), 2),           # config 3
         ("dragon_pt_1080p", "dragon_proxy", 1920, 1080, "pt", (0, 1), 2),           # config 2
-        ("sm_bdpt_960x540", "san_miguel_proxy", 960, 540, "bdpt", (0, 1), 2),       # config 4 integrator
+        ("sm_bdpt_1080p", "san_miguel_proxy", 1920, 1080, "bdpt", (0, 1), 2),       # config 4 integrator (bench size)
     ],
     "sobol_ieee": [
         ("sm_sobol_4k", "san_miguel_proxy", 3840, 2160, "pt", (0, 600), 2),        # config 5; frame 600: Q6 wrap
@@ -183,6 +197,9 @@ def scale_job(out_path, variant):
         nodes[name] = cs.nodes
         t0 = time.time()
         for f in frames:
+            if integ == "pt_taa":
+                res[f"{key}_f{f}"] = cs.render(taa_camera(name, W, H, f), frame=f, max_depth=D)
+                continue
             res[f"{key}_f{f}"] = (cs.render_bdpt if integ == "bdpt" else cs.render)(cam, frame=f, max_depth=D)
         if integ == "bdpt":
             N = W * H

@@ -3,8 +3,12 @@
 
   * headline + config 4's scene: San-Miguel proxy (9,984,786 triangles) 1920x1080, PT, D = 2,
     frames 0 and 1 -- every radiance value BIT-EXACT (PathTracing.cl + intersect_bvh2_lds.cl);
+  * the exact call bench.py times: ONE mcrt_render_frames call of 20 TAA-jittered frames
+    (129 .. 148) on that scene -- frames 1, 7 and 19 of the batch bit-exact against the reference
+    run live with the same cameras, and the accumulators and image after the call bit-identical
+    to 20 x (mcrt_render_frame + mcrt_accumulate);
   * config 3: Sponza proxy (16 x 1024^2 mip-mapped textures) 1920x1080, PT -- bit-exact;
-  * config 4: San-Miguel proxy BDPT at 960x540, frames 0 and 1 in sequence from fresh buffers
+  * config 4: San-Miguel proxy BDPT at 1920x1080 (the bench's BDPT object), frames 0 and 1 in sequence from fresh buffers
     (BDPT.cl) -- vertex counts bit-exact, every defined field of the vertices of every 17th pixel
     bit-exact, radiance within 4e-6 relative (splat atomics, tests/test_gpu_bdpt.py) and
     bit-exact where no light-tracing splat landed;
@@ -19,7 +23,7 @@ import sys
 import numpy as np
 import pytest
 
-from clref_job import BDPT_VERTEX_STRIDE, SCALE_CASES, scale_scene
+from clref_job import BDPT_VERTEX_STRIDE, SCALE_CASES, TIMED_F0, TIMED_STEPS, scale_scene, taa_camera
 from mcrt import types as T
 from mcrt.camera import scene_camera
 from oracle import pyoracle as po
@@ -65,6 +69,8 @@ def test_full_size_config_matches_reference(hip_ctx, clref_scale, variant, case)
     ref = clref_scale[variant]
     sampler = T.SAMPLER_SOBOL if variant.startswith("sobol") else T.SAMPLER_RANDOM
     ds = device_scene(hip_ctx, name)
+    if integ == "pt_taa":
+        return timed_call_matches(hip_ctx, ds, ref, key, name, W, H, frames, D)
     fb = lib.FrameBuffer(hip_ctx, W, H)
     cam = scene_camera(name, W, H)
     bad = []
@@ -97,5 +103,45 @@ def test_full_size_config_matches_reference(hip_ctx, clref_scale, variant, case)
             ours = our_planes(fb.read_bdpt(which), depths, N)[:, :, sel]
             theirs = ref[f"{key}_{which}"].view(po.REF_VERTEX_DTYPE).reshape(len(sel), depths)
             bad += compare_vertices(ours, theirs, counts[sel], depths, len(sel), which)
+    fb.close()
+    assert not bad, (key, bad)
+
+
+def _exact(g, r):
+    return (g.view(np.uint32) == r.view(np.uint32)) | (np.isnan(g) & np.isnan(r))
+
+
+def timed_call_matches(ctx, ds, ref, key, name, W, H, frames, D):
+    """bench.py's timed region: one 20-frame mcrt_render_frames call (packed camera / shading
+    waves, tile-major order, XCD remap) + one mcrt_accumulate, against the reference frame by frame
+    and against 20 single frames + accumulates (tools: bench.py step / run)."""
+    from mcrt import lib
+    box = T.make_filter(T.BOX)
+    cams = [taa_camera(name, W, H, f) for f in range(TIMED_F0, TIMED_F0 + TIMED_STEPS)]
+    bad = []
+    fa = lib.FrameBuffer(ctx, W, H)
+    fa.render_frames(ds, cams, frame=TIMED_F0, max_depth=D)
+    fa.accumulate(box, 0)   # 0: the batch's first frame overwrites, the others add (bench.py step)
+    batched = {f: fa.read_frame(f - TIMED_F0) for f in frames}
+    acc_a, img_a = fa.read(1), fa.read(2)
+    fa.close()
+    for f in frames:
+        g, r = batched[f][..., :3], ref[f"{key}_f{f}"][..., :3]
+        assert r.max() > 0, (key, f, "empty reference frame")
+        ex = _exact(g, r)
+        if not ex.all():
+            bad.append(f"batch frame {f - TIMED_F0} (frame {f}) vs reference: {int((~ex.all(-1)).sum())} pixels differ")
+    fb = lib.FrameBuffer(ctx, W, H)
+    for k in range(TIMED_STEPS):
+        fb.render(ds, cams[k], frame=TIMED_F0 + k, max_depth=D)
+        if TIMED_F0 + k in batched:
+            ex = _exact(fb.read(0), batched[TIMED_F0 + k])
+            if not ex.all():
+                bad.append(f"frame {TIMED_F0 + k}: batched vs single radiance differ at {int((~ex.all(-1)).sum())} px")
+        fb.accumulate(box, 0 if k == 0 else TIMED_F0 + k)
+    for nm, a, b in (("weighted sum", acc_a, fb.read(1)), ("image", img_a, fb.read(2))):
+        ex = _exact(a, b)
+        if not ex.all():
+            bad.append(f"{nm} after the batched call differs from 20 single frames at {int((~ex.all(-1)).sum())} px")
     fb.close()
     assert not bad, (key, bad)
