@@ -36,26 +36,7 @@
 #include "mcrt_traverse.h"
 #include "mcrt_shading.h"
 
-#ifndef BDPT_BLOCK
 #define BDPT_BLOCK 256
-// Occupancy targets (waves per SIMD) of the two large BDPT kernels; 0 = the compiler's choice.
-#ifndef MCRT_CONNECT_WAVES
-#define MCRT_CONNECT_WAVES 0
-#endif
-#ifndef MCRT_VERTEX_WAVES
-#define MCRT_VERTEX_WAVES 0
-#endif
-#if MCRT_CONNECT_WAVES > 0
-#define MCRT_CONNECT_ATTR __attribute__((amdgpu_waves_per_eu(MCRT_CONNECT_WAVES, MCRT_CONNECT_WAVES)))
-#else
-#define MCRT_CONNECT_ATTR
-#endif
-#if MCRT_VERTEX_WAVES > 0
-#define MCRT_VERTEX_ATTR __attribute__((amdgpu_waves_per_eu(MCRT_VERTEX_WAVES, MCRT_VERTEX_WAVES)))
-#else
-#define MCRT_VERTEX_ATTR
-#endif
-#endif
 
 // RTBDPTVertexType / RTBDPTVertexFlag (kernel_data.h:202-218)
 enum { RT_BDPT_CAMERA_VERTEX = 0, RT_BDPT_LIGHT_VERTEX = 1, RT_BDPT_SURFACE_VERTEX = 2 };
@@ -498,7 +479,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
 }
 
 // GenerateSecondaryVertices (BDPT.cl:317-458) for every queued subpath ray at depth d.
-__global__ __launch_bounds__(BDPT_BLOCK) MCRT_VERTEX_ATTR void k_bdpt_vertex(SceneArgs s, FrameArgs f, BdptArgs b, int depth,
+__global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameArgs f, BdptArgs b, int depth,
                                                             BdptQueue qIn, const float4* __restrict__ hits,
                                                             BdptQueue qOut) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -616,7 +597,7 @@ MCRT_DEV void pushConn(const BdptQueue& q, int slot, f3 o, float tmax, f3 d, int
 // Per pixel, one thread walks the strategies in the reference's (t, s) order.  Own strategies
 // (t >= 2) get a slot, written here (zero when they need no connection or contribute nothing);
 // strategies with a non-zero weighted contribution that need visibility are queued.
-__global__ __launch_bounds__(BDPT_BLOCK) MCRT_CONNECT_ATTR void k_bdpt_connect(SceneArgs s, FrameArgs f, BdptArgs b,
+__global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameArgs f, BdptArgs b,
                                                              const mcrt_camera* __restrict__ camp, BdptQueue qOut) {
     const int lane = threadIdx.x & 63;
     const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;

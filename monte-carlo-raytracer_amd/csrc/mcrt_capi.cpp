@@ -48,10 +48,6 @@ struct mcrt_ctx_s {
     hipStream_t stream = nullptr;
     int numCUs = 256;
     bool profiling = false;
-    bool fuseShadowExtend = true;   // MCRT_NO_FUSE=1 launches k_shadow and k_extend separately (A/B)
-    bool sortRays = false;          // MCRT_SORT_RAYS=1: global sort of the extension queue (mcrt_raysort.hip)
-    bool shadowCompact = false;     // MCRT_SHADOW_COMPACT=1: bounce-0 shadow rays on the descent-compact records
-    int envFramesInFlight = 0;      // MCRT_FRAMES_IN_FLIGHT=n overrides the frame buffers' setting (A/B)
     int* dFlags = nullptr;          // device flags: [0] traversal-stack overflow (mcrt_traverse.h), set by any launch
     std::string error;
     struct Pending {
@@ -162,10 +158,6 @@ struct mcrt_framebuffer_s {
     float* wts = nullptr;
     float4* image = nullptr;
     float4* denoised = nullptr;  // RTDenoisePass output (persistent: the reference keeps its image)
-    float4 *sortO = nullptr, *sortD = nullptr, *sortT = nullptr;   // sorted extension queue (MCRT_SORT_RAYS)
-    void* sortScratch = nullptr;
-    size_t sortTemp = 0;
-    size_t sortCap = 0;          // entries of the sort buffers (= the slot's queueCap when allocated)
     float4* display = nullptr;   // post-processed image (mcrt_postprocess)
     float4* hitsP = nullptr;     // primary hits by pixel
     float4* hitsE = nullptr;     // extension hits by queue slot
@@ -353,10 +345,6 @@ MCRT_API mcrt_status mcrt_ctx_create(int device, mcrt_ctx* out) {
     if (hipSetDevice(device) != hipSuccess) { delete c; return fail(nullptr, MCRT_ERROR_DEVICE, "hipSetDevice failed"); }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->numCUs = prop.multiProcessorCount;
-    if (const char* nf = std::getenv("MCRT_NO_FUSE")) c->fuseShadowExtend = nf[0] != '1';
-    if (const char* sr = std::getenv("MCRT_SORT_RAYS")) c->sortRays = sr[0] == '1';
-    if (const char* sc = std::getenv("MCRT_SHADOW_COMPACT")) c->shadowCompact = sc[0] == '1';
-    if (const char* fi = std::getenv("MCRT_FRAMES_IN_FLIGHT")) c->envFramesInFlight = std::atoi(fi);
     if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(nullptr, MCRT_ERROR_DEVICE, "hipStreamCreate failed");
@@ -1046,8 +1034,7 @@ static void slot_free(FrameSlot& k) {
 
 static void fb_free(mcrt_framebuffer fb) {
     for (auto& k : fb->slot) slot_free(k);
-    void* ptrs[] = {fb->wsum, fb->wts, fb->image, fb->denoised, fb->display, fb->sortO, fb->sortD, fb->sortT,
-                    fb->sortScratch};
+    void* ptrs[] = {fb->wsum, fb->wts, fb->image, fb->denoised, fb->display};
     for (void* p : ptrs)
         if (p) hipFree(p);
     fb_free_bdpt(fb);
@@ -1228,23 +1215,12 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
     f.rrStartDepth = p->rr_start_depth;
     f.textureLod = p->texture_lod ? 1 : 0;
     // batched frames: workgroups of the camera / first-bounce launches walk (tile, frame) with the
-    // frames of a tile adjacent, so one XCD traces a tile's batch of jittered frames back to back
-    // (MCRT_TILE_MAJOR=0: frame-major order, the A/B baseline); the order changes no result
-    static const int tileMajor = [] {
-        const char* e = std::getenv("MCRT_TILE_MAJOR");
-        return e ? std::atoi(e) : 1;
-    }();
-    f.tileMajor = tileMajor;
-    static const int primaryPack = [] {   // MCRT_PRIMARY_PACK=0: one frame's 8x8 tile per wave
-        const char* e = std::getenv("MCRT_PRIMARY_PACK");
-        return e ? std::atoi(e) : 1;
-    }();
-    f.primaryPack = primaryPack;
-    static const int shadePack = [] {   // MCRT_SHADE_PACK=0: one frame's pixels per shading wave
-        const char* e = std::getenv("MCRT_SHADE_PACK");
-        return e ? std::atoi(e) : 1;
-    }();
-    f.shadePack = shadePack;
+    // frames of a tile adjacent, so one XCD traces a tile's batch of jittered frames back to back,
+    // and a camera / first-shading wave holds 64 consecutive (pixel, frame) paths of one tile
+    // (profiles/r02/ab/README.txt items 11, 14, 15); the order changes no result
+    f.tileMajor = 1;
+    f.primaryPack = 1;
+    f.shadePack = 1;
     f.batch = 1;
     f.numBands = p->num_bands <= 0 ? 1 : p->num_bands;
     f.bandIndex = p->band_index;
@@ -1263,16 +1239,14 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
     return true;
 }
 
-// Frames in flight for a render: the frame buffer's setting (or the MCRT_FRAMES_IN_FLIGHT
-// override); auto = 2.  Each launch of a frame ends in a divergent tail of long rays that the next
+// Frames in flight for a render: the frame buffer's setting; auto = 2.  Each launch of a frame ends in a divergent tail of long rays that the next
 // frame's launches fill (San-Miguel proxy 1080p: 2.33 -> 1.91 ms/frame with 2 slots, 2.06 with 4;
 // tools/scale_emulate.py).  Small per-rank band shares are widened by batching frames
 // (mcrt_render_frames) rather than by more slots: 4 slots of 1/8-image frames reach 0.49 ms per
 // frame at N = 8, 2 slots of 16-frame batches 0.25.
 static int frames_in_flight(mcrt_framebuffer fb, const FrameArgs& f) {
-    int n = fb->ctx->envFramesInFlight > 0 ? fb->ctx->envFramesInFlight : fb->framesInFlight;
+    int n = fb->framesInFlight;
     if (n <= 0) n = 2;
-    if (fb->ctx->sortRays) n = 1;   // one set of sort buffers
     return std::max(1, std::min(n, MCRT_MAX_FRAMES_IN_FLIGHT));
 }
 
@@ -1491,51 +1465,15 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
             Timed t(ctx, K_SHADE0, nullptr, (int64_t)bandPaths, st);
             mcrt::launch_shade0(sa, f, dCam, fb->hitsP, fb->radiance, q, st);
         } else {
-            if (!ctx->fuseShadowExtend) {
-                Timed t(ctx, K_EXTEND, extCnt + b - 1, 0, st);
-                mcrt::launch_extend(tcs, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1], fb->hitsE,
-                                    qCap, st);
-            }
             Timed t(ctx, K_SHADEN, extCnt + b - 1, 0, st);
             mcrt::launch_shadeN(sa, f, b, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1],
                                 fb->eT[(b - 1) & 1], fb->hitsE, fb->radiance, q, qCap, st);
         }
-        if (ctx->sortRays && b + 1 < p->max_depth) {   // reorder the extension queue of bounce b
-            // the queue holds up to the batch's paths (slot.queueCap >= count x band paths): the
-            // sort buffers, which are swapped into the slot's queue, must have the same capacity
-            if (fb->sortCap < slot.queueCap) {
-                HIPCHK(ctx, hipStreamSynchronize(st));
-                void* old[] = {fb->sortO, fb->sortD, fb->sortT, fb->sortScratch};
-                for (void* q : old)
-                    if (q) hipFree(q);
-                fb->sortO = fb->sortD = fb->sortT = nullptr;
-                fb->sortScratch = nullptr;
-                fb->sortCap = 0;
-                const size_t cap = slot.queueCap;
-                fb->sortTemp = mcrt::ray_sort_temp_bytes((int)cap);
-                HIPCHK(ctx, hipMalloc(&fb->sortO, 16 * cap));
-                HIPCHK(ctx, hipMalloc(&fb->sortD, 16 * cap));
-                HIPCHK(ctx, hipMalloc(&fb->sortT, 16 * cap));
-                HIPCHK(ctx, hipMalloc(&fb->sortScratch, 16 * cap + fb->sortTemp));
-                fb->sortCap = cap;
-            }
-            const float3 lo = make_float3(s->bbLo[0], s->bbLo[1], s->bbLo[2]);
-            const float3 hi = make_float3(s->bbHi[0], s->bbHi[1], s->bbHi[2]);
-            HIPCHK(ctx, mcrt::sort_ray_queue(extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->eT[b & 1], fb->sortO,
-                                             fb->sortD, fb->sortT, (int)slot.queueCap, lo, hi, fb->sortScratch,
-                                             fb->sortTemp, st));
-            std::swap(slot.eO[b & 1], fb->sortO);
-            std::swap(slot.eD[b & 1], fb->sortD);
-            std::swap(slot.eT[b & 1], fb->sortT);
-            fb_bind(fb, ks);
-        }
-        if (ctx->fuseShadowExtend && b + 1 < p->max_depth) {
-            // shadow rays of bounce b + extension rays for bounce b+1 (both from this shading pass)
+        if (b + 1 < p->max_depth) {
+            // shadow rays of bounce b + extension rays for bounce b+1 (both from this shading pass) in
+            // one launch: separate k_extend + k_shadow launches cost 0.18 ms more per frame (r01)
             Timed t(ctx, K_SHADOW_EXTEND, extCnt + b, 0, st, shadowCnt + b);   // items: extension + shadow rays
-            // bounce 0's shadow rays come out of the packed first shading launch coherent: compact records
-            TraceCtx tss = (b == 0 && ctx->shadowCompact) ? compact_ctx(s) : tcs;
-            tss.spill = slot.spill;
-            mcrt::launch_shadow_extend(tcs, tss, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
+            mcrt::launch_shadow_extend(tcs, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
                                        fb->sO, fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
             Timed t(ctx, K_SHADOW, shadowCnt + b, 0, st);

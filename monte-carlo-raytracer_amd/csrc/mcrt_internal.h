@@ -94,9 +94,9 @@ void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const 
                    hipStream_t st);
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st);
-void launch_shadow_extend(const TraceCtx& c, const TraceCtx& cs, const int* extCount, const float4* qO,
-                          const float4* qD, float4* hits, const int* shadowCount, const float4* sO, const float4* sD,
-                          const float4* sL, float4* radiance, int maxExt, int maxShadow, hipStream_t st);
+void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
+                          const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
+                          float4* radiance, int maxExt, int maxShadow, hipStream_t st);
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st);
 void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,
@@ -147,13 +147,6 @@ struct HostRcp {
     bool ok = false;
 };
 const HostRcp& host_rcp_table();
-}
-// Optional extension-queue sort (mcrt_raysort.hip)
-namespace mcrt {
-size_t ray_sort_temp_bytes(int maxCount);
-hipError_t sort_ray_queue(const int* count, const float4* o, const float4* d, const float4* t, float4* o2, float4* d2,
-                          float4* t2, int maxCount, float3 sceneLo, float3 sceneHi, void* scratch, size_t tempBytes,
-                          hipStream_t st);
 }
 // Host BVH builder (mcrt_bvh.cpp)
 namespace mcrt {

@@ -19,27 +19,8 @@
 #include "mcrt_traverse.h"
 #include "mcrt_shading.h"
 
-// Occupancy experiments: extra LDS bytes per traversal workgroup (0 = none).
-#ifndef MCRT_LDS_PAD
-#define MCRT_LDS_PAD 0
-#endif
 // Shading workgroup size (threads; one queue atomic per workgroup and queue).
-#ifndef SHADE_BLOCK
 #define SHADE_BLOCK 256
-#endif
-// Group the extension queue by ray-direction octant within each shading block (1 = on).
-#ifndef MCRT_SORT_OCTANT
-#define MCRT_SORT_OCTANT 1
-#endif
-// Occupancy target of the shading kernels (waves per SIMD); 0 = compiler's choice.
-#ifndef MCRT_SHADE_WAVES
-#define MCRT_SHADE_WAVES 0
-#endif
-#if MCRT_SHADE_WAVES > 0
-#define MCRT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(MCRT_SHADE_WAVES, MCRT_SHADE_WAVES)))
-#else
-#define MCRT_SHADE_ATTR
-#endif
 
 // ---------------------------------------------------------------------------
 // RadeonRays-compatible queries on AoS rays (mcrt_trace_closest / mcrt_trace_any).
@@ -50,7 +31,7 @@
 template <bool ANY, int LAY>
 __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* __restrict__ rays, int n,
                                                    mcrt_intersection* __restrict__ hits, int* __restrict__ occl) {
-    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
+    __shared__ uint32_t lds[STACK_LDS * 64];
     const int lane = threadIdx.x;
     const int i = blockIdx.x * 64 + lane;
     if (i >= n) return;
@@ -127,7 +108,7 @@ MCRT_DEV void packedPath(const FrameArgs& f, int tileAll, int lane, int& k, int&
 template <int LAY>
 __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 float4* __restrict__ hitOut) {
-    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
+    __shared__ uint32_t lds[STACK_LDS * 64];
     const int lane = threadIdx.x;
     const int tileAll = xcdRemap(blockIdx.x, gridDim.x);
     int k, tile, pi = lane;
@@ -156,7 +137,7 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
 template <int LAY>
 __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ qO,
                                                const float4* __restrict__ qD, float4* __restrict__ hitOut) {
-    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
+    __shared__ uint32_t lds[STACK_LDS * 64];
     const int n = *count;
     if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
@@ -179,7 +160,7 @@ template <int LAY>
 __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ sO,
                                                const float4* __restrict__ sD, const float4* __restrict__ sL,
                                                float4* __restrict__ radiance) {
-    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
+    __shared__ uint32_t lds[STACK_LDS * 64];
     const int n = *count;
     if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
@@ -204,16 +185,13 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
 // Shadow rays of bounce b and extension rays of bounce b+1 in ONE launch: both only depend on
 // the shading of bounce b.  Extension workgroups come first (their rays are the longer ones),
 // shadow workgroups fill the extension launch's divergent tail instead of waiting for it.
-// SLAY: the shadow rays' record layout (cs).  The bounce-0 shadow rays leave the packed first
-// shading launch coherent (a wave's rays share the light sample's direction and nearly one origin),
-// so they take the descent-compact records like the camera rays; the extension rays keep LAY.
-template <int LAY, int SLAY>
-__global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, TraceCtx cs, const int* __restrict__ extCount,
+template <int LAY>
+__global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __restrict__ extCount,
                                                       const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                       float4* __restrict__ hitOut, const int* __restrict__ shadowCount,
                                                       const float4* __restrict__ sO, const float4* __restrict__ sD,
                                                       const float4* __restrict__ sL, float4* __restrict__ radiance) {
-    __shared__ uint32_t lds[STACK_LDS * 64 + MCRT_LDS_PAD / 4];
+    __shared__ uint32_t lds[STACK_LDS * 64];
     const int ne = *extCount;
     const int eb = (ne + 63) >> 6;
     const int lane = threadIdx.x;
@@ -241,7 +219,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, TraceCtx cs, c
         r.d = ld3(d);
         r.tmax = o.w;
         r.mask = -1;
-        const float V = traceAny<SLAY>(cs, r, lds + lane, raySpill(cs, blockIdx.x, lane)) ? 0.0f : 1.0f;
+        const float V = traceAny<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane)) ? 0.0f : 1.0f;
         const int pix = __float_as_int(d.w);
         float4 acc = radiance[pix];
         acc.x += L.x * V;
@@ -365,7 +343,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
 
 // Bounce 0: every pixel of the band (tile order); writes radiance[pix] (= `=` of ShadowPass).
 template <bool LOD>
-__global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArgs s, FrameArgs f, const mcrt_camera* __restrict__ camp,
+__global__ __launch_bounds__(SHADE_BLOCK) void k_shade0(SceneArgs s, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 const float4* __restrict__ hits, float4* __restrict__ radiance,
                                                 QueueArgs q) {
     const int lane = threadIdx.x & 63;
@@ -381,9 +359,7 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
     int x = 0, y = 0;
     bool valid = k < f.batch && tile < f.numTiles && tilePixel(f, tile, pi, x, y);
     __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
-#if MCRT_SORT_OCTANT
     __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];
-#endif
     ShadeOut o;
     o.pushS = o.pushE = false;
     o.eD = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -398,27 +374,21 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shade0(SceneArg
     }
     const int ss = blockAppend<SHADE_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
-#if MCRT_SORT_OCTANT
     // extension rays grouped by direction octant inside the block's queue slice
     const int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
     const int es = blockAppendGrouped<SHADE_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
-#else
-    const int es = blockAppend<SHADE_BLOCK / 64>(q.extCountOut, o.pushE, ldsWave);
-#endif
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 
 // Bounce >= 1: the compacted extension queue of the previous bounce.
-__global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
+__global__ __launch_bounds__(SHADE_BLOCK) void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
                                                 const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                 const float4* __restrict__ qT, const float4* __restrict__ hits,
                                                 float4* __restrict__ radiance, QueueArgs q) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = *countIn;
     __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
-#if MCRT_SORT_OCTANT
     __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];
-#endif
     if ((int)blockIdx.x * SHADE_BLOCK >= n) return;   // whole block past the queue: uniform exit
     ShadeOut o;
     o.pushS = o.pushE = false;
@@ -435,13 +405,9 @@ __global__ __launch_bounds__(SHADE_BLOCK) MCRT_SHADE_ATTR void k_shadeN(SceneArg
     }
     const int ss = blockAppend<SHADE_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
-#if MCRT_SORT_OCTANT
     // extension rays grouped by direction octant inside the block's queue slice
     const int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
     const int es = blockAppendGrouped<SHADE_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
-#else
-    const int es = blockAppend<SHADE_BLOCK / 64>(q.extCountOut, o.pushE, ldsWave);
-#endif
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 
@@ -784,18 +750,14 @@ void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const 
     hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_COMPACT>, k_shadow<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, sO, sD, sL, radiance);
 }
-void launch_shadow_extend(const TraceCtx& c, const TraceCtx& cs, const int* extCount, const float4* qO,
-                          const float4* qD, float4* hits, const int* shadowCount, const float4* sO, const float4* sD,
-                          const float4* sL, float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
+void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
+                          const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
+                          float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
     const int blocks = (maxExt + 63) / 64 + (maxShadow + 63) / 64;
-    // shadow rays on compact records only beside plain extension records (the two flat layouts)
-    const bool sc = !c.twoLevel && !c.compact && cs.compact;
-    auto k = c.twoLevel ? k_shadow_extend<LAY_TWO_LEVEL, LAY_TWO_LEVEL>
-             : c.compact ? k_shadow_extend<LAY_COMPACT, LAY_COMPACT>
-             : sc        ? k_shadow_extend<LAY_PLAIN, LAY_COMPACT>
-                         : k_shadow_extend<LAY_PLAIN, LAY_PLAIN>;
-    hipLaunchKernelGGL(k, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, sc ? cs : c, extCount, qO, qD, hits,
-                       shadowCount, sO, sD, sL, radiance);
+    hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_COMPACT>,
+                                  k_shadow_extend<LAY_PLAIN>),
+                       dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, extCount, qO, qD, hits, shadowCount, sO, sD,
+                       sL, radiance);
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {

@@ -60,18 +60,6 @@ MCRT_DEV float triHit(const TraceRay& r, float4 A, float4 E1, float4 E2, float t
 // the plane: the same floats, 12 fewer VALU instructions per internal node.  Camera tiles,
 // octant-grouped extension queues and directional-light shadow rays are mostly uniform; mixed
 // waves take the generic loop.
-#ifndef MCRT_OCT_TRAV
-#define MCRT_OCT_TRAV 1
-#endif
-// Wave-uniform compact-record fetches through the scalar cache (1 = on; A/B, tools/r2_gpu45.sh).
-#ifndef MCRT_UNIFORM_SLOAD
-#define MCRT_UNIFORM_SLOAD 0
-#endif
-// Packed slab tests (v_pk_fma_f32, two box planes per instruction) in the octant loops (1 = on).
-#ifndef MCRT_PK_SLAB
-#define MCRT_PK_SLAB 0
-#endif
-
 // Closest (ANY = false) or any (ANY = true) hit over the unified node array (mcrt_bvh.cpp):
 // the RadeonRays intersect_bvh2_lds.cl:107-178 loop -- one uniform 64-B fetch per step, an
 // internal node tests both child boxes (nearer child first, far child to the stack), a leaf
@@ -102,23 +90,7 @@ MCRT_DEV int traverseOct(const float4* __restrict__ nodes, const TraceRay& r, f3
         if (n3.x >= 0) {
             // slab tests of both children (RR intersect_bvh2_lds.cl:54-63, mad -> fma)
             float a0, a1, b0, b1;
-            if constexpr (OCT >= 0 && MCRT_PK_SLAB) {
-                // the same 12 fmas as below, two per v_pk_fma_f32 (bit-identical: each lane of a
-                // packed fma is an IEEE fma)
-                constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
-                const f2 invxy = f2{inv.x, inv.y}, oxixy = f2{oxi.x, oxi.y};
-                const f2 invzz = f2{inv.z, inv.z}, oxizz = f2{oxi.z, oxi.z};
-                const f2 an = __builtin_elementwise_fma(f2{SX ? n0.y : n0.x, SY ? n0.w : n0.z}, invxy, oxixy);
-                const f2 af = __builtin_elementwise_fma(f2{SX ? n0.x : n0.y, SY ? n0.z : n0.w}, invxy, oxixy);
-                const f2 bn = __builtin_elementwise_fma(f2{SX ? n1.y : n1.x, SY ? n1.w : n1.z}, invxy, oxixy);
-                const f2 bf = __builtin_elementwise_fma(f2{SX ? n1.x : n1.y, SY ? n1.z : n1.w}, invxy, oxixy);
-                const f2 zn = __builtin_elementwise_fma(f2{SZ ? n2.y : n2.x, SZ ? n2.w : n2.z}, invzz, oxizz);
-                const f2 zf = __builtin_elementwise_fma(f2{SZ ? n2.x : n2.y, SZ ? n2.z : n2.w}, invzz, oxizz);
-                a0 = fmaxf(fmaxf(an.x, an.y), fmaxf(zn.x, 0.0f));
-                a1 = fminf(fminf(af.x, af.y), fminf(zf.x, t));
-                b0 = fmaxf(fmaxf(bn.x, bn.y), fmaxf(zn.y, 0.0f));
-                b1 = fminf(fminf(bf.x, bf.y), fminf(zf.y, t));
-            } else if constexpr (OCT >= 0) {
+            if constexpr (OCT >= 0) {
                 constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
                 const float axn = fmaf(SX ? n0.y : n0.x, inv.x, oxi.x), axf = fmaf(SX ? n0.x : n0.y, inv.x, oxi.x);
                 const float ayn = fmaf(SY ? n0.w : n0.z, inv.y, oxi.y), ayf = fmaf(SY ? n0.z : n0.w, inv.y, oxi.y);
@@ -232,27 +204,10 @@ MCRT_DEV int traverseOct2(const float4* __restrict__ nodes, uint32_t rootWord, c
         const bool leaf = (word & CW_LEAF) != 0;
         const float4* q = nodes + 4 * (size_t)idx;
         float4 q0, q1, q2 = make_float4(0.f, 0.f, 0.f, 0.f), q3 = q2;
-#if MCRT_UNIFORM_SLOAD
-        // packed camera waves: when every active lane is at the same node, fetch the record once
-        // through the scalar cache (one s_load_dwordx16) instead of 64 lanes' vector loads
-        const uint32_t w0 = __builtin_amdgcn_readfirstlane(word);
-        if (__builtin_amdgcn_ballot_w64(word != w0) == 0) {
-            typedef float v4 __attribute__((ext_vector_type(4)));
-            typedef const __attribute__((address_space(4))) v4* cptr;
-            const cptr cq = (cptr)(uintptr_t)(nodes + 4 * (size_t)(w0 & CW_IDX));
-            const v4 a0 = cq[0], a1 = cq[1], a2 = cq[2], a3 = cq[3];
-            q0 = make_float4(a0.x, a0.y, a0.z, a0.w);
-            q1 = make_float4(a1.x, a1.y, a1.z, a1.w);
-            q2 = make_float4(a2.x, a2.y, a2.z, a2.w);
-            q3 = make_float4(a3.x, a3.y, a3.z, a3.w);
-        } else
-#endif
-        {
-            q0 = q[0];
-            q1 = q[1];
-            if (leaf || popped) q2 = q[2];
-            if (popped && !leaf) q3 = q[3];
-        }
+        q0 = q[0];
+        q1 = q[1];
+        if (leaf || popped) q2 = q[2];
+        if (popped && !leaf) q3 = q[3];
         bool pop = true;
         uint32_t next = CW_DONE;
         if (!leaf) {
@@ -351,7 +306,6 @@ MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint3
         else                                                                                                      \
             return traverseOct<ANY, OCT>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit);             \
     } while (0)
-#if MCRT_OCT_TRAV
     const int oct = (int)(__float_as_uint(inv.x) >> 31) | (int)((__float_as_uint(inv.y) >> 31) << 1) |
                     (int)((__float_as_uint(inv.z) >> 31) << 2);
     const int oct0 = __builtin_amdgcn_readfirstlane(oct);
@@ -368,7 +322,6 @@ MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint3
             default: break;
         }
     }
-#endif
     MCRT_TRAV_CALL(-1);
 #undef MCRT_TRAV_CALL
 }
@@ -573,9 +526,7 @@ MCRT_DEV bool traceAny(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint
 // are dealt to the XCDs in turn (XCD k gets runs k, k+8, ...), which keeps the per-XCD load
 // balanced across the image; the tail of < 8*SEG blocks is split in 8 contiguous parts.
 // A bijection on [0, S); SEG = 0 is the identity.
-#ifndef MCRT_XCD_SEG
 #define MCRT_XCD_SEG 128
-#endif
 MCRT_DEV int xcdRemap(int rel, int S) {
     if (MCRT_XCD_SEG <= 0) return rel;
     constexpr int R = 8 * MCRT_XCD_SEG;

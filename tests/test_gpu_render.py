@@ -256,35 +256,6 @@ def test_batched_frames_bit_exact(hip_ctx, mixed, num_bands, band_index, count):
     ds.close()
 
 
-def test_sorted_rays_batched_frames_bit_exact(hip_ctx, mixed, monkeypatch):
-    """MCRT_SORT_RAYS=1 (global sort of each extension queue) with batched frames: the sort
-    buffers cover the batch's queue (count x N paths), and reordering the queue changes nothing
-    (each path only touches its own pixel, in launch order), so the accumulators and the
-    first-frame radiance equal the unsorted render bit for bit."""
-    from mcrt import lib
-    sc, _ = mixed
-    W, H, D, count = 96, 72, 3, 4
-    cams = [scene_camera("mixed", W, H, frame=f, jitter=True) for f in range(2 * count)]
-    filt = T.make_filter(T.BOX)
-    monkeypatch.setenv("MCRT_SORT_RAYS", "1")
-    sctx = lib.Context(0)
-    monkeypatch.delenv("MCRT_SORT_RAYS")
-    out = []
-    for ctx in (hip_ctx, sctx):
-        ds = lib.DeviceScene(ctx, sc)
-        fb = lib.FrameBuffer(ctx, W, H)
-        for f0 in (0, count):
-            fb.render_frames(ds, cams[f0:f0 + count], frame=f0, max_depth=D)
-            fb.accumulate(filt, f0)
-        out.append((fb.read(0), fb.read(1), fb.read(2), fb.stats()))
-        fb.close()
-        ds.close()
-    for k in range(3):
-        np.testing.assert_array_equal(out[1][k].view(np.uint32), out[0][k].view(np.uint32))
-    assert out[1][3] == out[0][3]
-    sctx.close()
-
-
 def test_batched_no_lights_after_lit_batch(hip_ctx, mixed):
     """A batch rendered after the lights are removed accumulates zeros for EVERY frame of the
     batch (not stale radiance of the slot's previous batch), exactly as single frames do."""
