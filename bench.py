@@ -356,9 +356,6 @@ def main():
     ap.add_argument("--device-build", action="store_true", help="on-device linear BVH instead of the RR-identical tree")
     ap.add_argument("--host-build", action="store_true",
                     help="build the RR-identical tree on the host (mcrt_bvh.cpp) instead of the device (mcrt_sahbuild.hip)")
-    ap.add_argument("--tree", default="bvh2", choices=["bvh2", "wide"],
-                    help="traversal tree: the RadeonRays Bvh2 (bit-exact parity) or the 4-wide quantized tree "
-                         "collapsed from it (mcrt_wide.h; any-hit identical, closest hit up to equal-t ties)")
     ap.add_argument("--force-flat", action="store_true",
                     help="flat BVH even for instanced scenes (RR bvh.forceflat); default: RR's auto selection")
     ap.add_argument("--russian-roulette", action="store_true",
@@ -419,9 +416,7 @@ def main():
     ctx = lib.Context(local)
     t0 = time.perf_counter()
     ds = lib.DeviceScene(ctx, scene, device_build=1 if args.device_build else 3 if args.host_build else 2,
-                         force_flat=args.force_flat, tree=T.TREE_WIDE if args.tree == "wide" else T.TREE_BVH2)
-    if args.tree == "wide" and ds.tree() != T.TREE_WIDE:
-        raise SystemExit(f"--tree wide requested but not built: {lib.lib().mcrt_last_error(ctx.h).decode()}")
+                         force_flat=args.force_flat)
     info = ds.info()
     two_level = ds.layout()["two_level"] == 1
     log(f"[bench] upload+BVH {time.perf_counter() - t0:.1f}s (build {info['build_ms'] / 1e3:.1f}s, "

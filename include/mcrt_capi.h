@@ -211,15 +211,7 @@ typedef struct {
      * the reference passes Transform::getWorldToLocalMatrix).  NULL: the transpose of each
      * shape's toWorldInverseTranspose.  Used by the two-level structure only. */
     const mcrt_mat4* world_to_local;
-    /* Which tree the traversal kernels walk (flat structures).  0 (default): the Bvh2 above --
-     * every result bit-identical to the reference.  1: a 4-wide tree collapsed from it on the
-     * device (mcrt_wide.h: four 8-bit-quantized child boxes per 64-B record, ~0.58x the node
-     * fetches per ray); any-hit answers equal the Bvh2's, a closest hit may pick another triangle
-     * only where two lie at (nearly) the same distance.  The Bvh2 stays built underneath. */
-    int32_t traversal_tree;
 } mcrt_accel_opts;
-#define MCRT_TREE_BVH2 0
-#define MCRT_TREE_WIDE 1
 
 #define MCRT_SAMPLER_SOBOL  0   /* KRN/samplers.cl:16 */
 #define MCRT_SAMPLER_RANDOM 1   /* KRN/samplers.cl:17 (reference default) */
@@ -349,20 +341,6 @@ MCRT_API mcrt_status mcrt_accel_builder(mcrt_scene scene, int32_t* builder);
 MCRT_API mcrt_status mcrt_accel_build_host_records(const mcrt_scene_desc* desc, const mcrt_accel_opts* opts,
                                                    float* out_records, uint64_t max_records,
                                                    uint64_t* num_records, int32_t* info);
-/* The tree the traversal walks after mcrt_accel_build: MCRT_TREE_BVH2 or MCRT_TREE_WIDE (a wide
- * request on a two-level scene, or a wide build that failed, keeps the Bvh2; the reason is in
- * mcrt_last_error's text after the build). */
-MCRT_API mcrt_status mcrt_accel_tree(mcrt_scene scene, int32_t* tree);
-/* Copies of the device's wide tree (mcrt_wide.h): node records (16 uint32 each) and triangle
- * records (16 floats each); either pointer may be NULL to query the counts. */
-MCRT_API mcrt_status mcrt_accel_read_wide(mcrt_scene scene, uint32_t* nodes, uint64_t max_nodes, float* tris,
-                                          uint64_t max_tris, uint64_t* num_nodes, uint64_t* num_tris);
-/* Host-only build of the wide tree (the restatement mcrt_wide.cpp, from the host Bvh2 of
- * mcrt_accel_build_host_records), for tests and tools: the records mcrt_accel_read_wide returns
- * after a device build of the same scene. */
-MCRT_API mcrt_status mcrt_accel_build_host_wide(const mcrt_scene_desc* desc, const mcrt_accel_opts* opts,
-                                                uint32_t* nodes, uint64_t max_nodes, float* tris, uint64_t max_tris,
-                                                uint64_t* num_nodes, uint64_t* num_tris);
 
 /* ------------------------------------------------------------------------ */
 /* Ray queries on DEVICE buffers (IntersectionApi::QueryIntersection /

@@ -883,7 +883,7 @@ void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
 }
 void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st) {
     const int blocks = (maxCount + 63) / 64 > 0 ? (maxCount + 63) / 64 : 1;
-    hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_WIDE>, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_COMPACT>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks), dim3(64), 0, st, c, b, q.count,
+    hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_COMPACT>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks), dim3(64), 0, st, c, b, q.count,
                        q.o, q.d, q.t);
 }
 void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, hipStream_t st) {

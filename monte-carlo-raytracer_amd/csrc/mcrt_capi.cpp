@@ -24,7 +24,6 @@
 #include <vector>
 
 #include "mcrt_internal.h"
-#include "mcrt_wide.h"
 
 namespace {
 
@@ -98,13 +97,6 @@ struct mcrt_scene_s {
     int builder = 0;   // which builder made the flat structure: 0 host, 1 device LBVH, 2 device SAH
     int bvhDepth = 0;
     bool twoLevel = false;          // instanced scene: two-level records (mcrt_bvh2l.cpp)
-    // 4-wide quantized tree (mcrt_wide.h), built on the device from the Bvh2 when requested
-    bool wideRequested = false, wide = false, wideRootLeaf = false;
-    void* dWideNodes = nullptr;
-    void* dWideTris = nullptr;
-    uint32_t wideNodes = 0, wideTris = 0;
-    int wideDepth = 0;
-    std::string wideNote;           // why a requested wide tree is not in use
     int numMeshes = 0, numInstances = 0;
     // traversal scratch
     uint32_t* dSpill = nullptr;
@@ -304,10 +296,6 @@ static TraceCtx trace_ctx(mcrt_scene s) {
     c.spillCap = s->spillCap;
     c.overflow = s->ctx->dFlags;
     c.twoLevel = s->twoLevel ? 1 : 0;
-    c.wide = s->wide ? 1 : 0;
-    c.wnodes = (const uint4*)s->dWideNodes;
-    c.wtris = (const float4*)s->dWideTris;
-    c.wroot = s->wideRootLeaf ? WIDE_LEAF_BIT : 0u;
     return c;
 }
 
@@ -510,7 +498,7 @@ MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx) {
 static void scene_free_device(mcrt_scene s) {
     void** ptrs[] = {&s->dShapes, &s->dIndices, &s->dPositions, &s->dUvs, &s->dNormals, &s->dTextures,
                      &s->dTexData, &s->dSobol, &s->dLights, &s->dMaterials, &s->dNodes, &s->dTris,
-                     &s->dNodesC, &s->dSurf, &s->dSurfBase, &s->dSurfMeshes, &s->dWideNodes, &s->dWideTris};
+                     &s->dNodesC, &s->dSurf, &s->dSurfBase, &s->dSurfMeshes};
     for (void** p : ptrs) {
         if (*p) hipFree(*p);
         *p = nullptr;
@@ -703,9 +691,6 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     // (CalcIntersectionDevice::Preprocess, RR/src/device/calc_intersection_device.cpp:68-105)
     const bool use2 = (opts && opts->force_2level) ||
                       (!(opts && opts->force_flat) && mcrt::shapes_are_instanced(s->shapes.data(), s->shapes.size()));
-    if (opts && (opts->traversal_tree < 0 || opts->traversal_tree > MCRT_TREE_WIDE))
-        return fail(ctx, MCRT_ERROR_INVALID_ARG, "unknown traversal_tree");
-    s->wideRequested = false;
     if (use2) {
         int threads = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
         mcrt::Bvh2lOut b2;
@@ -730,7 +715,6 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     }
     s->twoLevel = false;
     s->numMeshes = s->numInstances = 0;
-    s->wideRequested = opts && opts->traversal_tree == MCRT_TREE_WIDE;
     const int buildMode = opts ? opts->device_build : 0;
     if (buildMode == 0 || buildMode == 2) {   // on-device SAH, node-identical to the host build
         hipSetDevice(ctx->device);
@@ -850,38 +834,7 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
     }
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
-    // the 4-wide tree (perf mode): collapsed on the device from the Bvh2 just built
-    if (s->dWideNodes) hipFree(s->dWideNodes);
-    if (s->dWideTris) hipFree(s->dWideTris);
-    s->dWideNodes = s->dWideTris = nullptr;
-    s->wide = s->wideRootLeaf = false;
-    s->wideNodes = s->wideTris = 0;
-    s->wideDepth = 0;
-    s->wideNote.clear();
-    if (s->wideRequested && !s->twoLevel) {
-        mcrt::WideDevice w;
-        const char* why = nullptr;
-        const hipError_t e = mcrt::gpu_build_wide((const float4*)s->dNodes, s->numNodes, (const mcrt_shape*)s->dShapes,
-                                                  (uint32_t)s->shapes.size(), (const uint32_t*)s->dIndices,
-                                                  (const float4*)s->dPositions, ctx->stream, w, &why);
-        if (e == hipSuccess) {
-            s->dWideNodes = w.nodes;
-            s->dWideTris = w.tris;
-            s->wideNodes = w.numNodes;
-            s->wideTris = w.numTris;
-            s->wideDepth = w.depth;
-            s->wideRootLeaf = w.rootIsLeaf;
-            s->wide = true;
-        } else {
-            (void)hipGetLastError();
-            s->wideNote = std::string("wide tree not built: ") + (why ? why : hipGetErrorString(e));
-            if (e != hipErrorInvalidValue && e != hipErrorOutOfMemory) return fail(ctx, MCRT_ERROR_DEVICE, s->wideNote);
-        }
-    } else if (s->wideRequested) {
-        s->wideNote = "wide tree not built: two-level (instanced) structure";
-    }
     int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries
-    if (s->wide) needCap = std::max(needCap, ((3 * s->wideDepth + 2 + 15) / 16) * 16);   // <= 3 pushes per level
     // test hook: MCRT_TEST_SPILL_CAP=k caps the spill columns at k entries (0 = LDS stack only) so a
     // test can drive a traversal past its capacity and check that the overflow is reported
     if (const char* tc = std::getenv("MCRT_TEST_SPILL_CAP")) needCap = std::max(0, std::atoi(tc) / 16 * 16);
@@ -920,8 +873,7 @@ MCRT_API mcrt_status mcrt_accel_info(mcrt_scene s, uint64_t* num_nodes, uint64_t
                                      uint32_t* num_triangles) {
     if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
     if (num_nodes) *num_nodes = s->numNodes;
-    if (device_bytes)
-        *device_bytes = (s->compact ? 128ull : 64ull) * s->numNodes + 64ull * ((uint64_t)s->wideNodes + s->wideTris);
+    if (device_bytes) *device_bytes = (s->compact ? 128ull : 64ull) * s->numNodes;
     if (build_ms) *build_ms = s->buildMs;
     if (num_triangles) *num_triangles = s->numTris;
     return MCRT_OK;
@@ -947,30 +899,6 @@ MCRT_API mcrt_status mcrt_accel_read_records(mcrt_scene s, float* out, uint64_t 
     hipSetDevice(ctx->device);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipMemcpy(out, s->dNodes, 64 * std::min<uint64_t>(max_records, s->numNodes), hipMemcpyDeviceToHost));
-    return MCRT_OK;
-}
-
-MCRT_API mcrt_status mcrt_accel_tree(mcrt_scene s, int32_t* tree) {
-    if (!s || !tree) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
-    if (!s->dNodes) return fail(s->ctx, MCRT_ERROR_NOT_READY, "mcrt_accel_build has not been called");
-    *tree = s->wide ? MCRT_TREE_WIDE : MCRT_TREE_BVH2;
-    if (s->wideRequested && !s->wide) (void)fail(s->ctx, MCRT_OK, s->wideNote);
-    return MCRT_OK;
-}
-
-MCRT_API mcrt_status mcrt_accel_read_wide(mcrt_scene s, uint32_t* nodes, uint64_t max_nodes, float* tris,
-                                          uint64_t max_tris, uint64_t* num_nodes, uint64_t* num_tris) {
-    if (!s || !num_nodes || !num_tris) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
-    if (!s->wide) return fail(s->ctx, MCRT_ERROR_NOT_READY, "scene has no wide tree");
-    *num_nodes = s->wideNodes;
-    *num_tris = s->wideTris;
-    mcrt_ctx ctx = s->ctx;
-    hipSetDevice(ctx->device);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    if (nodes && s->wideNodes)
-        HIPCHK(ctx, hipMemcpy(nodes, s->dWideNodes, 64 * std::min<uint64_t>(max_nodes, s->wideNodes), hipMemcpyDeviceToHost));
-    if (tris)
-        HIPCHK(ctx, hipMemcpy(tris, s->dWideTris, 64 * std::min<uint64_t>(max_tris, s->wideTris), hipMemcpyDeviceToHost));
     return MCRT_OK;
 }
 
@@ -1038,46 +966,6 @@ MCRT_API mcrt_status mcrt_accel_build_host_records(const mcrt_scene_desc* d, con
         mcrt::free_bvh(bvh);
     }
     if (info) std::memcpy(info, inf, sizeof(inf));
-    return MCRT_OK;
-}
-
-MCRT_API mcrt_status mcrt_accel_build_host_wide(const mcrt_scene_desc* d, const mcrt_accel_opts* opts, uint32_t* nodes,
-                                                uint64_t max_nodes, float* tris, uint64_t max_tris,
-                                                uint64_t* num_nodes, uint64_t* num_tris) {
-    if (!d || !d->shapes || !d->indices || !d->positions || !num_nodes || !num_tris)
-        return fail(nullptr, MCRT_ERROR_INVALID_ARG, "invalid arguments");
-    if (mcrt::shapes_are_instanced(d->shapes, d->num_shapes) && !(opts && opts->force_flat))
-        return fail(nullptr, MCRT_ERROR_INVALID_ARG, "instanced scene: two-level structure, no wide tree");
-    uint64_t n2 = 0;
-    int32_t info[4];
-    mcrt_status st = mcrt_accel_build_host_records(d, opts, nullptr, 0, &n2, info);
-    if (st != MCRT_OK) return st;
-    std::vector<float> rec(16 * n2);
-    st = mcrt_accel_build_host_records(d, opts, rec.data(), n2, &n2, info);
-    if (st != MCRT_OK) return st;
-    std::vector<float> tri;
-    std::vector<uint32_t> first(d->num_shapes);
-    uint32_t acc = 0;
-    for (uint32_t si = 0; si < d->num_shapes; ++si) {
-        const mcrt_shape& sh = d->shapes[si];
-        first[si] = acc;
-        acc += sh.numTriangles;
-        for (uint32_t f = 0; f < sh.numTriangles; ++f) {
-            float p[9];
-            for (int c = 0; c < 3; ++c)
-                xformPoint(sh.toWorldTransform, d->positions[sh.startVertex + d->indices[sh.startIdx + 3 * f + c]],
-                           &p[3 * c]);
-            tri.insert(tri.end(), p, p + 9);
-        }
-    }
-    mcrt::WideTree w;
-    std::string err;
-    if (!mcrt::build_wide(rec.data(), n2, tri.data(), first.data(), first.size(), acc, w, &err))
-        return fail(nullptr, MCRT_ERROR_INVALID_ARG, "wide build: " + err);
-    *num_nodes = w.numNodes;
-    *num_tris = w.numTris;
-    if (nodes) std::memcpy(nodes, w.nodes.data(), 64 * std::min<uint64_t>(max_nodes, w.numNodes));
-    if (tris) std::memcpy(tris, w.tris.data(), 64 * std::min<uint64_t>(max_tris, w.numTris));
     return MCRT_OK;
 }
 

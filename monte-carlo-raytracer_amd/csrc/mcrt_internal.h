@@ -81,12 +81,6 @@ struct TraceCtx {
     uint32_t* spill;
     int spillCap;           // spill entries per ray (a multiple of STACK_LDS)
     int* overflow;
-    // 4-wide quantized tree (mcrt_wide.h), the perf-mode structure: selects the kernels' LAY_WIDE
-    // instantiation (launch-time)
-    int wide;
-    const uint4* wnodes;
-    const float4* wtris;
-    uint32_t wroot;         // root reference: node 0, or triangle record 0 | WIDE_LEAF_BIT
 };
 
 namespace mcrt {
@@ -153,20 +147,6 @@ struct HostRcp {
     bool ok = false;
 };
 const HostRcp& host_rcp_table();
-}
-// 4-wide quantized tree (mcrt_wide.h) built on the device from the Bvh2 records
-// (mcrt_widebuild.hip); on failure *why names the reason
-namespace mcrt {
-struct WideDevice {
-    uint4* nodes = nullptr;
-    float4* tris = nullptr;
-    uint32_t numNodes = 0, numTris = 0;
-    int depth = 0;
-    bool rootIsLeaf = false;
-};
-hipError_t gpu_build_wide(const float4* dRec, size_t n2, const mcrt_shape* dShapes, uint32_t numShapes,
-                          const uint32_t* dIndices, const float4* dPositions, hipStream_t st, WideDevice& out,
-                          const char** why);
 }
 // Host BVH builder (mcrt_bvh.cpp)
 namespace mcrt {

@@ -719,11 +719,11 @@ void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n,
     const dim3 g((n + 63) / 64), b(64);
     {
         if (any)
-            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<true, LAY_WIDE>, k_trace_rays<true, LAY_TWO_LEVEL>,
+            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<true, LAY_TWO_LEVEL>,
                                           k_trace_rays<true, LAY_COMPACT>, k_trace_rays<true, LAY_PLAIN>),
                                g, b, 0, st, c, rays, n, hits, occl);
         else
-            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<false, LAY_WIDE>, k_trace_rays<false, LAY_TWO_LEVEL>,
+            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<false, LAY_TWO_LEVEL>,
                                           k_trace_rays<false, LAY_COMPACT>, k_trace_rays<false, LAY_PLAIN>),
                                g, b, 0, st, c, rays, n, hits, occl);
     }
@@ -737,24 +737,24 @@ void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshSt
 }
 
 void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st) {
-    hipLaunchKernelGGL(pickLayout(c, k_primary<LAY_WIDE>, k_primary<LAY_TWO_LEVEL>, k_primary<LAY_COMPACT>, k_primary<LAY_PLAIN>), dim3(f.numTiles * f.batch), dim3(64), 0, st, c, f, cam,
+    hipLaunchKernelGGL(pickLayout(c, k_primary<LAY_TWO_LEVEL>, k_primary<LAY_COMPACT>, k_primary<LAY_PLAIN>), dim3(f.numTiles * f.batch), dim3(64), 0, st, c, f, cam,
                        hits);
 }
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
                    hipStream_t st) {
-    hipLaunchKernelGGL(pickLayout(c, k_extend<LAY_WIDE>, k_extend<LAY_TWO_LEVEL>, k_extend<LAY_COMPACT>, k_extend<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+    hipLaunchKernelGGL(pickLayout(c, k_extend<LAY_TWO_LEVEL>, k_extend<LAY_COMPACT>, k_extend<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, qO, qD, hits);
 }
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st) {
-    hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_WIDE>, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_COMPACT>, k_shadow<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+    hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_COMPACT>, k_shadow<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, sO, sD, sL, radiance);
 }
 void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
                           const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
                           float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
     const int blocks = (maxExt + 63) / 64 + (maxShadow + 63) / 64;
-    hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_WIDE>, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_COMPACT>,
+    hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_COMPACT>,
                                   k_shadow_extend<LAY_PLAIN>),
                        dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, extCount, qO, qD, hits, shadowCount, sO, sD,
                        sL, radiance);

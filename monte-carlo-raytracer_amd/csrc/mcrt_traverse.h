@@ -3,7 +3,6 @@
 #pragma once
 #include "mcrt_device.h"
 #include "mcrt_internal.h"
-#include "mcrt_wide.h"
 
 // ---------------------------------------------------------------------------
 // traversal
@@ -16,14 +15,9 @@
 #define LAY_PLAIN 0       // mcrt_bvh.cpp records, traverseOct
 #define LAY_COMPACT 1     // descent-compact records, traverseOct2
 #define LAY_TWO_LEVEL 3   // mcrt_bvh2l.cpp records, traverse2L
-#define LAY_WIDE 4        // 4-wide quantized tree (mcrt_wide.h), traverseWide
 template <typename K>
 inline K pickLayout(const TraceCtx& c, K twoLevel, K compact, K plain) {
     return c.twoLevel ? twoLevel : c.compact ? compact : plain;
-}
-template <typename K>
-inline K pickLayout(const TraceCtx& c, K wide, K twoLevel, K compact, K plain) {
-    return c.wide ? wide : pickLayout(c, twoLevel, compact, plain);
 }
 
 struct TraceRay {
@@ -302,152 +296,12 @@ MCRT_DEV int traverseOct2(const float4* __restrict__ nodes, uint32_t rootWord, c
     return hit;
 }
 
-
-// ---------------------------------------------------------------------------
-// 4-wide quantized tree (mcrt_wide.h; perf mode).  One 64-B node record per step tests four
-// child boxes; triangles live in their own records and are reached as leaf references.
-//   * a child plane decodes to p = fma(q, 2^e, origin) (the builder's own float) and enters the
-//     reference's slab formula fma(p, 1/d, -o/d) (intersect_bvh2_lds.cl:54-63), monotone in p, so
-//     a decoded box never rejects a ray the Bvh2 box it contains accepts;
-//   * a triangle step first tests the triangle's exact Bvh2 box (vertex min / max, the box its
-//     Bvh2 parent record holds) with the current closest t, then the triangle with the Bvh2
-//     record's edges (v1 - v0, v2 - v0 -- the same floats): the triangles tested with the full ray
-//     interval are the reference's, so any-hit answers equal the Bvh2's and a closest hit can
-//     differ only between triangles at (nearly) the same t;
-//   * hit children are sorted by entry distance (5-exchange network); the nearest is descended,
-//     the others pushed far to near on the LDS stack (spilling like the Bvh2 loop).
-// ---------------------------------------------------------------------------
-#define WIDE_DONE 0xFFFFFFFFu
-
-// entry / exit distances of a box given per axis as (lo, hi) plane pairs: the reference's slab
-// arithmetic fma(plane, 1/d, -o/d) (intersect_bvh2_lds.cl:54-63), two planes per v_pk_fma_f32
-// (each half an IEEE fma, so the same floats as two v_fma_f32)
-template <int OCT>
-MCRT_DEV void wideSlab(f2 px, f2 py, f2 pz, f3 inv, f3 oxi, float t, float& t0, float& t1) {
-    const f2 tx = __builtin_elementwise_fma(px, f2{inv.x, inv.x}, f2{oxi.x, oxi.x});
-    const f2 ty = __builtin_elementwise_fma(py, f2{inv.y, inv.y}, f2{oxi.y, oxi.y});
-    const f2 tz = __builtin_elementwise_fma(pz, f2{inv.z, inv.z}, f2{oxi.z, oxi.z});
-    if constexpr (OCT >= 0) {
-        constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
-        t0 = fmaxf(fmaxf(SX ? tx.y : tx.x, SY ? ty.y : ty.x), fmaxf(SZ ? tz.y : tz.x, 0.0f));
-        t1 = fminf(fminf(SX ? tx.x : tx.y, SY ? ty.x : ty.y), fminf(SZ ? tz.x : tz.y, t));
-    } else {
-        t0 = fmaxf(fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y)), 0.0f);
-        t1 = fminf(fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y)), t);
-    }
-}
-
-MCRT_DEV float wideQ(uint32_t w, int c) { return (float)((w >> (8 * c)) & 255u); }   // v_cvt_f32_ubyte<c>
-
-template <bool ANY, int OCT>
-MCRT_DEV int traverseWide(const uint4* __restrict__ nodes, const float4* __restrict__ tris, uint32_t root,
-                          const TraceRay& r, f3 inv, uint32_t* stk, uint32_t* spill, int spillCap, int* overflowFlag,
-                          float& tHit) {
-    const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
-    float t = r.tmax;
-    int hit = -1;
-    uint32_t ref = root;
-    stk[0] = WIDE_DONE;
-    int sp = 1, spillTop = 0;
-    auto push = [&](uint32_t v) {
-        if (sp == STACK_LDS) {   // spill entries 1..15 (RR: intersect_bvh2_lds.cl:146-155)
-            if (spillTop + STACK_LDS - 1 <= spillCap) {
-                for (int k = 1; k < STACK_LDS; ++k) spill[(size_t)(spillTop + k - 1) * 64] = stk[k * 64];
-                spillTop += STACK_LDS - 1;
-            } else {
-                *overflowFlag = 1;   // depth beyond capacity: drop (reported by the host)
-            }
-            sp = 1;
-        }
-        stk[sp * 64] = v;
-        ++sp;
-    };
-    while (ref != WIDE_DONE) {
-        bool pop = true;
-        if (ref & WIDE_LEAF_BIT) {
-            const uint32_t k = ref & ~WIDE_LEAF_BIT;
-            const float4* tr = tris + 4 * (size_t)k;
-            const float4 A = tr[0], B = tr[1], C = tr[2];
-            float b0, b1;   // the Bvh2 leaf box (mcrt_bvh.cpp leafBox: per-axis vertex min / max)
-            wideSlab<OCT>(f2{fminf(fminf(A.x, B.x), C.x), fmaxf(fmaxf(A.x, B.x), C.x)},
-                          f2{fminf(fminf(A.y, B.y), C.y), fmaxf(fmaxf(A.y, B.y), C.y)},
-                          f2{fminf(fminf(A.z, B.z), C.z), fmaxf(fmaxf(A.z, B.z), C.z)}, inv, oxi, t, b0, b1);
-            if (b0 <= b1 && r.mask != __float_as_int(A.w)) {   // RR_RAY_MASK
-                const float4 E1 = make_float4(B.x - A.x, B.y - A.y, B.z - A.z, 0.0f);
-                const float4 E2 = make_float4(C.x - A.x, C.y - A.y, C.z - A.z, 0.0f);
-                const float th = triHit(r, A, E1, E2, t);
-                if (th < t) {
-                    t = th;
-                    hit = (int)k;
-                    if (ANY) {
-                        ref = WIDE_DONE;
-                        pop = false;
-                    }
-                }
-            }
-        } else {
-            const uint4* q = nodes + 4 * (size_t)ref;
-            const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-            const f3 o = f3{__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
-            const uint32_t meta = q0.w;
-            const f3 st = f3{__uint_as_float((meta & 255u) << 23), __uint_as_float(((meta >> 8) & 255u) << 23),
-                             __uint_as_float(((meta >> 16) & 255u) << 23)};
-            float key[WIDE_K];
-            uint32_t cr[WIDE_K];
-#pragma unroll
-            for (int c = 0; c < WIDE_K; ++c) {
-                float t0, t1;   // decoded planes fma(q, 2^e, origin): mcrt::wide_plane, two per v_pk_fma_f32
-                const f2 px = __builtin_elementwise_fma(f2{wideQ(q1.x, c), wideQ(q1.y, c)}, f2{st.x, st.x}, f2{o.x, o.x});
-                const f2 py = __builtin_elementwise_fma(f2{wideQ(q1.z, c), wideQ(q1.w, c)}, f2{st.y, st.y}, f2{o.y, o.y});
-                const f2 pz = __builtin_elementwise_fma(f2{wideQ(q2.x, c), wideQ(q2.y, c)}, f2{st.z, st.z}, f2{o.z, o.z});
-                wideSlab<OCT>(px, py, pz, inv, oxi, t, t0, t1);
-                const bool h = ((meta >> (24 + c)) & 1u) && t0 <= t1;
-                key[c] = h ? t0 : INFINITY;
-                const uint32_t w = c == 0 ? q2.z : c == 1 ? q2.w : c == 2 ? q3.x : q3.y;
-                cr[c] = w | (((meta >> (28 + c)) & 1u) ? WIDE_LEAF_BIT : 0u);
-            }
-#define WIDE_CSWAP(a, b)                                                    \
-    do {                                                                    \
-        const bool sw = key[b] < key[a];                                    \
-        const float ka = key[a], kb = key[b];                               \
-        const uint32_t ra = cr[a], rb = cr[b];                              \
-        key[a] = sw ? kb : ka; key[b] = sw ? ka : kb;                       \
-        cr[a] = sw ? rb : ra; cr[b] = sw ? ra : rb;                         \
-    } while (0)
-            WIDE_CSWAP(0, 1); WIDE_CSWAP(2, 3); WIDE_CSWAP(0, 2); WIDE_CSWAP(1, 3); WIDE_CSWAP(1, 2);
-#undef WIDE_CSWAP
-            if (key[3] != INFINITY) push(cr[3]);
-            if (key[2] != INFINITY) push(cr[2]);
-            if (key[1] != INFINITY) push(cr[1]);
-            if (key[0] != INFINITY) {
-                ref = cr[0];
-                pop = false;
-            }
-        }
-        if (pop) {
-            --sp;
-            ref = stk[sp * 64];
-            if (ref == WIDE_DONE && spillTop > 0) {   // refill (intersect_bvh2_lds.cl:182-191)
-                spillTop -= STACK_LDS - 1;
-                for (int k = 1; k < STACK_LDS; ++k) stk[k * 64] = spill[(size_t)(spillTop + k - 1) * 64];
-                sp = STACK_LDS - 1;
-                ref = stk[sp * 64];
-            }
-        }
-    }
-    tHit = t;
-    return hit;
-}
-
 template <bool ANY, int LAY>
 MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, float& tHit) {
     const f3 inv = safeInvDir(r.d);
 #define MCRT_TRAV_CALL(OCT)                                                                                       \
     do {                                                                                                          \
-        if constexpr (LAY == LAY_WIDE)                                                                            \
-            return traverseWide<ANY, OCT>(c.wnodes, c.wtris, c.wroot, r, inv, stk, spill, c.spillCap, c.overflow,  \
-                                          tHit);                                                                  \
-        else if constexpr (LAY == LAY_COMPACT)                                                                    \
+        if constexpr (LAY == LAY_COMPACT)                                                                         \
             return traverseOct2<ANY, OCT>(c.nodes, c.rootWord, r, inv, stk, spill, c.spillCap, c.overflow, tHit); \
         else                                                                                                      \
             return traverseOct<ANY, OCT>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit);             \
@@ -640,18 +494,6 @@ MCRT_DEV float4 closestRecord2L(const float4* __restrict__ nodes, const TraceRay
     return make_float4(uv.x, uv.y, __int_as_float(shape), E1.w);
 }
 
-// closest-hit record from a wide triangle record: the Bvh2 leaf's v0 and edges, so the same
-// barycentrics as closestRecord
-MCRT_DEV float4 closestRecordWide(const float4* __restrict__ tris, const TraceRay& r, int tri, float t) {
-    if (tri < 0) return make_float4(0.f, 0.f, __int_as_float(-1), __int_as_float(-1));
-    const float4 A = tris[4 * tri], B = tris[4 * tri + 1], C = tris[4 * tri + 2];
-    const float4 E1 = make_float4(B.x - A.x, B.y - A.y, B.z - A.z, 0.0f);
-    const float4 E2 = make_float4(C.x - A.x, C.y - A.y, C.z - A.z, 0.0f);
-    const f3 p = r.o + t * r.d;
-    const f2 uv = triBary(p, A, E1, E2);
-    return make_float4(uv.x, uv.y, A.w, B.w);
-}
-
 // Closest / any hit over the scene's record layout (LAY; LAY_TWO_LEVEL: RR's IntersectorTwoLevel).
 template <int LAY>
 MCRT_DEV float4 traceClosest(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, float& t) {
@@ -659,9 +501,6 @@ MCRT_DEV float4 traceClosest(const TraceCtx& c, const TraceRay& r, uint32_t* stk
         int inst;
         const int tri = traverse2L<false>(c.nodes, r, stk, spill, c.spillCap, c.overflow, t, inst);
         return closestRecord2L(c.nodes, r, tri, inst, t);
-    } else if constexpr (LAY == LAY_WIDE) {
-        const int tri = traverse<false, LAY>(c, r, stk, spill, t);
-        return closestRecordWide(c.wtris, r, tri, t);
     } else {
         const int tri = traverse<false, LAY>(c, r, stk, spill, t);
         return closestRecord(c.nodes, r, tri, t);   // leaf slots are the same in both flat layouts

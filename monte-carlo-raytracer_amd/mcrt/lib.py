@@ -43,9 +43,6 @@ SIGNATURES = {
     "mcrt_accel_info": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_accel_layout": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_accel_builder": (_c.c_int, [_vp, _vp]),
-    "mcrt_accel_tree": (_c.c_int, [_vp, _vp]),
-    "mcrt_accel_read_wide": (_c.c_int, [_vp, _vp, _c.c_uint64, _vp, _c.c_uint64, _vp, _vp]),
-    "mcrt_accel_build_host_wide": (_c.c_int, [_vp, _vp, _vp, _c.c_uint64, _vp, _c.c_uint64, _vp, _vp]),
     "mcrt_bdpt_splats_copy": (_c.c_int, [_vp, _vp]),
     "mcrt_bdpt_gather": (_c.c_int, [_vp, _vp]),
     "mcrt_obj_load": (_c.c_int, [_c.c_char_p, _c.c_uint32, _vp]),
@@ -187,13 +184,13 @@ class Context:
 
 
 def accel_opts(cost=10.0, bins=64, sah=True, device_build=False, force_2level=False, force_flat=False,
-               world_to_local=None, tree=T.TREE_BVH2):
+               world_to_local=None):
     """mcrt_accel_opts; device_build: 0/False (default) or 2 the RadeonRays-identical tree built on
     the device, 3 the same tree built on the host, 1/True device LBVH; world_to_local: optional (num_shapes, 4, 4) float32 array (kept alive by
-    the caller until the build returns); tree: the traversal tree (T.TREE_BVH2 parity, T.TREE_WIDE perf)."""
+    the caller until the build returns)."""
     w2l = None if world_to_local is None else world_to_local.ctypes.data
     return T.AccelOpts(cost, bins, 1 if sah else 0, int(device_build), 1 if force_2level else 0,
-                       1 if force_flat else 0, w2l, int(tree))
+                       1 if force_flat else 0, w2l)
 
 
 def build_host_records(scene, **opts):
@@ -213,23 +210,9 @@ def build_host_records(scene, **opts):
                  "meshes": int(info[3])}
 
 
-def build_host_wide(scene, **opts):
-    """Host restatement of the wide tree (mcrt_accel_build_host_wide): (nodes uint32 (n, 16),
-    triangle records float32 (m, 16))."""
-    desc = scene.desc()
-    o = accel_opts(**opts)
-    nn, nt = _c.c_uint64(), _c.c_uint64()
-    _check(lib().mcrt_accel_build_host_wide(_c.byref(desc), _c.byref(o), None, 0, None, 0, _c.byref(nn), _c.byref(nt)))
-    nodes = np.zeros((nn.value, 16), np.uint32)
-    tris = np.zeros((nt.value, 16), np.float32)
-    _check(lib().mcrt_accel_build_host_wide(_c.byref(desc), _c.byref(o), _p(nodes), nn.value, _p(tris), nt.value,
-                                            _c.byref(nn), _c.byref(nt)))
-    return nodes, tris
-
-
 class DeviceScene:
     def __init__(self, ctx, scene, build=True, cost=10.0, bins=64, sah=True, device_build=False,
-                 force_2level=False, force_flat=False, world_to_local=None, tree=T.TREE_BVH2):
+                 force_2level=False, force_flat=False, world_to_local=None):
         self.ctx = ctx
         self.scene = scene
         self._desc = scene.desc()
@@ -238,29 +221,13 @@ class DeviceScene:
         self.h = h
         ctx._adopt(self)
         if build:
-            self.build(cost, bins, sah, device_build, force_2level, force_flat, world_to_local, tree)
+            self.build(cost, bins, sah, device_build, force_2level, force_flat, world_to_local)
 
     def build(self, cost=10.0, bins=64, sah=True, device_build=False, force_2level=False, force_flat=False,
-              world_to_local=None, tree=T.TREE_BVH2):
+              world_to_local=None):
         w2l = None if world_to_local is None else np.ascontiguousarray(world_to_local, np.float32)
-        opts = accel_opts(cost, bins, sah, device_build, force_2level, force_flat, w2l, tree)
+        opts = accel_opts(cost, bins, sah, device_build, force_2level, force_flat, w2l)
         _check(lib().mcrt_accel_build(self.h, _c.byref(opts)), self.ctx.h)
-
-    def tree(self):
-        """The traversal tree in use (mcrt_accel_tree): T.TREE_BVH2 or T.TREE_WIDE."""
-        t = _c.c_int32()
-        _check(lib().mcrt_accel_tree(self.h, _c.byref(t)), self.ctx.h)
-        return t.value
-
-    def read_wide(self):
-        """The device's wide tree (mcrt_accel_read_wide): (nodes uint32 (n, 16), tris float32 (m, 16))."""
-        nn, nt = _c.c_uint64(), _c.c_uint64()
-        _check(lib().mcrt_accel_read_wide(self.h, None, 0, None, 0, _c.byref(nn), _c.byref(nt)), self.ctx.h)
-        nodes = np.zeros((nn.value, 16), np.uint32)
-        tris = np.zeros((nt.value, 16), np.float32)
-        _check(lib().mcrt_accel_read_wide(self.h, _p(nodes), nn.value, _p(tris), nt.value, _c.byref(nn),
-                                          _c.byref(nt)), self.ctx.h)
-        return nodes, tris
 
     def layout(self):
         tl, nm, ni, dp = _c.c_int32(), _c.c_uint32(), _c.c_uint32(), _c.c_int32()

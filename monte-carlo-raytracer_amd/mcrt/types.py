@@ -132,10 +132,7 @@ class SceneDesc(ctypes.Structure):
 class AccelOpts(ctypes.Structure):
     _fields_ = [("traversal_cost", ctypes.c_float), ("num_bins", ctypes.c_int), ("use_sah", ctypes.c_int),
                 ("device_build", ctypes.c_int), ("force_2level", ctypes.c_int), ("force_flat", ctypes.c_int),
-                ("world_to_local", ctypes.c_void_p), ("traversal_tree", ctypes.c_int32)]
-
-
-TREE_BVH2, TREE_WIDE = 0, 1   # mcrt_accel_opts.traversal_tree
+                ("world_to_local", ctypes.c_void_p)]
 
 
 class FrameParams(ctypes.Structure):

@@ -145,36 +145,3 @@ def timed_call_matches(ctx, ds, ref, key, name, W, H, frames, D):
             bad.append(f"{nm} after the batched call differs from 20 single frames at {int((~ex.all(-1)).sum())} px")
     fb.close()
     assert not bad, (key, bad)
-
-
-@pytest.mark.parametrize("key", ["sm_pt_1080p", "sm_pt_1080p_taa"])
-def test_wide_tree_full_size_vs_reference(hip_ctx, clref_scale, key):
-    """The perf-mode tree (MCRT_TREE_WIDE) at the headline size against the reference run live:
-    SURVEY App. A's tolerance (>= 99.5 % of pixels within 1e-4 relative) and, since only (near-)
-    equal-t ties can resolve differently (test_gpu_wide.py), >= 99.9 % of pixels bit-exact.  The
-    TAA case is the bench's timed call (one 20-frame mcrt_render_frames)."""
-    from mcrt import lib
-    case = [c for c in SCALE_CASES["ieee"] if c[0] == key][0]
-    _, name, W, H, integ, frames, D = case
-    ref = clref_scale["ieee"]
-    sc = scale_scene(name)
-    ds = lib.DeviceScene(hip_ctx, sc, tree=T.TREE_WIDE)
-    assert ds.tree() == T.TREE_WIDE
-    fb = lib.FrameBuffer(hip_ctx, W, H)
-    got = {}
-    if integ == "pt_taa":
-        cams = [taa_camera(name, W, H, f) for f in range(TIMED_F0, TIMED_F0 + TIMED_STEPS)]
-        fb.render_frames(ds, cams, frame=TIMED_F0, max_depth=D)
-        got = {f: fb.read_frame(f - TIMED_F0) for f in frames}
-    else:
-        for f in frames:
-            fb.render(ds, scene_camera(name, W, H), frame=f, max_depth=D)
-            got[f] = fb.read(0)
-    fb.close()
-    ds.close()
-    for f in frames:
-        g, r = got[f][..., :3].astype(np.float64), ref[f"{key}_f{f}"][..., :3].astype(np.float64)
-        exact = _exact(got[f][..., :3], ref[f"{key}_f{f}"][..., :3]).all(-1).mean()
-        within = (np.abs(g - r) <= 1e-4 * np.maximum(1.0, np.abs(r))).all(-1).mean()
-        print(f"{key} frame {f}: bit-exact {exact:.6f}, within 1e-4 {within:.6f}")
-        assert within >= 0.995 and exact >= 0.999, (key, f, exact, within)

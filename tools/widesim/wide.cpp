@@ -1,4 +1,4 @@
-// mcrt_wide.cpp -- host restatement of the 4-wide quantized tree build (mcrt_wide.h): the
+// wide.cpp -- host build of the 4-wide quantized tree (wide.h) of the round-3 experiment: the
 // specification the device builder (mcrt_widebuild.hip) is checked against record for record,
 // and the builder of the analysis tools.  Compiled with -ffp-contract=off.
 //
@@ -12,7 +12,7 @@
 // with wide_plane(q) <= lo and hi -> the smallest q with wide_plane(q) >= hi.  Each choice is a
 // predicate on the decoded fp32 plane itself, so host and device arrive at the same bytes, and
 // every decoded box contains its Bvh2 box.
-#include "mcrt_wide.h"
+#include "wide.h"
 
 #include <algorithm>
 #include <cmath>

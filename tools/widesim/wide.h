@@ -1,6 +1,6 @@
-// mcrt_wide.h -- 4-wide quantized BVH records (the perf-mode tree, mcrt_wide.cpp), shared by the
-// host builder, the HIP traversal (mcrt_traverse.h traverseWide) and the analysis tools.
-//
+// wide.h -- 4-wide quantized BVH records of the round-3 wide-tree experiment (tools/experiments/wide_tree.patch
+// holds the product integration; measured slower than the Bvh2, profiles/r03/ab/README.txt item 1), shared by the
+// host build and the traversal model of tools/widesim.
 // The RadeonRays Bvh2 (the parity tree, mcrt_bvh.cpp / mcrt_sahbuild.hip) is collapsed into
 // 4-wide nodes: each node's up to four children are the largest-area descendants of a Bvh2 node,
 // their boxes stored as 8-bit offsets from the node's origin in power-of-two steps, so a node --

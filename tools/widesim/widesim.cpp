@@ -1,9 +1,9 @@
 // widesim.cpp -- CPU model of the Bvh2 and the 4-wide quantized traversal (analysis tool).
-// Builds the wide tree with the product's builder (mcrt_wide.cpp), replays both traversals over
+// Builds the wide tree with the experiment's builder (wide.cpp), replays both traversals over
 // the same rays and reports per ray the internal steps, triangle steps and the closest hit, so
 // the node-visit reduction and the result agreement can be measured before any GPU run.
 // Build: g++ -O2 -std=c++17 -shared -fPIC -pthread tools/widesim/widesim.cpp \
-//          monte-carlo-raytracer_amd/csrc/mcrt_wide.cpp -o /tmp/widesim.so
+//          tools/widesim/wide.cpp -o /tmp/widesim.so
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -11,7 +11,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../monte-carlo-raytracer_amd/csrc/mcrt_wide.h"
+#include "wide.h"
 
 using mcrt::WideTree;
 

@@ -1,7 +1,7 @@
 """Bvh2 vs 4-wide quantized tree on the San-Miguel proxy (analysis tool, CPU).
 
 Builds the product's Bvh2 records on the host (mcrt.lib.build_host_records, the RR-identical
-tree), collapses them with the product's wide builder (mcrt_wide.cpp via tools/widesim), and
+tree), collapses them with the experiment's wide builder (tools/widesim/wide.cpp), and
 replays camera rays, one diffuse bounce and sun shadow rays through both trees: steps per query
 (internal / triangle) and whether the closest hits agree (same triangle, or the same t).
 usage: python tools/widesim/widesim.py [tris] [W] [H]
@@ -24,7 +24,7 @@ from trav_sim import camera_rays  # noqa: E402
 def load():
     so = "/tmp/widesim.so"
     src = [os.path.join(ROOT, "tools", "widesim", "widesim.cpp"),
-           os.path.join(ROOT, "monte-carlo-raytracer_amd", "csrc", "mcrt_wide.cpp")]
+           os.path.join(ROOT, "tools", "widesim", "wide.cpp")]
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", "-pthread", *src, "-o", so],
                    check=True)
     L = ctypes.CDLL(so)
