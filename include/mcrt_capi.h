@@ -356,6 +356,22 @@ MCRT_API mcrt_status mcrt_trace_closest(mcrt_scene scene, const mcrt_ray* d_rays
                                         mcrt_intersection* d_hits);
 MCRT_API mcrt_status mcrt_trace_any(mcrt_scene scene, const mcrt_ray* d_rays, int32_t n,
                                     int32_t* d_hits);
+/* The variants with the ray count in device memory (QueryIntersection / QueryOcclusion with
+ * `Buffer const* numrays, int maxrays`, RR/include/radeon_rays.h:272-277; the count a previous
+ * kernel wrote, read by the query kernel itself, so no host round trip): min(*d_numrays, maxrays)
+ * rays are traced, the grid covers maxrays.  Asynchronous on the context stream, as RR's queries:
+ * the query waits for wait_event (NULL: none) and, when done_event is not NULL, *done_event
+ * receives a new event recorded after it (RR's `Event** event`; mcrt_event_wait = Event::Wait,
+ * mcrt_event_destroy = IntersectionApi::DeleteEvent). */
+typedef struct mcrt_event_s* mcrt_event;
+MCRT_API mcrt_status mcrt_trace_closest_count(mcrt_scene scene, const mcrt_ray* d_rays, const int32_t* d_numrays,
+                                              int32_t maxrays, mcrt_intersection* d_hits, mcrt_event wait_event,
+                                              mcrt_event* done_event);
+MCRT_API mcrt_status mcrt_trace_any_count(mcrt_scene scene, const mcrt_ray* d_rays, const int32_t* d_numrays,
+                                          int32_t maxrays, int32_t* d_hits, mcrt_event wait_event,
+                                          mcrt_event* done_event);
+MCRT_API mcrt_status mcrt_event_wait(mcrt_event event);
+MCRT_API mcrt_status mcrt_event_destroy(mcrt_event event);
 
 /* ------------------------------------------------------------------------ */
 /* Frame buffer + integrator (RTPrimaryRaysPass, RTPathTracingPass,

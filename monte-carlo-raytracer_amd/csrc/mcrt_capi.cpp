@@ -28,6 +28,11 @@
 namespace {
 
 thread_local std::string g_lastError;
+}  // namespace
+namespace mcrt {
+void set_last_error(const std::string& msg) { g_lastError = msg; }
+}  // namespace mcrt
+namespace {
 
 #define MCRT_MAX_BOUNCES 32
 
@@ -740,10 +745,13 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
             return finish_accel(s, t0, nullptr);
         }
         // configurations the device path does not reproduce (> 64 bins, a host whose rcpps the
-        // table cannot model, pathological level counts) take the host build: same tree
-        if (e != hipErrorNotSupported && e != hipErrorInvalidValue)
+        // table cannot model, pathological level counts) take the host build: same tree; so does a
+        // device without room for the build's scratch (~230 B per triangle beyond the records)
+        if (e != hipErrorNotSupported && e != hipErrorInvalidValue && e != hipErrorOutOfMemory)
             return fail(ctx, MCRT_ERROR_DEVICE, std::string("device SAH build: ") + (why ? why : hipGetErrorString(e)));
         (void)hipGetLastError();
+        if (e == hipErrorOutOfMemory)
+            std::fprintf(stderr, "mcrt: device SAH build out of memory, building the same tree on the host\n");
     }
     s->builder = 0;
     if (buildMode == 1) {   // on-device linear BVH (mcrt_gpubuild.hip)
@@ -972,30 +980,80 @@ MCRT_API mcrt_status mcrt_accel_build_host_records(const mcrt_scene_desc* d, con
 // ---------------------------------------------------------------------------
 // RadeonRays-style queries
 // ---------------------------------------------------------------------------
-static mcrt_status trace_common(mcrt_scene s, const mcrt_ray* rays, int32_t n, mcrt_intersection* hits, int32_t* occl,
-                                bool any) {
+struct mcrt_event_s {
+    hipEvent_t e = nullptr;
+    int device = 0;
+};
+
+// n: the host count, or with countDev the grid's capacity (maxrays) and the device count
+static mcrt_status trace_common(mcrt_scene s, const mcrt_ray* rays, int32_t n, const int32_t* countDev,
+                                mcrt_intersection* hits, int32_t* occl, bool any, mcrt_event wait = nullptr,
+                                mcrt_event* done = nullptr) {
+    if (done) *done = nullptr;
     if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
     mcrt_ctx ctx = s->ctx;
     if (!s->dNodes) return fail(ctx, MCRT_ERROR_NOT_READY, "mcrt_accel_build has not been called");
     if (n < 0 || (n > 0 && !rays) || (n > 0 && !any && !hits) || (n > 0 && any && !occl))
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "invalid ray query arguments");
-    if (n == 0) return MCRT_OK;
     hipSetDevice(ctx->device);
-    if (!ensure_spill(s, (size_t)n)) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
-    {
-        Timed t(ctx, any ? K_TRACE_ANY : K_TRACE_CLOSEST, nullptr, n);
-        mcrt::launch_trace_rays(any, trace_ctx(s), rays, n, hits, occl, ctx->stream);
+    if (wait) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, wait->e, 0));
+    if (n > 0) {
+        if (!ensure_spill(s, (size_t)n)) return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
+        Timed t(ctx, any ? K_TRACE_ANY : K_TRACE_CLOSEST, countDev, countDev ? 0 : n);
+        mcrt::launch_trace_rays(any, trace_ctx(s), rays, n, countDev, hits, occl, ctx->stream);
     }
     HIPCHK(ctx, hipGetLastError());
+    if (done) {
+        auto* ev = new mcrt_event_s();
+        ev->device = ctx->device;
+        hipError_t e = hipEventCreateWithFlags(&ev->e, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(ev->e, ctx->stream);
+        if (e != hipSuccess) {
+            if (ev->e) hipEventDestroy(ev->e);
+            delete ev;
+            return fail(ctx, MCRT_ERROR_DEVICE, std::string("query event: ") + hipGetErrorString(e));
+        }
+        *done = ev;
+    }
     return MCRT_OK;
 }
 
 MCRT_API mcrt_status mcrt_trace_closest(mcrt_scene s, const mcrt_ray* d_rays, int32_t n, mcrt_intersection* d_hits) {
-    return trace_common(s, d_rays, n, d_hits, nullptr, false);
+    return trace_common(s, d_rays, n, nullptr, d_hits, nullptr, false);
 }
 
 MCRT_API mcrt_status mcrt_trace_any(mcrt_scene s, const mcrt_ray* d_rays, int32_t n, int32_t* d_hits) {
-    return trace_common(s, d_rays, n, nullptr, d_hits, true);
+    return trace_common(s, d_rays, n, nullptr, nullptr, d_hits, true);
+}
+
+MCRT_API mcrt_status mcrt_trace_closest_count(mcrt_scene s, const mcrt_ray* d_rays, const int32_t* d_numrays,
+                                              int32_t maxrays, mcrt_intersection* d_hits, mcrt_event wait_event,
+                                              mcrt_event* done_event) {
+    if (!d_numrays) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "d_numrays is NULL");
+    return trace_common(s, d_rays, maxrays, d_numrays, d_hits, nullptr, false, wait_event, done_event);
+}
+
+MCRT_API mcrt_status mcrt_trace_any_count(mcrt_scene s, const mcrt_ray* d_rays, const int32_t* d_numrays,
+                                          int32_t maxrays, int32_t* d_hits, mcrt_event wait_event,
+                                          mcrt_event* done_event) {
+    if (!d_numrays) return fail(s ? s->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "d_numrays is NULL");
+    return trace_common(s, d_rays, maxrays, d_numrays, nullptr, d_hits, true, wait_event, done_event);
+}
+
+MCRT_API mcrt_status mcrt_event_wait(mcrt_event ev) {
+    if (!ev) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "event is NULL");
+    hipSetDevice(ev->device);
+    const hipError_t e = hipEventSynchronize(ev->e);
+    if (e != hipSuccess) return fail(nullptr, MCRT_ERROR_DEVICE, std::string("event wait: ") + hipGetErrorString(e));
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_event_destroy(mcrt_event ev) {
+    if (!ev) return MCRT_OK;
+    hipSetDevice(ev->device);
+    hipEventDestroy(ev->e);
+    delete ev;
+    return MCRT_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <cstddef>
+#include <string>
 
 #include "../../include/mcrt_capi.h"
 
@@ -84,8 +85,9 @@ struct TraceCtx {
 };
 
 namespace mcrt {
-void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, mcrt_intersection* hits, int* occl,
-                       hipStream_t st);
+// n rays, or with countDev (device memory) min(*countDev, n) of them
+void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, const int* countDev,
+                       mcrt_intersection* hits, int* occl, hipStream_t st);
 void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshStartVertex, const uint32_t* meshBase,
                             int numMeshes, uint32_t numRecords, const uint32_t* indices, const float4* positions,
                             const float2* uvs, const float4* normals, float4* surf, hipStream_t st);
@@ -147,6 +149,10 @@ struct HostRcp {
     bool ok = false;
 };
 const HostRcp& host_rcp_table();
+}
+// the thread's mcrt_last_error(NULL) text (mcrt_capi.cpp), for entry points without a context
+namespace mcrt {
+void set_last_error(const std::string& msg);
 }
 // Host BVH builder (mcrt_bvh.cpp)
 namespace mcrt {

@@ -30,8 +30,10 @@
 // ---------------------------------------------------------------------------
 template <bool ANY, int LAY>
 __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* __restrict__ rays, int n,
+                                                   const int* __restrict__ countDev,
                                                    mcrt_intersection* __restrict__ hits, int* __restrict__ occl) {
     __shared__ uint32_t lds[STACK_LDS * 64];
+    if (countDev) n = min(n, *countDev);   // RR's numrays in remote memory (radeon_rays.h:272-277)
     const int lane = threadIdx.x;
     const int i = blockIdx.x * 64 + lane;
     if (i >= n) return;
@@ -714,18 +716,18 @@ __global__ void k_pack_compact(const float4* __restrict__ in, float4* __restrict
 
 namespace mcrt {
 
-void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, mcrt_intersection* hits, int* occl,
-                       hipStream_t st) {
+void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n, const int* countDev,
+                       mcrt_intersection* hits, int* occl, hipStream_t st) {
     const dim3 g((n + 63) / 64), b(64);
     {
         if (any)
             hipLaunchKernelGGL(pickLayout(c, k_trace_rays<true, LAY_TWO_LEVEL>,
                                           k_trace_rays<true, LAY_COMPACT>, k_trace_rays<true, LAY_PLAIN>),
-                               g, b, 0, st, c, rays, n, hits, occl);
+                               g, b, 0, st, c, rays, n, countDev, hits, occl);
         else
             hipLaunchKernelGGL(pickLayout(c, k_trace_rays<false, LAY_TWO_LEVEL>,
                                           k_trace_rays<false, LAY_COMPACT>, k_trace_rays<false, LAY_PLAIN>),
-                               g, b, 0, st, c, rays, n, hits, occl);
+                               g, b, 0, st, c, rays, n, countDev, hits, occl);
     }
 }
 void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshStartVertex, const uint32_t* meshBase,

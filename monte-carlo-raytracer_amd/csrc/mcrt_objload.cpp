@@ -65,6 +65,7 @@ bool readPng(const std::string& path, std::vector<uint8_t>& rgba, int& W, int& H
         const char* typ = (const char*)&d[pos + 4];
         const uint8_t* c = &d[pos + 8];
         if (!std::memcmp(typ, "IHDR", 4)) {
+            if (n < 13) { why = "truncated IHDR chunk"; return false; }
             W = (int)be32(c); H = (int)be32(c + 4); depth = c[8]; ctype = c[9]; interlace = c[12];
         } else if (!std::memcmp(typ, "IDAT", 4)) {
             idat.insert(idat.end(), c, c + n);
@@ -80,6 +81,7 @@ bool readPng(const std::string& path, std::vector<uint8_t>& rgba, int& W, int& H
     if (depth != 8 || interlace != 0) { why = "only 8-bit non-interlaced PNG is supported"; return false; }
     const int ch = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
     if (!ch || W <= 0 || H <= 0) { why = "unsupported PNG colour type"; return false; }
+    if (W > 65535 || H > 65535) { why = "image larger than a texture descriptor holds (65535)"; return false; }
     const size_t stride = (size_t)W * ch;
     std::vector<uint8_t> raw((stride + 1) * H);
     uLongf rawLen = (uLongf)raw.size();
@@ -190,9 +192,14 @@ void parseMtl(const std::string& path, std::map<std::string, Mtl>& mats) {
     }
 }
 
+// OBJ index token -> 0-based index into an array of n entries (1-based, or negative = relative
+// to the end); -1 when the token is not a valid reference (0, past the end, before the start)
 int objIndex(const std::string& tok, size_t n) {
-    const long i = std::strtol(tok.c_str(), nullptr, 10);
-    return i > 0 ? (int)(i - 1) : (int)((long)n + i);
+    char* end = nullptr;
+    const long i = std::strtol(tok.c_str(), &end, 10);
+    if (end == tok.c_str()) return -1;
+    const long k = i > 0 ? i - 1 : (long)n + i;
+    return (i == 0 || k < 0 || k >= (long)n) ? -1 : (int)k;
 }
 
 mcrt_material defaultMaterial() {   // RTMaterial constructor defaults (kernel_data.h:89-94)
@@ -304,7 +311,9 @@ MCRT_API mcrt_status mcrt_obj_load(const char* path, uint32_t flags, mcrt_obj_sc
     std::string curMat, curObj;
     bool haveMat = false, haveObj = false;
     std::string line;
+    size_t lineNo = 0;
     while (std::getline(f, line)) {
+        ++lineNo;
         const auto t = split(line);
         if (t.empty() || t[0][0] == '#') continue;
         const std::string& k = t[0];
@@ -325,9 +334,20 @@ MCRT_API mcrt_status mcrt_obj_load(const char* path, uint32_t flags, mcrt_obj_sc
                     else cur += ch;
                 }
                 p.push_back(cur);
-                face.push_back(objIndex(p[0], V.size() / 3));
-                face.push_back(p.size() > 1 && !p[1].empty() ? objIndex(p[1], VT.size() / 2) : -1);
-                face.push_back(p.size() > 2 && !p[2].empty() ? objIndex(p[2], VN.size() / 3) : -1);
+                const int v = objIndex(p[0], V.size() / 3);
+                const int vt = p.size() > 1 && !p[1].empty() ? objIndex(p[1], VT.size() / 2) : -2;
+                const int vn = p.size() > 2 && !p[2].empty() ? objIndex(p[2], VN.size() / 3) : -2;
+                if (v < 0 || vt == -1 || vn == -1) {   // a reference outside the arrays read so far
+                    mcrt::set_last_error(std::string(path) + ":" + std::to_string(lineNo) + ": face index '" + t[i] +
+                                         "' out of range (" + std::to_string(V.size() / 3) + " v, " +
+                                         std::to_string(VT.size() / 2) + " vt, " + std::to_string(VN.size() / 3) +
+                                         " vn so far)");
+                    delete S;
+                    return MCRT_ERROR_INVALID_ARG;
+                }
+                face.push_back(v);
+                face.push_back(vt < 0 ? -1 : vt);
+                face.push_back(vn < 0 ? -1 : vn);
             }
             const std::string obj = haveObj ? curObj : std::string("\x01"), mat = haveMat ? curMat : std::string("\x01");
             if (runs.empty() || runs.back().obj != obj || runs.back().mat != mat) runs.push_back(Run{obj, mat, {}});

@@ -55,6 +55,10 @@ SIGNATURES = {
     "mcrt_accel_build_host_records": (_c.c_int, [_vp, _vp, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64), _vp]),
     "mcrt_trace_closest": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
     "mcrt_trace_any": (_c.c_int, [_vp, _vp, _c.c_int32, _vp]),
+    "mcrt_trace_closest_count": (_c.c_int, [_vp, _vp, _vp, _c.c_int32, _vp, _vp, _c.POINTER(_vp)]),
+    "mcrt_trace_any_count": (_c.c_int, [_vp, _vp, _vp, _c.c_int32, _vp, _vp, _c.POINTER(_vp)]),
+    "mcrt_event_wait": (_c.c_int, [_vp]),
+    "mcrt_event_destroy": (_c.c_int, [_vp]),
     "mcrt_framebuffer_create": (_c.c_int, [_vp, _c.c_uint32, _c.c_uint32, _c.POINTER(_vp)]),
     "mcrt_framebuffer_destroy": (_c.c_int, [_vp]),
     "mcrt_framebuffer_set_frames_in_flight": (_c.c_int, [_vp, _c.c_int32]),
@@ -193,6 +197,14 @@ def accel_opts(cost=10.0, bins=64, sah=True, device_build=False, force_2level=Fa
                        1 if force_flat else 0, w2l)
 
 
+def event_wait(ev):
+    _check(lib().mcrt_event_wait(ev))
+
+
+def event_destroy(ev):
+    _check(lib().mcrt_event_destroy(ev))
+
+
 def build_host_records(scene, **opts):
     """Host-only build (no GPU): (records float32 (n, 16), info dict) of the structure
     mcrt_accel_build would upload for `scene` (mcrt.scenes.Scene)."""
@@ -271,6 +283,17 @@ class DeviceScene:
 
     def trace_any(self, rays_dev_ptr, n, out_dev_ptr):
         _check(lib().mcrt_trace_any(self.h, rays_dev_ptr, n, out_dev_ptr), self.ctx.h)
+
+    def trace_count(self, any_hit, rays_dev_ptr, count_dev_ptr, maxrays, out_dev_ptr, wait_event=None,
+                    want_event=False):
+        """mcrt_trace_closest_count / mcrt_trace_any_count: min(*count, maxrays) rays, the count in
+        device memory; waits for wait_event; returns the done event (a handle for event_wait /
+        event_destroy) when want_event."""
+        ev = _vp()
+        f = lib().mcrt_trace_any_count if any_hit else lib().mcrt_trace_closest_count
+        _check(f(self.h, rays_dev_ptr, count_dev_ptr, maxrays, out_dev_ptr, wait_event,
+                 _c.byref(ev) if want_event else None), self.ctx.h)
+        return ev.value if want_event else None
 
     def close(self):
         if self.h:

@@ -26,6 +26,13 @@ extern "C" {
         }                                                               \
     } while (0)
 
+// the harness links the host sources without mcrt_capi.cpp: its error-text store
+static std::string g_err;
+namespace mcrt {
+void set_last_error(const std::string& m) { g_err = m; }
+}
+extern "C" const char* mcrt_last_error(mcrt_ctx) { return g_err.c_str(); }
+
 static void write_file(const std::string& p, const char* text) {
     FILE* f = std::fopen(p.c_str(), "w");
     std::fputs(text, f);
@@ -65,6 +72,34 @@ int main() {
     // a missing file is an error, not a crash
     mcrt_obj_scene bad = nullptr;
     CHECK(mcrt_obj_load((d + "/missing.obj").c_str(), 0, &bad) != MCRT_OK);
+    // malformed face references are rejected at parse time (no read outside v / vt / vn)
+    const char* badFaces[] = {"v 0 0 0\nv 1 0 0\nv 0 1 0\nf 0 1 2\n",            // index 0
+                              "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 4\n",            // past the end
+                              "v 0 0 0\nv 1 0 0\nv 0 1 0\nf -1 -2 -4\n",         // before the start
+                              "v 0 0 0\nv 1 0 0\nv 0 1 0\nvt 0 0\nf 1/2 2/1 3/1\n",   // vt past the end
+                              "v 0 0 0\nv 1 0 0\nv 0 1 0\nvn 0 0 1\nf 1//1 2//1 3//-2\n",   // vn before the start
+                              "f 1 2 3\nv 0 0 0\nv 1 0 0\nv 0 1 0\n",            // forward reference
+                              "v 0 0 0\nv 1 0 0\nv 0 1 0\nf x 2 3\n"};           // not a number
+    for (const char* text : badFaces) {
+        write_file(d + "/bad.obj", text);
+        bad = nullptr;
+        CHECK(mcrt_obj_load((d + "/bad.obj").c_str(), 0, &bad) == MCRT_ERROR_INVALID_ARG && bad == nullptr);
+        CHECK(std::strstr(mcrt_last_error(nullptr), "out of range") != nullptr);
+    }
+    // a PNG whose IHDR chunk is truncated: the texture is skipped with a warning
+    {
+        const unsigned char png[] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n', 0, 0, 0, 4, 'I', 'H', 'D', 'R',
+                                     0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 'I', 'E', 'N', 'D', 0, 0, 0, 0};
+        FILE* f = std::fopen((d + "/t.png").c_str(), "wb");
+        std::fwrite(png, 1, sizeof(png), f);
+        std::fclose(f);
+        write_file(d + "/t.mtl", "newmtl m\nKd 1 1 1\nmap_Kd t.png\n");
+        write_file(d + "/t.obj", "mtllib t.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nusemtl m\nf 1 2 3\n");
+        mcrt_obj_scene ts = nullptr;
+        CHECK(mcrt_obj_load((d + "/t.obj").c_str(), 0, &ts) == MCRT_OK);
+        CHECK(std::strstr(mcrt_obj_warnings(ts), "IHDR") != nullptr);
+        mcrt_obj_free(ts);
+    }
 
     // oracle: BVH, traversal vs brute force, PT + BDPT frames, accumulate, post-process
     orc_scene* s = orc_scene_create(&desc);

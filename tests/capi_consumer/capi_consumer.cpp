@@ -153,6 +153,37 @@ int main(int argc, char** argv) {
         size_t nhit = 0;
         for (auto& h : hits) nhit += h.shapeid >= 0;
 
+        // ---- the device-count queries (QueryIntersection / QueryOcclusion with numrays in remote
+        // memory and events, radeon_rays.h:272-277): k = N/2 + 37 rays of a grid for N; the second
+        // query waits for the first's event; records past k stay untouched -------------------------
+        int countMatch = 1;
+        {
+            const int32_t k = (int32_t)(N / 2 + 37);
+            int32_t* dCount = nullptr;
+            hipCheck(hipMalloc(&dCount, sizeof(int32_t)));
+            hipCheck(hipMemcpy(dCount, &k, sizeof(int32_t), hipMemcpyHostToDevice));
+            hipCheck(hipMemset(dHits, 0xff, sizeof(mcrt_intersection) * N));
+            hipCheck(hipMemset(dOccl, 0x7f, sizeof(int32_t) * N));
+            mcrt_event e1 = nullptr, e2 = nullptr;
+            check(mcrt_trace_closest_count(scene, dRays, dCount, (int32_t)N, dHits, nullptr, &e1), ctx);
+            check(mcrt_trace_any_count(scene, dRays, dCount, (int32_t)N, dOccl, e1, &e2), ctx);
+            check(mcrt_event_wait(e2), ctx);
+            std::vector<mcrt_intersection> h2(N);
+            std::vector<int32_t> o2(N);
+            hipCheck(hipMemcpy(h2.data(), dHits, sizeof(mcrt_intersection) * N, hipMemcpyDeviceToHost));
+            hipCheck(hipMemcpy(o2.data(), dOccl, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < N; ++i) {
+                mcrt_intersection sentinel;
+                std::memset(&sentinel, 0xff, sizeof(sentinel));
+                const bool in = (int32_t)i < k;
+                if (std::memcmp(&h2[i], in ? &hits[i] : &sentinel, sizeof(mcrt_intersection)) != 0) countMatch = 0;
+                if (o2[i] != (in ? occl[i] : 0x7f7f7f7f)) countMatch = 0;
+            }
+            check(mcrt_event_destroy(e1), ctx);
+            check(mcrt_event_destroy(e2), ctx);
+            (void)hipFree(dCount);
+        }
+
         // ---- RTPathTracingPass::update + RTReconstructionPass::updateReconstruction ----------
         mcrt_framebuffer fb = nullptr;
         check(mcrt_framebuffer_create(ctx, cam.width, cam.height, &fb), ctx);
@@ -189,7 +220,8 @@ int main(int argc, char** argv) {
         double mean = 0.0;
         for (size_t i = 0; i < N; ++i) mean += image[4 * i] + image[4 * i + 1] + image[4 * i + 2];
         std::printf("{\"pixels\": %zu, \"closest_hits\": %zu, \"image_mean\": %.6f, \"error_caught\": %d, "
-                    "\"version\": \"%s\"}\n", N, nhit, mean / (3.0 * N), caught, mcrt_version());
+                    "\"count_queries_match\": %d, \"version\": \"%s\"}\n", N, nhit, mean / (3.0 * N), caught,
+                    countMatch, mcrt_version());
         check(mcrt_framebuffer_destroy(fb), ctx);
         check(mcrt_scene_destroy(scene), ctx);
         (void)hipFree(dRays);

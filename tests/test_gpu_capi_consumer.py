@@ -45,6 +45,8 @@ def test_cpp_consumer_matches_ctypes(hip_ctx, tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     info = json.loads(r.stdout.strip().splitlines()[-1])
     assert info["pixels"] == W * H and info["error_caught"] == 1 and info["closest_hits"] > 0, info
+    # device-count queries with events (radeon_rays.h:272-277) = the host-count ones on the first k rays
+    assert info["count_queries_match"] == 1, info
     out = lambda n, dt: np.fromfile(str(tmp_path / "out" / f"{n}.bin"), dt)   # noqa: E731
     # the same through ctypes
     ds = lib.DeviceScene(hip_ctx, sc)

@@ -164,3 +164,41 @@ def test_traversal_stack_overflow_is_reported(hip_ctx, monkeypatch):
         hip_ctx.sync()
     hip_ctx.sync()   # the flag is cleared once reported
     bad.close()
+
+
+def test_device_count_queries_with_events(hip_ctx):
+    """RR's QueryIntersection / QueryOcclusion with the ray count in device memory and events
+    (radeon_rays.h:272-277): min(*count, maxrays) rays are traced -- bit-identical to the
+    host-count call on those rays -- the rest of the output is untouched; a count above maxrays
+    is clamped; the second query waits on the first's event."""
+    import torch
+    from mcrt import lib
+    sc = scenes.test_scene()
+    n = 5000
+    rays = random_rays(sc, n, seed=3)
+    ds = lib.DeviceScene(hip_ctx, sc)
+    r = torch.from_numpy(rays.view(np.uint8).copy()).cuda()
+    ref_h = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    ref_o = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ds.trace_closest(r.data_ptr(), n, ref_h.data_ptr())
+    ds.trace_any(r.data_ptr(), n, ref_o.data_ptr())
+    hip_ctx.sync()
+    for k in (0, 1, 1234, n, n + 999):
+        cnt = torch.tensor([k], dtype=torch.int32, device="cuda")
+        h = torch.full((n * 32,), 0xAB, dtype=torch.uint8, device="cuda")
+        o = torch.full((n,), -5, dtype=torch.int32, device="cuda")
+        e1 = ds.trace_count(False, r.data_ptr(), cnt.data_ptr(), n, h.data_ptr(), want_event=True)
+        e2 = ds.trace_count(True, r.data_ptr(), cnt.data_ptr(), n, o.data_ptr(), wait_event=e1, want_event=True)
+        lib.event_wait(e2)
+        m = min(k, n)
+        hh, rh = h.cpu().numpy().reshape(n, 32), ref_h.cpu().numpy().reshape(n, 32)
+        np.testing.assert_array_equal(hh[:m], rh[:m])
+        assert (hh[m:] == 0xAB).all()
+        oo, ro = o.cpu().numpy(), ref_o.cpu().numpy()
+        np.testing.assert_array_equal(oo[:m], ro[:m])
+        assert (oo[m:] == -5).all()
+        lib.event_destroy(e1)
+        lib.event_destroy(e2)
+    with pytest.raises(lib.MCRTError):
+        ds.trace_count(False, r.data_ptr(), None, n, ref_h.data_ptr())
+    ds.close()
