@@ -1,8 +1,9 @@
 """Benchmark: Mpaths/s of the MI355X path tracer on the San-Miguel proxy at 1920x1080
 (BASELINE.json metric), PT with maxDepth 2 (the reference default), random sampler.
 `--integrator bdpt` measures the BDPT integrator instead: one path =
-one camera + one light subpath with all their connections; N GPUs split frames (each rank
-renders whole frames f = rank + N*i, "scaling": "weak"), since light-tracing splats land anywhere.
+one camera + one light subpath with all their connections; N GPUs split each frame into 8-row
+bands (light-tracing splats land anywhere: one rank-major reduce-scatter of the splats per frame,
+"scaling": "strong"; --bdpt-split frame: whole frames per rank, "weak").
 
 One step = one 1-spp frame of the whole image (mcrt_render_frame + mcrt_accumulate).
 N GPUs: one process per GPU (torch.distributed.run), the image is tile-split into 8-row bands
@@ -18,7 +19,7 @@ Also reported (one JSON line on rank 0):
                 memory-side bytes per launch from the committed counter summary (profiles/)
   cpu_baseline  the oracle (C restatement of the reference kernels) on a bounded sample of rows of
                 the same frames, all host cores (rank 0, N = 1 only)
-  bdpt          SURVEY config 4's integrator (BDPT) on the same scene: Mpaths/s (frame split over
+  bdpt          SURVEY config 4's integrator (BDPT) on the same scene: Mpaths/s (band split over
                 the ranks), per-kernel times, roofline of its dominant kernel (k_extend) and a CPU
                 baseline of the oracle's BDPT restatement
 """
@@ -188,10 +189,10 @@ def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
         return None
 
 
-def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing, split="frame"):
+def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing, split="band"):
     """Config 4's integrator on the same scene and GPU(s): BDPT (RTBDPTPass::update), 1 spp per
     step, split over the ranks by frames (rank r renders frames r, r + N, ...; light-tracing splats
-    land anywhere in the image) or by 8-row bands (one splat all-reduce per frame,
+    land anywhere in the image) or by 8-row bands (one splat reduce-scatter per frame,
     mcrt.dist.exchange_splats), and the same single reduce of the accumulators.  Returns the
     measured numbers plus an untimed one-slot per-kernel timing pass."""
     import torch
@@ -203,7 +204,10 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     filt = T.make_filter(T.BOX)
     first = [True]
     band = split == "band" and world > 1
-    splat_buf = torch.zeros(4 * W * H, dtype=torch.float32, device="cuda") if band else None
+    if band:   # rank-major splats (chunks of this rank count x 8-row blocks) and this rank's chunk
+        cr = mdist.splat_chunk_rows(H, 8, world)
+        splat_full = torch.zeros(4 * W * cr * world, dtype=torch.float32, device="cuda")
+        splat_own = torch.zeros(4 * W * cr, dtype=torch.float32, device="cuda")
 
     def run(i0, count):
         for i in range(i0, i0 + count):
@@ -211,7 +215,7 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
                 f = i
                 fb.render(ds, cam_of(f), frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT,
                           band_rows=8, num_bands=world, band_index=rank)
-                mdist.exchange_splats(fb, splat_buf)
+                mdist.exchange_splats(fb, splat_full, splat_own)
             else:
                 f = rank + world * i
                 fb.render(ds, cam_of(f), frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT)
@@ -248,7 +252,7 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     out = {"value": round(W * H * steps * (1 if band else world) / el / 1e6, 3), "unit": "Mpaths/s", "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong" if band else "weak",
            "workload": f"same scene {W}x{H}, BDPT, maxDepth {D}, 1 spp per step (SURVEY config 4's integrator), "
-                       + (f"band split x {world} + 1 splat all-reduce per frame + 1 RCCL reduce" if band else
+                       + (f"band split x {world} + 1 splat reduce-scatter per frame + 1 RCCL reduce" if band else
                           f"frame split x {world} + 1 RCCL reduce"),
            "rays_per_path": {"subpath": round(st["closest_rays"] / (W * H), 4),
                              "connection": round(st["any_rays"] / (W * H), 4)}}
@@ -346,10 +350,10 @@ def main():
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     ap.add_argument("--no-bdpt", action="store_true", help="skip the BDPT object (config 4) of the PT run")
     ap.add_argument("--bdpt-steps", type=int, default=8, help="timed BDPT frames of the BDPT object")
-    ap.add_argument("--bdpt-split", default="frame", choices=["frame", "band"],
-                    help="multi-GPU BDPT: whole frames per rank (no per-frame exchange; each rank's sampled-light "
-                         "history differs, BDPT.cl:585) or 8-row bands per rank with one splat all-reduce per frame "
-                         "(the 1-GPU image up to splat summation order; mcrt.dist.exchange_splats)")
+    ap.add_argument("--bdpt-split", default="band", choices=["frame", "band"],
+                    help="multi-GPU BDPT: 8-row bands per rank with one splat reduce-scatter per frame (default: "
+                         "the 1-GPU image up to splat summation order; mcrt.dist.exchange_splats) or whole frames "
+                         "per rank (no per-frame exchange; each rank's sampled-light history differs, BDPT.cl:585)")
     ap.add_argument("--save-image", default=None, help="rank 0 saves the final accumulated image (.npy)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the product path); gloo only rehearses N ranks on one GPU")
@@ -425,11 +429,11 @@ def main():
     filt = T.make_filter(T.BOX)
     bdpt = args.integrator == "bdpt"
     band_bdpt = bdpt and args.bdpt_split == "band" and world > 1
-    splat_buf = None
     if band_bdpt:   # band split: every rank renders every frame's rows of its bands
         band = dict(band_rows=8, num_bands=world, band_index=rank, integrator=T.INTEGRATOR_BDPT)
-        import torch
-        splat_buf = torch.zeros(4 * W * H, dtype=torch.float32, device="cuda")
+        cr = mdist.splat_chunk_rows(H, 8, world)
+        splat_full = torch.zeros(4 * W * cr * world, dtype=torch.float32, device="cuda")
+        splat_own = torch.zeros(4 * W * cr, dtype=torch.float32, device="cuda")
     elif bdpt:   # frame split: whole frames per rank
         band = dict(band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_BDPT)
     else:
@@ -451,7 +455,7 @@ def main():
         if n == 1:
             fb.render(ds, cam_of(frame), frame=frame, **kw)
             if band_bdpt:
-                mdist.exchange_splats(fb, splat_buf)
+                mdist.exchange_splats(fb, splat_full, splat_own)
         else:
             fb.render_frames(ds, [cam_of(frame + k) for k in range(n)], frame=frame, **kw)
         fb.accumulate(filt, 0 if first[0] else frame)   # 0: the first accumulation overwrites
@@ -556,7 +560,7 @@ def main():
                            "device LBVH" if args.device_build else
                            "RadeonRays-identical SAH, " + ("host build" if args.host_build else "device build")),
                    "bvh_build_ms": round(info["build_ms"], 1),
-                   "parallelism": (f"band split x {world}, 1 splat all-reduce per frame + 1 RCCL reduce" if band_bdpt
+                   "parallelism": (f"band split x {world}, 1 splat reduce-scatter per frame + 1 RCCL reduce" if band_bdpt
                                    else f"frame split x {world} + 1 RCCL reduce" if bdpt else
                                    f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL "
                                    + ("band gather" if args.end_collective == "gather" else "reduce")),

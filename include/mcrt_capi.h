@@ -235,8 +235,8 @@ typedef struct {
     /* MCRT_INTEGRATOR_PT (0, default) or MCRT_INTEGRATOR_BDPT (RTBDPTPass::update,
      * APP/.../RTBDPTPass.cpp:67-128).  BDPT with num_bands > 1 renders the band's camera and
      * light subpaths; its light-tracing strategies splat into any pixel, so the frame stops after
-     * the visibility pass: the caller sums the ranks' splats (mcrt_bdpt_splats_copy + an
-     * all-reduce) and completes it with mcrt_bdpt_gather. */
+     * the visibility pass: the caller sums the ranks' splats (mcrt_bdpt_splats_copy + a
+     * reduce-scatter) and completes it with mcrt_bdpt_gather. */
     int32_t integrator;
     /* 1: textures at camera-ray hits are read mip-mapped over the pixel footprint (ray
      * differentials, computeSurfaceInteractionWithDifferentials + readTexture2Df_lod +
@@ -483,14 +483,23 @@ MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which,
  *         4: own-strategy contributions ((C-D) planes)   5: persistent s=1 sampled light vertices (D planes)
  *         6: light-tracing (t=1) splat sums of the frame (float4 x W*H)
  * Copies min(bytes, size) bytes; *needed = the array's size (host_dst may be NULL to query it). */
-/* Band-split BDPT (num_bands > 1): copy this rank's light-tracing splats (float4 x W*H, device
- * memory) after synchronising the frame; then mcrt_bdpt_gather with the sum over all ranks
- * (NULL: this rank's own) completes the frame's radiance for the rank's bands (the reference's
- * ConnectVertices atomics + CopyBuffer, BDPT.cl:671-913).  Rendering or accumulating in between
- * fails with MCRT_ERROR_NOT_READY.  With no frame pending (a light-less scene, a whole-image
- * frame) the copy writes zeros and the gather does nothing. */
+/* Band-split BDPT (num_bands > 1): the frame's light-tracing splats land in any pixel, so the ranks
+ * exchange them once per frame (the reference's ConnectVertices atomics + CopyBuffer,
+ * BDPT.cl:671-913).  The splats are laid out RANK-MAJOR: `chunks` (= num_bands) chunks of
+ * `chunk_pixels` float4, chunk r holding the rows of rank r's bands in its own tile order (zero
+ * past its last row), so ONE reduce-scatter hands each rank exactly its rows' sums:
+ *   mcrt_bdpt_splat_layout   the chunk geometry of the last frame's band split;
+ *   mcrt_bdpt_splats_copy    this rank's splats, rank-major, into d_dst (chunks x chunk_pixels
+ *                            float4 of device memory), returning when they are written;
+ *   mcrt_bdpt_gather         completes the rank's bands with d_own_chunk = chunk band_index of the
+ *                            ranks' summed buffers (chunk_pixels float4; NULL: the rank's own splats
+ *                            in its natural layout -- a 1-rank check).  It reads d_own_chunk on the
+ *                            frame's stream; a later mcrt_bdpt_splats_copy waits for it.
+ * Rendering or accumulating in between fails with MCRT_ERROR_NOT_READY.  With no frame pending (a
+ * light-less scene, a whole-image frame) the copy writes zeros and the gather does nothing. */
+MCRT_API mcrt_status mcrt_bdpt_splat_layout(mcrt_framebuffer fb, uint64_t* chunk_pixels, int32_t* chunks);
 MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst);
-MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_splat_sum);
+MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_own_chunk);
 MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, void* host_dst, uint64_t bytes,
                                                 uint64_t* needed);
 

@@ -838,8 +838,11 @@ __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const i
 }
 
 // Own strategies summed in (t, s) order (the reference's per-thread atomicAdd_f order), then the
-// splats; radiance = float4(sum, 0) as CopyBuffer (BDPT.cl:916-932).  Clears the splat buffer.
-__global__ __launch_bounds__(256) void k_bdpt_gather(FrameArgs f, BdptArgs b, float4* __restrict__ radiance) {
+// splats; radiance = float4(sum, 0) as CopyBuffer (BDPT.cl:916-932).  chunk (band split): this
+// rank's rows of the ranks' summed splats in the rank-major layout of k_bdpt_splat_pack (local
+// 8-row block tb of the rank at rows 8 tb .. 8 tb + 7), instead of the rank's own splat buffer.
+__global__ __launch_bounds__(256) void k_bdpt_gather(FrameArgs f, BdptArgs b, float4* __restrict__ radiance,
+                                                     const float4* __restrict__ chunk) {
     const int lane = threadIdx.x & 63;
     const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     int x, y;
@@ -853,8 +856,23 @@ __global__ __launch_bounds__(256) void k_bdpt_gather(FrameArgs f, BdptArgs b, fl
         ry += c.y;
         rz += c.z;
     }
-    const float4 sp = b.splat[pix];
+    const int tb = tile / f.tilesX;
+    const float4 sp = chunk ? chunk[(size_t)(tb * 8 + (lane >> 3)) * f.W + x] : b.splat[pix];
     radiance[pix] = make_float4(rx + sp.x, ry + sp.y, rz + sp.z, 0.0f);
+}
+
+// Band split: the splat buffer (W x H, any pixel) in rank-major order -- chunk r (chunkPixels
+// float4) holds the rows of rank r's bands, its local 8-row block tb (tilePixel's numbering) at
+// rows 8 tb .. 8 tb + 7 -- so ONE reduce-scatter hands every rank the summed splats of exactly its
+// own rows (mcrt.dist.exchange_splats).  Rows past a rank's last block stay zero (memset).
+__global__ __launch_bounds__(256) void k_bdpt_splat_pack(int W, int H, int bpb, int numBands, size_t chunkPixels,
+                                                         const float4* __restrict__ splat, float4* __restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)W * H) return;
+    const int y = (int)(i / W), x = (int)(i - (size_t)y * W);
+    const int gb = y >> 3;
+    const int r = (gb / bpb) % numBands, tb = (gb / (bpb * numBands)) * bpb + gb % bpb;
+    out[(size_t)r * chunkPixels + (size_t)(tb * 8 + (y & 7)) * W + x] = splat[i];
 }
 
 // Splats that land outside the rank's bands (multi-GPU band split): added by the rank that owns
@@ -886,9 +904,14 @@ void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, i
     hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_COMPACT>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks), dim3(64), 0, st, c, b, q.count,
                        q.o, q.d, q.t);
 }
-void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, hipStream_t st) {
+void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, const float4* chunk, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + 255) / 256;
-    hipLaunchKernelGGL(k_bdpt_gather, dim3(blocks), dim3(256), 0, st, f, b, radiance);
+    hipLaunchKernelGGL(k_bdpt_gather, dim3(blocks), dim3(256), 0, st, f, b, radiance, chunk);
+}
+void launch_bdpt_splat_pack(const FrameArgs& f, size_t chunkPixels, const float4* splat, float4* out, hipStream_t st) {
+    const size_t n = (size_t)f.W * f.H;
+    hipLaunchKernelGGL(k_bdpt_splat_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (int)f.W, (int)f.H,
+                       f.bandRows >> 3, f.numBands, chunkPixels, splat, out);
 }
 void launch_bdpt_clear_splat(int n, float4* splat, hipStream_t st) {
     hipLaunchKernelGGL(k_bdpt_clear_splat, dim3((n + 255) / 256), dim3(256), 0, st, n, splat);

@@ -1397,7 +1397,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         fb->bdptPendingGather = true;
     } else {
         Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)f.numTiles * 64, st);
-        mcrt::launch_bdpt_gather(f, b, fb->radiance, st);
+        mcrt::launch_bdpt_gather(f, b, fb->radiance, nullptr, st);
     }
     HIPCHK(ctx, hipGetLastError());
     fb->lastPixels = (int64_t)f.numTiles * 64;
@@ -1777,36 +1777,60 @@ MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which,
     return MCRT_OK;
 }
 
-MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst) {
-    if (!fb || !d_dst) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
-    mcrt_ctx ctx = fb->ctx;
-    hipSetDevice(ctx->device);
-    if (!fb->bdptPendingGather) {   // e.g. a scene without lights: the frame is complete, no splats
-        HIPCHK(ctx, hipMemset(d_dst, 0, 16 * fb->N));
-        return MCRT_OK;
+// Rank-major splat layout of a band split of H rows into num_bands interleaved sets of band_rows
+// rows: chunks = num_bands, each of (the largest rank's 8-row block count) x 8 rows x W pixels.
+static size_t splat_chunk_pixels(const FrameArgs& f) {
+    const int blocksTotal = (int)((f.H + 7) / 8), bpb = f.bandRows / 8;
+    int maxBlocks = 0;
+    for (int r = 0; r < f.numBands; ++r) {
+        int nb = 0;
+        for (int gb = 0; gb < blocksTotal; ++gb) nb += ((gb / bpb) % f.numBands == r) ? 1 : 0;
+        maxBlocks = std::max(maxBlocks, nb);
     }
-    FrameSlot& slot = fb->slot[fb->cur];
-    HIPCHK(ctx, hipStreamSynchronize(slot.stream));
-    HIPCHK(ctx, hipMemcpy(d_dst, fb->splat, 16 * fb->N, hipMemcpyDeviceToDevice));
+    return (size_t)maxBlocks * 8 * f.W;
+}
+
+MCRT_API mcrt_status mcrt_bdpt_splat_layout(mcrt_framebuffer fb, uint64_t* chunk_pixels, int32_t* chunks) {
+    if (!fb || !chunk_pixels || !chunks) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    if (!fb->haveBands) return fail(fb->ctx, MCRT_ERROR_NOT_READY, "no frame rendered yet");
+    *chunk_pixels = splat_chunk_pixels(fb->bands);
+    *chunks = fb->bands.numBands;
     return MCRT_OK;
 }
 
-MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_splat_sum) {
+MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst) {
+    if (!fb || !d_dst) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    mcrt_ctx ctx = fb->ctx;
+    if (!fb->haveBands) return fail(ctx, MCRT_ERROR_NOT_READY, "no frame rendered yet");
+    hipSetDevice(ctx->device);
+    const size_t chunk = splat_chunk_pixels(fb->bands), total = chunk * (size_t)fb->bands.numBands;
+    FrameSlot& slot = fb->slot[fb->cur];
+    hipStream_t st = slot.stream ? slot.stream : ctx->stream;
+    // the caller's buffer may still be read by an earlier frame's gather on another slot's stream
+    for (auto& k : fb->slot)
+        if (k.stream && k.stream != st) HIPCHK(ctx, hipStreamWaitEvent(st, k.done, 0));
+    HIPCHK(ctx, hipMemsetAsync(d_dst, 0, 16 * total, st));
+    if (fb->bdptPendingGather)   // (else, e.g. a scene without lights: the frame is complete, no splats)
+        mcrt::launch_bdpt_splat_pack(fb->bands, chunk, fb->splat, (float4*)d_dst, st);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipStreamSynchronize(st));   // the collective reads d_dst on another stream next
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_own_chunk) {
     if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
     mcrt_ctx ctx = fb->ctx;
     if (!fb->bdptPendingGather) return MCRT_OK;   // nothing deferred (whole-image or light-less frame)
     hipSetDevice(ctx->device);
     FrameSlot& slot = fb->slot[fb->cur];
     hipStream_t st = slot.stream;
-    if (d_splat_sum && d_splat_sum != fb->splat)
-        HIPCHK(ctx, hipMemcpyAsync(fb->splat, d_splat_sum, 16 * fb->N, hipMemcpyDeviceToDevice, st));
     BdptArgs b{};
     b.slots = fb->slots;
     b.splat = fb->splat;
     b.ownSlots = bdpt_max_connections(fb->bdptDepth) - fb->bdptDepth;
     {
         Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)fb->bands.numTiles * 64, st);
-        mcrt::launch_bdpt_gather(fb->bands, b, fb->radiance, st);
+        mcrt::launch_bdpt_gather(fb->bands, b, fb->radiance, (const float4*)d_own_chunk, st);
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(slot.done, st));

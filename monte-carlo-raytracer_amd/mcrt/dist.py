@@ -42,26 +42,65 @@ def band_rows_of(height, band_rows, num_bands, band_index):
     return rows[rows < height]
 
 
-def exchange_splats(fb, buf, group=None):
-    """Band-split BDPT (mcrt_frame_params.num_bands > 1): the frame's light-tracing strategies
-    splat into any pixel of the image, so after each rank rendered its bands the ranks' splat
-    buffers (float4 x W*H) are summed with ONE all-reduce and every rank completes its bands
-    with the sum (mcrt_bdpt_splats_copy / mcrt_bdpt_gather).  Each pixel's camera subpath, light
-    subpath and persistent sampled-light vertex (BDPT.cl:585-586) stay on the rank that owns the
-    pixel, so the N-rank frame equals the 1-GPU frame up to the order of the splat sums (which
-    the reference's own CAS atomics leave open).  buf: a float32 tensor of 4 * W * H on the GPU."""
-    import torch
+def splat_chunk_rows(height, band_rows, num_bands):
+    """Rows of one chunk of the rank-major splat layout (mcrt_bdpt_splat_layout): the largest
+    rank's 8-row block count x 8."""
+    return max(len(band_blocks(height, band_rows, num_bands, r)) for r in range(num_bands)) * 8
+
+
+def rank_major_pack(img, band_rows, num_bands):
+    """(H, W, C) -> (num_bands, chunk_rows, W, C): chunk r = rank r's rows in its tile order
+    (band_rows_of), zero past its last row -- the layout k_bdpt_splat_pack writes."""
+    H = img.shape[0]
+    cr = splat_chunk_rows(H, band_rows, num_bands)
+    out = np.zeros((num_bands, cr) + img.shape[1:], img.dtype)
+    for r in range(num_bands):
+        rows = band_rows_of(H, band_rows, num_bands, r)
+        out[r, :len(rows)] = img[rows]
+    return out
+
+
+def reduce_scatter_chunks(full, chunk, group=None):
+    """chunk <- sum over ranks of chunk `rank` of `full` (ONE reduce-scatter: every xGMI link
+    carries 1/N of the frame; float32 tensors, full = N x chunk).  gloo has no reduce-scatter:
+    an all-reduce of a host copy, then the rank's slice (the CPU tests and the one-GPU rehearsal)."""
     import torch.distributed as dist
-    fb.bdpt_splats_copy(buf.data_ptr())
-    if buf.is_cuda and dist.get_backend(group) == "gloo":   # gloo rehearsal: via a host copy
-        h = buf.cpu()
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    n = chunk.numel()
+    if full.numel() != world * n:
+        raise ValueError("full buffer must hold world x chunk elements")
+    if dist.get_backend(group) == "gloo":
+        h = full.cpu() if full.is_cuda else full.clone()
         dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
-        buf.copy_(h)
+        chunk.copy_(h[rank * n:(rank + 1) * n])
     else:
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-    if buf.is_cuda:
-        torch.cuda.current_stream(buf.device).synchronize()
-    fb.bdpt_gather(buf.data_ptr())
+        dist.reduce_scatter_tensor(chunk, full, op=dist.ReduceOp.SUM, group=group)
+
+
+def splat_buffers(fb, device="cuda"):
+    """The two device buffers of exchange_splats for frame buffer fb after a band-split frame:
+    (full rank-major buffer, own chunk), float32."""
+    import torch
+    cp, chunks = fb.bdpt_splat_layout()
+    return (torch.zeros(4 * cp * chunks, dtype=torch.float32, device=device),
+            torch.zeros(4 * cp, dtype=torch.float32, device=device))
+
+
+def exchange_splats(fb, full, chunk, group=None):
+    """Band-split BDPT (mcrt_frame_params.num_bands > 1): the frame's light-tracing strategies
+    splat into any pixel of the image, so after each rank rendered its bands the ranks' splats are
+    exchanged once: each rank writes its splats rank-major (mcrt_bdpt_splats_copy: chunk r = the
+    rows of rank r's bands), ONE reduce-scatter hands every rank the sums of its own rows, and the
+    rank completes its bands with them (mcrt_bdpt_gather).  Each pixel's camera subpath, light
+    subpath and persistent sampled-light vertex (BDPT.cl:585-586) stay on the rank that owns the
+    pixel, so the N-rank frame equals the 1-GPU frame up to the order of the splat sums (which the
+    reference's own CAS atomics leave open).  full, chunk: from splat_buffers."""
+    import torch
+    fb.bdpt_splats_copy(full.data_ptr())
+    reduce_scatter_chunks(full, chunk, group)
+    if chunk.is_cuda:
+        torch.cuda.current_stream(chunk.device).synchronize()
+    fb.bdpt_gather(chunk.data_ptr())
 
 
 def frame_split(num_frames, world, rank):

@@ -44,6 +44,7 @@ SIGNATURES = {
     "mcrt_accel_layout": (_c.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "mcrt_accel_builder": (_c.c_int, [_vp, _vp]),
     "mcrt_bdpt_splats_copy": (_c.c_int, [_vp, _vp]),
+    "mcrt_bdpt_splat_layout": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_int32)]),
     "mcrt_bdpt_gather": (_c.c_int, [_vp, _vp]),
     "mcrt_obj_load": (_c.c_int, [_c.c_char_p, _c.c_uint32, _vp]),
     "mcrt_obj_add_directional_light": (_c.c_int, [_vp, _vp, _vp]),
@@ -380,13 +381,21 @@ class FrameBuffer:
     def copy_device(self, which, dst_ptr):
         _check(lib().mcrt_framebuffer_copy_device(self.h, which, dst_ptr), self.ctx.h)
 
+    def bdpt_splat_layout(self):
+        """(chunk_pixels, chunks) of the rank-major splat layout of the last band split."""
+        cp, ch = _c.c_uint64(), _c.c_int32()
+        _check(lib().mcrt_bdpt_splat_layout(self.h, _c.byref(cp), _c.byref(ch)), self.ctx.h)
+        return cp.value, ch.value
+
     def bdpt_splats_copy(self, dst_ptr):
-        """Band-split BDPT: this rank's light-tracing splats (float4 x W*H) into device memory."""
+        """Band-split BDPT: this rank's light-tracing splats, rank-major (chunks x chunk_pixels
+        float4), into device memory."""
         _check(lib().mcrt_bdpt_splats_copy(self.h, dst_ptr), self.ctx.h)
 
-    def bdpt_gather(self, splat_sum_ptr=None):
-        """Completes a band-split BDPT frame with the ranks' summed splats (None: own splats)."""
-        _check(lib().mcrt_bdpt_gather(self.h, splat_sum_ptr), self.ctx.h)
+    def bdpt_gather(self, own_chunk_ptr=None):
+        """Completes a band-split BDPT frame with this rank's chunk of the summed splats (None:
+        the rank's own splats)."""
+        _check(lib().mcrt_bdpt_gather(self.h, own_chunk_ptr), self.ctx.h)
 
     def set_accumulation(self, wsum_ptr, wts_ptr):
         _check(lib().mcrt_framebuffer_set_accumulation(self.h, wsum_ptr, wts_ptr), self.ctx.h)

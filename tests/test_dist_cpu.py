@@ -169,9 +169,9 @@ def test_two_rank_frame_split_matches_single_process(tmp_path):
 
 def _bdpt_band_worker(rank, world, port, out_path):
     """Band-split BDPT with the oracle's BDPT: rank r renders the subpaths of its bands (its
-    splats land anywhere), the ranks' radiance buffers are summed with ONE all-reduce per frame
-    (own strategies are non-zero only on the owner's rows), and the per-rank sampled-light state
-    persists across frames on the owner."""
+    splats land anywhere), the ranks' radiance buffers are laid out rank-major and summed with ONE
+    reduce-scatter per frame (mcrt.dist.reduce_scatter_chunks; own strategies are non-zero only on
+    the owner's rows), and the per-rank sampled-light state persists across frames on the owner."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -184,8 +184,15 @@ def _bdpt_band_worker(rank, world, port, out_path):
     out = {}
     for f in range(FRAMES):
         rad, cc, _, _ = b.render(cam, frame=f, rows=rows, threads=2)
-        t = torch.from_numpy(rad.reshape(-1).copy())
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        # the product's exchange: rank-major chunks, ONE reduce-scatter -> this rank's rows
+        full = torch.from_numpy(mdist.rank_major_pack(rad, BAND_ROWS, world).reshape(-1).copy())
+        chunk = torch.zeros(full.numel() // world, dtype=torch.float32)
+        mdist.reduce_scatter_chunks(full, chunk)
+        own = chunk.numpy().reshape(-1, W, 4)[:len(rows)]
+        img = np.zeros((H, W, 4), np.float32)
+        img[rows] = own
+        t = torch.from_numpy(img.reshape(-1).copy())
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)   # (test only: assemble the image on every rank)
         cct = torch.from_numpy(cc.copy())
         dist.all_reduce(cct, op=dist.ReduceOp.SUM)   # counts are zero off the owner's rows
         out[f"rad{f}"] = t.numpy().reshape(H, W, 4)
@@ -196,9 +203,11 @@ def _bdpt_band_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_bdpt_band_split_matches_whole_frames(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_bdpt_band_split_matches_whole_frames(tmp_path, world):
     out = str(tmp_path / "bdpt.npz")
-    mp.start_processes(_bdpt_band_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_bdpt_band_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
     z = np.load(out)
     sc = scenes.test_scene(n_sphere=12)
     o = po.OracleScene(sc)
@@ -210,3 +219,21 @@ def test_bdpt_band_split_matches_whole_frames(tmp_path):
         np.testing.assert_array_equal(z[f"cc{f}"], cc)   # every subpath, on exactly one rank
         d = np.abs(z[f"rad{f}"][..., :3].astype(np.float64) - rad[..., :3])
         assert (d <= 1e-5 * np.maximum(1.0, np.abs(rad[..., :3]))).all(), f   # splat sum order only
+
+
+@pytest.mark.parametrize("height,band_rows,world", [(36, 8, 2), (64, 8, 3), (1080, 8, 8), (1080, 16, 3), (100, 24, 4)])
+def test_rank_major_splat_layout(height, band_rows, world):
+    """The rank-major splat layout of the BDPT band split (k_bdpt_splat_pack): chunk r holds exactly
+    rank r's rows (band_rows_of order) then zeros; every row of the image lands in one chunk."""
+    W = 5
+    img = np.arange(height * W * 2, dtype=np.float32).reshape(height, W, 2) + 1
+    packed = mdist.rank_major_pack(img, band_rows, world)
+    cr = mdist.splat_chunk_rows(height, band_rows, world)
+    assert packed.shape == (world, cr, W, 2)
+    seen = np.zeros(height, int)
+    for r in range(world):
+        rows = mdist.band_rows_of(height, band_rows, world, r)
+        np.testing.assert_array_equal(packed[r, :len(rows)], img[rows])
+        assert (packed[r, len(rows):] == 0).all()
+        seen[rows] += 1
+    assert (seen == 1).all()

@@ -183,9 +183,10 @@ def test_bdpt_frames_in_flight(hip_ctx):
 @pytest.mark.parametrize("ranks", [2, 3])
 def test_bdpt_band_split_matches_whole_frames(hip_ctx, ranks):
     """Band-split BDPT (multi-GPU, emulated on one GPU with one framebuffer per rank): rank r
-    renders the camera and light subpaths of its 8-row bands; the ranks' splat buffers are summed
-    (the all-reduce of mcrt.dist.exchange_splats, in rank order here) and every rank completes its
-    bands with mcrt_bdpt_gather; the accumulators are summed at the end.  Against whole frames in
+    renders the camera and light subpaths of its 8-row bands; the ranks' rank-major splat buffers
+    are summed (mcrt.dist.exchange_splats' reduce-scatter, in rank order here) and every rank
+    completes its bands with ITS chunk of the sum (mcrt_bdpt_gather); the accumulators are summed
+    at the end.  Against whole frames in
     one framebuffer, over 5 frames (the sampled-light state, BDPT.cl:585-586, persists on the
     pixel's owner):
       * camera / light vertex counts and the sampled-light planes of every pixel: bit-exact;
@@ -201,7 +202,8 @@ def test_bdpt_band_split_matches_whole_frames(hip_ctx, ranks):
     full = lib.FrameBuffer(hip_ctx, W, H)
     fbs = [lib.FrameBuffer(hip_ctx, W, H) for _ in range(ranks)]
     rows = [mdist.band_rows_of(H, 8, ranks, r) for r in range(ranks)]
-    bufs = [torch.zeros(4 * W * H, dtype=torch.float32, device="cuda") for _ in range(ranks)]
+    cr = mdist.splat_chunk_rows(H, 8, ranks)
+    bufs = [torch.zeros(4 * W * cr * ranks, dtype=torch.float32, device="cuda") for _ in range(ranks)]
     N = W * H
     for f in range(frames):
         full.render(ds, cam, frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT)
@@ -211,13 +213,21 @@ def test_bdpt_band_split_matches_whole_frames(hip_ctx, ranks):
                       band_index=r)
             with pytest.raises(lib.MCRTError):   # the frame is not complete before the exchange
                 fb.accumulate(filt, f)
+            assert fb.bdpt_splat_layout() == (cr * W, ranks)
             fb.bdpt_splats_copy(bufs[r].data_ptr())
         total = bufs[0].clone()
         for r in range(1, ranks):
             total += bufs[r]
+        if f == 0:   # the rank-major layout: chunk r = rank r's rows of the summed splat image
+            img = np.zeros((H, W, 4), np.float32)
+            for fb in fbs:
+                img += fb.read_bdpt("splat").view(np.float32).reshape(H, W, 4)
+            np.testing.assert_allclose(total.cpu().numpy().reshape(ranks, cr, W, 4),
+                                       mdist.rank_major_pack(img, 8, ranks), rtol=1e-6, atol=1e-30)
+        chunks = [total[r * 4 * W * cr:(r + 1) * 4 * W * cr].clone() for r in range(ranks)]
         torch.cuda.synchronize()
-        for fb in fbs:
-            fb.bdpt_gather(total.data_ptr())
+        for r, fb in enumerate(fbs):
+            fb.bdpt_gather(chunks[r].data_ptr())
             fb.accumulate(filt, f)
         ref = full.read(0)
         for r, fb in enumerate(fbs):

@@ -3,7 +3,10 @@
 For N in --ns, renders K frames of each rank's bands (band_index = r of num_bands = N) one rank
 at a time on cuda:0 and reports the slowest rank's ms/frame next to the 1-GPU ms/frame.  The
 ratio is the compute part of the strong-scaling efficiency (the final RCCL reduce and the
-launch gaps of concurrent processes are not in it).  Prints one JSON line.
+launch gaps of concurrent processes are not in it).  --integrator bdpt: the band-split BDPT frame
+of each rank (render, rank-major splat pack, gather of its own chunk) and the bytes of the one
+splat reduce-scatter per frame, against the full-frame all-reduce it replaced.  Prints one JSON
+line.
 """
 import argparse
 import json
@@ -26,6 +29,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1, help="frames per mcrt_render_frames call (0 = N)")
     ap.add_argument("--chunks", default="", help="frames per call, cycled, each rounded down to a power of two "
                                                  "(bench.py's plan; overrides --batch)")
+    ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     ap.add_argument("--base-ms", type=float, default=None,
                     help="1-GPU ms/frame (the efficiency base) when --ns does not include 1")
     args = ap.parse_args()
@@ -40,7 +44,11 @@ def main():
     fb = lib.FrameBuffer(ctx, W, H)
     filt = T.make_filter(T.BOX)
     fb.set_frames_in_flight(args.fif)
-    out = {"fif": args.fif, "batch": args.batch, "chunks": args.chunks, "scene": args.scene, "steps": args.steps, "band_rows": args.band_rows, "per_n": {}}
+    out = {"fif": args.fif, "batch": args.batch, "chunks": args.chunks, "scene": args.scene, "steps": args.steps,
+           "band_rows": args.band_rows, "integrator": args.integrator, "per_n": {}}
+    if args.integrator == "bdpt":
+        bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out)
+        return
     for n in [int(x) for x in args.ns.split(",")]:
         per_rank = []
         for r in range(n):
@@ -73,6 +81,51 @@ def main():
                            "min_ms": round(min(per_rank), 4)}
     # efficiency is relative to ONE GPU rendering the whole image: the N = 1 run of this sweep, or
     # --base-ms from a separate N = 1 run (never the smallest N of the sweep, which may be > 1)
+    base = out["per_n"][1]["max_ms"] if 1 in out["per_n"] else args.base_ms
+    out["base_ms_n1"] = base
+    for n, v in out["per_n"].items():
+        v["compute_eff"] = round(base / (n * v["max_ms"]), 4) if base else None
+    print(json.dumps(out), flush=True)
+    fb.close()
+    ds.close()
+    ctx.close()
+
+
+def bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out):
+    """Band-split BDPT per rank: render the rank's bands, pack its splats rank-major, complete its
+    rows from its own chunk (the values do not matter for the timing), accumulate."""
+    import torch
+    from mcrt import dist as mdist
+    from mcrt import types as T
+    for n in [int(x) for x in args.ns.split(",")]:
+        per_rank = []
+        cr = mdist.splat_chunk_rows(H, args.band_rows, n)
+        full = torch.zeros(4 * W * cr * n, dtype=torch.float32, device="cuda")
+        for r in range(n):
+            band = dict(band_rows=args.band_rows, num_bands=n, band_index=r, integrator=T.INTEGRATOR_BDPT)
+            own = full[r * 4 * W * cr:(r + 1) * 4 * W * cr]
+
+            def run(f0, count):
+                for i in range(count):
+                    fb.render(ds, cams[(f0 + i) % 64], frame=f0 + i, max_depth=2, **band)
+                    if n > 1:
+                        fb.bdpt_splats_copy(full.data_ptr())
+                        fb.bdpt_gather(own.data_ptr())
+                    fb.accumulate(filt, f0 + i)
+            run(0, 3)
+            ctx.sync()
+            t0 = time.perf_counter()
+            run(16, args.steps)
+            ctx.sync()
+            per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
+        full_bytes = 16 * W * cr * n
+        out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
+                           "min_ms": round(min(per_rank), 4),
+                           "splat_exchange": {"reduce_scatter_in_bytes_per_rank": full_bytes if n > 1 else 0,
+                                              "reduce_scatter_out_bytes_per_rank": full_bytes // n if n > 1 else 0,
+                                              "ring_bytes_per_link": (n - 1) * full_bytes // n if n > 1 else 0,
+                                              "allreduce_ring_bytes_per_link_before": 2 * (n - 1) * 16 * W * H // n
+                                              if n > 1 else 0}}
     base = out["per_n"][1]["max_ms"] if 1 in out["per_n"] else args.base_ms
     out["base_ms_n1"] = base
     for n, v in out["per_n"].items():
