@@ -490,7 +490,9 @@ MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which,
  * past its last row), so ONE reduce-scatter hands each rank exactly its rows' sums:
  *   mcrt_bdpt_splat_layout   the chunk geometry of the last frame's band split;
  *   mcrt_bdpt_splats_copy    this rank's splats, rank-major, into d_dst (chunks x chunk_pixels
- *                            float4 of device memory), returning when they are written;
+ *                            float4 of device memory), ENQUEUED on the frame's stream
+ *                            (mcrt_framebuffer_stream): order the collective after it there (no
+ *                            host synchronisation, so frames in flight keep overlapping);
  *   mcrt_bdpt_gather         completes the rank's bands with d_own_chunk = chunk band_index of the
  *                            ranks' summed buffers (chunk_pixels float4; NULL: the rank's own splats
  *                            in its natural layout -- a 1-rank check).  It reads d_own_chunk on the
@@ -498,6 +500,8 @@ MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which,
  * Rendering or accumulating in between fails with MCRT_ERROR_NOT_READY.  With no frame pending (a
  * light-less scene, a whole-image frame) the copy writes zeros and the gather does nothing. */
 MCRT_API mcrt_status mcrt_bdpt_splat_layout(mcrt_framebuffer fb, uint64_t* chunk_pixels, int32_t* chunks);
+/* The HIP stream (hipStream_t) the last frame of fb was enqueued on (its frame slot's). */
+MCRT_API mcrt_status mcrt_framebuffer_stream(mcrt_framebuffer fb, void** stream);
 MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst);
 MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_own_chunk);
 MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, void* host_dst, uint64_t bytes,

@@ -1813,7 +1813,13 @@ MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst) {
     if (fb->bdptPendingGather)   // (else, e.g. a scene without lights: the frame is complete, no splats)
         mcrt::launch_bdpt_splat_pack(fb->bands, chunk, fb->splat, (float4*)d_dst, st);
     HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipStreamSynchronize(st));   // the collective reads d_dst on another stream next
+    return MCRT_OK;   // enqueued on the frame's stream (mcrt_framebuffer_stream): no host sync
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_stream(mcrt_framebuffer fb, void** stream) {
+    if (!fb || !stream) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    const FrameSlot& slot = fb->slot[fb->cur];
+    *stream = (void*)(slot.stream ? slot.stream : fb->ctx->stream);
     return MCRT_OK;
 }
 

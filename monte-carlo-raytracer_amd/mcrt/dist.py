@@ -96,10 +96,18 @@ def exchange_splats(fb, full, chunk, group=None):
     pixel, so the N-rank frame equals the 1-GPU frame up to the order of the splat sums (which the
     reference's own CAS atomics leave open).  full, chunk: from splat_buffers."""
     import torch
-    fb.bdpt_splats_copy(full.data_ptr())
-    reduce_scatter_chunks(full, chunk, group)
-    if chunk.is_cuda:
-        torch.cuda.current_stream(chunk.device).synchronize()
+    import torch.distributed as dist
+    fb.bdpt_splats_copy(full.data_ptr())   # enqueued on the frame's stream
+    if full.is_cuda and dist.get_backend(group) != "gloo":
+        # RCCL: the collective is ordered after the pack on the frame's own stream, and the gather
+        # (the same stream) after the collective -- no host synchronisation in the exchange
+        s = torch.cuda.ExternalStream(fb.stream(), device=full.device)
+        with torch.cuda.stream(s):
+            reduce_scatter_chunks(full, chunk, group)
+    else:   # gloo rehearsal / CPU: through the host
+        if full.is_cuda:
+            torch.cuda.synchronize(full.device)
+        reduce_scatter_chunks(full, chunk, group)
     fb.bdpt_gather(chunk.data_ptr())
 
 

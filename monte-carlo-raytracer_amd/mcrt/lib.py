@@ -45,6 +45,7 @@ SIGNATURES = {
     "mcrt_accel_builder": (_c.c_int, [_vp, _vp]),
     "mcrt_bdpt_splats_copy": (_c.c_int, [_vp, _vp]),
     "mcrt_bdpt_splat_layout": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_int32)]),
+    "mcrt_framebuffer_stream": (_c.c_int, [_vp, _c.POINTER(_vp)]),
     "mcrt_bdpt_gather": (_c.c_int, [_vp, _vp]),
     "mcrt_obj_load": (_c.c_int, [_c.c_char_p, _c.c_uint32, _vp]),
     "mcrt_obj_add_directional_light": (_c.c_int, [_vp, _vp, _vp]),
@@ -386,6 +387,12 @@ class FrameBuffer:
         cp, ch = _c.c_uint64(), _c.c_int32()
         _check(lib().mcrt_bdpt_splat_layout(self.h, _c.byref(cp), _c.byref(ch)), self.ctx.h)
         return cp.value, ch.value
+
+    def stream(self):
+        """hipStream_t (int) of the last frame's slot (mcrt_framebuffer_stream)."""
+        st = _vp()
+        _check(lib().mcrt_framebuffer_stream(self.h, _c.byref(st)), self.ctx.h)
+        return st.value or 0
 
     def bdpt_splats_copy(self, dst_ptr):
         """Band-split BDPT: this rank's light-tracing splats, rank-major (chunks x chunk_pixels

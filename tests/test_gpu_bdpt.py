@@ -214,7 +214,8 @@ def test_bdpt_band_split_matches_whole_frames(hip_ctx, ranks):
             with pytest.raises(lib.MCRTError):   # the frame is not complete before the exchange
                 fb.accumulate(filt, f)
             assert fb.bdpt_splat_layout() == (cr * W, ranks)
-            fb.bdpt_splats_copy(bufs[r].data_ptr())
+            fb.bdpt_splats_copy(bufs[r].data_ptr())   # enqueued on the frame's stream
+        torch.cuda.synchronize()
         total = bufs[0].clone()
         for r in range(1, ranks):
             total += bufs[r]

@@ -178,7 +178,7 @@ def test_device_count_queries_with_events(hip_ctx):
     rays = random_rays(sc, n, seed=3)
     ds = lib.DeviceScene(hip_ctx, sc)
     r = torch.from_numpy(rays.view(np.uint8).copy()).cuda()
-    ref_h = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    ref_h = torch.full((n * 32,), 0xAB, dtype=torch.uint8, device="cuda")   # a miss leaves uvwt untouched
     ref_o = torch.zeros(n, dtype=torch.int32, device="cuda")
     ds.trace_closest(r.data_ptr(), n, ref_h.data_ptr())
     ds.trace_any(r.data_ptr(), n, ref_o.data_ptr())

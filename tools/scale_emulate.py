@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--base-ms", type=float, default=None,
                     help="1-GPU ms/frame (the efficiency base) when --ns does not include 1")
     args = ap.parse_args()
+    import torch
+    torch.cuda.init()   # torch's HIP runtime before the library's context (as bench.py)
     from mcrt import lib, scenes
     from mcrt import types as T
     from mcrt.camera import scene_camera
