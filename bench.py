@@ -345,7 +345,7 @@ def main():
     ap.add_argument("--no-roofline-model", action="store_true",
                     help="skip the oracle pass that counts the distinct BVH nodes of one launch")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--stats-launches", type=int, default=4,
+    ap.add_argument("--stats-launches", type=int, default=2,
                     help="launch sequences of the untimed per-kernel timing pass (one frame slot)")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     ap.add_argument("--no-bdpt", action="store_true", help="skip the BDPT object (config 4) of the PT run")
@@ -444,9 +444,9 @@ def main():
     # sweep tools/r2_gpu27.sh measured 1297 / 1315 Mpaths/s at 16 / 32 frames per launch, and a
     # 1/N band share x 32 frames keeps every multi-GPU launch at >= 4 whole images of paths
     batch = 1 if bdpt else (args.batch if args.batch > 0 else (32 if W * H <= 2_100_000 else 16))
-    # the untimed per-kernel pass and the roofline price launches of (at most) 4 frames, which
-    # keeps the oracle's distinct-node count of one launch to ~10 s of CPU
-    stats_batch = min(batch, 4)
+    # the untimed per-kernel pass and the roofline price the TIMED launch shape: calls of
+    # min(batch, steps) frames (the driver's 20 steps are one 20-frame call)
+    stats_batch = min(batch, args.steps)
 
     def step(i, n=1):
         """frames i .. i+n-1 (one mcrt_render_frames call when n > 1)"""
@@ -483,6 +483,7 @@ def main():
     warm = max(args.warmup, 4 * batch)
     run(0, warm)
     ctx.sync()
+    warm_frames = warm + 1   # + the untimed statistics frame below (the driver's W is a minimum)
     # per-frame path statistics (device queue sizes) from one untimed frame
     step(warm)
     ctx.sync()
@@ -526,8 +527,8 @@ def main():
     kstats = {}
     if not args.no_kernel_timing:
         # per-kernel HIP-event durations in a separate, untimed pass: one frame slot (kernels do not
-        # share the GPU with another frame's launches, so each duration is the kernel's own), at
-        # most 4 frames per launch (stats_batch)
+        # share the GPU with another frame's launches, so each duration is the kernel's own), calls
+        # of the timed region's shape (stats_batch frames each)
         fb.set_frames_in_flight(1)
         run(frame0 + args.steps, stats_batch, stats_batch)   # the slot re-binds outside the profiled launches
         ctx.sync()
@@ -548,7 +549,8 @@ def main():
     value = paths / elapsed / 1e6
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "warmup": args.warmup, "warmup_frames_run": warm_frames,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak" if bdpt and not band_bdpt else "strong", "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic: deterministic {args.scene} ({scene.num_triangles} tris, seeded generator mcrt/scenes.py)",
         "config": {"workload": f"{args.scene} {W}x{H}, {'BDPT' if bdpt else 'unidirectional PT'}, maxDepth {D}, "
@@ -564,7 +566,7 @@ def main():
                                    else f"frame split x {world} + 1 RCCL reduce" if bdpt else
                                    f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL "
                                    + ("band gather" if args.end_collective == "gather" else "reduce")),
-                   "frames_per_launch": batch},
+                   "frames_per_launch": stats_batch, "max_frames_per_call": batch},
     }
     if rank == 0:
         rays = {"closest": fstats["closest_rays"] / (W * H / world), "any": fstats["any_rays"] / (W * H / world),
@@ -595,7 +597,8 @@ def main():
                                   "items_per_launch": round(v["items"] / max(v["launches"], 1), 1)}
                               for k, v in kstats.items()}
             out["kernels_note"] = ("HIP-event durations from an untimed pass after the timed region: one frame slot "
-                                   f"(no overlap with another frame's launches), {stats_batch} frames per launch (the timed region uses {batch})")
+                                   f"(no overlap with another frame's launches), {args.stats_launches} calls of "
+                                   f"{stats_batch} frames, the timed region's launch shape")
             dom = max(kstats, key=lambda k: kstats[k]["ms"])
             if oracle_ok and dom == "k_shadow_extend" and not args.no_roofline_model:
                 avg_ms = kstats[dom]["ms"] / max(kstats[dom]["launches"], 1)

@@ -27,8 +27,10 @@ def main():
     ap.add_argument("--scene", default="san_miguel_proxy")
     ap.add_argument("--fif", type=int, default=0, help="frames in flight (0 = the library's auto choice)")
     ap.add_argument("--batch", type=int, default=1, help="frames per mcrt_render_frames call (0 = N)")
-    ap.add_argument("--chunks", default="", help="frames per call, cycled, each rounded down to a power of two "
-                                                 "(bench.py's plan; overrides --batch)")
+    ap.add_argument("--chunks", default="", help="frames per call, cycled (overrides --batch)")
+    ap.add_argument("--pow2", action="store_true", help="round each call of --chunks down to a power of two")
+    ap.add_argument("--kernels", action="store_true",
+                    help="also report rank 0's per-kernel HIP-event ms per frame (a separate profiled pass)")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     ap.add_argument("--base-ms", type=float, default=None,
                     help="1-GPU ms/frame (the efficiency base) when --ns does not include 1")
@@ -63,7 +65,7 @@ def main():
                 i = calls = 0
                 while i < count:
                     k = min(plan[calls % len(plan)], count - i)
-                    if args.chunks:
+                    if args.chunks and args.pow2:
                         k = 1 << (k.bit_length() - 1)
                     calls += 1
                     if k == 1:
@@ -79,8 +81,18 @@ def main():
             run(16, args.steps)
             ctx.sync()
             per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
+            if args.kernels and r == 0:
+                ctx.set_profiling(True)
+                ctx.reset_stats()
+                run(16 + args.steps, args.steps)
+                ctx.sync()
+                ks = ctx.kernel_stats()
+                ctx.set_profiling(False)
+                kern = {k: round(v["ms"] / args.steps, 4) for k, v in ks.items()}
         out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
                            "min_ms": round(min(per_rank), 4)}
+        if args.kernels:
+            out["per_n"][n]["rank0_kernel_ms_per_frame"] = kern
     # efficiency is relative to ONE GPU rendering the whole image: the N = 1 run of this sweep, or
     # --base-ms from a separate N = 1 run (never the smallest N of the sweep, which may be > 1)
     base = out["per_n"][1]["max_ms"] if 1 in out["per_n"] else args.base_ms
