@@ -116,9 +116,12 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
     alg = batch * (n_ext * 48 + n_sh * 80) + 64 * n_nodes
     achieved = alg / (avg_ms * 1e-3) / 1e9
     tr = pmc_traffic("k_shadow_extend")
+    traffic = None
+    if tr is not None:   # streamed reads: ray (o, d) 32 B, shadow ray 48 B + radiance 16 B
+        traffic = calibrated_traffic(tr["fetch_raw"], tr["write"], batch * (n_ext * 32 + n_sh * 64))
     out = {"bound": "hbm", "kernel": "k_shadow_extend", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-           "traffic": None if tr is None else round(tr["bytes_per_launch"]),
+           "traffic": None if traffic is None else round(traffic),
            "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(avg_ms, 4),
            "model": ("compulsory bytes per launch: 48 B per extension ray + 80 B per shadow ray + 64 B per "
                      "DISTINCT BVH node the launch visits (oracle-counted over the launch's frames)"),
@@ -127,8 +130,10 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
            "node_count_pass_s": round(el, 1)}
     if tr is not None:
         out["traffic_source"] = tr["source"]
-        out["traffic_rate_gbs"] = round(tr["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9, 1)
-        out["traffic_over_alg"] = round(tr["bytes_per_launch"] / alg, 2)
+        out["traffic_rule"] = ("FETCH_SIZE x 1024 (exact for 64-B node gathers, calibrated) + half the launch's "
+                               "streamed ray-record reads (reported at half) + WRITE_SIZE x 1024")
+        out["traffic_rate_gbs"] = round(traffic / (avg_ms * 1e-3) / 1e9, 1)
+        out["traffic_over_alg"] = round(traffic / alg, 2)
         if "limiter" in tr:
             out["limiter"] = tr["limiter"]
     try:   # attainable HBM bandwidth of an in-repo stream copy
@@ -163,10 +168,18 @@ def gather_ceiling(ctx, rl, vq, avg_ms):
     return out
 
 
+# FETCH_SIZE x 1024 is exact for the traversal's 64-B node gathers but reports half of a coalesced
+# 16-B/lane streamed read (profiles/r03/fetch_size_calibration.json, MI355X_MICROARCH.md "HBM"):
+# memory-side bytes = raw fetch + the unreported half of the launch's streamed reads + writes.
+def calibrated_traffic(fetch_raw, write, streamed_read_bytes):
+    return fetch_raw + 0.5 * streamed_read_bytes + write
+
+
 def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
-    """Memory-side bytes per launch of `kernel` (and the SQ limiter summary, if measured) from a
-    committed rocprofv3 counter summary under profiles/ (tools/pmc_json.py).  last_launches > 0:
-    also the summed bytes of the kernel's last `last_launches` dispatches (one BDPT frame)."""
+    """Raw FETCH_SIZE / WRITE_SIZE bytes per launch of `kernel` (and the SQ limiter summary, if
+    measured) from a committed rocprofv3 counter summary under profiles/ (tools/pmc_json.py).
+    last_launches > 0: also the summed bytes of the kernel's last `last_launches` dispatches (one
+    BDPT frame).  Callers apply calibrated_traffic with their launch's streamed-read bytes."""
     path = os.path.join(ROOT, "profiles", summary)
     if not os.path.exists(path):
         return None
@@ -175,13 +188,14 @@ def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
         k = d.get("kernels", {}).get(kernel)
         if k is None:
             return None
-        r = {"bytes_per_launch": float(k["hbm_bytes_per_launch"]),
+        c = k.get("counters", {})
+        r = {"fetch_raw": float(c["FETCH_SIZE"]) * 1024, "write": float(c["WRITE_SIZE"]) * 1024,
              "source": f"profiles/{summary} ({d.get('config', 'config not recorded')})"}
         raw = k.get("last_dispatches", {})
         if last_launches and len(raw.get("FETCH_SIZE", [])) >= last_launches and \
                 len(raw.get("WRITE_SIZE", [])) >= last_launches:
-            r["bytes_last"] = sum(2 * f * 1024 for f in raw["FETCH_SIZE"][-last_launches:]) + \
-                sum(w * 1024 for w in raw["WRITE_SIZE"][-last_launches:])
+            r["fetch_raw_last"] = sum(f * 1024 for f in raw["FETCH_SIZE"][-last_launches:])
+            r["write_last"] = sum(w * 1024 for w in raw["WRITE_SIZE"][-last_launches:])
         if "limiter" in k:
             r["limiter"] = k["limiter"]
         return r
@@ -305,9 +319,10 @@ def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s):
                            "model": "compulsory bytes per frame: 48 B per subpath ray + 64 B per DISTINCT BVH node the "
                                     "frame's subpath rays visit (oracle BDPT, frame 0)"}
         pm = pmc_traffic("k_extend", "pmc_bdpt.json", last_launches=D + 1)
-        if pm and "bytes_last" in pm:   # the last frame's D + 1 k_extend dispatches of the counter run
-            out["roofline"].update(traffic=int(pm["bytes_last"]), traffic_source=pm["source"],
-                                   traffic_over_alg=round(pm["bytes_last"] / alg, 2))
+        if pm and "fetch_raw_last" in pm:   # the last frame's D + 1 k_extend dispatches of the counter run
+            tr = calibrated_traffic(pm["fetch_raw_last"], pm["write_last"], rays * 32)   # streamed: ray (o, d)
+            out["roofline"].update(traffic=int(tr), traffic_source=pm["source"], traffic_over_alg=round(tr / alg, 2),
+                                   traffic_rule="FETCH_SIZE x 1024 + half the streamed ray reads + WRITE_SIZE x 1024")
         if pm and "limiter" in pm:
             out["roofline"]["limiter"] = pm["limiter"]
     # CPU baseline: whole frames 1, 2, ... until ~target_s (frame 0 above carried the node marks)

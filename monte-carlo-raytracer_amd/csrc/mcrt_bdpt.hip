@@ -593,14 +593,52 @@ MCRT_DEV void pushConn(const BdptQueue& q, int slot, f3 o, float tmax, f3 d, int
     q.t[slot] = make_float4(c.x, c.y, c.z, 0.0f);
 }
 
-// PrepareConnections (BDPT.cl:460-646) + the MIS weights of ConnectVertices (BDPT.cl:739-876).
-// Per pixel, one thread walks the strategies in the reference's (t, s) order.  Own strategies
-// (t >= 2) get a slot, written here (zero when they need no connection or contribute nothing);
-// strategies with a non-zero weighted contribution that need visibility are queued.
+// PrepareConnections (BDPT.cl:460-646) + the MIS weights of ConnectVertices (BDPT.cl:739-876),
+// one thread per (pixel, strategy).  The reference walks a pixel's strategies serially in (t, s)
+// order; only two things tie them together, and both are restated per strategy here:
+//   * the sampler: each s = 1 strategy whose camera vertex is live and connectible draws 3 values
+//     (light choice + 2D) from the pixel's connection stream, so strategy (t, 1) starts that stream
+//     3 draws later per such earlier strategy (t' < t, counted from the camera vertices' flags);
+//   * the stale sampled-light slot (BDPT.cl:585-586): strategy (t, 1) alone reads and rewrites
+//     slot t - 2, so its frame-to-frame read-before-write order is kept.
+// Strategies are split into four classes, one launch each, so every kernel carries only its own
+// registers: EMIT (s = 0), LIGHT (t = 1, light tracing), NEE (s = 1), GENERAL (t, s >= 2).  A wave
+// holds one strategy of one 8x8 tile (wave-uniform branches); the waves of a tile are adjacent,
+// so its vertex planes are re-read from L2.  Own strategies (t >= 2) write their slot (zero when
+// absent, not connectible or contributing nothing); strategies with a non-zero weighted
+// contribution that need visibility are queued.
+enum { CONN_EMIT = 0, CONN_LIGHT = 1, CONN_NEE = 2, CONN_GENERAL = 3 };
+
+MCRT_DEV int ownSlotOf(int t, int sI, int D) {   // index among the t >= 2 strategies in (t, s) order
+    int k = sI;
+    for (int u = 2; u < t; ++u) k += D + 3 - u;
+    return k;
+}
+template <int CLS>
+MCRT_DEV void strategyOf(int k, int D, int& t, int& sI) {
+    if (CLS == CONN_EMIT) { t = k + 2; sI = 0; }
+    else if (CLS == CONN_LIGHT) { t = 1; sI = k + 2; }
+    else if (CLS == CONN_NEE) { t = k + 2; sI = 1; }
+    else {
+        t = 2;
+        sI = 2;
+        for (int u = 2; u <= D; ++u) {
+            const int n = D + 1 - u;   // s = 2 .. D + 2 - u
+            if (k < n) { t = u; sI = k + 2; break; }
+            k -= n;
+        }
+    }
+}
+
+template <int CLS>
 __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameArgs f, BdptArgs b,
-                                                             const mcrt_camera* __restrict__ camp, BdptQueue qOut) {
+                                                             const mcrt_camera* __restrict__ camp, BdptQueue qOut,
+                                                             int numStrat) {
     const int lane = threadIdx.x & 63;
-    const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int tile = wave / numStrat;
+    int t, sI;
+    strategyOf<CLS>(wave - tile * numStrat, f.maxDepth, t, sI);
     int x = 0, y = 0;
     const bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y) && s.numLights > 0;
     __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
@@ -610,200 +648,198 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
     const mcrt_camera& cam = *camp;
     const int camCount = valid ? b.camCount[pix] : 0;
     const int lightCount = valid ? b.lightCount[pix] : 0;
-    Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, (D + 1) + (D + 2), f.W, f.H, s.sobol);
-    int ownSlot = 0;
-    // Every thread of the block runs the same number of append rounds (block-wide barrier).
-    for (int t = 1; t <= D + 2; ++t) {
-        for (int sI = 0; sI <= D + 1; ++sI) {
-            const int curDepth = t + sI - 2;
-            if ((t == 1 && sI == 1) || curDepth < 0 || curDepth > D) continue;   // uniform skip
-            const bool live = t <= camCount && sI <= lightCount;
-            bool push = false, needRay = false;
-            f3 L = splat3(0.0f), rayO = splat3(0.0f), rayD = splat3(0.0f);
-            float rayT = 0.0f;
-            int code = 0;
-            if (live) {
-                const BVertex cv = loadVertex(b.camV, t - 1, pix, N);
-                // sampled vertices of the t = 1 / s = 1 strategies (replace pt / qs in the MIS)
-                BVertex samp;
-                if (sI == 0) {
-                    // ConnectVertices (BDPT.cl:723-731): emission of a camera vertex that is a light
-                    if (cv.type == RT_BDPT_LIGHT_VERTEX || cv.lightIdx != -1) {
-                        const f3 Le = evalLightLe(s.lights[cv.lightIdx], cv.fr.gn, cv.wo);
-                        L = Le * cv.throughput;
-                    }
-                } else if (t == 1) {
-                    const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
-                    if (isConnectible(lv.flags)) {
-                        // samplePinholeCameraWi (cameras.cl:61-69)
-                        f3 wi = ld3(cam.pos) - lv.fr.p;
-                        const float dist = cl_length(wi);
-                        wi = cl_div(wi, dist);
-                        const float pdf = cl_div((dist * dist), absDot(ld3(cam.direction), wi));
-                        f2 nip = f2{cl_div((float)x, (float)f.W), cl_div((float)y, (float)f.H)};
-                        const float imp = evalPinholeCameraWe(cam, ld3(cam.pos), -wi, &nip);
-                        const f3 importance = splat3(imp);
-                        if (pdf > 0.0f && isNotBlack(importance)) {
-                            samp = createCameraVertex(ld3(cam.pos), cl_div(importance, pdf));
-                            int ix = (int)floorf(nip.x * f.W + 0.5f), iy = (int)floorf(nip.y * f.H + 0.5f);
-                            ix = min(max(ix, 0), (int)f.W - 1);
-                            iy = min(max(iy, 0), (int)f.H - 1);
-                            code = ~(ix + iy * (int)f.W);
-                            L = lv.throughput * samp.throughput * evalVertex_f(lv, pix, N, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
-                            if (isVertexOnSurface(lv.fr.gn)) L *= absDot(wi, lv.fr.sn);
-                            rayO = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
-                            rayT = cl_distance(rayO, ld3(cam.pos));
-                            rayD = cl_div(ld3(cam.pos) - rayO, rayT);
-                            needRay = true;
-                        }
-                    }
-                } else if (sI == 1) {
-                    if (isConnectible(cv.flags)) {
-                        const int chosen = min((int)floorf(getSample1D(sampler) * s.numLights), s.numLights - 1);
-                        const mcrt_light light = s.lights[chosen];
-                        const float lightPdf = light.choicePdf;
-                        const f2 u = getSample2D(sampler);
-                        const LightSample ls = sampleLightLi(s, light, cv.fr, cv.traceErrorOffset, u);
-                        if (isNotNearZero(ls.pdf) && isNotBlack(ls.Li)) {
-                            // the reference evaluates pdfFwd on the PREVIOUS content of the sampled
-                            // vertex slot before overwriting it (BDPT.cl:585-586)
-                            float4* stale = b.sampLight + (size_t)(t - 2) * N + pix;
-                            const float4 st = *stale;
-                            const int stBits = __float_as_int(st.w);
-                            const int stFlags = stBits >> 16, stLight = (int)(short)(stBits & 0xffff);
-                            const float pdfFwdS = evalVertexPdfLightOrigin(s, ld3(st), splat3(0.0f), stFlags, stLight,
-                                                                          cv.fr.p);
-                            samp = createLightVertex(chosen, ls.lightPos, ls.lightNormal, cl_div(ls.Li, (lightPdf * ls.pdf)),
-                                                     pdfFwdS, light.flags);
-                            *stale = make_float4(samp.fr.p.x, samp.fr.p.y, samp.fr.p.z,
-                                                 __int_as_float((samp.flags << 16) | (chosen & 0xffff)));
-                            const f3 fm = evaluateMaterialV(cv, pix, N, cv.wo, ls.wi, TRANSPORT_MODE_RADIANCE);
-                            L = cv.throughput * samp.throughput * fm;
-                            if (isVertexOnSurface(cv.fr.gn)) L *= absDot(ls.wi, cv.fr.sn);
-                            if (ls.shadowSet) {
-                                rayO = ls.shadowO;
-                                rayT = ls.shadowT;
-                                rayD = ls.wi;
-                                needRay = true;
-                            }
-                        }
-                    }
-                } else {
-                    const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
-                    if (isConnectible(cv.flags) && isConnectible(lv.flags)) {
-                        const f3 lvf = evalVertex_f(lv, pix, N, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
-                        const f3 cvf = evalVertex_f(cv, pix, N, lv.fr.p, TRANSPORT_MODE_RADIANCE);
-                        const f3 lp = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
-                        const f3 cp = cv.fr.p + cv.fr.gn * cv.traceErrorOffset;
-                        f3 w = cp - lp;
-                        const float sqDist = cl_dot(w, w);
-                        const float dist = cl_sqrt(sqDist);
-                        w = cl_div(w, dist);
-                        if (isNotNearZero(sqDist)) {
-                            const float g = cl_div(absDot(cv.fr.sn, w) * absDot(lv.fr.sn, w), sqDist);
-                            L = lv.throughput * cv.throughput * lvf * cvf * g;
-                        }
-                        if (isNotBlack(L)) {
-                            rayO = lp;
-                            rayT = dist;
-                            rayD = w;
-                            needRay = true;
-                        }
-                    }
-                }
-                // MIS weight (BDPT.cl:739-876), independent of visibility
-                float misWeight = 1.0f;
-                if (isBlack(L)) {
-                    misWeight = 0.0f;
-                } else if (sI + t != 2) {
-                    // pt = camera vertex t-1 (or the sampled camera vertex), qs = light vertex s-1 (or the
-                    // sampled light vertex), with their delta flags cleared and pdfRev re-evaluated
-                    BVertex pt = t == 1 ? samp : cv;
-                    BVertex qs;
-                    if (sI == 1) qs = samp;
-                    else if (sI > 1) qs = loadVertex(b.lightV, sI - 1, pix, N);
-                    BVertexPos ptPrev, qsPrev;
-                    if (t > 1) ptPrev = loadVertexPos(b.camV, t - 2, pix, N);
-                    if (sI > 1) qsPrev = loadVertexPos(b.lightV, sI - 2, pix, N);
-                    pt.flags &= ~VF_DELTA;
-                    if (sI > 0) qs.flags &= ~VF_DELTA;
-                    const float ptRev = sI > 0 ? evalVertexPdf(s, cam, qs, pix, N, sI > 1, qsPrev.p, posOf(pt))
-                                               : evalVertexPdfLightOrigin(s, pt.fr.p, pt.fr.gn, pt.flags, pt.lightIdx, ptPrev.p);
-                    float ptPrevRev = 0.0f, qsRev = 0.0f, qsPrevRev = 0.0f;
-                    if (t > 1)
-                        ptPrevRev = sI > 0 ? evalVertexPdf(s, cam, pt, pix, N, true, qs.fr.p, ptPrev)
-                                           : evalVertexPdfLight(s, pt.fr.p, pt.fr.gn, pt.flags, pt.lightIdx, ptPrev);
-                    if (sI > 0) qsRev = evalVertexPdf(s, cam, pt, pix, N, t > 1, ptPrev.p, posOf(qs));
-                    if (sI > 1) qsPrevRev = evalVertexPdf(s, cam, qs, pix, N, true, pt.fr.p, qsPrev);
-                    float sumRi = 0.0f;
-                    // camera subpath (BDPT.cl:819-827)
-                    float ri = 1.0f;
-                    int flagsHi = pt.flags;   // flags of vertex i (walking down from t-1)
-                    for (int i = t - 1; i > 0; --i) {
-                        float rev, fwd;
-                        int fl, flLo;
-                        if (i == t - 1) {
-                            rev = ptRev;
-                            fwd = pt.pdfFwd;
-                            fl = pt.flags;
-                        } else {
-                            const float4 pb = vplane(b.camV, i, 1, N)[pix];
-                            const float4 pc = vplane(b.camV, i, 2, N)[pix];
-                            fwd = pb.w;
-                            rev = (i == t - 2) ? ptPrevRev : pc.w;
-                            fl = flagsHi;
-                        }
-                        flLo = reinterpret_cast<const int4*>(&vplane(b.camV, i - 1, 7, N)[pix])->y;
-                        ri *= cl_div(remap0(rev), remap0(fwd));
-                        if (!isDeltaV(fl) && !isDeltaV(flLo)) sumRi += ri;
-                        flagsHi = flLo;
-                    }
-                    // light subpath (BDPT.cl:829-838)
-                    ri = 1.0f;
-                    for (int i = sI - 1; i >= 0; --i) {
-                        float rev, fwd;
-                        int fl;
-                        if (i == sI - 1) {
-                            rev = qsRev;
-                            fwd = qs.pdfFwd;
-                            fl = qs.flags;
-                        } else {
-                            const float4 pb = vplane(b.lightV, i, 1, N)[pix];
-                            const float4 pc = vplane(b.lightV, i, 2, N)[pix];
-                            fwd = pb.w;
-                            rev = (i == sI - 2) ? qsPrevRev : pc.w;
-                            fl = reinterpret_cast<const int4*>(&vplane(b.lightV, i, 7, N)[pix])->y;
-                        }
-                        ri *= cl_div(remap0(rev), remap0(fwd));
-                        bool deltaLightVertex;
-                        if (i > 0) {
-                            deltaLightVertex = isDeltaV(reinterpret_cast<const int4*>(&vplane(b.lightV, i - 1, 7, N)[pix])->y);
-                        } else {
-                            const int f0 = (sI == 1) ? qs.flags
-                                                     : reinterpret_cast<const int4*>(&vplane(b.lightV, 0, 7, N)[pix])->y;
-                            deltaLightVertex = isDeltaLightV(f0);
-                        }
-                        if (!isDeltaV(fl) && !deltaLightVertex) sumRi += ri;
-                    }
-                    misWeight = cl_div(1.0f, (1.0f + sumRi));
-                }
-                const f3 c = L * misWeight;
-                const bool nonzero = c.x != 0.0f || c.y != 0.0f || c.z != 0.0f;
-                if (sI > 0 && nonzero) push = needRay;   // no connection ray = not visible (contributes 0)
-                if (t >= 2) {
-                    const f3 own = (sI == 0 || push) ? c : splat3(0.0f);
-                    b.slots[(size_t)ownSlot * N + pix] = make_float4(own.x, own.y, own.z, 0.0f);
-                    if (push) code = ownSlot * N + pix;
-                }
-                L = c;
-            } else if (valid && t >= 2) {
-                b.slots[(size_t)ownSlot * N + pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // strategy absent
+    const bool live = valid && t <= camCount && sI <= lightCount;
+    bool push = false, needRay = false;
+    f3 L = splat3(0.0f), rayO = splat3(0.0f), rayD = splat3(0.0f);
+    float rayT = 0.0f;
+    int code = 0;
+    if (live) {
+        BVertex cv, samp;   // samp: the sampled vertex of a t = 1 / s = 1 strategy (pt / qs in the MIS)
+        if (CLS != CONN_LIGHT) cv = loadVertex(b.camV, t - 1, pix, N);
+        if (CLS == CONN_EMIT) {
+            // ConnectVertices (BDPT.cl:723-731): emission of a camera vertex that is a light
+            if (cv.type == RT_BDPT_LIGHT_VERTEX || cv.lightIdx != -1) {
+                const f3 Le = evalLightLe(s.lights[cv.lightIdx], cv.fr.gn, cv.wo);
+                L = Le * cv.throughput;
             }
-            if (t >= 2) ++ownSlot;
-            const int qs = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
-            if (push) pushConn(qOut, qs, rayO, rayT, rayD, code, L);
+        } else if (CLS == CONN_LIGHT) {
+            const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
+            if (isConnectible(lv.flags)) {
+                // samplePinholeCameraWi (cameras.cl:61-69)
+                f3 wi = ld3(cam.pos) - lv.fr.p;
+                const float dist = cl_length(wi);
+                wi = cl_div(wi, dist);
+                const float pdf = cl_div((dist * dist), absDot(ld3(cam.direction), wi));
+                f2 nip = f2{cl_div((float)x, (float)f.W), cl_div((float)y, (float)f.H)};
+                const float imp = evalPinholeCameraWe(cam, ld3(cam.pos), -wi, &nip);
+                const f3 importance = splat3(imp);
+                if (pdf > 0.0f && isNotBlack(importance)) {
+                    samp = createCameraVertex(ld3(cam.pos), cl_div(importance, pdf));
+                    int ix = (int)floorf(nip.x * f.W + 0.5f), iy = (int)floorf(nip.y * f.H + 0.5f);
+                    ix = min(max(ix, 0), (int)f.W - 1);
+                    iy = min(max(iy, 0), (int)f.H - 1);
+                    code = ~(ix + iy * (int)f.W);
+                    L = lv.throughput * samp.throughput * evalVertex_f(lv, pix, N, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                    if (isVertexOnSurface(lv.fr.gn)) L *= absDot(wi, lv.fr.sn);
+                    rayO = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
+                    rayT = cl_distance(rayO, ld3(cam.pos));
+                    rayD = cl_div(ld3(cam.pos) - rayO, rayT);
+                    needRay = true;
+                }
+            }
+        } else if (CLS == CONN_NEE) {
+            if (isConnectible(cv.flags)) {
+                // the pixel's connection stream, past the draws of the earlier s = 1 strategies
+                Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, (D + 1) + (D + 2), f.W, f.H, s.sobol);
+                int skip = 0;
+                for (int u = 2; u < t; ++u)
+                    if (u <= camCount && isConnectible(reinterpret_cast<const int4*>(&vplane(b.camV, u - 1, 7, N)[pix])->y))
+                        skip += 3;
+                if (sampler.mats) sampler.dim += (uint32_t)skip;
+                else
+                    for (int u = 0; u < skip; ++u) xorshift(sampler.idx);
+                const int chosen = min((int)floorf(getSample1D(sampler) * s.numLights), s.numLights - 1);
+                const mcrt_light light = s.lights[chosen];
+                const float lightPdf = light.choicePdf;
+                const f2 u = getSample2D(sampler);
+                const LightSample ls = sampleLightLi(s, light, cv.fr, cv.traceErrorOffset, u);
+                if (isNotNearZero(ls.pdf) && isNotBlack(ls.Li)) {
+                    // the reference evaluates pdfFwd on the PREVIOUS content of the sampled
+                    // vertex slot before overwriting it (BDPT.cl:585-586)
+                    float4* stale = b.sampLight + (size_t)(t - 2) * N + pix;
+                    const float4 st = *stale;
+                    const int stBits = __float_as_int(st.w);
+                    const int stFlags = stBits >> 16, stLight = (int)(short)(stBits & 0xffff);
+                    const float pdfFwdS = evalVertexPdfLightOrigin(s, ld3(st), splat3(0.0f), stFlags, stLight, cv.fr.p);
+                    samp = createLightVertex(chosen, ls.lightPos, ls.lightNormal, cl_div(ls.Li, (lightPdf * ls.pdf)),
+                                             pdfFwdS, light.flags);
+                    *stale = make_float4(samp.fr.p.x, samp.fr.p.y, samp.fr.p.z,
+                                         __int_as_float((samp.flags << 16) | (chosen & 0xffff)));
+                    const f3 fm = evaluateMaterialV(cv, pix, N, cv.wo, ls.wi, TRANSPORT_MODE_RADIANCE);
+                    L = cv.throughput * samp.throughput * fm;
+                    if (isVertexOnSurface(cv.fr.gn)) L *= absDot(ls.wi, cv.fr.sn);
+                    if (ls.shadowSet) {
+                        rayO = ls.shadowO;
+                        rayT = ls.shadowT;
+                        rayD = ls.wi;
+                        needRay = true;
+                    }
+                }
+            }
+        } else {
+            const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
+            if (isConnectible(cv.flags) && isConnectible(lv.flags)) {
+                const f3 lvf = evalVertex_f(lv, pix, N, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                const f3 cvf = evalVertex_f(cv, pix, N, lv.fr.p, TRANSPORT_MODE_RADIANCE);
+                const f3 lp = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
+                const f3 cp = cv.fr.p + cv.fr.gn * cv.traceErrorOffset;
+                f3 w = cp - lp;
+                const float sqDist = cl_dot(w, w);
+                const float dist = cl_sqrt(sqDist);
+                w = cl_div(w, dist);
+                if (isNotNearZero(sqDist)) {
+                    const float g = cl_div(absDot(cv.fr.sn, w) * absDot(lv.fr.sn, w), sqDist);
+                    L = lv.throughput * cv.throughput * lvf * cvf * g;
+                }
+                if (isNotBlack(L)) {
+                    rayO = lp;
+                    rayT = dist;
+                    rayD = w;
+                    needRay = true;
+                }
+            }
         }
+        // MIS weight (BDPT.cl:739-876), independent of visibility
+        float misWeight = 1.0f;
+        if (isBlack(L)) {
+            misWeight = 0.0f;
+        } else if (sI + t != 2) {
+            // pt = camera vertex t-1 (or the sampled camera vertex), qs = light vertex s-1 (or the
+            // sampled light vertex), with their delta flags cleared and pdfRev re-evaluated
+            BVertex pt = CLS == CONN_LIGHT ? samp : cv;
+            BVertex qs;
+            if (CLS == CONN_NEE) qs = samp;
+            else if (CLS == CONN_LIGHT || CLS == CONN_GENERAL) qs = loadVertex(b.lightV, sI - 1, pix, N);
+            BVertexPos ptPrev, qsPrev;
+            if (CLS != CONN_LIGHT) ptPrev = loadVertexPos(b.camV, t - 2, pix, N);
+            if (CLS == CONN_LIGHT || CLS == CONN_GENERAL) qsPrev = loadVertexPos(b.lightV, sI - 2, pix, N);
+            pt.flags &= ~VF_DELTA;
+            if (CLS != CONN_EMIT) qs.flags &= ~VF_DELTA;
+            const float ptRev = CLS != CONN_EMIT ? evalVertexPdf(s, cam, qs, pix, N, sI > 1, qsPrev.p, posOf(pt))
+                                                 : evalVertexPdfLightOrigin(s, pt.fr.p, pt.fr.gn, pt.flags, pt.lightIdx, ptPrev.p);
+            float ptPrevRev = 0.0f, qsRev = 0.0f, qsPrevRev = 0.0f;
+            if (CLS != CONN_LIGHT)
+                ptPrevRev = CLS != CONN_EMIT ? evalVertexPdf(s, cam, pt, pix, N, true, qs.fr.p, ptPrev)
+                                             : evalVertexPdfLight(s, pt.fr.p, pt.fr.gn, pt.flags, pt.lightIdx, ptPrev);
+            if (CLS != CONN_EMIT) qsRev = evalVertexPdf(s, cam, pt, pix, N, t > 1, ptPrev.p, posOf(qs));
+            if (CLS == CONN_LIGHT || CLS == CONN_GENERAL) qsPrevRev = evalVertexPdf(s, cam, qs, pix, N, true, pt.fr.p, qsPrev);
+            float sumRi = 0.0f;
+            // camera subpath (BDPT.cl:819-827)
+            float ri = 1.0f;
+            int flagsHi = pt.flags;   // flags of vertex i (walking down from t-1)
+            for (int i = t - 1; i > 0; --i) {
+                float rev, fwd;
+                int fl, flLo;
+                if (i == t - 1) {
+                    rev = ptRev;
+                    fwd = pt.pdfFwd;
+                    fl = pt.flags;
+                } else {
+                    const float4 pb = vplane(b.camV, i, 1, N)[pix];
+                    const float4 pc = vplane(b.camV, i, 2, N)[pix];
+                    fwd = pb.w;
+                    rev = (i == t - 2) ? ptPrevRev : pc.w;
+                    fl = flagsHi;
+                }
+                flLo = reinterpret_cast<const int4*>(&vplane(b.camV, i - 1, 7, N)[pix])->y;
+                ri *= cl_div(remap0(rev), remap0(fwd));
+                if (!isDeltaV(fl) && !isDeltaV(flLo)) sumRi += ri;
+                flagsHi = flLo;
+            }
+            // light subpath (BDPT.cl:829-838)
+            ri = 1.0f;
+            for (int i = sI - 1; i >= 0; --i) {
+                float rev, fwd;
+                int fl;
+                if (i == sI - 1) {
+                    rev = qsRev;
+                    fwd = qs.pdfFwd;
+                    fl = qs.flags;
+                } else {
+                    const float4 pb = vplane(b.lightV, i, 1, N)[pix];
+                    const float4 pc = vplane(b.lightV, i, 2, N)[pix];
+                    fwd = pb.w;
+                    rev = (i == sI - 2) ? qsPrevRev : pc.w;
+                    fl = reinterpret_cast<const int4*>(&vplane(b.lightV, i, 7, N)[pix])->y;
+                }
+                ri *= cl_div(remap0(rev), remap0(fwd));
+                bool deltaLightVertex;
+                if (i > 0) {
+                    deltaLightVertex = isDeltaV(reinterpret_cast<const int4*>(&vplane(b.lightV, i - 1, 7, N)[pix])->y);
+                } else {
+                    const int f0 = (sI == 1) ? qs.flags : reinterpret_cast<const int4*>(&vplane(b.lightV, 0, 7, N)[pix])->y;
+                    deltaLightVertex = isDeltaLightV(f0);
+                }
+                if (!isDeltaV(fl) && !deltaLightVertex) sumRi += ri;
+            }
+            misWeight = cl_div(1.0f, (1.0f + sumRi));
+        }
+        const f3 c = L * misWeight;
+        const bool nonzero = c.x != 0.0f || c.y != 0.0f || c.z != 0.0f;
+        if (CLS != CONN_EMIT && nonzero) push = needRay;   // no connection ray = not visible (contributes 0)
+        if (CLS != CONN_LIGHT) {
+            const int own = ownSlotOf(t, sI, D);
+            const f3 o = (CLS == CONN_EMIT || push) ? c : splat3(0.0f);
+            b.slots[(size_t)own * N + pix] = make_float4(o.x, o.y, o.z, 0.0f);
+            if (push) code = own * N + pix;
+        }
+        L = c;
+    } else if (valid && CLS != CONN_LIGHT) {
+        b.slots[(size_t)ownSlotOf(t, sI, D) * N + pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // strategy absent
     }
+    if (CLS == CONN_EMIT) return;   // emission needs no connection ray (wave-uniform: the whole block)
+    const int qslot = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
+    if (push) pushConn(qOut, qslot, rayO, rayT, rayD, code, L);
 }
 
 // Any hit over the connection queue (RR occluded_main semantics): occluded own strategies are
@@ -896,8 +932,19 @@ void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& 
 }
 void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                          const BdptQueue& q, hipStream_t st) {
-    const int blocks = (f.numTiles * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK;
-    hipLaunchKernelGGL(k_bdpt_connect, dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, q);
+    // strategies per class for maxDepth D (C = (D+2)(D+3)/2 - 2 in all): s = 0: D+1, t = 1: D,
+    // s = 1: D, t, s >= 2: the rest
+    const int D = f.maxDepth;
+    const int C = (D + 2) * (D + 3) / 2 - 2;
+    const int counts[4] = {D + 1, D, D, C - 3 * D - 1};
+    void (*kern[4])(SceneArgs, FrameArgs, BdptArgs, const mcrt_camera*, BdptQueue, int) = {
+        k_bdpt_connect<CONN_EMIT>, k_bdpt_connect<CONN_LIGHT>, k_bdpt_connect<CONN_NEE>, k_bdpt_connect<CONN_GENERAL>};
+    for (int c = 0; c < 4; ++c) {
+        if (counts[c] <= 0) continue;
+        const int64_t waves = (int64_t)f.numTiles * counts[c];
+        const int blocks = (int)((waves * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK);
+        hipLaunchKernelGGL(kern[c], dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, q, counts[c]);
+    }
 }
 void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st) {
     const int blocks = (maxCount + 63) / 64 > 0 ? (maxCount + 63) / 64 : 1;

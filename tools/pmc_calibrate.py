@@ -8,12 +8,13 @@ every lane following its own chain of uniformly random records.  With the record
 than every cache (the HBM case) nearly every step misses L2, so the memory-side demand is known:
 one 64-B record per step.  This program runs the probe at L2 (2 MiB), Infinity-Cache (122 MiB)
 and HBM (the 10 M-triangle tree's 1.28 GB) residency; run it under rocprofv3 --pmc passes and
-summarise with `python tools/pmc_calibrate.py --summarise DIR`:
+summarise with `python tools/pmc_calibrate.py --summarise DIR`.
 
-    factor = (steps x 64 B) / (FETCH_SIZE x 1024)     per k_chase dispatch, HBM case
-
-so that bytes = FETCH_SIZE x 1024 x factor is the record traffic of this pattern (the streaming
-rule's factor is 2).
+Result (profiles/r03/fetch_size_calibration.json, MI355X round 3): FETCH_SIZE x 1024 = 64 B x
+TCC_MISS to 0.1 % at Infinity-Cache and HBM residency, i.e. a 64-B random gather is counted at
+its full size (the streaming rule halves only 128-B requests), and L2 misses served by the
+Infinity Cache are counted too.  The demand/fetch ratio is NOT 1 even at HBM residency because
+random chains merge (a random functional graph): 19 % of the steps hit L2 there.
 """
 import glob
 import json
@@ -74,11 +75,14 @@ def summarise(d):
         if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
             c["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1), 4)
             c["l2_misses_per_step"] = round(c["TCC_MISS_sum"] / c["steps_per_dispatch"], 4)
+    for c in res["cases"].values():
+        if "FETCH_SIZE" in c and "TCC_MISS_sum" in c:
+            c["fetch_bytes_per_l2_miss"] = round(c["FETCH_SIZE"] * 1024 / max(c["TCC_MISS_sum"], 1), 3)
     hbm = res["cases"].get("hbm_1.28GB", {})
-    if "factor_demand_over_fetch" in hbm:
-        res["factor"] = hbm["factor_demand_over_fetch"]
-        res["rule"] = ("record-traffic bytes = FETCH_SIZE x 1024 x factor for this gather pattern, calibrated where "
-                       "every step's 64-B record comes from beyond L2 (HBM residency)")
+    if "fetch_bytes_per_l2_miss" in hbm:
+        res["factor"] = round(64.0 / hbm["fetch_bytes_per_l2_miss"], 4)
+        res["rule"] = ("64-B random gathers: memory-side bytes = FETCH_SIZE x 1024 x factor (factor = 64 B per L2 miss / "
+                       "reported bytes per L2 miss, HBM residency); coalesced 16-B/lane streams keep the guide's x2")
     out = os.path.join(ROOT, "profiles", "r03", "fetch_size_calibration.json")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))

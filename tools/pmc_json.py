@@ -2,16 +2,21 @@
 rocprofv3 PMC passes of one bench.py command (tools/r2_gpu2.sh runs them, each pass in its own
 process because FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
 
-  python tools/pmc_json.py DIR_WITH_RESULTS_DBS "bench command" [launches_per_kernel_in_stats_pass]
-                           [pass_dir_prefix (default pmc_)] [output (default profiles/pmc_latest.json)]
+  python tools/pmc_json.py DIR_WITH_RESULTS_DBS "bench command" [launches] [pass_dir_prefix (default pmc_)]
+                           [output (default profiles/pmc_latest.json)] [description of those launches]
 
-Per kernel the figures are the MEDIAN over the dispatches of bench.py's untimed one-slot
-kernel-timing pass (its last `--stats-launches` dispatches of that kernel), i.e. the same launches
-whose HIP-event durations price roofline.achieved.
+Per kernel the figures are the MEDIAN over the kernel's last `launches` dispatches.  Round 3: the
+passes profile `bench.py --no-kernel-timing ...`, so the last dispatch of each PT kernel IS the
+timed render_frames call (20 frames packed into one launch per kernel) and launches = 1.
 
-Corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE counts 128-B memory-side read requests at
-64 B, so it is doubled; WRITE_SIZE is taken as is; both are KB.  These L2-to-fabric counters also
-count Infinity-Cache hits, so the figure is L2-miss traffic (an upper bound on HBM bytes).
+Bytes (MI355X_MICROARCH.md "HBM" + profiles/r03/fetch_size_calibration.json): FETCH_SIZE counts a
+128-B memory-side read request of a coalesced 16-B/lane stream at 64 B (the guide: double it), but
+a 64-B random gather -- the traversal's node fetch -- exactly (calibrated here: FETCH_SIZE x 1024 =
+64 B x TCC_MISS to 0.1 % on the dependent-gather probe at HBM and Infinity-Cache residency).  So
+the JSON keeps the raw figure (fetch_bytes_raw = FETCH_SIZE x 1024, exact for the gathers) and
+the streaming-rule upper bound (2x); bench.py adds back the unreported half of the launch's known
+streamed reads (ray records).  WRITE_SIZE is exact for 16-B stores and float atomics.  These
+L2-to-fabric counters also count Infinity-Cache hits: the figure is bytes beyond L2.
 Limiter (SQ block, per dispatch; SQ_WAVE_CYCLES / WAIT_* / ACTIVE_INST_* in the same unit, so
 their ratios are unit-free): share of wave time waiting on memory (SQ_WAIT_ANY), stalled at issue
 (SQ_WAIT_INST_ANY) and issuing (SQ_ACTIVE_INST_ANY); VALU pipe busy = SQ_INSTS_VALU x 2 cycles
@@ -57,21 +62,24 @@ def collect(dbs, last, keep=12):
 def main():
     d = sys.argv[1]
     cmd = sys.argv[2] if len(sys.argv) > 2 else "bench.py"
-    last = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    last = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     prefix = sys.argv[4] if len(sys.argv) > 4 else "pmc_"
     dbs = sorted(glob.glob(os.path.join(d, prefix + "*", "*_results.db")))
     pmc, ms, raw = collect(dbs, last)
     res = {"source": f"rocprofv3 --kernel-trace --pmc passes ({', '.join(os.path.basename(os.path.dirname(x)) for x in dbs)})",
-           "config": f"{cmd}; medians over the last {last} dispatches of each kernel = the untimed one-slot "
-                     "kernel-timing pass " + ("(1 frame per launch)" if "bdpt" in cmd else "(4 frames per launch)"),
-           "correction": "hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (MI355X_MICROARCH.md HBM section)",
+           "config": f"{cmd}; medians over the last {last} dispatch(es) of each kernel = " +
+                     (sys.argv[6] if len(sys.argv) > 6 else "the timed render_frames call (one launch per kernel)"),
+           "correction": ("fetch_bytes_raw = FETCH_SIZE x 1024 (exact for 64-B gathers, half of coalesced 16-B/lane "
+                          "streams: profiles/r03/fetch_size_calibration.json); fetch_bytes_stream_rule = 2 x raw "
+                          "(upper bound); write_bytes = WRITE_SIZE x 1024"),
            "kernels": {}}
     for k, c in pmc.items():
         r = {"dispatch_ms_median": round(ms[k], 4), "counters": {n: v for n, v in sorted(c.items())},
              "last_dispatches": {n: raw[k][n] for n in ("FETCH_SIZE", "WRITE_SIZE") if n in raw.get(k, {})}}
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            fb, wb = 2 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
-            r.update(fetch_bytes_corrected=fb, write_bytes=wb, hbm_bytes_per_launch=fb + wb)
+            fb, wb = c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
+            r.update(fetch_bytes_raw=fb, fetch_bytes_stream_rule=2 * fb, write_bytes=wb,
+                     memory_side_bytes_bounds=[fb + wb, 2 * fb + wb])
         if all(x in c for x in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE")):
             wc = c["SQ_WAVE_CYCLES"]
             cyc = c["GRBM_GUI_ACTIVE"] / 8.0
@@ -83,8 +91,8 @@ def main():
                 lim["wave_time_issuing"] = round(c["SQ_ACTIVE_INST_ANY"] / wc, 3)
             if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
                 lim["l2_hit_rate"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 3)
-            if "hbm_bytes_per_launch" in r:
-                lim["memory_side_tb_s"] = round(r["hbm_bytes_per_launch"] / (ms[k] * 1e-3) / 1e12, 3)
+            if "memory_side_bytes_bounds" in r:
+                lim["memory_side_tb_s_bounds"] = [round(x / (ms[k] * 1e-3) / 1e12, 3) for x in r["memory_side_bytes_bounds"]]
             if "TA_TA_BUSY_sum" in c:   # vector-memory address path, per CU (256 CUs)
                 lim["ta_busy"] = round(c["TA_TA_BUSY_sum"] / (256 * cyc), 3)
                 if "TA_ADDR_STALLED_BY_TC_CYCLES_sum" in c:
@@ -93,7 +101,7 @@ def main():
                 lim["l1_miss_latency_cycles"] = round(c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"], 1)
                 lim["l1_hit_rate"] = round(1 - c["TCP_TCC_READ_REQ_sum"] / max(c["TCP_TOTAL_CACHE_ACCESSES_sum"], 1), 3)
             mem, iss = lim["wave_time_waiting_on_memory"], lim["wave_time_issue_stalled"]
-            bw = lim.get("memory_side_tb_s", 0.0)
+            bw = lim.get("memory_side_tb_s_bounds", [0.0, 0.0])[1]
             lim["binding"] = ("HBM bandwidth" if bw >= 5.0 else
                               "vector-memory pipeline (TA busy) + memory latency"
                               if lim.get("ta_busy", 0.0) >= 0.85 and mem >= 0.4 else
