@@ -2,7 +2,9 @@
 //
 // One frame (1 sample per pixel, maxDepth D) is, per rank band:
 //   k_bdpt_start          camera vertex 0 + light vertex 0 of every pixel (GenerateStartVertices,
-//                         BDPT.cl:240-312); both first rays go to one compacted ray queue
+//                         BDPT.cl:240-312); the first camera rays and light rays go to two queues
+//                         (d = 1: k_extend + k_bdpt_vertex once per queue, the camera rays over
+//                         the descent-compact records)
 //   for d in 1..D+1:
 //     k_extend            closest hit over the queue (camera and light rays together)
 //     k_bdpt_vertex       GenerateSecondaryVertices (BDPT.cl:317-458) for every queued ray: the
@@ -432,14 +434,15 @@ MCRT_DEV void pushRay(const BdptQueue& q, int slot, f3 o, int tag, f3 d, float f
     q.t[slot] = make_float4(tp.x, tp.y, tp.z, 0.0f);
 }
 
-// GenerateStartVertices (BDPT.cl:240-312) over the rank's 8x8 tiles; both first rays queued.
+// GenerateStartVertices (BDPT.cl:240-312) over the rank's 8x8 tiles; the first camera rays go to
+// camQ (tile order: coherent, traced over the descent-compact records), the light rays to lightQ.
 __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArgs f, BdptArgs b,
-                                                           const mcrt_camera* __restrict__ camp, BdptQueue qOut) {
+                                                           const mcrt_camera* __restrict__ camp, BdptQueue camQ,
+                                                           BdptQueue lightQ) {
     const int lane = threadIdx.x & 63;
     const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     int x = 0, y = 0;
     const bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y) && s.numLights > 0;
-    __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
     const int N = (int)(f.W * f.H);
     const int pix = y * (int)f.W + x;
     f3 camDir = splat3(0.0f), camPos = splat3(0.0f), lo = splat3(0.0f), ld = splat3(0.0f), lt = splat3(0.0f);
@@ -472,10 +475,15 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
         lt = cl_div(le.Le * absDot(le.normal, le.dir), (lightPdf * le.pdfPos * le.pdfDir));
         lightPdfDir = le.pdfDir;
     }
-    const int cs = blockAppend<BDPT_BLOCK / 64>(qOut.count, valid, ldsWave);
-    if (valid) pushRay(qOut, cs, camPos, 2 * pix, camDir, camPdf, splat3(1.0f));
-    const int ls = blockAppend<BDPT_BLOCK / 64>(qOut.count, valid, ldsWave);
-    if (valid) pushRay(qOut, ls, lo, 2 * pix + 1, ld, lightPdfDir, lt);
+    // slot = the lane's place in the tile walk, so both queues keep tile order (a lane outside the
+    // image queues a harmless ray with tag -1, skipped by k_bdpt_vertex)
+    if (tile < f.numTiles) {
+        const int slot = tile * 64 + lane;
+        const f3 up = f3{0.0f, 1.0f, 0.0f};
+        pushRay(camQ, slot, camPos, valid ? 2 * pix : -1, valid ? camDir : up, camPdf, splat3(1.0f));
+        pushRay(lightQ, slot, lo, valid ? 2 * pix + 1 : -1, valid ? ld : up, lightPdfDir, lt);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) camQ.count[0] = lightQ.count[0] = f.numTiles * 64;
 }
 
 // GenerateSecondaryVertices (BDPT.cl:317-458) for every queued subpath ray at depth d.
@@ -492,9 +500,10 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
     f3 no = splat3(0.0f), nd = splat3(0.0f), ntp = splat3(0.0f);
     float nPdf = 0.0f;
     int tag = 0;
-    if (i < n) {
-        const float4 O = qIn.o[i], Dd = qIn.d[i], Tp = qIn.t[i];
-        tag = __float_as_int(O.w);
+    const float4 O = i < n ? qIn.o[i] : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+    tag = __float_as_int(O.w);
+    if (tag >= 0) {   // tag -1: a start-queue slot outside the image
+        const float4 Dd = qIn.d[i], Tp = qIn.t[i];
         const int pix = tag >> 1;
         const bool isCamera = (tag & 1) == 0;
         float4* V = isCamera ? b.camV : b.lightV;
@@ -920,9 +929,9 @@ __global__ __launch_bounds__(256) void k_bdpt_clear_splat(int n, float4* __restr
 
 namespace mcrt {
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
-                       const BdptQueue& q, hipStream_t st) {
+                       const BdptQueue& camQ, const BdptQueue& lightQ, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK;
-    hipLaunchKernelGGL(k_bdpt_start, dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, q);
+    hipLaunchKernelGGL(k_bdpt_start, dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, camQ, lightQ);
 }
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
                         const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st) {

@@ -191,6 +191,9 @@ struct mcrt_framebuffer_s {
     bool bdptPendingGather = false;   // band-split BDPT frame waiting for the ranks' summed splats
 };
 
+// BDPT queue counters (64 ints per frame set): [d] the subpath-ray queue of depth d (d <= 33;
+// at depth 0 the light rays only), then these
+enum { BDPT_CNT_CONN = 40, BDPT_CNT_CAM0 = 41 };
 static int bdpt_max_connections(int D) { const int t = D + 2; return t * (t + 1) / 2 - 2; }   // RTBDPTPass.cpp:404-408
 
 // ---------------------------------------------------------------------------
@@ -1156,7 +1159,9 @@ static void ctx_wait_slots(mcrt_framebuffer fb) {
         if (k.stream) hipStreamWaitEvent(fb->ctx->stream, k.done, 0);
 }
 
-static hipError_t bset_alloc(BdptSet& b, size_t N, int D) {
+// NQ = the pixels of the whole 8x8 tiles covering the image (>= N): the start queues hold one slot
+// per lane of the tile walk.  Ray queues and hits hold 2 x NQ (the depth-1 camera and light halves).
+static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D) {
     const size_t C = (size_t)bdpt_max_connections(D);
     hipError_t e = hipSuccess;
     auto A = [&](auto** p, size_t bytes) {
@@ -1169,8 +1174,8 @@ static hipError_t bset_alloc(BdptSet& b, size_t N, int D) {
     A(&b.camCount, 4 * N);
     A(&b.lightCount, 4 * N);
     A(&b.bdptCounters, 64 * sizeof(int));
-    for (int i = 0; i < 2; ++i) { A(&b.bqO[i], 32 * N); A(&b.bqD[i], 32 * N); A(&b.bqT[i], 32 * N); }
-    A(&b.bHits, 32 * N);
+    for (int i = 0; i < 2; ++i) { A(&b.bqO[i], 32 * NQ); A(&b.bqD[i], 32 * NQ); A(&b.bqT[i], 32 * NQ); }
+    A(&b.bHits, 32 * NQ);
     A(&b.cO, 16 * N * C);
     A(&b.cD, 16 * N * C);
     A(&b.cL, 16 * N * C);
@@ -1193,6 +1198,9 @@ static void fb_bind_bdpt(mcrt_framebuffer fb, int k) {
 // RTBDPTPass::createBuffers (RTBDPTPass.cpp:442-479), sized for max depth D: set k of the
 // per-frame arrays, plus the persistent sampled-light-vertex planes, which start zeroed (the
 // reference's buffer starts with whatever the allocation holds; its clref runner zero-fills it too).
+static size_t bdpt_queue_cap(mcrt_framebuffer fb) {
+    return (size_t)((fb->W + 7) / 8) * ((fb->H + 7) / 8) * 64;
+}
 static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k) {
     const size_t N = fb->N;
     if (fb->bdptDepth != D) {
@@ -1206,7 +1214,7 @@ static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k) {
         if (e != hipSuccess) { fb_free_bdpt(fb); return e; }
         fb->bdptDepth = D;
     }
-    if (!fb->bset[k].camV) return bset_alloc(fb->bset[k], N, D);
+    if (!fb->bset[k].camV) return bset_alloc(fb->bset[k], N, bdpt_queue_cap(fb), D);
     return hipSuccess;
 }
 
@@ -1332,7 +1340,8 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     }
     const size_t N = fb->N, C = (size_t)bdpt_max_connections(D);
     BdptSet& bs = fb->bset[k];
-    const size_t spillWords = (std::max(2 * N, C * N) + 63) / 64 * 64 * (size_t)s->spillCap;
+    const size_t NQ = bdpt_queue_cap(fb);
+    const size_t spillWords = (std::max(2 * NQ, C * N) + 63) / 64 * 64 * (size_t)s->spillCap;
     if (bs.spillWords < spillWords) {
         HIPCHK(ctx, hipStreamSynchronize(st));
         if (bs.spill) hipFree(bs.spill);
@@ -1353,7 +1362,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     b.slots = fb->slots;
     b.splat = fb->splat;
     b.ownSlots = (int)C - D;
-    int* cnt = fb->bdptCounters;   // [d] ray queue of depth d, [32] connection queue
+    int* cnt = fb->bdptCounters;   // [d] ray queue of depth d (d <= D + 1 <= 33), BDPT_CNT_* below
     auto queue = [&](int d) {
         BdptQueue q;
         q.count = cnt + d;
@@ -1365,11 +1374,35 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     const bool bandSplit = f.numBands > 1;
     if (bandSplit)   // splats of this rank's light paths land in any pixel: clear the whole buffer
         mcrt::launch_bdpt_clear_splat((int)N, fb->splat, st);
+    // depth 0: camera rays (coherent, 8x8 tiles in order) in the first half of queue 0's buffers
+    // with their own count, light rays in the second half with count [0]; ONE launch traces both,
+    // the camera rays over the descent-compact records like PT's camera rays (compact_ctx); both
+    // halves then feed the depth-1 vertex launches, which append to queue 1
+    BdptQueue camQ = queue(0), lightQ = queue(0);
+    camQ.count = cnt + BDPT_CNT_CAM0;
+    lightQ.o += NQ;
+    lightQ.d += NQ;
+    lightQ.t += NQ;
     {
         Timed t(ctx, K_BDPT_START, nullptr, (int64_t)f.numTiles * 64, st);
-        mcrt::launch_bdpt_start(sa, f, b, dCam, queue(0), st);
+        mcrt::launch_bdpt_start(sa, f, b, dCam, camQ, lightQ, st);
     }
-    for (int d = 1; d <= D + 1; ++d) {
+    {
+        TraceCtx tcc = compact_ctx(s);
+        tcc.spill = bs.spill;
+        Timed t(ctx, K_EXTEND, camQ.count, 0, st);
+        mcrt::launch_extend_pair(tcc, tcs, camQ.count, camQ.o, camQ.d, fb->bHits, lightQ.count, lightQ.o, lightQ.d,
+                                 fb->bHits + NQ, (int)NQ, (int)NQ, st);
+    }
+    {
+        Timed t(ctx, K_BDPT_VERTEX, camQ.count, 0, st);
+        mcrt::launch_bdpt_vertex(sa, f, b, 1, camQ, fb->bHits, queue(1), (int)NQ, st);
+    }
+    {
+        Timed t(ctx, K_BDPT_VERTEX, lightQ.count, 0, st);
+        mcrt::launch_bdpt_vertex(sa, f, b, 1, lightQ, fb->bHits + NQ, queue(1), (int)NQ, st);
+    }
+    for (int d = 2; d <= D + 1; ++d) {
         const BdptQueue qIn = queue(d - 1), qOut = queue(d);
         {
             Timed t(ctx, K_EXTEND, qIn.count, 0, st);
@@ -1379,7 +1412,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         mcrt::launch_bdpt_vertex(sa, f, b, d, qIn, fb->bHits, qOut, (int)(2 * N), st);
     }
     BdptQueue cq;
-    cq.count = cnt + 32;
+    cq.count = cnt + BDPT_CNT_CONN;
     cq.o = fb->cO;
     cq.d = fb->cD;
     cq.t = fb->cL;
@@ -1440,7 +1473,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     if (bdpt && ks != 0 && fb->bdptDepth == p->max_depth && !fb->bset[ks].camV) {
         // each BDPT set holds ~C x N x 48 B of connection rays (2.5 GB at 1080p, D = 2): when a
         // second one does not fit, fall back to one frame in flight instead of failing the frame
-        const hipError_t e = bset_alloc(fb->bset[ks], fb->N, p->max_depth);
+        const hipError_t e = bset_alloc(fb->bset[ks], fb->N, bdpt_queue_cap(fb), p->max_depth);
         if (e == hipErrorOutOfMemory) {
             hipGetLastError();
             fb->bdptOneSet = true;
@@ -1720,8 +1753,9 @@ MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closes
         HIPCHK(ctx, hipMemcpy(c, fb->bdptCounters, sizeof(c), hipMemcpyDeviceToHost));
         int64_t cl = 0;
         for (int d = 0; d <= fb->lastMaxDepth; ++d) cl += c[d];
+        cl += c[BDPT_CNT_CAM0];
         if (closest_rays) *closest_rays = cl;
-        if (any_rays) *any_rays = c[32];
+        if (any_rays) *any_rays = c[BDPT_CNT_CONN];
         if (shaded_paths) *shaded_paths = cl;
         return MCRT_OK;
     }

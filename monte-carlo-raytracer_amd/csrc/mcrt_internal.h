@@ -92,6 +92,10 @@ void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshSt
                             int numMeshes, uint32_t numRecords, const uint32_t* indices, const float4* positions,
                             const float2* uvs, const float4* normals, float4* surf, hipStream_t st);
 void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st);
+// closest hit over two queues in one launch: queue 0 over cc's records, queue 1 over c's
+void launch_extend_pair(const TraceCtx& cc, const TraceCtx& c, const int* count0, const float4* qO0, const float4* qD0,
+                        float4* hit0, const int* count1, const float4* qO1, const float4* qD1, float4* hit1,
+                        int maxCount0, int maxCount1, hipStream_t st);
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
                    hipStream_t st);
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
@@ -118,7 +122,7 @@ void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* s
 // the exact-union property or an index does not fit the 27-bit child word
 void launch_pack_compact(const float4* in, float4* out, uint32_t n, int* bad, hipStream_t st);
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
-                       const BdptQueue& q, hipStream_t st);
+                       const BdptQueue& camQ, const BdptQueue& lightQ, hipStream_t st);
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
                         const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st);
 void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,

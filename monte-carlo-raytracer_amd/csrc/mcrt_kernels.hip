@@ -231,6 +231,42 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
     }
 }
 
+// Closest hit over two queues in ONE launch, each over its own records: BDPT's first camera rays
+// (coherent: descent-compact records, cc) and first light rays (plain records, c).  The camera
+// workgroups come first; the light workgroups fill their tail (as k_shadow_extend).
+template <int LAY0, int LAY1>
+__global__ __launch_bounds__(64) void k_extend_pair(TraceCtx cc, TraceCtx c, const int* __restrict__ count0,
+                                                    const float4* __restrict__ qO0, const float4* __restrict__ qD0,
+                                                    float4* __restrict__ hit0, const int* __restrict__ count1,
+                                                    const float4* __restrict__ qO1, const float4* __restrict__ qD1,
+                                                    float4* __restrict__ hit1) {
+    __shared__ uint32_t lds[STACK_LDS * 64];
+    const int n0 = *count0;
+    const int b0 = (n0 + 63) >> 6;
+    const int lane = threadIdx.x;
+    TraceRay r;
+    r.tmax = RT_MAX_TRACE_F;
+    r.mask = -1;
+    float t;
+    if ((int)blockIdx.x < b0) {
+        const int blk = xcdRemap(blockIdx.x, b0);
+        const int i = blk * 64 + lane;
+        if (i >= n0) return;
+        r.o = ld3(qO0[i]);
+        r.d = ld3(qD0[i]);
+        hit0[i] = traceClosest<LAY0>(cc, r, lds + lane, raySpill(cc, blk, lane), t);
+    } else {
+        const int n1 = *count1;
+        const int b1 = (n1 + 63) >> 6;
+        if ((int)blockIdx.x - b0 >= b1) return;
+        const int i = xcdRemap((int)blockIdx.x - b0, b1) * 64 + lane;
+        if (i >= n1) return;
+        r.o = ld3(qO1[i]);
+        r.d = ld3(qD1[i]);
+        hit1[i] = traceClosest<LAY1>(c, r, lds + lane, raySpill(c, blockIdx.x, lane), t);
+    }
+}
+
 // PathTracing kernel body (PathTracing.cl:52-184) for one path.
 // Returns the radiance term added at this vertex by emission (or by a NaN NEE term
 // with no shadow ray).  NEE terms go to the shadow queue.
@@ -746,6 +782,15 @@ void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const 
                    hipStream_t st) {
     hipLaunchKernelGGL(pickLayout(c, k_extend<LAY_TWO_LEVEL>, k_extend<LAY_COMPACT>, k_extend<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, qO, qD, hits);
+}
+void launch_extend_pair(const TraceCtx& cc, const TraceCtx& c, const int* count0, const float4* qO0, const float4* qD0,
+                        float4* hit0, const int* count1, const float4* qO1, const float4* qD1, float4* hit1,
+                        int maxCount0, int maxCount1, hipStream_t st) {
+    auto k = c.twoLevel ? k_extend_pair<LAY_TWO_LEVEL, LAY_TWO_LEVEL>
+             : cc.compact ? k_extend_pair<LAY_COMPACT, LAY_PLAIN> : k_extend_pair<LAY_PLAIN, LAY_PLAIN>;
+    const int blocks = (maxCount0 + 63) / 64 + (maxCount1 + 63) / 64;
+    hipLaunchKernelGGL(k, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, cc, c, count0, qO0, qD0, hit0, count1, qO1,
+                       qD1, hit1);
 }
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st) {

@@ -90,7 +90,7 @@ def main():
                 ctx.set_profiling(False)
                 kern = {k: round(v["ms"] / args.steps, 4) for k, v in ks.items()}
         out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
-                           "min_ms": round(min(per_rank), 4)}
+                           "min_ms": round(min(per_rank), 4), "rank_ms": [round(x, 4) for x in per_rank]}
         if args.kernels:
             out["per_n"][n]["rank0_kernel_ms_per_frame"] = kern
     # efficiency is relative to ONE GPU rendering the whole image: the N = 1 run of this sweep, or
