@@ -509,6 +509,8 @@ def main():
     ctx.reset_stats()
     if world > 1:
         acc_buf, acc_s, acc_w = mdist.packed_accumulators(W * H, "cuda")   # one buffer -> one reduce
+        if args.end_collective == "gather" and dist.get_backend() not in ("nccl", "gloo"):
+            args.end_collective = "reduce"   # decided from the backend, identically on every rank
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
@@ -517,13 +519,11 @@ def main():
         fb.copy_device(1, acc_s.data_ptr())
         fb.copy_device(3, acc_w.data_ptr())
         ctx.sync()
+        # no try/except here: a fallback taken by one rank while the others sit in the gather would
+        # hang the job; an error exits this rank and torch.distributed.run stops the others
         if args.end_collective == "gather":
-            try:
-                mdist.gather_bands(acc_s, acc_w, H, W, args.band_rows, dst=0)
-            except (RuntimeError, NotImplementedError) as e:   # a backend without gather: every rank raises
-                log(f"[bench] band gather failed ({e}); full-frame reduce instead")
-                args.end_collective = "reduce"
-        if args.end_collective == "reduce":
+            mdist.gather_bands(acc_s, acc_w, H, W, args.band_rows, dst=0)
+        else:
             mdist.reduce_packed(acc_buf, dst=0)
         if rank == 0:
             torch.cuda.synchronize()
