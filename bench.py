@@ -203,7 +203,8 @@ def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
         return None
 
 
-def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing, split="band"):
+def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing, split="band",
+                 batch=4):
     """Config 4's integrator on the same scene and GPU(s): BDPT (RTBDPTPass::update), 1 spp per
     step, split over the ranks by frames (rank r renders frames r, r + N, ...; light-tracing splats
     land anywhere in the image) or by 8-row bands (one splat reduce-scatter per frame,
@@ -218,27 +219,30 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     filt = T.make_filter(T.BOX)
     first = [True]
     band = split == "band" and world > 1
-    if band:   # rank-major splats (chunks of this rank count x 8-row blocks) and this rank's chunk
+    if band:   # rank-major splats (chunks of this rank count x 8-row blocks x batch frames) + own chunk
         cr = mdist.splat_chunk_rows(H, 8, world)
-        splat_full = torch.zeros(4 * W * cr * world, dtype=torch.float32, device="cuda")
-        splat_own = torch.zeros(4 * W * cr, dtype=torch.float32, device="cuda")
+        splat_full = torch.zeros(4 * W * cr * batch * world, dtype=torch.float32, device="cuda")
+        splat_own = torch.zeros(4 * W * cr * batch, dtype=torch.float32, device="cuda")
 
     def run(i0, count):
-        for i in range(i0, i0 + count):
+        # calls of up to `batch` consecutive frames (mcrt_render_frames): band split: every rank the
+        # same frames; frame split: rank r its own consecutive block of frame indices (its RNG streams)
+        i = i0
+        while i < i0 + count:
+            k = min(batch, i0 + count - i)
+            f = i if band else rank * (1 << 20) + i
+            cams = [cam_of(f + j) for j in range(k)]
+            bands = dict(band_rows=8, num_bands=world, band_index=rank) if band else {}
+            fb.render_frames(ds, cams, frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT, **bands)
             if band:
-                f = i
-                fb.render(ds, cam_of(f), frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT,
-                          band_rows=8, num_bands=world, band_index=rank)
                 mdist.exchange_splats(fb, splat_full, splat_own)
-            else:
-                f = rank + world * i
-                fb.render(ds, cam_of(f), frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT)
-            fb.accumulate(filt, 0 if first[0] else f)
+            fb.accumulate_frames([filt] * k, 0 if first[0] else f)
             first[0] = False
+            i += k
 
-    run(0, max(warmup, 2))
+    f0 = max(warmup, 3 * batch)   # every frame slot holds a whole batch before timing
+    run(0, f0)
     ctx.sync()
-    f0 = max(warmup, 2)
     if world > 1:
         acc_buf, acc_s, acc_w = mdist.packed_accumulators(W * H, "cuda")
         dist.barrier()
@@ -270,18 +274,21 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
                           f"frame split x {world} + 1 RCCL reduce"),
            "rays_per_path": {"subpath": round(st["closest_rays"] / (W * H), 4),
                              "connection": round(st["any_rays"] / (W * H), 4)}}
-    if kernel_timing:
+    if kernel_timing:   # one slot, one call of `batch` frames (the timed calls' shape)
+        kb = min(batch, steps)
         fb.set_frames_in_flight(1)
-        run(f0 + steps, 1)
+        run(f0 + steps, kb)
         ctx.sync()
         ctx.set_profiling(True)
         ctx.reset_stats()
-        run(f0 + steps + 1, 2)
+        run(f0 + steps + kb, kb)
         ctx.sync()
         ks = ctx.kernel_stats()
         ctx.set_profiling(False)
         out["kernels"] = {k: {"avg_ms": round(v["ms"] / max(v["launches"], 1), 4), "launches": v["launches"],
-                              "ms_per_frame": round(v["ms"] / 2, 4)} for k, v in ks.items()}
+                              "ms_per_frame": round(v["ms"] / kb, 4)} for k, v in ks.items()}
+        out["kernels_note"] = f"one frame slot, one call of {kb} frames (per-kernel HIP events)"
+    out["frames_per_call"] = batch
     out["_fb"] = fb
     return out
 
@@ -364,7 +371,7 @@ def main():
                     help="launch sequences of the untimed per-kernel timing pass (one frame slot)")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     ap.add_argument("--no-bdpt", action="store_true", help="skip the BDPT object (config 4) of the PT run")
-    ap.add_argument("--bdpt-steps", type=int, default=8, help="timed BDPT frames of the BDPT object")
+    ap.add_argument("--bdpt-steps", type=int, default=16, help="timed BDPT frames of the BDPT object")
     ap.add_argument("--bdpt-split", default="band", choices=["frame", "band"],
                     help="multi-GPU BDPT: 8-row bands per rank with one splat reduce-scatter per frame (default: "
                          "the 1-GPU image up to splat summation order; mcrt.dist.exchange_splats) or whole frames "
@@ -384,6 +391,8 @@ def main():
                     help="A/B only: round every call's frame count down to a power of two (16 + 4 for 20 steps)")
     ap.add_argument("--chunks", default="",
                     help="A/B only: comma-separated frames per call of the timed region, cycled (e.g. 4,16)")
+    ap.add_argument("--bdpt-batch", type=int, default=4,
+                    help="BDPT frames per mcrt_render_frames call (the BDPT object and --integrator bdpt)")
     ap.add_argument("--batch", type=int, default=0,
                     help="PT frames per mcrt_render_frames call (one launch sequence for all of them); "
                          "0 = auto (32 up to 1080p, 16 above)")
@@ -447,8 +456,8 @@ def main():
     if band_bdpt:   # band split: every rank renders every frame's rows of its bands
         band = dict(band_rows=8, num_bands=world, band_index=rank, integrator=T.INTEGRATOR_BDPT)
         cr = mdist.splat_chunk_rows(H, 8, world)
-        splat_full = torch.zeros(4 * W * cr * world, dtype=torch.float32, device="cuda")
-        splat_own = torch.zeros(4 * W * cr, dtype=torch.float32, device="cuda")
+        splat_full = torch.zeros(4 * W * cr * args.bdpt_batch * world, dtype=torch.float32, device="cuda")
+        splat_own = torch.zeros(4 * W * cr * args.bdpt_batch, dtype=torch.float32, device="cuda")
     elif bdpt:   # frame split: whole frames per rank
         band = dict(band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_BDPT)
     else:
@@ -458,21 +467,22 @@ def main():
     # camera and first-shading waves then hold 2 pixels x 32 jittered frames (packed waves); the
     # sweep tools/r2_gpu27.sh measured 1297 / 1315 Mpaths/s at 16 / 32 frames per launch, and a
     # 1/N band share x 32 frames keeps every multi-GPU launch at >= 4 whole images of paths
-    batch = 1 if bdpt else (args.batch if args.batch > 0 else (32 if W * H <= 2_100_000 else 16))
+    batch = args.bdpt_batch if bdpt else (args.batch if args.batch > 0 else (32 if W * H <= 2_100_000 else 16))
     # the untimed per-kernel pass and the roofline price the TIMED launch shape: calls of
     # min(batch, steps) frames (the driver's 20 steps are one 20-frame call)
     stats_batch = min(batch, args.steps)
 
     def step(i, n=1):
         """frames i .. i+n-1 (one mcrt_render_frames call when n > 1)"""
-        frame = rank + world * i if bdpt and not band_bdpt else i
+        # BDPT frame split: rank r renders its own consecutive block of frame indices (RNG streams)
+        frame = rank * (1 << 20) + i if bdpt and not band_bdpt else i
         kw = dict(max_depth=D, sampler=sampler, rr=args.russian_roulette, rr_start=args.rr_start, **band)
         if n == 1:
             fb.render(ds, cam_of(frame), frame=frame, **kw)
-            if band_bdpt:
-                mdist.exchange_splats(fb, splat_full, splat_own)
         else:
             fb.render_frames(ds, [cam_of(frame + k) for k in range(n)], frame=frame, **kw)
+        if band_bdpt:   # one splat exchange per call (all its frames)
+            mdist.exchange_splats(fb, splat_full, splat_own)
         fb.accumulate(filt, 0 if first[0] else frame)   # 0: the first accumulation overwrites
         first[0] = False
 
@@ -558,7 +568,7 @@ def main():
     bd = None
     if not bdpt and not args.no_bdpt and not two_level:   # config 4's integrator beside the PT headline
         bd = bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, args.bdpt_steps, args.warmup,
-                          not args.no_kernel_timing, args.bdpt_split)
+                          not args.no_kernel_timing, args.bdpt_split, args.bdpt_batch)
 
     paths = W * H * args.steps * (world if bdpt and not band_bdpt else 1)
     value = paths / elapsed / 1e6
@@ -609,7 +619,8 @@ def main():
             out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 4)
         if kstats:
             out["kernels"] = {k: {"avg_ms": round(v["ms"] / max(v["launches"], 1), 4), "launches": v["launches"],
-                                  "items_per_launch": round(v["items"] / max(v["launches"], 1), 1)}
+                                  "items_per_launch": round(v["items"] / max(v["launches"], 1), 1),
+                                  "ms_per_frame": round(v["ms"] / (args.stats_launches * stats_batch), 4)}
                               for k, v in kstats.items()}
             out["kernels_note"] = ("HIP-event durations from an untimed pass after the timed region: one frame slot "
                                    f"(no overlap with another frame's launches), {args.stats_launches} calls of "

@@ -400,7 +400,7 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene scene, mcrt_framebuffer fb, co
  * After mcrt_render_frames it accumulates every frame of that batch in frame order
  * (frame_index = the batch's first frame), all with this filter. */
 MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* filter, int32_t frame_index);
-/* Batched frames (PT): renders the `count` (1..32) consecutive 1-spp frames
+/* Batched frames (PT and BDPT): renders the `count` (1..32) consecutive 1-spp frames
  * params->frame_index + k, k < count, with cameras[k] (per-frame TAA jitter), in ONE pass --
  * every launch (camera rays, shading, shadow + extension rays) covers all count frames' paths,
  * so a small per-rank band share (tile split over N GPUs) still fills the 256 CUs and the
@@ -409,7 +409,12 @@ MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* fil
  * mcrt_render_frame; mcrt_accumulate_frames (or mcrt_accumulate) then sums them in frame order,
  * so the image equals count x (mcrt_render_frame + mcrt_accumulate) bit for bit.  Radiance read
  * back (mcrt_framebuffer_read 0) is the batch's first frame.  The reference renders one frame
- * per RTPathTracingPass::update; this is the same sequence, launched wider. */
+ * per RTPathTracingPass::update; this is the same sequence, launched wider.
+ * BDPT (RTBDPTPass::update per frame): every launch covers the batch's (tile, frame) paths; the
+ * s = 1 strategies walk the batch's frames in order, so the sampled-light-vertex slot each frame
+ * reads is the one the previous frame wrote (BDPT.cl:585-586), as in count single calls; vertices
+ * and own strategies are those of count single calls bit for bit, splat sums up to atomic order.
+ * With a band split, mcrt_bdpt_splat_layout's chunk then holds the batch's frames. */
 MCRT_API mcrt_status mcrt_render_frames(mcrt_scene scene, mcrt_framebuffer fb, const mcrt_camera* cameras,
                                         int32_t count, const mcrt_frame_params* params);
 /* filters: `count` filters (one per frame of the last mcrt_render_frames; the per-frame filter

@@ -434,21 +434,33 @@ MCRT_DEV void pushRay(const BdptQueue& q, int slot, f3 o, int tag, f3 d, float f
     q.t[slot] = make_float4(tp.x, tp.y, tp.z, 0.0f);
 }
 
-// GenerateStartVertices (BDPT.cl:240-312) over the rank's 8x8 tiles; the first camera rays go to
-// camQ (tile order: coherent, traced over the descent-compact records), the light rays to lightQ.
+// Batched frames (mcrt_render_frames, f.batch = B): frame k of the batch is path p = k * N + pixel
+// in every per-frame plane (vertices, counts, slots, splats: plane stride NB = N * B), samples with
+// frame index f.frame + k and camera camp[k]; launches over (tile, frame) walk a tile's frames
+// back to back (their jittered camera rays share nodes).
+MCRT_DEV void tileFrame(const FrameArgs& f, int tileAll, int& tile, int& k) {
+    tile = tileAll / f.batch;
+    k = tileAll - tile * f.batch;
+}
+
+// GenerateStartVertices (BDPT.cl:240-312) over the rank's 8x8 tiles x batch frames; the first
+// camera rays go to camQ (tile order: coherent, traced over the descent-compact records), the
+// light rays to lightQ.
 __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArgs f, BdptArgs b,
                                                            const mcrt_camera* __restrict__ camp, BdptQueue camQ,
                                                            BdptQueue lightQ) {
     const int lane = threadIdx.x & 63;
-    const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int tileAll = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int tile, k;
+    tileFrame(f, tileAll, tile, k);
     int x = 0, y = 0;
     const bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y) && s.numLights > 0;
-    const int N = (int)(f.W * f.H);
-    const int pix = y * (int)f.W + x;
+    const int N = (int)(f.W * f.H), NB = N * f.batch;
+    const int px = y * (int)f.W + x, pix = k * N + px;   // pix: the path (plane index)
     f3 camDir = splat3(0.0f), camPos = splat3(0.0f), lo = splat3(0.0f), ld = splat3(0.0f), lt = splat3(0.0f);
     float camPdf = 0.0f, lightPdfDir = 0.0f;
     if (valid) {
-        const mcrt_camera& cam = *camp;
+        const mcrt_camera& cam = camp[k];
         b.splat[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         b.camCount[pix] = 1;
         b.lightCount[pix] = 1;
@@ -457,10 +469,10 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
         const f2 uv = f2{(float)x * r.x, (float)y * r.y};
         camDir = lerpDirection(ld3(cam.r00), ld3(cam.r10), ld3(cam.r11), ld3(cam.r01), uv.x, uv.y);
         camPos = ld3(cam.pos);
-        storeVertex(b.camV, 0, pix, N, createCameraVertex(camPos, splat3(1.0f)));
+        storeVertex(b.camV, 0, pix, NB, createCameraVertex(camPos, splat3(1.0f)));
         camPdf = evalPinholeCameraPdfWe(cam, camPos, camDir);
         // light (BDPT.cl:294-311)
-        Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, 0, f.W, f.H, s.sobol);
+        Sampler sampler = makeSampler(f.sampler, (uint32_t)px, f.frame + k, 0, f.W, f.H, s.sobol);
         const int chosen = (int)(((uint32_t)floorf(getSample1D(sampler) * s.numLights)) % (uint32_t)s.numLights);
         const mcrt_light light = s.lights[chosen];
         const float lightPdf = light.choicePdf;
@@ -469,7 +481,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
         const LightLe le = sampleLightLe(s, light, u1, u2);
         BVertex lv = createLightVertex(chosen, le.origin, le.normal, le.Le, le.pdfPos * lightPdf, light.flags);
         lv.pdfPos = le.pdfPos;
-        storeVertex(b.lightV, 0, pix, N, lv);
+        storeVertex(b.lightV, 0, pix, NB, lv);
         lo = le.origin;
         ld = le.dir;
         lt = cl_div(le.Le * absDot(le.normal, le.dir), (lightPdf * le.pdfPos * le.pdfDir));
@@ -478,12 +490,12 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
     // slot = the lane's place in the tile walk, so both queues keep tile order (a lane outside the
     // image queues a harmless ray with tag -1, skipped by k_bdpt_vertex)
     if (tile < f.numTiles) {
-        const int slot = tile * 64 + lane;
+        const int slot = tileAll * 64 + lane;
         const f3 up = f3{0.0f, 1.0f, 0.0f};
         pushRay(camQ, slot, camPos, valid ? 2 * pix : -1, valid ? camDir : up, camPdf, splat3(1.0f));
         pushRay(lightQ, slot, lo, valid ? 2 * pix + 1 : -1, valid ? ld : up, lightPdfDir, lt);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) camQ.count[0] = lightQ.count[0] = f.numTiles * 64;
+    if (blockIdx.x == 0 && threadIdx.x == 0) camQ.count[0] = lightQ.count[0] = f.numTiles * f.batch * 64;
 }
 
 // GenerateSecondaryVertices (BDPT.cl:317-458) for every queued subpath ray at depth d.
@@ -494,7 +506,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
     const int n = *qIn.count;
     __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
     if ((int)blockIdx.x * BDPT_BLOCK >= n) return;
-    const int N = (int)(f.W * f.H);
+    const int N = (int)(f.W * f.H) * f.batch;   // plane stride (NB)
     const int D = f.maxDepth;
     bool push = false;
     f3 no = splat3(0.0f), nd = splat3(0.0f), ntp = splat3(0.0f);
@@ -504,7 +516,8 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
     tag = __float_as_int(O.w);
     if (tag >= 0) {   // tag -1: a start-queue slot outside the image
         const float4 Dd = qIn.d[i], Tp = qIn.t[i];
-        const int pix = tag >> 1;
+        const int pix = tag >> 1;   // path k * (W*H) + pixel
+        const int kf = pix / (int)(f.W * f.H), px = pix - kf * (int)(f.W * f.H);
         const bool isCamera = (tag & 1) == 0;
         float4* V = isCamera ? b.camV : b.lightV;
         const float4 hit = hits[i];
@@ -555,7 +568,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                 if (hasMaterialNonDeltaComponents(s, materialIdx, cur.fr)) cur.flags |= VF_CONNECTIBLE;
                 storeVertex(V, depth, pix, N, cur);
             } else {
-                Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, depth + (D + 1) * (isCamera ? 1 : 0),
+                Sampler sampler = makeSampler(f.sampler, (uint32_t)px, f.frame + kf, depth + (D + 1) * (isCamera ? 1 : 0),
                                               f.W, f.H, s.sobol);
                 const f3 wo = cur.wo;
                 const f2 bsdfSample = getSample2D(sampler);
@@ -645,16 +658,26 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                                                              int numStrat) {
     const int lane = threadIdx.x & 63;
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int tile = wave / numStrat;
+    // a wave = (tile, strategy, batch frame); NEE waves walk the batch's frames in order in-thread
+    // (frame k's s = 1 strategy reads the sampled-light slot frame k - 1 wrote)
+    const int kb = CLS == CONN_NEE ? 1 : f.batch;
+    const int per = numStrat * kb;
+    const int tile = wave / per;
+    const int rem = wave - tile * per;
+    const int si = rem / kb;
     int t, sI;
-    strategyOf<CLS>(wave - tile * numStrat, f.maxDepth, t, sI);
+    strategyOf<CLS>(si, f.maxDepth, t, sI);
     int x = 0, y = 0;
     const bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y) && s.numLights > 0;
     __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
-    const int N = (int)(f.W * f.H);
+    const int N0 = (int)(f.W * f.H);
+    const int N = N0 * f.batch;   // plane stride
     const int D = f.maxDepth;
-    const int pix = y * (int)f.W + x;
-    const mcrt_camera& cam = *camp;
+    const int px = y * (int)f.W + x;
+    const int kBegin = CLS == CONN_NEE ? 0 : rem - si * kb, kEnd = CLS == CONN_NEE ? f.batch : kBegin + 1;
+    for (int k = kBegin; k < kEnd; ++k) {
+    const int pix = k * N0 + px;   // the path (plane index)
+    const mcrt_camera& cam = camp[k];
     const int camCount = valid ? b.camCount[pix] : 0;
     const int lightCount = valid ? b.lightCount[pix] : 0;
     const bool live = valid && t <= camCount && sI <= lightCount;
@@ -687,7 +710,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                     int ix = (int)floorf(nip.x * f.W + 0.5f), iy = (int)floorf(nip.y * f.H + 0.5f);
                     ix = min(max(ix, 0), (int)f.W - 1);
                     iy = min(max(iy, 0), (int)f.H - 1);
-                    code = ~(ix + iy * (int)f.W);
+                    code = ~(k * N0 + ix + iy * (int)f.W);   // frame k's splat plane
                     L = lv.throughput * samp.throughput * evalVertex_f(lv, pix, N, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
                     if (isVertexOnSurface(lv.fr.gn)) L *= absDot(wi, lv.fr.sn);
                     rayO = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
@@ -699,7 +722,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
         } else if (CLS == CONN_NEE) {
             if (isConnectible(cv.flags)) {
                 // the pixel's connection stream, past the draws of the earlier s = 1 strategies
-                Sampler sampler = makeSampler(f.sampler, (uint32_t)pix, f.frame, (D + 1) + (D + 2), f.W, f.H, s.sobol);
+                Sampler sampler = makeSampler(f.sampler, (uint32_t)px, f.frame + k, (D + 1) + (D + 2), f.W, f.H, s.sobol);
                 int skip = 0;
                 for (int u = 2; u < t; ++u)
                     if (u <= camCount && isConnectible(reinterpret_cast<const int4*>(&vplane(b.camV, u - 1, 7, N)[pix])->y))
@@ -715,7 +738,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                 if (isNotNearZero(ls.pdf) && isNotBlack(ls.Li)) {
                     // the reference evaluates pdfFwd on the PREVIOUS content of the sampled
                     // vertex slot before overwriting it (BDPT.cl:585-586)
-                    float4* stale = b.sampLight + (size_t)(t - 2) * N + pix;
+                    float4* stale = b.sampLight + (size_t)(t - 2) * N0 + px;   // per pixel, across frames
                     const float4 st = *stale;
                     const int stBits = __float_as_int(st.w);
                     const int stFlags = stBits >> 16, stLight = (int)(short)(stBits & 0xffff);
@@ -846,9 +869,11 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
     } else if (valid && CLS != CONN_LIGHT) {
         b.slots[(size_t)ownSlotOf(t, sI, D) * N + pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // strategy absent
     }
-    if (CLS == CONN_EMIT) return;   // emission needs no connection ray (wave-uniform: the whole block)
-    const int qslot = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
-    if (push) pushConn(qOut, qslot, rayO, rayT, rayD, code, L);
+    if (CLS != CONN_EMIT) {   // emission needs no connection ray (class-uniform: the whole block)
+        const int qslot = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
+        if (push) pushConn(qOut, qslot, rayO, rayT, rayD, code, L);
+    }
+    }
 }
 
 // Any hit over the connection queue (RR occluded_main semantics): occluded own strategies are
@@ -857,67 +882,77 @@ template <int LAY>
 __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const int* __restrict__ count,
                                                  const float4* __restrict__ sO, const float4* __restrict__ sD,
                                                  const float4* __restrict__ sL) {
+    // grid-stride over the queue (a batch's C x N slots would need one spill column per slot)
     __shared__ uint32_t lds[STACK_LDS * 64];
     const int n = *count;
-    if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
-    const int i = blockIdx.x * 64 + lane;
-    if (i >= n) return;
-    const float4 o = sO[i], d = sD[i];
-    TraceRay r;
-    r.o = ld3(o);
-    r.d = ld3(d);
-    r.tmax = o.w;
-    r.mask = -1;
-    const bool occluded = traceAny<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane));
-    const int code = __float_as_int(d.w);
-    if (code >= 0) {
-        if (occluded) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    } else if (!occluded) {
-        const float4 L = sL[i];
-        float* dst = reinterpret_cast<float*>(&b.splat[~code]);
-        atomicAdd(dst + 0, L.x);
-        atomicAdd(dst + 1, L.y);
-        atomicAdd(dst + 2, L.z);
+    for (int base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
+        const int i = base + lane;
+        if (i >= n) return;
+        const float4 o = sO[i], d = sD[i];
+        TraceRay r;
+        r.o = ld3(o);
+        r.d = ld3(d);
+        r.tmax = o.w;
+        r.mask = -1;
+        const bool occluded = traceAny<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane));
+        const int code = __float_as_int(d.w);
+        if (code >= 0) {
+            if (occluded) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        } else if (!occluded) {
+            const float4 L = sL[i];
+            float* dst = reinterpret_cast<float*>(&b.splat[~code]);
+            atomicAdd(dst + 0, L.x);
+            atomicAdd(dst + 1, L.y);
+            atomicAdd(dst + 2, L.z);
+        }
     }
 }
 
 // Own strategies summed in (t, s) order (the reference's per-thread atomicAdd_f order), then the
-// splats; radiance = float4(sum, 0) as CopyBuffer (BDPT.cl:916-932).  chunk (band split): this
-// rank's rows of the ranks' summed splats in the rank-major layout of k_bdpt_splat_pack (local
-// 8-row block tb of the rank at rows 8 tb .. 8 tb + 7), instead of the rank's own splat buffer.
+// splats; radiance = float4(sum, 0) as CopyBuffer (BDPT.cl:916-932), frame k of a batch at
+// radiance[k * W*H + pixel].  chunk (band split): this rank's rows of the ranks' summed splats in
+// the rank-major layout of k_bdpt_splat_pack (frame k's rows at k * chunkPixels, the rank's local
+// 8-row block tb at rows 8 tb .. 8 tb + 7), instead of the rank's own splat planes.
 __global__ __launch_bounds__(256) void k_bdpt_gather(FrameArgs f, BdptArgs b, float4* __restrict__ radiance,
-                                                     const float4* __restrict__ chunk) {
+                                                     const float4* __restrict__ chunk, size_t chunkPixels) {
     const int lane = threadIdx.x & 63;
-    const int tile = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int tileAll = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int tile, k;
+    tileFrame(f, tileAll, tile, k);
     int x, y;
     if (tile >= f.numTiles || !tilePixel(f, tile, lane, x, y)) return;
-    const int N = (int)(f.W * f.H);
-    const int pix = y * (int)f.W + x;
+    const int N0 = (int)(f.W * f.H), N = N0 * f.batch;
+    const int pix = k * N0 + y * (int)f.W + x;
     float rx = 0.0f, ry = 0.0f, rz = 0.0f;
-    for (int k = 0; k < b.ownSlots; ++k) {
-        const float4 c = b.slots[(size_t)k * N + pix];
+    for (int j = 0; j < b.ownSlots; ++j) {
+        const float4 c = b.slots[(size_t)j * N + pix];
         rx += c.x;
         ry += c.y;
         rz += c.z;
     }
     const int tb = tile / f.tilesX;
-    const float4 sp = chunk ? chunk[(size_t)(tb * 8 + (lane >> 3)) * f.W + x] : b.splat[pix];
+    const float4 sp = chunk ? chunk[(size_t)k * chunkPixels + (size_t)(tb * 8 + (lane >> 3)) * f.W + x] : b.splat[pix];
     radiance[pix] = make_float4(rx + sp.x, ry + sp.y, rz + sp.z, 0.0f);
 }
 
-// Band split: the splat buffer (W x H, any pixel) in rank-major order -- chunk r (chunkPixels
-// float4) holds the rows of rank r's bands, its local 8-row block tb (tilePixel's numbering) at
-// rows 8 tb .. 8 tb + 7 -- so ONE reduce-scatter hands every rank the summed splats of exactly its
-// own rows (mcrt.dist.exchange_splats).  Rows past a rank's last block stay zero (memset).
-__global__ __launch_bounds__(256) void k_bdpt_splat_pack(int W, int H, int bpb, int numBands, size_t chunkPixels,
-                                                         const float4* __restrict__ splat, float4* __restrict__ out) {
+// Band split: the splat planes (W x H per batch frame, any pixel) in rank-major order -- chunk r
+// (batch x chunkPixels float4) holds, frame after frame, the rows of rank r's bands, its local 8-row
+// block tb (tilePixel's numbering) at rows 8 tb .. 8 tb + 7 -- so ONE reduce-scatter hands every
+// rank the summed splats of exactly its own rows (mcrt.dist.exchange_splats).  Rows past a rank's
+// last block stay zero (memset).
+__global__ __launch_bounds__(256) void k_bdpt_splat_pack(int W, int H, int batch, int bpb, int numBands,
+                                                         size_t chunkPixels, const float4* __restrict__ splat,
+                                                         float4* __restrict__ out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)W * H) return;
-    const int y = (int)(i / W), x = (int)(i - (size_t)y * W);
+    const size_t N0 = (size_t)W * H;
+    if (i >= N0 * batch) return;
+    const int k = (int)(i / N0);
+    const size_t q = i - (size_t)k * N0;
+    const int y = (int)(q / W), x = (int)(q - (size_t)y * W);
     const int gb = y >> 3;
     const int r = (gb / bpb) % numBands, tb = (gb / (bpb * numBands)) * bpb + gb % bpb;
-    out[(size_t)r * chunkPixels + (size_t)(tb * 8 + (y & 7)) * W + x] = splat[i];
+    out[(size_t)r * batch * chunkPixels + (size_t)k * chunkPixels + (size_t)(tb * 8 + (y & 7)) * W + x] = splat[i];
 }
 
 // Splats that land outside the rank's bands (multi-GPU band split): added by the rank that owns
@@ -930,7 +965,7 @@ __global__ __launch_bounds__(256) void k_bdpt_clear_splat(int n, float4* __restr
 namespace mcrt {
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& camQ, const BdptQueue& lightQ, hipStream_t st) {
-    const int blocks = (f.numTiles * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK;
+    const int blocks = (f.numTiles * f.batch * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK;
     hipLaunchKernelGGL(k_bdpt_start, dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, camQ, lightQ);
 }
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
@@ -950,24 +985,25 @@ void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
         k_bdpt_connect<CONN_EMIT>, k_bdpt_connect<CONN_LIGHT>, k_bdpt_connect<CONN_NEE>, k_bdpt_connect<CONN_GENERAL>};
     for (int c = 0; c < 4; ++c) {
         if (counts[c] <= 0) continue;
-        const int64_t waves = (int64_t)f.numTiles * counts[c];
+        const int64_t waves = (int64_t)f.numTiles * counts[c] * (c == CONN_NEE ? 1 : f.batch);
         const int blocks = (int)((waves * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK);
         hipLaunchKernelGGL(kern[c], dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, q, counts[c]);
     }
 }
 void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st) {
-    const int blocks = (maxCount + 63) / 64 > 0 ? (maxCount + 63) / 64 : 1;
+    const int blocks = std::max(1, std::min((maxCount + 63) / 64, BDPT_VIS_MAX_WAVES));
     hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_COMPACT>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks), dim3(64), 0, st, c, b, q.count,
                        q.o, q.d, q.t);
 }
-void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, const float4* chunk, hipStream_t st) {
-    const int blocks = (f.numTiles * 64 + 255) / 256;
-    hipLaunchKernelGGL(k_bdpt_gather, dim3(blocks), dim3(256), 0, st, f, b, radiance, chunk);
+void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, const float4* chunk,
+                        size_t chunkPixels, hipStream_t st) {
+    const int blocks = (f.numTiles * f.batch * 64 + 255) / 256;
+    hipLaunchKernelGGL(k_bdpt_gather, dim3(blocks), dim3(256), 0, st, f, b, radiance, chunk, chunkPixels);
 }
 void launch_bdpt_splat_pack(const FrameArgs& f, size_t chunkPixels, const float4* splat, float4* out, hipStream_t st) {
-    const size_t n = (size_t)f.W * f.H;
+    const size_t n = (size_t)f.W * f.H * f.batch;
     hipLaunchKernelGGL(k_bdpt_splat_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (int)f.W, (int)f.H,
-                       f.bandRows >> 3, f.numBands, chunkPixels, splat, out);
+                       f.batch, f.bandRows >> 3, f.numBands, chunkPixels, splat, out);
 }
 void launch_bdpt_clear_splat(int n, float4* splat, hipStream_t st) {
     hipLaunchKernelGGL(k_bdpt_clear_splat, dim3((n + 255) / 256), dim3(256), 0, st, n, splat);

@@ -147,6 +147,7 @@ struct BdptSet {
     float4 *bqO[2] = {}, *bqD[2] = {}, *bqT[2] = {}, *bHits = nullptr;
     float4 *cO = nullptr, *cD = nullptr, *cL = nullptr;
     uint32_t* spill = nullptr;   // traversal spill columns of this set's launches
+    int frames = 0;              // batch frames the per-frame arrays hold (plane stride N x frames)
     size_t spillWords = 0;
 };   // [0..127] ints: counters; cameras (176 B each, <= MCRT_MAX_BATCH_FRAMES) from byte 512
 
@@ -187,6 +188,7 @@ struct mcrt_framebuffer_s {
     float4 *bqO[2] = {}, *bqD[2] = {}, *bqT[2] = {}, *bHits = nullptr;
     float4 *cO = nullptr, *cD = nullptr, *cL = nullptr;   // connection queue
     int lastIntegrator = MCRT_INTEGRATOR_PT;
+    int bdptBatch = 1;           // frames of the last BDPT call (plane stride N x bdptBatch)
     bool bdptOneSet = false;     // a second BDPT set did not fit in HBM: BDPT frames use slot 0 only
     bool bdptPendingGather = false;   // band-split BDPT frame waiting for the ranks' summed splats
 };
@@ -1161,8 +1163,10 @@ static void ctx_wait_slots(mcrt_framebuffer fb) {
 
 // NQ = the pixels of the whole 8x8 tiles covering the image (>= N): the start queues hold one slot
 // per lane of the tile walk.  Ray queues and hits hold 2 x NQ (the depth-1 camera and light halves).
-static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D) {
+static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D, int frames) {
     const size_t C = (size_t)bdpt_max_connections(D);
+    N *= frames;    // every per-frame array holds the batch's frames
+    NQ *= frames;
     hipError_t e = hipSuccess;
     auto A = [&](auto** p, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
@@ -1183,6 +1187,7 @@ static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D) {
     if (e == hipSuccess) e = hipMemset(b.camV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 2));
     if (e == hipSuccess) e = hipMemset(b.lightV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 1));
     if (e != hipSuccess) bset_free(b);
+    else b.frames = frames;
     return e;
 }
 
@@ -1201,7 +1206,7 @@ static void fb_bind_bdpt(mcrt_framebuffer fb, int k) {
 static size_t bdpt_queue_cap(mcrt_framebuffer fb) {
     return (size_t)((fb->W + 7) / 8) * ((fb->H + 7) / 8) * 64;
 }
-static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k) {
+static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k, int frames) {
     const size_t N = fb->N;
     if (fb->bdptDepth != D) {
         for (auto& sl : fb->slot)
@@ -1214,7 +1219,15 @@ static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k) {
         if (e != hipSuccess) { fb_free_bdpt(fb); return e; }
         fb->bdptDepth = D;
     }
-    if (!fb->bset[k].camV) return bset_alloc(fb->bset[k], N, bdpt_queue_cap(fb), D);
+    BdptSet& bs = fb->bset[k];
+    if (bs.camV && bs.frames < frames) {   // a larger batch: the set's last frames must be done
+        for (auto& sl : fb->slot)
+            if (sl.stream) hipStreamSynchronize(sl.stream);
+        hipStreamSynchronize(fb->ctx->stream);
+        bset_free(bs);
+        bs = BdptSet{};
+    }
+    if (!bs.camV) return bset_alloc(bs, N, bdpt_queue_cap(fb), D, frames);
     return hipSuccess;
 }
 
@@ -1324,24 +1337,28 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     // and writer of the shared sampled-light-vertex planes) waits for the previous frame's connect
     mcrt_ctx ctx = s->ctx;
     const int D = p->max_depth;
-    HIPCHK(ctx, fb_ensure_bdpt(fb, D, k));
+    const int B = f.batch;   // frames of this call (mcrt_render_frames): path = k * W*H + pixel
+    HIPCHK(ctx, fb_ensure_bdpt(fb, D, k, B));
     fb_bind_bdpt(fb, k);
     fb->lastMaxDepth = D;
     fb->lastPixels = 0;
     fb->bands = f;
     fb->haveBands = true;
     fb->lastIntegrator = MCRT_INTEGRATOR_BDPT;
+    fb->bdptBatch = B;
     mcrt_camera* dCam = reinterpret_cast<mcrt_camera*>(fb->counters + 128);
-    HIPCHK(ctx, hipMemcpyAsync(dCam, cam, sizeof(mcrt_camera), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(dCam, cam, sizeof(mcrt_camera) * B, hipMemcpyHostToDevice, st));
     HIPCHK(ctx, hipMemsetAsync(fb->bdptCounters, 0, 64 * sizeof(int), st));
     if (s->numLights == 0) {   // RTBDPTPass.cpp:69: no lights -> pass skipped
-        HIPCHK(ctx, hipMemsetAsync(fb->radiance, 0, 16 * fb->N, st));
+        HIPCHK(ctx, hipMemsetAsync(fb->radiance, 0, 16 * fb->N * (size_t)B, st));
         return MCRT_OK;
     }
-    const size_t N = fb->N, C = (size_t)bdpt_max_connections(D);
+    const size_t N = fb->N * (size_t)B, C = (size_t)bdpt_max_connections(D);   // N: paths of the batch
     BdptSet& bs = fb->bset[k];
-    const size_t NQ = bdpt_queue_cap(fb);
-    const size_t spillWords = (std::max(2 * NQ, C * N) + 63) / 64 * 64 * (size_t)s->spillCap;
+    const size_t NQ = bdpt_queue_cap(fb) * (size_t)B;
+    // spill columns: one per ray of the widest closest-hit launch (2 NQ) and one per wave of the
+    // grid-stride visibility launch (mcrt::BDPT_VIS_MAX_WAVES)
+    const size_t spillWords = (std::max(2 * NQ, (size_t)mcrt::BDPT_VIS_MAX_WAVES * 64) + 63) / 64 * 64 * (size_t)s->spillCap;
     if (bs.spillWords < spillWords) {
         HIPCHK(ctx, hipStreamSynchronize(st));
         if (bs.spill) hipFree(bs.spill);
@@ -1384,7 +1401,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     lightQ.d += NQ;
     lightQ.t += NQ;
     {
-        Timed t(ctx, K_BDPT_START, nullptr, (int64_t)f.numTiles * 64, st);
+        Timed t(ctx, K_BDPT_START, nullptr, (int64_t)f.numTiles * 64 * B, st);
         mcrt::launch_bdpt_start(sa, f, b, dCam, camQ, lightQ, st);
     }
     {
@@ -1418,7 +1435,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     cq.t = fb->cL;
     HIPCHK(ctx, hipStreamWaitEvent(st, fb->bdptConnect, 0));   // sampled-light planes in frame order
     {
-        Timed t(ctx, K_BDPT_CONNECT, nullptr, (int64_t)f.numTiles * 64, st);
+        Timed t(ctx, K_BDPT_CONNECT, nullptr, (int64_t)f.numTiles * 64 * B, st);
         mcrt::launch_bdpt_connect(sa, f, b, dCam, cq, st);
     }
     HIPCHK(ctx, hipEventRecord(fb->bdptConnect, st));
@@ -1429,11 +1446,11 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     if (bandSplit) {   // completed by mcrt_bdpt_gather once the ranks' splats are summed
         fb->bdptPendingGather = true;
     } else {
-        Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)f.numTiles * 64, st);
-        mcrt::launch_bdpt_gather(f, b, fb->radiance, nullptr, st);
+        Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)f.numTiles * 64 * B, st);
+        mcrt::launch_bdpt_gather(f, b, fb->radiance, nullptr, 0, st);
     }
     HIPCHK(ctx, hipGetLastError());
-    fb->lastPixels = (int64_t)f.numTiles * 64;
+    fb->lastPixels = (int64_t)f.numTiles * 64 * B;
     return MCRT_OK;
 }
 
@@ -1448,8 +1465,11 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     for (int k = 0; k < count; ++k)
         if (cam[k].width != fb->W || cam[k].height != fb->H)
             return fail(ctx, MCRT_ERROR_INVALID_ARG, "camera size differs from the frame buffer");
-    if (count > 1 && p->integrator != MCRT_INTEGRATOR_PT)
-        return fail(ctx, MCRT_ERROR_INVALID_ARG, "batched frames are PT only");
+    if (p->integrator == MCRT_INTEGRATOR_BDPT) {   // slot codes (own strategy x paths) and ray tags are int32
+        const uint64_t NB = (uint64_t)fb->N * count, C = (uint64_t)bdpt_max_connections(p->max_depth);
+        if ((C - (uint64_t)p->max_depth) * NB >= (1ull << 31) || 2 * NB >= (1ull << 31))
+            return fail(ctx, MCRT_ERROR_INVALID_ARG, "BDPT: strategies x frames x pixels must stay below 2^31");
+    }
     if ((uint64_t)fb->N * count >= (1ull << 31))
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame count x pixels must stay below 2^31 (path ids are int32)");
     if (p->max_depth < 1 || p->max_depth > MCRT_MAX_BOUNCES) return fail(ctx, MCRT_ERROR_INVALID_ARG, "max_depth out of range");
@@ -1473,7 +1493,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     if (bdpt && ks != 0 && fb->bdptDepth == p->max_depth && !fb->bset[ks].camV) {
         // each BDPT set holds ~C x N x 48 B of connection rays (2.5 GB at 1080p, D = 2): when a
         // second one does not fit, fall back to one frame in flight instead of failing the frame
-        const hipError_t e = bset_alloc(fb->bset[ks], fb->N, bdpt_queue_cap(fb), p->max_depth);
+        const hipError_t e = bset_alloc(fb->bset[ks], fb->N, bdpt_queue_cap(fb), p->max_depth, count);
         if (e == hipErrorOutOfMemory) {
             hipGetLastError();
             fb->bdptOneSet = true;
@@ -1484,11 +1504,18 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     }
     FrameSlot& slot = fb->slot[ks];
     if (bdpt) {   // BDPT frames overlap the same way (set ks)
-        if (!slot.stream) HIPCHK(ctx, slot_alloc(slot, fb->N));
+        if (!slot.stream) {
+            HIPCHK(ctx, slot_alloc(slot, fb->N, count));
+        } else if (slot.frames < count) {   // radiance planes for a larger batch
+            HIPCHK(ctx, hipEventSynchronize(slot.free));
+            HIPCHK(ctx, hipStreamSynchronize(slot.stream));
+            slot_free(slot);
+            HIPCHK(ctx, slot_alloc(slot, fb->N, count));
+        }
         HIPCHK(ctx, hipStreamWaitEvent(slot.stream, slot.free, 0));
         fb_bind(fb, ks);
         fb->next = (ks + 1) % (fb->bdptOneSet ? 1 : S);
-        slot.lastBatch = 1;
+        slot.lastBatch = count;
         const mcrt_status r = render_bdpt(s, fb, cam, p, f, ks, slot.stream);
         slot.lastMaxDepth = fb->lastMaxDepth;
         slot.lastPixels = fb->lastPixels;
@@ -1636,7 +1663,7 @@ static mcrt_status accumulate(mcrt_framebuffer fb, const mcrt_filter* filters, i
     }
     hipSetDevice(ctx->device);
     FrameSlot& slot = fb->slot[fb->cur];
-    const int batch = fb->lastIntegrator == MCRT_INTEGRATOR_PT ? slot.lastBatch : 1;
+    const int batch = slot.lastBatch;
     if (nfilters != 1 && nfilters != batch)
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "one filter, or one per frame of the last mcrt_render_frames");
     BatchFilters w{};   // weights are evaluated on the device (k_accumulate, filters.cl)
@@ -1709,7 +1736,7 @@ MCRT_API mcrt_status mcrt_framebuffer_read(mcrt_framebuffer fb, int which, float
 MCRT_API mcrt_status mcrt_framebuffer_read_frame(mcrt_framebuffer fb, int32_t k, float* host_rgba) {
     if (!fb || !host_rgba) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
     mcrt_ctx ctx = fb->ctx;
-    const int batch = fb->lastIntegrator == MCRT_INTEGRATOR_PT ? fb->slot[fb->cur].lastBatch : 1;
+    const int batch = fb->slot[fb->cur].lastBatch;
     if (k < 0 || k >= std::max(batch, 1))
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame index outside the last mcrt_render_frames batch");
     hipSetDevice(ctx->device);
@@ -1827,7 +1854,7 @@ static size_t splat_chunk_pixels(const FrameArgs& f) {
 MCRT_API mcrt_status mcrt_bdpt_splat_layout(mcrt_framebuffer fb, uint64_t* chunk_pixels, int32_t* chunks) {
     if (!fb || !chunk_pixels || !chunks) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
     if (!fb->haveBands) return fail(fb->ctx, MCRT_ERROR_NOT_READY, "no frame rendered yet");
-    *chunk_pixels = splat_chunk_pixels(fb->bands);
+    *chunk_pixels = splat_chunk_pixels(fb->bands) * (size_t)std::max(fb->bands.batch, 1);   // batch frames per chunk
     *chunks = fb->bands.numBands;
     return MCRT_OK;
 }
@@ -1837,7 +1864,8 @@ MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst) {
     mcrt_ctx ctx = fb->ctx;
     if (!fb->haveBands) return fail(ctx, MCRT_ERROR_NOT_READY, "no frame rendered yet");
     hipSetDevice(ctx->device);
-    const size_t chunk = splat_chunk_pixels(fb->bands), total = chunk * (size_t)fb->bands.numBands;
+    const size_t chunk = splat_chunk_pixels(fb->bands);   // per frame; a rank's chunk holds batch of them
+    const size_t total = chunk * (size_t)std::max(fb->bands.batch, 1) * (size_t)fb->bands.numBands;
     FrameSlot& slot = fb->slot[fb->cur];
     hipStream_t st = slot.stream ? slot.stream : ctx->stream;
     // the caller's buffer may still be read by an earlier frame's gather on another slot's stream
@@ -1869,8 +1897,9 @@ MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_own_chu
     b.splat = fb->splat;
     b.ownSlots = bdpt_max_connections(fb->bdptDepth) - fb->bdptDepth;
     {
-        Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)fb->bands.numTiles * 64, st);
-        mcrt::launch_bdpt_gather(fb->bands, b, fb->radiance, (const float4*)d_own_chunk, st);
+        Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)fb->bands.numTiles * 64 * fb->bands.batch, st);
+        mcrt::launch_bdpt_gather(fb->bands, b, fb->radiance, (const float4*)d_own_chunk,
+                                 splat_chunk_pixels(fb->bands), st);
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(slot.done, st));
@@ -1883,7 +1912,9 @@ MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, 
     if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
     mcrt_ctx ctx = fb->ctx;
     if (fb->bdptDepth <= 0) return fail(ctx, MCRT_ERROR_INVALID_ARG, "no BDPT frame rendered yet");
-    const size_t N = fb->N, D = (size_t)fb->bdptDepth, C = (size_t)bdpt_max_connections(fb->bdptDepth);
+    // the planes of the last BDPT call's batch (plane stride N x batch)
+    const size_t N = fb->N * (size_t)fb->bdptBatch, D = (size_t)fb->bdptDepth;
+    const size_t C = (size_t)bdpt_max_connections(fb->bdptDepth);
     const void* src = nullptr;
     size_t sz = 0;
     switch (which) {
@@ -1892,7 +1923,7 @@ MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, 
     case 2: src = fb->camCount; sz = 4 * N; break;
     case 3: src = fb->lightCount; sz = 4 * N; break;
     case 4: src = fb->slots; sz = 16 * N * (C - D); break;
-    case 5: src = fb->sampLight; sz = 16 * N * D; break;
+    case 5: src = fb->sampLight; sz = 16 * fb->N * D; break;   // per pixel, carried across frames
     case 6: src = fb->splat; sz = 16 * N; break;
     default: return fail(ctx, MCRT_ERROR_INVALID_ARG, "which must be 0..6");
     }

@@ -94,9 +94,15 @@ def exchange_splats(fb, full, chunk, group=None):
     rank completes its bands with them (mcrt_bdpt_gather).  Each pixel's camera subpath, light
     subpath and persistent sampled-light vertex (BDPT.cl:585-586) stay on the rank that owns the
     pixel, so the N-rank frame equals the 1-GPU frame up to the order of the splat sums (which the
-    reference's own CAS atomics leave open).  full, chunk: from splat_buffers."""
+    reference's own CAS atomics leave open).  A batched call (mcrt_render_frames) exchanges all its
+    frames at once: a rank's chunk holds them frame after frame.  full, chunk: from splat_buffers,
+    or larger (the leading chunks x chunk_pixels of the current layout are used)."""
     import torch
     import torch.distributed as dist
+    cp, chunks = fb.bdpt_splat_layout()
+    if full.numel() < 4 * cp * chunks or chunk.numel() < 4 * cp:
+        raise ValueError("splat buffers smaller than the frame's layout (mcrt.dist.splat_buffers)")
+    full, chunk = full[:4 * cp * chunks], chunk[:4 * cp]
     fb.bdpt_splats_copy(full.data_ptr())   # enqueued on the frame's stream
     if full.is_cuda and dist.get_backend(group) != "gloo":
         # RCCL: the collective is ordered after the pack on the frame's own stream, and the gather

@@ -330,10 +330,10 @@ class FrameBuffer:
         _check(lib().mcrt_render_frame(dscene.h, self.h, _p(cam), _c.byref(p)), self.ctx.h)
 
     def render_frames(self, dscene, cams, frame=0, max_depth=2, sampler=T.SAMPLER_RANDOM, rr=False, rr_start=3,
-                      band_rows=8, num_bands=1, band_index=0):
-        """mcrt_render_frames: len(cams) consecutive frames frame, frame+1, ... in one pass (PT)."""
+                      band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_PT):
+        """mcrt_render_frames: len(cams) consecutive frames frame, frame+1, ... in one pass (PT or BDPT)."""
         p = T.FrameParams(frame, max_depth, sampler, 1 if rr else 0, rr_start, band_rows, num_bands, band_index,
-                          T.INTEGRATOR_PT, 0)
+                          integrator, 0)
         cams = _records(cams)
         _check(lib().mcrt_render_frames(dscene.h, self.h, _p(cams), len(cams), _c.byref(p)), self.ctx.h)
 

@@ -257,3 +257,118 @@ def test_bdpt_band_split_matches_whole_frames(hip_ctx, ranks):
     for fb in fbs + [full]:
         fb.close()
     ds.close()
+
+
+def _frame_planes(raw, depths, frames, N):
+    """(depths, planes, frames, N, 4) view of a batched call's vertex planes (stride N x frames)."""
+    f = raw.view(np.float32)
+    return f.reshape(depths, f.size // (depths * frames * N * 4), frames, N, 4)
+
+
+@pytest.mark.parametrize("calls", [(3, 4), (1, 2, 4)])
+def test_bdpt_batched_frames_match_single_calls(hip_ctx, calls):
+    """mcrt_render_frames with the BDPT integrator (frame k of a call = path k*N + pixel in every
+    plane; the s = 1 strategies walk the call's frames in order, BDPT.cl:585-586) against one
+    mcrt_render_frame per frame, on the TAA-jittered mixed scene:
+      * per frame: both subpaths' vertex counts and every live vertex's 8 planes, and the own-strategy
+        slots -- bit-exact (no atomics involved);
+      * the sampled-light planes after each call: bit-exact;
+      * per frame radiance (mcrt_framebuffer_read_frame): bit-exact wherever no splat landed, within
+        the splat tolerance elsewhere; the accumulated image within the tolerance."""
+    from mcrt import lib
+    name, W, H, D = "mixed", 96, 64, 2
+    N = W * H
+    ds = lib.DeviceScene(hip_ctx, build_scene(name))
+    total = sum(calls)
+    cams = [scene_camera(name, W, H, frame=f, jitter=True) for f in range(total)]
+    filt = T.make_filter(T.BOX)
+    one = lib.FrameBuffer(hip_ctx, W, H)
+    single = []
+    for f in range(total):
+        one.render(ds, cams[f], frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT)
+        one.accumulate(filt, f)
+        single.append({"rad": one.read(0), "splat": one.read_bdpt("splat"),
+                       **{k: one.read_bdpt(k) for k in ("camera_vertices", "light_vertices", "camera_counts",
+                                                        "light_counts", "slots", "sampled_light")}})
+    img_one = one.read(2)
+    one.close()
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    f0 = 0
+    for B in calls:
+        fb.render_frames(ds, cams[f0:f0 + B], frame=f0, max_depth=D, integrator=T.INTEGRATOR_BDPT)
+        fb.accumulate_frames([filt] * B, f0)
+        cv = _frame_planes(fb.read_bdpt("camera_vertices"), D + 2, B, N)
+        lv = _frame_planes(fb.read_bdpt("light_vertices"), D + 1, B, N)
+        cc = fb.read_bdpt("camera_counts").view(np.int32).reshape(B, N)
+        lc = fb.read_bdpt("light_counts").view(np.int32).reshape(B, N)
+        slots = fb.read_bdpt("slots").view(np.uint32).reshape(-1, B, N, 4)
+        splat = fb.read_bdpt("splat").view(np.float32).reshape(B, H, W, 4)
+        for k in range(B):
+            s = single[f0 + k]
+            np.testing.assert_array_equal(cc[k], s["camera_counts"].view(np.int32), err_msg=f"f{f0 + k} camera counts")
+            np.testing.assert_array_equal(lc[k], s["light_counts"].view(np.int32), err_msg=f"f{f0 + k} light counts")
+            for got, ref, cnt, depths in ((cv, s["camera_vertices"], cc[k], D + 2), (lv, s["light_vertices"], lc[k], D + 1)):
+                a = got[:, :8, k].view(np.uint32)
+                b = our_planes(ref, depths, N)[:, :8].view(np.uint32)
+                live = cnt[None, :] > np.arange(depths)[:, None]
+                ne = (a != b).any(-1).any(1)
+                assert not (ne & live).any(), (f0 + k, depths, int((ne & live).sum()))
+            np.testing.assert_array_equal(slots[:, k], s["slots"].view(np.uint32).reshape(-1, N, 4),
+                                          err_msg=f"f{f0 + k} own-strategy slots")
+            g, r = fb.read_frame(k)[..., :3], s["rad"][..., :3]
+            nosplat = (splat[k][..., :3] == 0).all(-1) & (s["splat"].view(np.float32).reshape(H, W, 4)[..., :3] == 0).all(-1)
+            assert (g[nosplat].view(np.uint32) == r[nosplat].view(np.uint32)).all(), f0 + k
+            close = np.abs(g - r) <= REL_TOL * (np.abs(g) + np.abs(r)) + 1e-30
+            assert close.all(), (f0 + k, int((~close).sum()))
+        np.testing.assert_array_equal(fb.read_bdpt("sampled_light"), single[f0 + B - 1]["sampled_light"],
+                                      err_msg=f"sampled-light planes after frames {f0}..{f0 + B - 1}")
+        f0 += B
+    img = fb.read(2)[..., :3]
+    close = np.abs(img - img_one[..., :3]) <= 2 * REL_TOL * np.abs(img_one[..., :3]) + 1e-30
+    assert close.all(), int((~close).sum())
+    assert img.max() > 0
+    fb.close()
+    ds.close()
+
+
+def test_bdpt_batched_band_split(hip_ctx):
+    """Batched band-split BDPT (2 ranks emulated on one GPU, 3 frames per call): the rank-major
+    splat chunk of a rank holds the call's frames (mcrt_bdpt_splat_layout), one sum of the ranks'
+    buffers completes every frame; each rank's rows of every frame match whole single frames
+    within the splat tolerance."""
+    import torch
+    from mcrt import lib
+    from mcrt import dist as mdist
+    name, W, H, D, B, ranks = "mixed", 96, 64, 2, 3, 2
+    ds = lib.DeviceScene(hip_ctx, build_scene(name))
+    cams = [scene_camera(name, W, H, frame=f, jitter=True) for f in range(B)]
+    one = lib.FrameBuffer(hip_ctx, W, H)
+    ref = []
+    for f in range(B):
+        one.render(ds, cams[f], frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT)
+        ref.append(one.read(0))
+    one.close()
+    cr = mdist.splat_chunk_rows(H, 8, ranks)
+    rows = [mdist.band_rows_of(H, 8, ranks, r) for r in range(ranks)]
+    fbs = [lib.FrameBuffer(hip_ctx, W, H) for _ in range(ranks)]
+    bufs = []
+    for r, fb in enumerate(fbs):
+        fb.render_frames(ds, cams, frame=0, max_depth=D, integrator=T.INTEGRATOR_BDPT, band_rows=8,
+                         num_bands=ranks, band_index=r)
+        assert fb.bdpt_splat_layout() == (cr * W * B, ranks)
+        bufs.append(torch.zeros(4 * W * cr * B * ranks, dtype=torch.float32, device="cuda"))
+        fb.bdpt_splats_copy(bufs[r].data_ptr())
+    torch.cuda.synchronize()
+    total = bufs[0] + bufs[1]
+    per = 4 * W * cr * B
+    for r, fb in enumerate(fbs):
+        chunk = total[r * per:(r + 1) * per].clone()
+        torch.cuda.synchronize()
+        fb.bdpt_gather(chunk.data_ptr())
+        for k in range(B):
+            a, b = fb.read_frame(k)[rows[r], :, :3], ref[k][rows[r], :, :3]
+            close = np.abs(a - b) <= REL_TOL * (np.abs(a) + np.abs(b)) + 1e-30
+            assert close.all(), (r, k, int((~close).sum()))
+    for fb in fbs:
+        fb.close()
+    ds.close()
