@@ -1122,6 +1122,9 @@ static hipError_t slot_alloc(FrameSlot& k, size_t N, int frames = 1, size_t Q = 
     k.queueCap = Q;
     if (e == hipSuccess) e = hipMemset(k.radiance, 0, 16 * N * frames);
     if (e == hipSuccess) e = hipMemset(k.counters, 0, SLOT_COUNTER_BYTES);
+    // hipMemset runs on the null stream, which the non-blocking slot streams do not wait for: finish
+    // it before any slot launch can touch these buffers
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&k.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&k.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&k.free, hipEventDisableTiming);
@@ -1186,6 +1189,9 @@ static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D, int frames)
     if (e == hipSuccess) e = hipMemset(b.splat, 0, 16 * N);
     if (e == hipSuccess) e = hipMemset(b.camV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 2));
     if (e == hipSuccess) e = hipMemset(b.lightV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 1));
+    // the null-stream memsets must land before the set's first launch on a (non-blocking) slot
+    // stream: a 3 GB vertex-plane memset still running under k_bdpt_start zeroes its vertices
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) bset_free(b);
     else b.frames = frames;
     return e;
@@ -1215,6 +1221,7 @@ static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k, int frames) 
         fb_free_bdpt(fb);
         hipError_t e = hipMalloc(&fb->sampLight, 16 * N * D);
         if (e == hipSuccess) e = hipMemset(fb->sampLight, 0, 16 * N * D);
+        if (e == hipSuccess) e = hipDeviceSynchronize();   // before the slot streams read it
         if (e == hipSuccess) e = hipEventCreateWithFlags(&fb->bdptConnect, hipEventDisableTiming);
         if (e != hipSuccess) { fb_free_bdpt(fb); return e; }
         fb->bdptDepth = D;
@@ -1258,6 +1265,7 @@ MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint3
     if (e == hipSuccess) e = hipMemset(fb->image, 0, 16 * N);
     if (e == hipSuccess) e = hipMemset(fb->denoised, 0, 16 * N);
     if (e == hipSuccess) e = hipMemset(fb->display, 0, 16 * N);
+    if (e == hipSuccess) e = hipDeviceSynchronize();   // null-stream memsets before any slot-stream launch
     if (e != hipSuccess) {
         fb_free(fb);
         delete fb;

@@ -111,28 +111,33 @@ def bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out):
     import torch
     from mcrt import dist as mdist
     from mcrt import types as T
+    B = max(args.batch, 1)   # BDPT frames per mcrt_render_frames call
     for n in [int(x) for x in args.ns.split(",")]:
         per_rank = []
         cr = mdist.splat_chunk_rows(H, args.band_rows, n)
-        full = torch.zeros(4 * W * cr * n, dtype=torch.float32, device="cuda")
+        full = torch.zeros(4 * W * cr * n * B, dtype=torch.float32, device="cuda")
         for r in range(n):
             band = dict(band_rows=args.band_rows, num_bands=n, band_index=r, integrator=T.INTEGRATOR_BDPT)
-            own = full[r * 4 * W * cr:(r + 1) * 4 * W * cr]
+            own = full[r * 4 * W * cr * B:(r + 1) * 4 * W * cr * B]
 
             def run(f0, count):
-                for i in range(count):
-                    fb.render(ds, cams[(f0 + i) % 64], frame=f0 + i, max_depth=2, **band)
+                i = 0
+                while i < count:
+                    k = min(B, count - i)
+                    fb.render_frames(ds, [cams[(f0 + i + j) % 64] for j in range(k)], frame=f0 + i, max_depth=2,
+                                     **band)
                     if n > 1:
                         fb.bdpt_splats_copy(full.data_ptr())
                         fb.bdpt_gather(own.data_ptr())
-                    fb.accumulate(filt, f0 + i)
-            run(0, 3)
+                    fb.accumulate_frames([filt] * k, f0 + i)
+                    i += k
+            run(0, 3 * B)
             ctx.sync()
             t0 = time.perf_counter()
-            run(16, args.steps)
+            run(16 * B, args.steps)
             ctx.sync()
             per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
-        full_bytes = 16 * W * cr * n
+        full_bytes = 16 * W * cr * n   # per frame
         out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
                            "min_ms": round(min(per_rank), 4),
                            "splat_exchange": {"reduce_scatter_in_bytes_per_rank": full_bytes if n > 1 else 0,
