@@ -204,7 +204,7 @@ def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
 
 
 def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing, split="band",
-                 batch=4):
+                 batch=8):
     """Config 4's integrator on the same scene and GPU(s): BDPT (RTBDPTPass::update), 1 spp per
     step, split over the ranks by frames (rank r renders frames r, r + N, ...; light-tracing splats
     land anywhere in the image) or by 8-row bands (one splat reduce-scatter per frame,
@@ -391,7 +391,7 @@ def main():
                     help="A/B only: round every call's frame count down to a power of two (16 + 4 for 20 steps)")
     ap.add_argument("--chunks", default="",
                     help="A/B only: comma-separated frames per call of the timed region, cycled (e.g. 4,16)")
-    ap.add_argument("--bdpt-batch", type=int, default=4,
+    ap.add_argument("--bdpt-batch", type=int, default=8,
                     help="BDPT frames per mcrt_render_frames call (the BDPT object and --integrator bdpt)")
     ap.add_argument("--batch", type=int, default=0,
                     help="PT frames per mcrt_render_frames call (one launch sequence for all of them); "
