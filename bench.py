@@ -391,6 +391,10 @@ def main():
                     help="A/B only: round every call's frame count down to a power of two (16 + 4 for 20 steps)")
     ap.add_argument("--chunks", default="",
                     help="A/B only: comma-separated frames per call of the timed region, cycled (e.g. 4,16)")
+    ap.add_argument("--bvh-bins", type=int, default=64,
+                    help="SAH bins (64 = RTScene::commit's setting; others are host-built A/B trees)")
+    ap.add_argument("--perf-tree", action="store_true",
+                    help="A/B: the host 3-axis SAH tree (device_build 4) instead of the reference's Bvh2")
     ap.add_argument("--bdpt-batch", type=int, default=8,
                     help="BDPT frames per mcrt_render_frames call (the BDPT object and --integrator bdpt)")
     ap.add_argument("--batch", type=int, default=0,
@@ -443,8 +447,9 @@ def main():
 
     ctx = lib.Context(local)
     t0 = time.perf_counter()
-    ds = lib.DeviceScene(ctx, scene, device_build=1 if args.device_build else 3 if args.host_build else 2,
-                         force_flat=args.force_flat)
+    ds = lib.DeviceScene(ctx, scene, device_build=4 if args.perf_tree else 1 if args.device_build else
+                         3 if args.host_build else 2,
+                         force_flat=args.force_flat, bins=args.bvh_bins)
     info = ds.info()
     two_level = ds.layout()["two_level"] == 1
     log(f"[bench] upload+BVH {time.perf_counter() - t0:.1f}s (build {info['build_ms'] / 1e3:.1f}s, "

@@ -196,7 +196,9 @@ typedef struct {
      * 10 M triangles); falls back to 3 for num_bins > 64.  3: the same tree built on the host
      * (mcrt_bvh.cpp; ~2 s for 10 M triangles).  1: on-device linear BVH (Morton order, rocPRIM
      * radix sort), same record format and triangle data, different tree (equal-t hit ties may
-     * resolve differently from the reference); ignores the three SAH fields. */
+     * resolve differently from the reference); ignores the three SAH fields.  4: perf tree (A/B
+     * option, not the parity default): host binned SAH over all three axes, the cheapest split
+     * wins (RR bins the largest centroid axis only); same records and traversal, another tree. */
     int   device_build;
     /* Two-level (instanced) structure: RadeonRays' IntersectorTwoLevel, which RR selects when a
      * shape is an instance (RTScene::attachMesh -> CreateInstance for every further entity that
@@ -332,7 +334,7 @@ MCRT_API const char* mcrt_obj_warnings(mcrt_obj_scene s);   /* missing MTL / ski
 MCRT_API void mcrt_obj_free(mcrt_obj_scene s);
 
 /* Which builder made the flat structure: 0 host (or two-level), 1 device LBVH, 2 device SAH
- * (mcrt_accel_opts.device_build 0 and 2). */
+ * (mcrt_accel_opts.device_build 0 and 2), 4 the host 3-axis SAH perf tree (device_build 4). */
 MCRT_API mcrt_status mcrt_accel_builder(mcrt_scene scene, int32_t* builder);
 /* Host-only build of the structure mcrt_accel_build would upload (no device needed): 64-B
  * records (mcrt_bvh.cpp / mcrt_bvh2l.cpp layouts) into out_records (up to max_records; may be

@@ -4,6 +4,8 @@
 // Split policy = RadeonRays Bvh2 (RR/src/accelerator/bvh2.cpp:144-712, options from
 // RTScene::commit: SAH, 64 bins, traversal cost 10): split axis = largest centroid extent,
 // binned SAH on that axis only (> 8 primitives), median fallback, 1 triangle per leaf,
+// (axes3 = the perf tree, mcrt_accel_opts.device_build 4: the binned SAH of all three axes,
+// cheapest wins -- same records and traversal, a different tree),
 // depth-first numbering (left = i + 1, right = i + 2 * nLeft).  The SSE arithmetic of the
 // reference (_mm_rcp_ps / _mm_dp_ps) is kept so the tree -- and with it the node-visit
 // counts the roofline is priced on -- matches the reference on the same host.
@@ -72,9 +74,10 @@ struct Builder {
     uint32_t bins;
     float cost;
     bool sah;
+    bool axes3 = false;   // perf tree: the binned SAH over all three axes (not the reference's tree)
     std::atomic<int> maxDepth{0};
 
-    float sahSplit(const Req& rq, uint32_t axis) {   // bvh2.cpp:331-492
+    float sahSplit(const Req& rq, uint32_t axis, float* costOut = nullptr) {   // bvh2.cpp:331-492
         const uint32_t nb = bins;
         std::vector<uint32_t> cnt(nb, 0);
         std::vector<__m128> bmn(nb, _mm_set1_ps(INFINITY)), bmx(nb, _mm_set1_ps(-INFINITY));
@@ -128,6 +131,7 @@ struct Builder {
             float s = cost + ((float)lc * lane(sa4(tmn, tmx), 0) + (float)rc * lane(sa4(rmn[i], rmx[i]), 0)) * areaInv;
             if (s < best) { split = (int)i; best = s; }
         }
+        if (costOut) *costOut = best;
         return cm + (float)(split + 1) * (ce / (float)nb);
     }
 
@@ -141,7 +145,7 @@ struct Builder {
             leafRef[rq.index] = refs[rq.start];
             return false;
         }
-        const uint32_t ax = maxAxis(rq.cmin, rq.cmax);
+        uint32_t ax = maxAxis(rq.cmin, rq.cmax);
         const float ext = lane(_mm_sub_ps(rq.cmax, rq.cmin), ax);
         float split = lane(_mm_mul_ps(_mm_set1_ps(0.5f), _mm_add_ps(rq.cmax, rq.cmin)), ax);
         size_t splitIdx = rq.start;
@@ -163,7 +167,19 @@ struct Builder {
             rcmx = _mm_max_ps(rcmx, c);
         };
         if (ext > 0.0f) {
-            if (sah && rq.num > 8) split = sahSplit(rq, ax);
+            if (sah && rq.num > 8) {
+                if (axes3) {   // perf tree: the cheapest of the three axes' binned SAH splits
+                    float bestCost = FLT_MAX;
+                    for (uint32_t a = 0; a < 3; ++a) {
+                        if (!(lane(_mm_sub_ps(rq.cmax, rq.cmin), a) > 0.0f)) continue;
+                        float c;
+                        const float sp = sahSplit(rq, a, &c);
+                        if (c < bestCost) { bestCost = c; ax = a; split = sp; }
+                    }
+                } else {
+                    split = sahSplit(rq, ax);
+                }
+            }
             size_t first = rq.start, last = rq.start + rq.num;
             for (;;) {
                 while (first != last && acen[4 * R[first] + ax] < split) { addL(R[first]); ++first; }
@@ -253,9 +269,10 @@ const HostRcp& host_rcp_table() {
 }
 
 bool build_bvh(const float* tri, const int32_t* shapeOf, const int32_t* primOf, std::size_t n, float cost, int bins,
-               bool sah, int threads, BvhOut& out) {
+               bool sah, int threads, BvhOut& out, bool axes3) {
     if (n == 0) return false;
     Builder b;
+    b.axes3 = axes3;
     b.tri = tri;
     b.n = n;
     b.bins = (uint32_t)bins;

@@ -794,8 +794,9 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
     }
     int threads = (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
     mcrt::BvhOut bvh;
-    if (!mcrt::build_bvh(tri.data(), shapeOf.data(), primOf.data(), n, cost, bins, sah, threads, bvh))
+    if (!mcrt::build_bvh(tri.data(), shapeOf.data(), primOf.data(), n, cost, bins, sah, threads, bvh, buildMode == 4))
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "BVH build failed");
+    if (buildMode == 4) s->builder = 4;   // the perf tree (3-axis SAH), not the reference's
     hipSetDevice(ctx->device);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (s->dNodes) hipFree(s->dNodes);
@@ -970,7 +971,8 @@ MCRT_API mcrt_status mcrt_accel_build_host_records(const mcrt_scene_desc* d, con
             }
         }
         mcrt::BvhOut bvh;
-        if (!mcrt::build_bvh(tri.data(), shapeOf.data(), primOf.data(), n, cost, bins, sah, threads, bvh))
+        if (!mcrt::build_bvh(tri.data(), shapeOf.data(), primOf.data(), n, cost, bins, sah, threads, bvh,
+                             opts && opts->device_build == 4))
             return fail(nullptr, MCRT_ERROR_INVALID_ARG, "BVH build failed");
         *num_records = bvh.numNodes;
         if (out_records) std::memcpy(out_records, bvh.nodes, 64 * std::min<uint64_t>(max_records, bvh.numNodes));

@@ -174,7 +174,7 @@ struct BvhOut {
 };
 // world-space triangles (9 floats each), shape id / prim id per triangle
 bool build_bvh(const float* tri, const int32_t* shapeOf, const int32_t* primOf, std::size_t n, float cost, int bins,
-               bool sah, int threads, BvhOut& out);
+               bool sah, int threads, BvhOut& out, bool axes3 = false);
 void free_bvh(BvhOut& out);
 }  // namespace mcrt
 // Host two-level (instanced) build (mcrt_bvh2l.cpp)

@@ -109,3 +109,37 @@ def test_device_build_large_scene_speed(hip_ctx):
     assert eq.mean() >= 0.999, eq.mean()
     host.close()
     dev.close()
+
+
+@pytest.mark.parametrize("which", ["mixed", "dragon"])
+def test_perf_tree_frames_within_reference_tolerance(hip_ctx, which):
+    """The perf tree (device_build 4: host binned SAH over all three axes, an A/B option) against
+    the reference's Bvh2 (device_build 2, bit-exact with the reference's kernels): the same
+    triangles in another tree, so only equal-t hit ties may resolve differently -- frames at
+    SURVEY App. A's tolerance (|dL| <= 1e-4 max(1, |L|) on >= 99.5 % of pixels), closest hits on
+    random rays identical in distance."""
+    from mcrt import lib
+    sc = scenes.test_scene() if which == "mixed" else scenes.dragon_proxy(tris=200_000)
+    W, H = 160, 120
+    cam = scene_camera("mixed" if which == "mixed" else "dragon_proxy", W, H)
+    rays = random_rays(sc, 20000, seed=7)
+    out, hits = [], []
+    for mode in (2, 4):
+        ds = lib.DeviceScene(hip_ctx, sc, device_build=mode)
+        if mode == 4:
+            assert ds.builder() == 4
+        fb = lib.FrameBuffer(hip_ctx, W, H)
+        imgs = []
+        for f in range(2):
+            fb.render(ds, cam, frame=f, max_depth=3)
+            imgs.append(fb.read(0)[..., :3].copy())
+        out.append(np.stack(imgs))
+        hits.append(_trace(ds, rays))
+        fb.close()
+        ds.close()
+    ok = (np.abs(out[1] - out[0]) <= 1e-4 * np.maximum(1.0, np.abs(out[0]))).all(-1)
+    assert ok.mean() >= 0.995, ok.mean()
+    t0, t1 = hits[0]["uvwt"][:, 3], hits[1]["uvwt"][:, 3]
+    miss0, miss1 = hits[0]["shapeid"] < 0, hits[1]["shapeid"] < 0
+    np.testing.assert_array_equal(miss0, miss1)
+    np.testing.assert_array_equal(t0[~miss0], t1[~miss1])
