@@ -224,12 +224,15 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
         splat_full = torch.zeros(4 * W * cr * batch * world, dtype=torch.float32, device="cuda")
         splat_own = torch.zeros(4 * W * cr * batch, dtype=torch.float32, device="cuda")
 
+    last = [1]   # frames of the last call (fb.stats() counts that call's queues)
+
     def run(i0, count):
         # calls of up to `batch` consecutive frames (mcrt_render_frames): band split: every rank the
         # same frames; frame split: rank r its own consecutive block of frame indices (its RNG streams)
         i = i0
         while i < i0 + count:
             k = min(batch, i0 + count - i)
+            last[0] = k
             f = i if band else rank * (1 << 20) + i
             cams = [cam_of(f + j) for j in range(k)]
             bands = dict(band_rows=8, num_bands=world, band_index=rank) if band else {}
@@ -270,10 +273,11 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     out = {"value": round(W * H * steps * (1 if band else world) / el / 1e6, 3), "unit": "Mpaths/s", "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong" if band else "weak",
            "workload": f"same scene {W}x{H}, BDPT, maxDepth {D}, 1 spp per step (SURVEY config 4's integrator), "
-                       + (f"band split x {world} + 1 splat reduce-scatter per frame + 1 RCCL reduce" if band else
-                          f"frame split x {world} + 1 RCCL reduce"),
-           "rays_per_path": {"subpath": round(st["closest_rays"] / (W * H), 4),
-                             "connection": round(st["any_rays"] / (W * H), 4)}}
+                       f"{batch} frames per mcrt_render_frames call, "
+                       + (f"band split x {world} + 1 splat reduce-scatter per call + 1 RCCL reduce" if band else
+                          f"frame split x {world} + 1 RCCL reduce" if world > 1 else "1 GPU"),
+           "rays_per_path": {"subpath": round(st["closest_rays"] / (W * H * last[0]), 4),
+                             "connection": round(st["any_rays"] / (W * H * last[0]), 4)}}
     if kernel_timing:   # one slot, one call of `batch` frames (the timed calls' shape)
         kb = min(batch, steps)
         fb.set_frames_in_flight(1)
@@ -326,8 +330,11 @@ def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s):
                            "model": "compulsory bytes per frame: 48 B per subpath ray + 64 B per DISTINCT BVH node the "
                                     "frame's subpath rays visit (oracle BDPT, frame 0)"}
         pm = pmc_traffic("k_extend", "pmc_bdpt.json", last_launches=D + 1)
-        if pm and "fetch_raw_last" in pm:   # the last frame's D + 1 k_extend dispatches of the counter run
-            tr = calibrated_traffic(pm["fetch_raw_last"], pm["write_last"], rays * 32)   # streamed: ray (o, d)
+        if pm and "fetch_raw_last" in pm:
+            # the last call's D + 1 k_extend dispatches of the counter run (one call of
+            # res["frames_per_call"] frames, the timed calls' shape) -> bytes per frame
+            fpc = max(int(res.get("frames_per_call", 1)), 1)
+            tr = calibrated_traffic(pm["fetch_raw_last"] / fpc, pm["write_last"] / fpc, rays * 32)   # streamed: ray (o, d)
             out["roofline"].update(traffic=int(tr), traffic_source=pm["source"], traffic_over_alg=round(tr / alg, 2),
                                    traffic_rule="FETCH_SIZE x 1024 + half the streamed ray reads + WRITE_SIZE x 1024")
         if pm and "limiter" in pm:

@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 P=gpurun_out/bp
 mkdir -p $P
-B="python3 bench.py --integrator bdpt --steps 8 --warmup 2 --no-cpu-baseline --no-roofline-model"
+B="python3 bench.py --integrator bdpt --steps 16 --warmup 2 --no-kernel-timing --no-cpu-baseline --no-roofline-model"
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $P/trace -o k -- $B > $P/trace.log 2>&1 || { tail -5 $P/trace.log; exit 7; }
 grep -v "^\[\|^W20\|^I20" $P/trace.log | tail -2 | cut -c1-400
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $P/pmc_fetch -o f -- $B > $P/f.log 2>&1 || { tail -5 $P/f.log; exit 8; }
