@@ -329,11 +329,11 @@ def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s):
                            "distinct_nodes_per_frame": n_nodes,
                            "model": "compulsory bytes per frame: 48 B per subpath ray + 64 B per DISTINCT BVH node the "
                                     "frame's subpath rays visit (oracle BDPT, frame 0)"}
-        pm = pmc_traffic("k_extend", "pmc_bdpt.json", last_launches=D + 1)
+        pm = pmc_traffic("k_extend", "pmc_bdpt.json", last_launches=2 * (D + 1))
         if pm and "fetch_raw_last" in pm:
-            # the last call's D + 1 k_extend dispatches of the counter run (one call of
-            # res["frames_per_call"] frames, the timed calls' shape) -> bytes per frame
-            fpc = max(int(res.get("frames_per_call", 1)), 1)
+            # the counter run's last two calls (2 x (D + 1) k_extend dispatches, interleaved by the
+            # two frames in flight; res["frames_per_call"] frames each, the timed calls' shape)
+            fpc = 2 * max(int(res.get("frames_per_call", 1)), 1)
             tr = calibrated_traffic(pm["fetch_raw_last"] / fpc, pm["write_last"] / fpc, rays * 32)   # streamed: ray (o, d)
             out["roofline"].update(traffic=int(tr), traffic_source=pm["source"], traffic_over_alg=round(tr / alg, 2),
                                    traffic_rule="FETCH_SIZE x 1024 + half the streamed ray reads + WRITE_SIZE x 1024")
