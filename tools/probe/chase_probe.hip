@@ -11,6 +11,8 @@
 //   quad   one chain per 4 lanes, each lane loads one 16-B quarter (one load instruction per
 //          step covers 16 records), the next index comes from the quad's lane 3
 //   dual4  two chains per lane, both records' loads issued before either is waited for
+//   lane3 / lane3d / lane2  48 B as 3 loads / 3 loads + a 4-B link / 32 B as 2 loads
+//   act2 / act4  lane4 with every 2nd / 4th lane following a chain (steps/s counts active chains)
 //   coop4  one chain per lane; the 4 lanes {c, c+16, c+32, c+48} fetch each other's records
 //          cooperatively (load k: every lane of the group reads quarter `row` of the record of
 //          the group's row-k chain, so one load instruction touches 16 records, not 64), then a
@@ -100,6 +102,79 @@ __global__ __launch_bounds__(64) void k_dual4(const int4* __restrict__ rec, unsi
     if (acc == 0xdeadbeefu) sink[0] = i0 ^ i1;
 }
 
+// lane3: the record as three 16-B loads (link in the third); lane3d: three 16-B loads plus one
+// 4-B load of the link word at offset 48; lane2: two 16-B loads (link in the second).
+__global__ __launch_bounds__(64) void k_lane3(const int4* __restrict__ rec, unsigned n, int steps, unsigned* sink) {
+    const unsigned chain = blockIdx.x * 64 + threadIdx.x;
+    unsigned idx = start_of(chain, n);
+    unsigned acc = 0;
+    for (int s = 0; s < steps; ++s) {
+        const int4 a = rec[4 * (size_t)idx + 0], b = rec[4 * (size_t)idx + 1], c = rec[4 * (size_t)idx + 2];
+        asm volatile("" ::"v"(a.y), "v"(b.y), "v"(c.y));
+        acc += (unsigned)(a.z ^ b.z ^ c.x);
+        idx = (unsigned)c.w;
+    }
+    if (acc == 0xdeadbeefu) sink[0] = idx;
+}
+__global__ __launch_bounds__(64) void k_lane3d(const int4* __restrict__ rec, unsigned n, int steps, unsigned* sink) {
+    const unsigned chain = blockIdx.x * 64 + threadIdx.x;
+    unsigned idx = start_of(chain, n);
+    unsigned acc = 0;
+    for (int s = 0; s < steps; ++s) {
+        const int4 a = rec[4 * (size_t)idx + 0], b = rec[4 * (size_t)idx + 1], c = rec[4 * (size_t)idx + 2];
+        const int d = reinterpret_cast<const int*>(rec + 4 * (size_t)idx + 3)[0];
+        asm volatile("" ::"v"(a.y), "v"(b.y), "v"(c.y), "v"(c.w));
+        acc += (unsigned)(a.z ^ b.z ^ c.x);
+        idx = (unsigned)d;
+    }
+    if (acc == 0xdeadbeefu) sink[0] = idx;
+}
+__global__ __launch_bounds__(64) void k_lane3q(const int4* __restrict__ rec, unsigned n, int steps, unsigned* sink) {
+    const unsigned chain = blockIdx.x * 64 + threadIdx.x;
+    unsigned idx = start_of(chain, n);
+    unsigned acc = 0;
+    for (int s = 0; s < steps; ++s) {
+        const int4 a = rec[4 * (size_t)idx + 0], b = rec[4 * (size_t)idx + 1], c = rec[4 * (size_t)idx + 2];
+        const int2 d = reinterpret_cast<const int2*>(rec + 4 * (size_t)idx + 3)[0];
+        asm volatile("" ::"v"(a.y), "v"(b.y), "v"(c.y), "v"(c.w), "v"(d.y));
+        acc += (unsigned)(a.z ^ b.z ^ c.x);
+        idx = (unsigned)d.x;
+    }
+    if (acc == 0xdeadbeefu) sink[0] = idx;
+}
+__global__ __launch_bounds__(64) void k_lane2(const int4* __restrict__ rec, unsigned n, int steps, unsigned* sink) {
+    const unsigned chain = blockIdx.x * 64 + threadIdx.x;
+    unsigned idx = start_of(chain, n);
+    unsigned acc = 0;
+    for (int s = 0; s < steps; ++s) {
+        const int4 a = rec[4 * (size_t)idx + 0], b = rec[4 * (size_t)idx + 1];
+        asm volatile("" ::"v"(a.y), "v"(b.y));
+        acc += (unsigned)(a.z ^ b.x);
+        idx = (unsigned)b.w;
+    }
+    if (acc == 0xdeadbeefu) sink[0] = idx;
+}
+// lane4 with only every ACT-th lane of a wave following a chain (the others idle in the loop,
+// exec-masked): does a gather cost by the lanes it serves or by the instruction?
+template <int ACT>
+__global__ __launch_bounds__(64) void k_lane4_act(const int4* __restrict__ rec, unsigned n, int steps, unsigned* sink) {
+    const unsigned chain = blockIdx.x * 64 + threadIdx.x;
+    unsigned idx = start_of(chain, n);
+    unsigned acc = 0;
+    const bool on = (threadIdx.x % ACT) == 0;
+    for (int s = 0; s < steps; ++s) {
+        if (on) {
+            const int4 a = rec[4 * (size_t)idx + 0], b = rec[4 * (size_t)idx + 1];
+            const int4 c = rec[4 * (size_t)idx + 2], d = rec[4 * (size_t)idx + 3];
+            asm volatile("" ::"v"(a.y), "v"(b.y), "v"(c.y));
+            acc += (unsigned)(a.z ^ b.z ^ c.z);
+            idx = (unsigned)d.w;
+        }
+        __builtin_amdgcn_s_barrier();   // keep the idle lanes' wave in the loop (one wave per block)
+    }
+    if (acc == 0xdeadbeefu) sink[0] = idx;
+}
+
 // 4x4 transpose across the lane group {c, c+16, c+32, c+48}: element (row r, register k) <->
 // (row k, register r).  permlane32_swap(vdst, src0) swaps lanes 32-63 of vdst with lanes 0-31 of
 // src0; permlane16_swap swaps the odd 16-lane rows of vdst with the even rows of src0.
@@ -172,6 +247,12 @@ int main(int argc, char** argv) {
     else if (!strcmp(mode, "quad")) { kern = k_quad; chainsPerWave = 16; }
     else if (!strcmp(mode, "dual4")) { kern = k_dual4; chainsPerWave = 128; }
     else if (!strcmp(mode, "coop4")) kern = k_coop4;
+    else if (!strcmp(mode, "lane3")) kern = k_lane3;
+    else if (!strcmp(mode, "lane3d")) kern = k_lane3d;
+    else if (!strcmp(mode, "lane2")) kern = k_lane2;
+    else if (!strcmp(mode, "lane3q")) kern = k_lane3q;
+    else if (!strcmp(mode, "act2")) { kern = k_lane4_act<2>; chainsPerWave = 32; }
+    else if (!strcmp(mode, "act4")) { kern = k_lane4_act<4>; chainsPerWave = 16; }
     else if (!strcmp(mode, "ttest")) {
         unsigned* d;
         CK(hipMalloc(&d, 256 * 4));
