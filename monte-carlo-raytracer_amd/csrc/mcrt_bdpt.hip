@@ -444,7 +444,7 @@ MCRT_DEV void tileFrame(const FrameArgs& f, int tileAll, int& tile, int& k) {
 }
 
 // GenerateStartVertices (BDPT.cl:240-312) over the rank's 8x8 tiles x batch frames; the first
-// camera rays go to camQ (tile order: coherent, traced over the descent-compact records), the
+// camera rays go to camQ (tile order: coherent, traced as wave packets), the
 // light rays to lightQ.
 __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArgs f, BdptArgs b,
                                                            const mcrt_camera* __restrict__ camp, BdptQueue camQ,
@@ -657,14 +657,17 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                                                              const mcrt_camera* __restrict__ camp, BdptQueue qOut,
                                                              int numStrat) {
     const int lane = threadIdx.x & 63;
-    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    // a wave = (tile, strategy, batch frame); NEE waves walk the batch's frames in order in-thread
-    // (frame k's s = 1 strategy reads the sampled-light slot frame k - 1 wrote)
+    // a wave = (tile, batch frame, strategy), strategies fastest: the strategies of one path read
+    // the same vertices (the MIS walks share every vertex below the connection), so they run in
+    // one workgroup or its neighbours, and xcdRemap keeps neighbouring workgroups on one XCD (one
+    // L2).  NEE waves walk the batch's frames in order in-thread (frame k's s = 1 strategy reads
+    // the sampled-light slot frame k - 1 wrote).
+    const int wave = xcdRemap((int)blockIdx.x, (int)gridDim.x) * (BDPT_BLOCK / 64) + (int)(threadIdx.x >> 6);
     const int kb = CLS == CONN_NEE ? 1 : f.batch;
     const int per = numStrat * kb;
     const int tile = wave / per;
     const int rem = wave - tile * per;
-    const int si = rem / kb;
+    const int si = rem % numStrat;
     int t, sI;
     strategyOf<CLS>(si, f.maxDepth, t, sI);
     int x = 0, y = 0;
@@ -674,7 +677,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
     const int N = N0 * f.batch;   // plane stride
     const int D = f.maxDepth;
     const int px = y * (int)f.W + x;
-    const int kBegin = CLS == CONN_NEE ? 0 : rem - si * kb, kEnd = CLS == CONN_NEE ? f.batch : kBegin + 1;
+    const int kBegin = CLS == CONN_NEE ? 0 : rem / numStrat, kEnd = CLS == CONN_NEE ? f.batch : kBegin + 1;
     for (int k = kBegin; k < kEnd; ++k) {
     const int pix = k * N0 + px;   // the path (plane index)
     const mcrt_camera& cam = camp[k];
@@ -992,7 +995,7 @@ void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
 }
 void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st) {
     const int blocks = std::max(1, std::min((maxCount + 63) / 64, BDPT_VIS_MAX_WAVES));
-    hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_COMPACT>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks), dim3(64), 0, st, c, b, q.count,
+    hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks), dim3(64), 0, st, c, b, q.count,
                        q.o, q.d, q.t);
 }
 void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, const float4* chunk,

@@ -93,9 +93,7 @@ struct mcrt_scene_s {
     // BVH
     void* dNodes = nullptr;
     void* dTris = nullptr;
-    void* dNodesC = nullptr;   // descent-compact traversal records of a flat tree (k_pack_compact)
-    bool compact = false;
-    bool compactAll = false;   // MCRT_COMPACT_TRAV=2: every launch uses them (test hook)
+    bool packets = false;      // coherent launches as wave packets (finish_accel)
     uint64_t numNodes = 0;
     uint32_t numTris = 0;
     double buildMs = 0.0;
@@ -299,9 +297,8 @@ static bool ensure_spill(mcrt_scene s, size_t rays) {
 
 static TraceCtx trace_ctx(mcrt_scene s) {
     TraceCtx c;
-    c.nodes = (const float4*)(s->compactAll ? s->dNodesC : s->dNodes);
-    c.compact = s->compactAll ? 1 : 0;
-    c.rootWord = s->numNodes == 1 ? 0x08000000u : 0u;   // a one-triangle tree's root is a leaf
+    c.nodes = (const float4*)s->dNodes;
+    c.packet = 0;
     c.spill = s->dSpill;
     c.spillCap = s->spillCap;
     c.overflow = s->ctx->dFlags;
@@ -309,11 +306,10 @@ static TraceCtx trace_ctx(mcrt_scene s) {
     return c;
 }
 
-// the camera-ray launch's view: descent-compact records when the scene has them
-static TraceCtx compact_ctx(mcrt_scene s) {
+// the coherent launches' view (camera rays, bounce-0 shadow rays): wave packets when the tree allows
+static TraceCtx packet_ctx(mcrt_scene s) {
     TraceCtx c = trace_ctx(s);
-    c.nodes = (const float4*)(s->compact ? s->dNodesC : s->dNodes);
-    c.compact = s->compact ? 1 : 0;
+    c.packet = s->packets ? 1 : 0;
     return c;
 }
 
@@ -508,7 +504,7 @@ MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx) {
 static void scene_free_device(mcrt_scene s) {
     void** ptrs[] = {&s->dShapes, &s->dIndices, &s->dPositions, &s->dUvs, &s->dNormals, &s->dTextures,
                      &s->dTexData, &s->dSobol, &s->dLights, &s->dMaterials, &s->dNodes, &s->dTris,
-                     &s->dNodesC, &s->dSurf, &s->dSurfBase, &s->dSurfMeshes};
+                     &s->dSurf, &s->dSurfBase, &s->dSurfMeshes};
     for (void** p : ptrs) {
         if (*p) hipFree(*p);
         *p = nullptr;
@@ -816,36 +812,11 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
 // (allocated by ensure_spill for the largest launch)
 static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_point t0, const float* box6) {
     mcrt_ctx ctx = s->ctx;
-    // descent-compact traversal records for flat trees (mcrt_traverse.h traverseOct2), used by
-    // the camera-ray launch (compact_ctx).  MCRT_COMPACT_TRAV=0 keeps the plain records
-    // everywhere (A/B), =2 uses the compact ones in every launch (test hook); a tree without the exact-union property or with more than 2^27 nodes
-    // keeps them too.
-    if (s->dNodesC) hipFree(s->dNodesC);
-    s->dNodesC = nullptr;
-    s->compact = s->compactAll = false;
-    const char* ce = std::getenv("MCRT_COMPACT_TRAV");
-    if (!s->twoLevel && !(ce && std::atoi(ce) == 0) && s->numNodes <= 0x08000000ull) {
-        void* dc = nullptr;
-        int* dBad = nullptr;
-        if (hipMalloc(&dc, 64 * s->numNodes) == hipSuccess && hipMalloc(&dBad, sizeof(int)) == hipSuccess) {
-            int bad = 0;
-            HIPCHK(ctx, hipMemsetAsync(dBad, 0, sizeof(int), ctx->stream));
-            mcrt::launch_pack_compact((const float4*)s->dNodes, (float4*)dc, (uint32_t)s->numNodes, dBad, ctx->stream);
-            HIPCHK(ctx, hipGetLastError());
-            HIPCHK(ctx, hipMemcpyAsync(&bad, dBad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-            HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-            if (!bad) {
-                s->dNodesC = dc;
-                s->compact = true;
-                s->compactAll = ce && std::atoi(ce) == 2;
-                dc = nullptr;
-            }
-        } else {
-            (void)hipGetLastError();   // no room for a second copy: keep the plain records
-        }
-        if (dc) hipFree(dc);
-        if (dBad) hipFree(dBad);
-    }
+    // wave packets for the coherent launches (mcrt_traverse.h traversePacket): flat trees whose
+    // depth fits the packet stack (2 entries per level).  MCRT_CAMERA_PACKETS=0 walks them per ray
+    // (A/B and tests: the results are the same bit for bit).
+    const char* pe = std::getenv("MCRT_CAMERA_PACKETS");
+    s->packets = !s->twoLevel && 2 * (s->bvhDepth + 1) <= MCRT_PK_STACK && !(pe && std::atoi(pe) == 0);
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
     int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries
@@ -887,7 +858,7 @@ MCRT_API mcrt_status mcrt_accel_info(mcrt_scene s, uint64_t* num_nodes, uint64_t
                                      uint32_t* num_triangles) {
     if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
     if (num_nodes) *num_nodes = s->numNodes;
-    if (device_bytes) *device_bytes = (s->compact ? 128ull : 64ull) * s->numNodes;
+    if (device_bytes) *device_bytes = 64ull * s->numNodes;
     if (build_ms) *build_ms = s->buildMs;
     if (num_triangles) *num_triangles = s->numTris;
     return MCRT_OK;
@@ -1403,7 +1374,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         mcrt::launch_bdpt_clear_splat((int)N, fb->splat, st);
     // depth 0: camera rays (coherent, 8x8 tiles in order) in the first half of queue 0's buffers
     // with their own count, light rays in the second half with count [0]; ONE launch traces both,
-    // the camera rays over the descent-compact records like PT's camera rays (compact_ctx); both
+    // the camera rays as wave packets like PT's camera rays (packet_ctx); both
     // halves then feed the depth-1 vertex launches, which append to queue 1
     BdptQueue camQ = queue(0), lightQ = queue(0);
     camQ.count = cnt + BDPT_CNT_CAM0;
@@ -1415,7 +1386,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         mcrt::launch_bdpt_start(sa, f, b, dCam, camQ, lightQ, st);
     }
     {
-        TraceCtx tcc = compact_ctx(s);
+        TraceCtx tcc = packet_ctx(s);
         tcc.spill = bs.spill;
         Timed t(ctx, K_EXTEND, camQ.count, 0, st);
         mcrt::launch_extend_pair(tcc, tcs, camQ.count, camQ.o, camQ.d, fb->bHits, lightQ.count, lightQ.o, lightQ.d,
@@ -1579,7 +1550,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     const int qCap = bandPaths;
     {
         Timed t(ctx, K_PRIMARY, nullptr, (int64_t)bandPaths, st);
-        TraceCtx tcp = compact_ctx(s);   // coherent camera rays: descent-compact records
+        TraceCtx tcp = packet_ctx(s);   // coherent camera rays: wave packets
         tcp.spill = slot.spill;
         mcrt::launch_primary(tcp, f, dCam, fb->hitsP, st);
     }
@@ -1601,7 +1572,10 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
             // shadow rays of bounce b + extension rays for bounce b+1 (both from this shading pass) in
             // one launch: separate k_extend + k_shadow launches cost 0.18 ms more per frame (r01)
             Timed t(ctx, K_SHADOW_EXTEND, extCnt + b, 0, st, shadowCnt + b);   // items: extension + shadow rays
-            mcrt::launch_shadow_extend(tcs, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
+            // bounce-0 shadow rays are coherent (a packed wave's paths share a pixel): wave packets
+            TraceCtx tse = b == 0 ? packet_ctx(s) : tcs;
+            tse.spill = slot.spill;
+            mcrt::launch_shadow_extend(tse, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
                                        fb->sO, fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
             Timed t(ctx, K_SHADOW, shadowCnt + b, 0, st);
@@ -1642,7 +1616,7 @@ MCRT_API mcrt_status mcrt_render_aov(mcrt_scene s, mcrt_framebuffer fb, const mc
     HIPCHK(ctx, hipMemcpyAsync(dCam, cam, sizeof(mcrt_camera), hipMemcpyHostToDevice, st));
     if (!ensure_spill(s, std::max((size_t)f.numTiles * 64, 2 * fb->N + 64)))
         return fail(ctx, MCRT_ERROR_OUT_OF_MEMORY, "traversal spill buffer");
-    const TraceCtx tcs = compact_ctx(s);
+    const TraceCtx tcs = packet_ctx(s);
     mcrt::launch_primary(tcs, f, dCam, fb->hitsP, st);
     const size_t stride = aov == MCRT_AOV_TEXTURE_LOD ? 3 : 1;
     float4* dOut = nullptr;

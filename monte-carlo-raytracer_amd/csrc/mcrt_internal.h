@@ -73,12 +73,14 @@ struct BdptQueue {
     float4 *o, *d, *t;
 };
 
+// entries of a wave packet's LDS stack (node word + 64-bit lane mask); a level pushes at most 2
+#define MCRT_PK_STACK 128
 struct TraceCtx {
     const float4* nodes;   // 4 float4 per node (mcrt_bvh.cpp): internal = child boxes + indices, leaf = triangle
                            // two-level (mcrt_bvh2l.cpp): + instance records (world->object rows, bottom root)
     int twoLevel;          // selects the kernels' two-level instantiation (launch-time, not per lane)
-    int compact;           // flat-tree record layout: 0 plain (traverseOct), 1 descent-compact (traverseOct2)
-    uint32_t rootWord;     // compact records: the root's child word (index | leaf bit)
+    int packet;            // coherent launches (camera rays, bounce-0 shadow rays) walk the tree as wave
+                           // packets (mcrt_traverse.h traversePacket); flat trees of depth <= MCRT_PK_STACK/2 - 1
     uint32_t* spill;
     int spillCap;           // spill entries per ray (a multiple of STACK_LDS)
     int* overflow;
@@ -120,7 +122,6 @@ void launch_chase_init(void* rec, uint32_t n, hipStream_t st);
 void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* sink, hipStream_t st);
 // descent-compact traversal records (mcrt_traverse.h traverseOct2); *bad = 1 if the tree lacks
 // the exact-union property or an index does not fit the 27-bit child word
-void launch_pack_compact(const float4* in, float4* out, uint32_t n, int* bad, hipStream_t st);
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& camQ, const BdptQueue& lightQ, hipStream_t st);
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,

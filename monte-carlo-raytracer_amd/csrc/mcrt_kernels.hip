@@ -32,7 +32,7 @@ template <bool ANY, int LAY>
 __global__ __launch_bounds__(64) void k_trace_rays(TraceCtx c, const mcrt_ray* __restrict__ rays, int n,
                                                    const int* __restrict__ countDev,
                                                    mcrt_intersection* __restrict__ hits, int* __restrict__ occl) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[STACK_LDS * 64];
     if (countDev) n = min(n, *countDev);   // RR's numrays in remote memory (radeon_rays.h:272-277)
     const int lane = threadIdx.x;
     const int i = blockIdx.x * 64 + lane;
@@ -110,7 +110,7 @@ MCRT_DEV void packedPath(const FrameArgs& f, int tileAll, int lane, int& k, int&
 template <int LAY>
 __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 float4* __restrict__ hitOut) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[STACK_LDS * 64];
     const int lane = threadIdx.x;
     const int tileAll = xcdRemap(blockIdx.x, gridDim.x);
     int k, tile, pi = lane;
@@ -134,12 +134,43 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
         traceClosest<LAY>(c, r, lds + lane, raySpill(c, tileAll, lane), t);
 }
 
+// The camera-ray launch with wave-packet traversal (traversePacket, plain records): the same rays
+// and hit records as k_primary.
+__global__ __launch_bounds__(64) void k_primary_pk(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
+                                                   float4* __restrict__ hitOut) {
+    __shared__ uint32_t stkN[PK_STACK];
+    __shared__ uint64_t stkM[PK_STACK];
+    const int lane = threadIdx.x;
+    const int tileAll = xcdRemap(blockIdx.x, gridDim.x);
+    int k, tile, pi = lane;
+    if (f.primaryPack && f.batch > 1) {
+        packedPath(f, tileAll, lane, k, tile, pi);
+    } else {
+        splitTileFrame(f, tileAll, k, tile);
+    }
+    int x = 0, y = 0;
+    const bool valid = tile < f.numTiles && k < f.batch && tilePixel(f, tile, pi, x, y);
+    TraceRay r;
+    r.o = splat3(0.0f);
+    r.d = f3{0.0f, 0.0f, 1.0f};
+    if (valid) {
+        const mcrt_camera& cam = camp[k];
+        r.o = ld3(cam.pos);
+        r.d = cameraDir(cam, x, y);
+    }
+    r.tmax = 1000.0f;
+    r.mask = -1;
+    float t;
+    const int tri = traversePacket<false>(c.nodes, r, valid, stkN, stkM, c.overflow, t);
+    if (valid) hitOut[(size_t)k * f.W * f.H + (size_t)y * f.W + x] = closestRecord(c.nodes, r, tri, t);
+}
+
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
 // The grid covers the queue's capacity; workgroups past the device-side count exit at once.
 template <int LAY>
 __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ qO,
                                                const float4* __restrict__ qD, float4* __restrict__ hitOut) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[STACK_LDS * 64];
     const int n = *count;
     if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
@@ -162,7 +193,7 @@ template <int LAY>
 __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ sO,
                                                const float4* __restrict__ sD, const float4* __restrict__ sL,
                                                float4* __restrict__ radiance) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[STACK_LDS * 64];
     const int n = *count;
     if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
@@ -193,7 +224,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
                                                       float4* __restrict__ hitOut, const int* __restrict__ shadowCount,
                                                       const float4* __restrict__ sO, const float4* __restrict__ sD,
                                                       const float4* __restrict__ sL, float4* __restrict__ radiance) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[STACK_LDS * 64];
     const int ne = *extCount;
     const int eb = (ne + 63) >> 6;
     const int lane = threadIdx.x;
@@ -214,6 +245,37 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         const int sb = (ns + 63) >> 6;
         if ((int)blockIdx.x - eb >= sb) return;
         const int i = xcdRemap((int)blockIdx.x - eb, sb) * 64 + lane;
+        if (LAY == LAY_PLAIN && c.packet) {
+            // bounce-0 shadow rays: a wave's rays leave a few pixels for one light (packed waves), so
+            // they walk the tree as one packet (any hit: the answers do not depend on the order)
+            const bool valid = i < ns;
+            TraceRay r;
+            r.o = splat3(0.0f);
+            r.d = f3{0.0f, 0.0f, 1.0f};
+            r.tmax = 0.0f;
+            float4 d = make_float4(0.f, 0.f, 1.f, 0.f);
+            if (valid) {
+                const float4 o = sO[i];
+                d = sD[i];
+                r.o = ld3(o);
+                r.d = ld3(d);
+                r.tmax = o.w;
+            }
+            r.mask = -1;
+            float tt;
+            const bool occ = traversePacket<true>(c.nodes, r, valid, lds, pkMasks(lds), c.overflow, tt) >= 0;
+            if (valid) {
+                const float V = occ ? 0.0f : 1.0f;
+                const float4 L = sL[i];
+                const int pix = __float_as_int(d.w);
+                float4 acc = radiance[pix];
+                acc.x += L.x * V;
+                acc.y += L.y * V;
+                acc.z += L.z * V;
+                radiance[pix] = acc;
+            }
+            return;
+        }
         if (i >= ns) return;
         const float4 o = sO[i], d = sD[i], L = sL[i];
         TraceRay r;
@@ -240,7 +302,7 @@ __global__ __launch_bounds__(64) void k_extend_pair(TraceCtx cc, TraceCtx c, con
                                                     float4* __restrict__ hit0, const int* __restrict__ count1,
                                                     const float4* __restrict__ qO1, const float4* __restrict__ qD1,
                                                     float4* __restrict__ hit1) {
-    __shared__ uint32_t lds[STACK_LDS * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[STACK_LDS * 64];
     const int n0 = *count0;
     const int b0 = (n0 + 63) >> 6;
     const int lane = threadIdx.x;
@@ -251,6 +313,14 @@ __global__ __launch_bounds__(64) void k_extend_pair(TraceCtx cc, TraceCtx c, con
     if ((int)blockIdx.x < b0) {
         const int blk = xcdRemap(blockIdx.x, b0);
         const int i = blk * 64 + lane;
+        if (LAY0 == LAY_PLAIN && cc.packet) {   // camera rays of 8x8 tiles: wave packets
+            const bool valid = i < n0;
+            r.o = valid ? ld3(qO0[i]) : splat3(0.0f);
+            r.d = valid ? ld3(qD0[i]) : f3{0.0f, 0.0f, 1.0f};
+            const int tri = traversePacket<false>(cc.nodes, r, valid, lds, pkMasks(lds), cc.overflow, t);
+            if (valid) hit0[i] = closestRecord(cc.nodes, r, tri, t);
+            return;
+        }
         if (i >= n0) return;
         r.o = ld3(qO0[i]);
         r.d = ld3(qD0[i]);
@@ -692,63 +762,6 @@ __global__ __launch_bounds__(256) void k_stream_copy(const f4* __restrict__ src,
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
-// Descent-compact records (mcrt_traverse.h traverseOct2) from the mcrt_bvh.cpp records, one
-// thread per node.  Internal node i: per coordinate slot the union value X_s (the node's own box,
-// which its parent record holds as a child box), the other child's value S_s and the owner bit.
-// Each thread also checks, for each internal child, that the box its own record carries for
-// that child equals the union of the child's two boxes -- the property the compact decode rests
-// on (RR pulls bounds into parents); a mismatch sets *bad and the host keeps the plain layout.
-__global__ void k_pack_compact(const float4* __restrict__ in, float4* __restrict__ out, uint32_t n, int* bad) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int4* in4 = reinterpret_cast<const int4*>(in);
-    const float4 n0 = in[4 * (size_t)i], n1 = in[4 * (size_t)i + 1], n2 = in[4 * (size_t)i + 2];
-    const int4 n3 = in4[4 * (size_t)i + 3];
-    float4* o = out + 4 * (size_t)i;
-    if (n3.x < 0) {   // leaf: unchanged
-        o[0] = n0;
-        o[1] = n1;
-        o[2] = n2;
-        reinterpret_cast<int4*>(o)[3] = n3;
-        return;
-    }
-    const float A[6] = {n0.x, n0.y, n0.z, n0.w, n2.x, n2.y};
-    const float B[6] = {n1.x, n1.y, n1.z, n1.w, n2.z, n2.w};
-    float X[6], S[6];
-    uint32_t own = 0;
-    for (int k = 0; k < 6; ++k) {
-        X[k] = (k & 1) ? fmaxf(A[k], B[k]) : fminf(A[k], B[k]);
-        const bool a = A[k] == X[k];
-        own |= (a ? 1u : 0u) << k;
-        S[k] = a ? B[k] : A[k];
-    }
-    const uint32_t l = (uint32_t)n3.x, r = (uint32_t)n3.y;
-    bool leaf[2];
-    for (int c = 0; c < 2; ++c) {
-        const uint32_t ch = c ? r : l;
-        if (ch >= n) {
-            *bad = 1;
-            leaf[c] = false;
-            continue;
-        }
-        const int4 m = in4[4 * (size_t)ch + 3];
-        leaf[c] = m.x < 0;
-        if (leaf[c]) continue;
-        const float4 c0 = in[4 * (size_t)ch], c1 = in[4 * (size_t)ch + 1], c2 = in[4 * (size_t)ch + 2];
-        const float* P = c ? B : A;
-        const float U[6] = {fminf(c0.x, c1.x), fmaxf(c0.y, c1.y), fminf(c0.z, c1.z),
-                            fmaxf(c0.w, c1.w), fminf(c2.x, c2.z), fmaxf(c2.y, c2.w)};
-        for (int k = 0; k < 6; ++k)
-            if (!(U[k] == P[k])) *bad = 1;
-    }
-    if (l > CW_IDX || r > CW_IDX) *bad = 1;
-    const uint32_t wA = (l & CW_IDX) | (leaf[0] ? CW_LEAF : 0u) | ((own & 7u) << 28);
-    const uint32_t wB = (r & CW_IDX) | (leaf[1] ? CW_LEAF : 0u) | ((own >> 3) << 28);
-    o[0] = make_float4(S[0], S[1], S[2], S[3]);
-    o[1] = make_float4(S[4], S[5], __uint_as_float(wA), __uint_as_float(wB));
-    o[2] = make_float4(X[0], X[1], X[2], X[3]);
-    o[3] = make_float4(X[4], X[5], 0.0f, 0.0f);
-}
 
 namespace mcrt {
 
@@ -757,12 +770,10 @@ void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n,
     const dim3 g((n + 63) / 64), b(64);
     {
         if (any)
-            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<true, LAY_TWO_LEVEL>,
-                                          k_trace_rays<true, LAY_COMPACT>, k_trace_rays<true, LAY_PLAIN>),
+            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<true, LAY_TWO_LEVEL>, k_trace_rays<true, LAY_PLAIN>),
                                g, b, 0, st, c, rays, n, countDev, hits, occl);
         else
-            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<false, LAY_TWO_LEVEL>,
-                                          k_trace_rays<false, LAY_COMPACT>, k_trace_rays<false, LAY_PLAIN>),
+            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<false, LAY_TWO_LEVEL>, k_trace_rays<false, LAY_PLAIN>),
                                g, b, 0, st, c, rays, n, countDev, hits, occl);
     }
 }
@@ -775,34 +786,36 @@ void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshSt
 }
 
 void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st) {
-    hipLaunchKernelGGL(pickLayout(c, k_primary<LAY_TWO_LEVEL>, k_primary<LAY_COMPACT>, k_primary<LAY_PLAIN>), dim3(f.numTiles * f.batch), dim3(64), 0, st, c, f, cam,
+    if (c.packet && !c.twoLevel) {
+        hipLaunchKernelGGL(k_primary_pk, dim3(f.numTiles * f.batch), dim3(64), 0, st, c, f, cam, hits);
+        return;
+    }
+    hipLaunchKernelGGL(pickLayout(c, k_primary<LAY_TWO_LEVEL>, k_primary<LAY_PLAIN>), dim3(f.numTiles * f.batch), dim3(64), 0, st, c, f, cam,
                        hits);
 }
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
                    hipStream_t st) {
-    hipLaunchKernelGGL(pickLayout(c, k_extend<LAY_TWO_LEVEL>, k_extend<LAY_COMPACT>, k_extend<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+    hipLaunchKernelGGL(pickLayout(c, k_extend<LAY_TWO_LEVEL>, k_extend<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, qO, qD, hits);
 }
 void launch_extend_pair(const TraceCtx& cc, const TraceCtx& c, const int* count0, const float4* qO0, const float4* qD0,
                         float4* hit0, const int* count1, const float4* qO1, const float4* qD1, float4* hit1,
                         int maxCount0, int maxCount1, hipStream_t st) {
-    auto k = c.twoLevel ? k_extend_pair<LAY_TWO_LEVEL, LAY_TWO_LEVEL>
-             : cc.compact ? k_extend_pair<LAY_COMPACT, LAY_PLAIN> : k_extend_pair<LAY_PLAIN, LAY_PLAIN>;
+    auto k = c.twoLevel ? k_extend_pair<LAY_TWO_LEVEL, LAY_TWO_LEVEL> : k_extend_pair<LAY_PLAIN, LAY_PLAIN>;
     const int blocks = (maxCount0 + 63) / 64 + (maxCount1 + 63) / 64;
     hipLaunchKernelGGL(k, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, cc, c, count0, qO0, qD0, hit0, count1, qO1,
                        qD1, hit1);
 }
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st) {
-    hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_COMPACT>, k_shadow<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+    hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, sO, sD, sL, radiance);
 }
 void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
                           const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
                           float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
     const int blocks = (maxExt + 63) / 64 + (maxShadow + 63) / 64;
-    hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_COMPACT>,
-                                  k_shadow_extend<LAY_PLAIN>),
+    hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_PLAIN>),
                        dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, extCount, qO, qD, hits, shadowCount, sO, sD,
                        sL, radiance);
 }
@@ -851,9 +864,6 @@ void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, h
                        reinterpret_cast<f4*>(dst), n4);
 }
 
-void launch_pack_compact(const float4* in, float4* out, uint32_t n, int* bad, hipStream_t st) {
-    hipLaunchKernelGGL(k_pack_compact, dim3((n + 255) / 256), dim3(256), 0, st, in, out, n, bad);
-}
 
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st) {
     const int n = (int)(W * H);

@@ -9,15 +9,14 @@
 // ---------------------------------------------------------------------------
 #define STACK_LDS 16
 
-// Node-record layouts of the traversal kernels' template parameter LAY (TraceCtx::compact,
-// TraceCtx::twoLevel): each layout gets its own kernel instantiation, so a kernel's register
-// budget is that of the one loop it runs.
-#define LAY_PLAIN 0       // mcrt_bvh.cpp records, traverseOct
-#define LAY_COMPACT 1     // descent-compact records, traverseOct2
+// Node-record layouts of the traversal kernels' template parameter LAY (TraceCtx::twoLevel): each
+// layout gets its own kernel instantiation, so a kernel's register budget is that of the one loop
+// it runs.
+#define LAY_PLAIN 0       // mcrt_bvh.cpp records, traverseOct (and traversePacket)
 #define LAY_TWO_LEVEL 3   // mcrt_bvh2l.cpp records, traverse2L
 template <typename K>
-inline K pickLayout(const TraceCtx& c, K twoLevel, K compact, K plain) {
-    return c.twoLevel ? twoLevel : c.compact ? compact : plain;
+inline K pickLayout(const TraceCtx& c, K twoLevel, K plain) {
+    return c.twoLevel ? twoLevel : plain;
 }
 
 struct TraceRay {
@@ -158,154 +157,183 @@ MCRT_DEV int traverseOct(const float4* __restrict__ nodes, const TraceRay& r, f3
 }
 
 // ---------------------------------------------------------------------------
-// Descent-compact records (mcrt_kernels.hip k_pack_compact), used by the camera-ray launch.
+// Wave-packet traversal (closest hit, plain records) for coherent camera rays.
 //
-// A coherent launch is bound by the vector-memory path, not the ALUs: every step gathers four
-// 16-B pieces per lane from a record (measured on k_primary: TA busy 92 % of its cycles, L2 hit
-// 94 %).  The records are re-laid out to need fewer loads per step without changing a single box
-// value the slab tests see:
-//   * a parent's two child boxes are exact float min/max unions (RR bvh2.cpp pulls bounds into
-//     parents), so per coordinate slot s (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z) one child holds
-//     the node's own value X_s and only the OTHER child's value S_s must be stored, plus a bit
-//     saying which child owns X_s;
-//   * 80 % of internal steps descend into a child whose box the previous step just tested, so
-//     X's slab distances are already in registers (dX_s = fma(X_s, 1/d, -o/d), the same floats).
-// Record of internal node i (children A = left, B = right):
-//   q0 = (S0, S1, S2, S3), q1 = (S4, S5, wA, wB),      <- a descent reads only these 32 B
-//   q2 = (X.lo.x, X.hi.x, X.lo.y, X.hi.y), q3 = (X.lo.z, X.hi.z, 0, 0)   <- + these after a pop
-//   child word w = index (bits 0-26) | leaf (bit 27) | owner bits of 3 slots (28-30)
-// Leaf record: (v0, shapeId), (v1 - v0, primId), (v2 - v0, 0), (-1, -1, 0, 0) as before: 48 B,
-// and the leaf bit in the parent's word says so before the fetch.  A step loads 2, 3 (leaf) or
-// 4 (after a pop) pieces instead of 4; the decode reproduces both child boxes exactly (the
-// owner's value is X_s bit for bit up to the sign of a zero, which no slab decision can see),
-// so the visit order, every box test and every triangle test are those of traverseOct.
-// Measured (SM proxy 1080p): k_primary -9 %; the incoherent extension / shadow launches are
-// bound by L2 misses instead and ran 2-5 % slower with it, so they keep the plain records.
+// The 64 lanes of a wave walk ONE node at a time: the node index and the lane mask are wave-
+// uniform, so the 64-B record comes through the scalar cache (s_load, no vector-memory address
+// work) and every step runs one path (internal or leaf) instead of both.  At an internal node each
+// lane in the mask tests both child boxes with its own ray and its own closest t, exactly as
+// traverseOct does; the wave descends into a child if any lane hits it, carrying the mask of the
+// lanes that do, and defers the other child (with its mask) on a per-wave LDS stack.  When lanes
+// hit both children the wave goes first where most of them would (nearer child first per ray).
+// So every lane tests exactly the nodes whose box it hit at the parent -- the per-ray traversal's
+// rule -- and the closest hit is the same; only the ORDER of a lane's leaves can differ from
+// nearer-first, which matters for exactly-equal t (a tie) alone, as for any other visit order.
 // ---------------------------------------------------------------------------
-#define CW_IDX 0x07FFFFFFu
-#define CW_LEAF 0x08000000u
-#define CW_NODE 0x0FFFFFFFu   // index | leaf, the part the stack keeps
-#define CW_DONE 0x80000000u
+#define PK_STACK MCRT_PK_STACK
+typedef float __attribute__((ext_vector_type(4))) PkV4;
+typedef const __attribute__((address_space(4))) PkV4* PkNodes;   // uniform loads -> s_load
+// A kernel that also runs per-ray traversals keeps the packet stack in its per-ray LDS stack array
+// (STACK_LDS x 64 words): node words in the first PK_STACK words, lane masks after them.
+static_assert(PK_STACK * 3 <= STACK_LDS * 64, "packet stack must fit the per-ray LDS stack");
+MCRT_DEV uint64_t* pkMasks(uint32_t* lds) { return reinterpret_cast<uint64_t*>(lds + PK_STACK); }
+MCRT_DEV float4 pkLoad(PkNodes p, int i) {
+    const PkV4 v = p[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 
 template <bool ANY, int OCT>
-MCRT_DEV int traverseOct2(const float4* __restrict__ nodes, uint32_t rootWord, const TraceRay& r, f3 inv,
-                          uint32_t* stk, uint32_t* spill, int spillCap, int* overflowFlag, float& tHit) {
+MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay& r, f3 inv, bool valid,
+                               uint32_t* stkN, uint64_t* stkM, int* overflowFlag, float& tHit) {
+    const PkNodes cn = (PkNodes)(const void*)nodes;
     const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
+    const int lane = (int)__lane_id();
+    const int leader = __builtin_amdgcn_readfirstlane(lane);
     float t = r.tmax;
     int hit = -1;
-    uint32_t word = rootWord;
-    bool popped = true;   // the root's own box comes from its record
-    // slab distances of the node's own box per slot (valid after a descent)
-    float dx0 = 0.f, dx1 = 0.f, dx2 = 0.f, dx3 = 0.f, dx4 = 0.f, dx5 = 0.f;
-    stk[0] = CW_DONE;
-    int sp = 1, spillTop = 0;
-    while (word != CW_DONE) {
-        const uint32_t idx = word & CW_IDX;
-        const bool leaf = (word & CW_LEAF) != 0;
-        const float4* q = nodes + 4 * (size_t)idx;
-        float4 q0, q1, q2 = make_float4(0.f, 0.f, 0.f, 0.f), q3 = q2;
-        q0 = q[0];
-        q1 = q[1];
-        if (leaf || popped) q2 = q[2];
-        if (popped && !leaf) q3 = q[3];
-        bool pop = true;
-        uint32_t next = CW_DONE;
-        if (!leaf) {
-            if (popped) {
-                dx0 = fmaf(q2.x, inv.x, oxi.x); dx1 = fmaf(q2.y, inv.x, oxi.x);
-                dx2 = fmaf(q2.z, inv.y, oxi.y); dx3 = fmaf(q2.w, inv.y, oxi.y);
-                dx4 = fmaf(q3.x, inv.z, oxi.z); dx5 = fmaf(q3.y, inv.z, oxi.z);
-            }
-            const uint32_t wA = __float_as_uint(q1.z), wB = __float_as_uint(q1.w);
-            const float ds0 = fmaf(q0.x, inv.x, oxi.x), ds1 = fmaf(q0.y, inv.x, oxi.x);
-            const float ds2 = fmaf(q0.z, inv.y, oxi.y), ds3 = fmaf(q0.w, inv.y, oxi.y);
-            const float ds4 = fmaf(q1.x, inv.z, oxi.z), ds5 = fmaf(q1.y, inv.z, oxi.z);
-            // owner masks (all ones: A holds X_s) and the two children's slot distances
-            const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)wA, 28, 1);
-            const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)wA, 29, 1);
-            const uint32_t m2 = (uint32_t)__builtin_amdgcn_sbfe((int)wA, 30, 1);
-            const uint32_t m3 = (uint32_t)__builtin_amdgcn_sbfe((int)wB, 28, 1);
-            const uint32_t m4 = (uint32_t)__builtin_amdgcn_sbfe((int)wB, 29, 1);
-            const uint32_t m5 = (uint32_t)__builtin_amdgcn_sbfe((int)wB, 30, 1);
-#define MCRT_SEL(m, a, b) __uint_as_float(((m) & __float_as_uint(a)) | (~(m) & __float_as_uint(b)))
-            const float A0 = MCRT_SEL(m0, dx0, ds0), B0 = MCRT_SEL(m0, ds0, dx0);
-            const float A1 = MCRT_SEL(m1, dx1, ds1), B1 = MCRT_SEL(m1, ds1, dx1);
-            const float A2 = MCRT_SEL(m2, dx2, ds2), B2 = MCRT_SEL(m2, ds2, dx2);
-            const float A3 = MCRT_SEL(m3, dx3, ds3), B3 = MCRT_SEL(m3, ds3, dx3);
-            const float A4 = MCRT_SEL(m4, dx4, ds4), B4 = MCRT_SEL(m4, ds4, dx4);
-            const float A5 = MCRT_SEL(m5, dx5, ds5), B5 = MCRT_SEL(m5, ds5, dx5);
-#undef MCRT_SEL
+    uint64_t mask = __ballot(valid);
+    uint64_t alive = mask;   // any hit: lanes still without a hit
+    int node = 0, sp = 0;
+    while (mask != 0) {
+        const int nu = __builtin_amdgcn_readfirstlane(node);
+        const float4 n0 = pkLoad(cn, 4 * nu + 0), n1 = pkLoad(cn, 4 * nu + 1), n2 = pkLoad(cn, 4 * nu + 2),
+                     n3f = pkLoad(cn, 4 * nu + 3);
+        const int c0 = __builtin_amdgcn_readfirstlane(__float_as_int(n3f.x));
+        const int c1 = __builtin_amdgcn_readfirstlane(__float_as_int(n3f.y));
+        const bool act = (((ANY ? mask & alive : mask) >> lane) & 1ull) != 0;
+        uint64_t nextMask = 0;
+        int nextNode = 0;
+        if (c0 >= 0) {
             float a0, a1, b0, b1;
             if constexpr (OCT >= 0) {
-                // per axis the entry plane is lo for 1/d > 0 and hi otherwise (fma is monotone)
                 constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
-                a0 = fmaxf(fmaxf(SX ? A1 : A0, SY ? A3 : A2), fmaxf(SZ ? A5 : A4, 0.0f));
-                a1 = fminf(fminf(SX ? A0 : A1, SY ? A2 : A3), fminf(SZ ? A4 : A5, t));
-                b0 = fmaxf(fmaxf(SX ? B1 : B0, SY ? B3 : B2), fmaxf(SZ ? B5 : B4, 0.0f));
-                b1 = fminf(fminf(SX ? B0 : B1, SY ? B2 : B3), fminf(SZ ? B4 : B5, t));
+                const float axn = fmaf(SX ? n0.y : n0.x, inv.x, oxi.x), axf = fmaf(SX ? n0.x : n0.y, inv.x, oxi.x);
+                const float ayn = fmaf(SY ? n0.w : n0.z, inv.y, oxi.y), ayf = fmaf(SY ? n0.z : n0.w, inv.y, oxi.y);
+                const float azn = fmaf(SZ ? n2.y : n2.x, inv.z, oxi.z), azf = fmaf(SZ ? n2.x : n2.y, inv.z, oxi.z);
+                const float bxn = fmaf(SX ? n1.y : n1.x, inv.x, oxi.x), bxf = fmaf(SX ? n1.x : n1.y, inv.x, oxi.x);
+                const float byn = fmaf(SY ? n1.w : n1.z, inv.y, oxi.y), byf = fmaf(SY ? n1.z : n1.w, inv.y, oxi.y);
+                const float bzn = fmaf(SZ ? n2.w : n2.z, inv.z, oxi.z), bzf = fmaf(SZ ? n2.z : n2.w, inv.z, oxi.z);
+                a0 = fmaxf(fmaxf(axn, ayn), fmaxf(azn, 0.0f));
+                a1 = fminf(fminf(axf, ayf), fminf(azf, t));
+                b0 = fmaxf(fmaxf(bxn, byn), fmaxf(bzn, 0.0f));
+                b1 = fminf(fminf(bxf, byf), fminf(bzf, t));
             } else {   // RR intersect_bvh2_lds.cl:54-63 (fast_intersect_bbox2)
-                a0 = fmaxf(fmaxf(fmaxf(fminf(A0, A1), fminf(A2, A3)), fminf(A4, A5)), 0.0f);
-                a1 = fminf(fminf(fminf(fmaxf(A0, A1), fmaxf(A2, A3)), fmaxf(A4, A5)), t);
-                b0 = fmaxf(fmaxf(fmaxf(fminf(B0, B1), fminf(B2, B3)), fminf(B4, B5)), 0.0f);
-                b1 = fminf(fminf(fminf(fmaxf(B0, B1), fmaxf(B2, B3)), fmaxf(B4, B5)), t);
+                const float ax0 = fmaf(n0.x, inv.x, oxi.x), ax1 = fmaf(n0.y, inv.x, oxi.x);
+                const float ay0 = fmaf(n0.z, inv.y, oxi.y), ay1 = fmaf(n0.w, inv.y, oxi.y);
+                const float az0 = fmaf(n2.x, inv.z, oxi.z), az1 = fmaf(n2.y, inv.z, oxi.z);
+                const float bx0 = fmaf(n1.x, inv.x, oxi.x), bx1 = fmaf(n1.y, inv.x, oxi.x);
+                const float by0 = fmaf(n1.z, inv.y, oxi.y), by1 = fmaf(n1.w, inv.y, oxi.y);
+                const float bz0 = fmaf(n2.z, inv.z, oxi.z), bz1 = fmaf(n2.w, inv.z, oxi.z);
+                a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
+                a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), t);
+                b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
+                b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), t);
             }
-            const bool h0 = a0 <= a1, h1 = b0 <= b1;
-            const bool c1first = h1 && (a0 > b0);   // intersect_bvh2_lds.cl:128-141
-            if (h0 && h1) {   // defer the far child
-                if (sp == STACK_LDS) {   // spill entries 1..15 (RR: intersect_bvh2_lds.cl:146-155)
-                    if (spillTop + STACK_LDS - 1 <= spillCap) {
-                        for (int k = 1; k < STACK_LDS; ++k) spill[(size_t)(spillTop + k - 1) * 64] = stk[k * 64];
-                        spillTop += STACK_LDS - 1;
-                    } else {
-                        *overflowFlag = 1;   // depth beyond capacity: drop (reported by the host)
+            const bool h0 = act && a0 <= a1, h1 = act && b0 <= b1;
+            const uint64_t mL = __ballot(h0), mR = __ballot(h1);
+            if (mL != 0 && mR != 0) {
+                // lanes hitting both children go to the nearer one first: the right one where
+                // a0 > b0 (intersect_bvh2_lds.cl:128-141).  The wave takes the majority's first
+                // child F with every lane that hits F and prefers it (or hits F only), then the
+                // other child S with every lane that hits S, then F AGAIN with the lanes that hit
+                // both but preferred S: so each lane visits its two children in its own order, and
+                // every lane's sequence of tests -- hence its t at every culling test and the
+                // first of equal-t hits it keeps -- is exactly traverseOct's.  (Any hit: the
+                // answer does not depend on the order, so no third pass.)
+                const uint64_t both = mL & mR;
+                const uint64_t pr = __ballot(h0 && h1 && a0 > b0);   // prefer right
+                const bool goR = 2 * __popcll(pr) > __popcll(both);
+                const uint64_t late = ANY ? 0ull : (goR ? both & ~pr : pr);   // first child, later
+                const uint64_t mF = goR ? mR : mL, mS = goR ? mL : mR;
+                const int cF = goR ? c1 : c0, cS = goR ? c0 : c1;
+                if (sp + (late != 0 ? 2 : 1) <= PK_STACK) {
+                    if (late != 0) {
+                        if (lane == leader) {
+                            stkN[sp] = (uint32_t)cF;
+                            stkM[sp] = late;
+                        }
+                        ++sp;
                     }
-                    sp = 1;
+                    if (lane == leader) {
+                        stkN[sp] = (uint32_t)cS;
+                        stkM[sp] = mS;
+                    }
+                    ++sp;
+                } else if (lane == leader) {
+                    *overflowFlag = 1;   // deeper than the wave stack: reported by the host
                 }
-                stk[sp * 64] = (c1first ? wA : wB) & CW_NODE;
-                ++sp;
+                nextNode = cF;
+                nextMask = mF & ~late;
+            } else if (mL != 0) {
+                nextNode = c0;
+                nextMask = mL;
+            } else if (mR != 0) {
+                nextNode = c1;
+                nextMask = mR;
             }
-            if (h0 || h1) {
-                const bool toB = c1first || !h0;
-                next = (toB ? wB : wA) & CW_NODE;
-                dx0 = toB ? B0 : A0; dx1 = toB ? B1 : A1; dx2 = toB ? B2 : A2;
-                dx3 = toB ? B3 : A3; dx4 = toB ? B4 : A4; dx5 = toB ? B5 : A5;
-                pop = false;
-            }
-        } else if (r.mask != __float_as_int(q0.w)) {   // RR_RAY_MASK
-            const float th = triHit(r, q0, q1, q2, t);
+        } else if (act && r.mask != __float_as_int(n0.w)) {   // RR_RAY_MASK
+            const float th = triHit(r, n0, n1, n2, t);
             if (th < t) {
                 t = th;
-                hit = (int)idx;
-                if (ANY) pop = false;   // next = DONE
+                hit = nu;
             }
         }
-        if (pop) {
+        if (ANY) {   // a lane with a hit is done (traverseOct<true>: next = DONE)
+            alive &= ~__ballot(hit >= 0);
+            if (alive == 0) break;
+        }
+        while (ANY && nextMask == 0 && sp > 0) {   // skip deferred children whose lanes are all done
             --sp;
-            next = stk[sp * 64];
-            if (next == CW_DONE && spillTop > 0) {   // refill (intersect_bvh2_lds.cl:182-191)
-                spillTop -= STACK_LDS - 1;
-                for (int k = 1; k < STACK_LDS; ++k) stk[k * 64] = spill[(size_t)(spillTop + k - 1) * 64];
-                sp = STACK_LDS - 1;
-                next = stk[sp * 64];
-            }
+            nextNode = __builtin_amdgcn_readfirstlane((int)stkN[sp]);
+            const uint64_t m = stkM[sp];
+            nextMask = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m)) & alive;
         }
-        popped = pop;
-        word = next;
+        if (!ANY && nextMask == 0 && sp > 0) {
+            --sp;
+            nextNode = __builtin_amdgcn_readfirstlane((int)stkN[sp]);
+            const uint64_t m = stkM[sp];
+            nextMask = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m);
+        }
+        node = nextNode;
+        mask = nextMask;
     }
     tHit = t;
     return hit;
 }
 
+// Closest (ANY = false) or any hit of the wave's rays over plain records; lanes with valid = false take
+// no part.  Returns the hit leaf's node index or -1 per lane.
+template <bool ANY>
+MCRT_DEV int traversePacket(const float4* __restrict__ nodes, const TraceRay& r, bool valid, uint32_t* stkN,
+                            uint64_t* stkM, int* overflowFlag, float& tHit) {
+    const f3 inv = safeInvDir(r.d);
+    const int oct = (int)(__float_as_uint(inv.x) >> 31) | (int)((__float_as_uint(inv.y) >> 31) << 1) |
+                    (int)((__float_as_uint(inv.z) >> 31) << 2);
+    const uint64_t vm = __ballot(valid);
+    const int first = vm ? (int)__builtin_ctzll(vm) : 0;
+    const int oct0 = __builtin_amdgcn_readfirstlane(__shfl(oct, first));
+    if (__all(!valid || oct == oct0)) {
+        switch (oct0) {
+            case 0: return traversePacketOct<ANY, 0>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+            case 1: return traversePacketOct<ANY, 1>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+            case 2: return traversePacketOct<ANY, 2>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+            case 3: return traversePacketOct<ANY, 3>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+            case 4: return traversePacketOct<ANY, 4>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+            case 5: return traversePacketOct<ANY, 5>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+            case 6: return traversePacketOct<ANY, 6>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+            case 7: return traversePacketOct<ANY, 7>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+            default: break;
+        }
+    }
+    return traversePacketOct<ANY, -1>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+}
+
 template <bool ANY, int LAY>
 MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, float& tHit) {
     const f3 inv = safeInvDir(r.d);
-#define MCRT_TRAV_CALL(OCT)                                                                                       \
-    do {                                                                                                          \
-        if constexpr (LAY == LAY_COMPACT)                                                                         \
-            return traverseOct2<ANY, OCT>(c.nodes, c.rootWord, r, inv, stk, spill, c.spillCap, c.overflow, tHit); \
-        else                                                                                                      \
-            return traverseOct<ANY, OCT>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit);             \
-    } while (0)
+#define MCRT_TRAV_CALL(OCT) return traverseOct<ANY, OCT>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit)
     const int oct = (int)(__float_as_uint(inv.x) >> 31) | (int)((__float_as_uint(inv.y) >> 31) << 1) |
                     (int)((__float_as_uint(inv.z) >> 31) << 2);
     const int oct0 = __builtin_amdgcn_readfirstlane(oct);
@@ -503,7 +531,7 @@ MCRT_DEV float4 traceClosest(const TraceCtx& c, const TraceRay& r, uint32_t* stk
         return closestRecord2L(c.nodes, r, tri, inst, t);
     } else {
         const int tri = traverse<false, LAY>(c, r, stk, spill, t);
-        return closestRecord(c.nodes, r, tri, t);   // leaf slots are the same in both flat layouts
+        return closestRecord(c.nodes, r, tri, t);
     }
 }
 template <int LAY>

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-3 checkpoint: full GPU suite, smoke, default bench, kernel trace of the default bench
 export TMPDIR=/tmp
-P=gpurun_out/full3
+P=gpurun_out/${FULL_DIR:-full3}
 mkdir -p $P
 timeout -k 10 1500 python -u -m pytest tests/ -m gpu -x -v --timeout 600 --timeout-method thread > $P/pytest_gpu.log 2>&1 || { tail -30 $P/pytest_gpu.log; exit 3; }
 tail -3 $P/pytest_gpu.log
