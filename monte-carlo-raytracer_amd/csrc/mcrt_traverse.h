@@ -182,56 +182,72 @@ MCRT_DEV float4 pkLoad(PkNodes p, int i) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// triHit (RR common.cl:177-218) without branches: the same arithmetic, the early outs become one
+// final select, so a packet's leaf step costs no exec-mask bookkeeping (scalar instructions are
+// what a packet step is short of, not vector ones).
+MCRT_DEV float triHitSel(const TraceRay& r, float4 A, float4 E1, float4 E2, float tmax) {
+    const f3 e1 = ld3(E1), e2 = ld3(E2);
+    const f3 s1 = cl_cross(r.d, e2);
+    const float denom = cl_dot(s1, e1);
+    const float invd = __builtin_amdgcn_rcpf(denom);
+    const f3 d = r.o - ld3(A);
+    const float b1 = cl_dot(d, s1) * invd;
+    const f3 s2 = cl_cross(d, e1);
+    const float b2 = cl_dot(r.d, s2) * invd;
+    const float temp = cl_dot(e2, s2) * invd;
+    const bool miss = denom == 0.f || b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || temp < 0.f || temp > tmax;
+    return miss ? tmax : temp;
+}
+
 template <bool ANY, int OCT>
 MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay& r, f3 inv, bool valid,
                                uint32_t* stkN, uint64_t* stkM, int* overflowFlag, float& tHit) {
     const PkNodes cn = (PkNodes)(const void*)nodes;
     const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
     const int lane = (int)__lane_id();
-    const int leader = __builtin_amdgcn_readfirstlane(lane);
+    const bool leader = lane == __builtin_amdgcn_readfirstlane(lane);
+    const uint64_t laneBit = 1ull << lane;
     float t = r.tmax;
     int hit = -1;
     uint64_t mask = __ballot(valid);
     uint64_t alive = mask;   // any hit: lanes still without a hit
-    int node = 0, sp = 0;
-    while (mask != 0) {
-        const int nu = __builtin_amdgcn_readfirstlane(node);
-        const float4 n0 = pkLoad(cn, 4 * nu + 0), n1 = pkLoad(cn, 4 * nu + 1), n2 = pkLoad(cn, 4 * nu + 2),
-                     n3f = pkLoad(cn, 4 * nu + 3);
-        const int c0 = __builtin_amdgcn_readfirstlane(__float_as_int(n3f.x));
-        const int c1 = __builtin_amdgcn_readfirstlane(__float_as_int(n3f.y));
-        const bool act = (((ANY ? mask & alive : mask) >> lane) & 1ull) != 0;
-        uint64_t nextMask = 0;
-        int nextNode = 0;
-        if (c0 >= 0) {
-            float a0, a1, b0, b1;
-            if constexpr (OCT >= 0) {
-                constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
-                const float axn = fmaf(SX ? n0.y : n0.x, inv.x, oxi.x), axf = fmaf(SX ? n0.x : n0.y, inv.x, oxi.x);
-                const float ayn = fmaf(SY ? n0.w : n0.z, inv.y, oxi.y), ayf = fmaf(SY ? n0.z : n0.w, inv.y, oxi.y);
-                const float azn = fmaf(SZ ? n2.y : n2.x, inv.z, oxi.z), azf = fmaf(SZ ? n2.x : n2.y, inv.z, oxi.z);
-                const float bxn = fmaf(SX ? n1.y : n1.x, inv.x, oxi.x), bxf = fmaf(SX ? n1.x : n1.y, inv.x, oxi.x);
-                const float byn = fmaf(SY ? n1.w : n1.z, inv.y, oxi.y), byf = fmaf(SY ? n1.z : n1.w, inv.y, oxi.y);
-                const float bzn = fmaf(SZ ? n2.w : n2.z, inv.z, oxi.z), bzf = fmaf(SZ ? n2.z : n2.w, inv.z, oxi.z);
-                a0 = fmaxf(fmaxf(axn, ayn), fmaxf(azn, 0.0f));
-                a1 = fminf(fminf(axf, ayf), fminf(azf, t));
-                b0 = fmaxf(fmaxf(bxn, byn), fmaxf(bzn, 0.0f));
-                b1 = fminf(fminf(bxf, byf), fminf(bzf, t));
-            } else {   // RR intersect_bvh2_lds.cl:54-63 (fast_intersect_bbox2)
-                const float ax0 = fmaf(n0.x, inv.x, oxi.x), ax1 = fmaf(n0.y, inv.x, oxi.x);
-                const float ay0 = fmaf(n0.z, inv.y, oxi.y), ay1 = fmaf(n0.w, inv.y, oxi.y);
-                const float az0 = fmaf(n2.x, inv.z, oxi.z), az1 = fmaf(n2.y, inv.z, oxi.z);
-                const float bx0 = fmaf(n1.x, inv.x, oxi.x), bx1 = fmaf(n1.y, inv.x, oxi.x);
-                const float by0 = fmaf(n1.z, inv.y, oxi.y), by1 = fmaf(n1.w, inv.y, oxi.y);
-                const float bz0 = fmaf(n2.z, inv.z, oxi.z), bz1 = fmaf(n2.w, inv.z, oxi.z);
-                a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
-                a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), t);
-                b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
-                b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), t);
-            }
-            const bool h0 = act && a0 <= a1, h1 = act && b0 <= b1;
-            const uint64_t mL = __ballot(h0), mR = __ballot(h1);
-            if (mL != 0 && mR != 0) {
+    uint32_t node = 0;
+    int sp = 0;
+    while (true) {
+        if (ANY) mask &= alive;
+        if (mask != 0) {
+            const PkNodes q = (PkNodes)((const char __attribute__((address_space(4)))*)cn + ((size_t)node << 6));
+            const float4 n0 = pkLoad(q, 0), n1 = pkLoad(q, 1), n2 = pkLoad(q, 2), n3f = pkLoad(q, 3);
+            const int c0 = __builtin_amdgcn_readfirstlane(__float_as_int(n3f.x));
+            const int c1 = __builtin_amdgcn_readfirstlane(__float_as_int(n3f.y));
+            if (c0 >= 0) {
+                float a0, a1, b0, b1;
+                if constexpr (OCT >= 0) {
+                    constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
+                    const float axn = fmaf(SX ? n0.y : n0.x, inv.x, oxi.x), axf = fmaf(SX ? n0.x : n0.y, inv.x, oxi.x);
+                    const float ayn = fmaf(SY ? n0.w : n0.z, inv.y, oxi.y), ayf = fmaf(SY ? n0.z : n0.w, inv.y, oxi.y);
+                    const float azn = fmaf(SZ ? n2.y : n2.x, inv.z, oxi.z), azf = fmaf(SZ ? n2.x : n2.y, inv.z, oxi.z);
+                    const float bxn = fmaf(SX ? n1.y : n1.x, inv.x, oxi.x), bxf = fmaf(SX ? n1.x : n1.y, inv.x, oxi.x);
+                    const float byn = fmaf(SY ? n1.w : n1.z, inv.y, oxi.y), byf = fmaf(SY ? n1.z : n1.w, inv.y, oxi.y);
+                    const float bzn = fmaf(SZ ? n2.w : n2.z, inv.z, oxi.z), bzf = fmaf(SZ ? n2.z : n2.w, inv.z, oxi.z);
+                    a0 = fmaxf(fmaxf(axn, ayn), fmaxf(azn, 0.0f));
+                    a1 = fminf(fminf(axf, ayf), fminf(azf, t));
+                    b0 = fmaxf(fmaxf(bxn, byn), fmaxf(bzn, 0.0f));
+                    b1 = fminf(fminf(bxf, byf), fminf(bzf, t));
+                } else {   // RR intersect_bvh2_lds.cl:54-63 (fast_intersect_bbox2)
+                    const float ax0 = fmaf(n0.x, inv.x, oxi.x), ax1 = fmaf(n0.y, inv.x, oxi.x);
+                    const float ay0 = fmaf(n0.z, inv.y, oxi.y), ay1 = fmaf(n0.w, inv.y, oxi.y);
+                    const float az0 = fmaf(n2.x, inv.z, oxi.z), az1 = fmaf(n2.y, inv.z, oxi.z);
+                    const float bx0 = fmaf(n1.x, inv.x, oxi.x), bx1 = fmaf(n1.y, inv.x, oxi.x);
+                    const float by0 = fmaf(n1.z, inv.y, oxi.y), by1 = fmaf(n1.w, inv.y, oxi.y);
+                    const float bz0 = fmaf(n2.z, inv.z, oxi.z), bz1 = fmaf(n2.w, inv.z, oxi.z);
+                    a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
+                    a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), t);
+                    b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
+                    b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), t);
+                }
+                // lane masks straight from the compares (the lanes outside `mask` drop out here)
+                const uint64_t mL = __ballot(a0 <= a1) & mask, mR = __ballot(b0 <= b1) & mask;
                 // lanes hitting both children go to the nearer one first: the right one where
                 // a0 > b0 (intersect_bvh2_lds.cl:128-141).  The wave takes the majority's first
                 // child F with every lane that hits F and prefers it (or hits F only), then the
@@ -241,63 +257,47 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                 // first of equal-t hits it keeps -- is exactly traverseOct's.  (Any hit: the
                 // answer does not depend on the order, so no third pass.)
                 const uint64_t both = mL & mR;
-                const uint64_t pr = __ballot(h0 && h1 && a0 > b0);   // prefer right
-                const bool goR = 2 * __popcll(pr) > __popcll(both);
-                const uint64_t late = ANY ? 0ull : (goR ? both & ~pr : pr);   // first child, later
+                const uint64_t pr = __ballot(a0 > b0) & both;   // lanes preferring the right child
+                const bool goR = mL == 0 || 2 * __popcll(pr) > __popcll(both);
+                const uint64_t late = ANY ? 0ull : (goR ? both & ~pr : pr);   // first child, visited later
                 const uint64_t mF = goR ? mR : mL, mS = goR ? mL : mR;
-                const int cF = goR ? c1 : c0, cS = goR ? c0 : c1;
-                if (sp + (late != 0 ? 2 : 1) <= PK_STACK) {
-                    if (late != 0) {
-                        if (lane == leader) {
-                            stkN[sp] = (uint32_t)cF;
-                            stkM[sp] = late;
+                const uint32_t cF = (uint32_t)(goR ? c1 : c0), cS = (uint32_t)(goR ? c0 : c1);
+                // deferred entries, bottom to top: F for the late lanes, then S
+                const int nPush = (late != 0 ? 1 : 0) + (mS != 0 ? 1 : 0);
+                if (nPush != 0) {
+                    if (sp + nPush <= PK_STACK) {
+                        if (leader) {
+                            stkN[sp] = late != 0 ? cF : cS;
+                            stkM[sp] = late != 0 ? late : mS;
+                            stkN[sp + 1] = cS;
+                            stkM[sp + 1] = mS;
                         }
-                        ++sp;
+                        sp += nPush;
+                    } else if (leader) {
+                        *overflowFlag = 1;   // deeper than the wave stack: reported by the host
                     }
-                    if (lane == leader) {
-                        stkN[sp] = (uint32_t)cS;
-                        stkM[sp] = mS;
-                    }
-                    ++sp;
-                } else if (lane == leader) {
-                    *overflowFlag = 1;   // deeper than the wave stack: reported by the host
                 }
-                nextNode = cF;
-                nextMask = mF & ~late;
-            } else if (mL != 0) {
-                nextNode = c0;
-                nextMask = mL;
-            } else if (mR != 0) {
-                nextNode = c1;
-                nextMask = mR;
-            }
-        } else if (act && r.mask != __float_as_int(n0.w)) {   // RR_RAY_MASK
-            const float th = triHit(r, n0, n1, n2, t);
-            if (th < t) {
-                t = th;
-                hit = nu;
+                node = cF;
+                mask = mF & ~late;
+            } else {
+                // every lane computes, the lanes of the mask that pass RR_RAY_MASK take the hit
+                const float th = triHitSel(r, n0, n1, n2, t);
+                const bool take = (mask & laneBit) != 0 && r.mask != __float_as_int(n0.w) && th < t;
+                hit = take ? (int)node : hit;
+                t = take ? th : t;
+                if (ANY) alive &= ~__ballot(take);   // a lane with a hit is done (next = DONE)
+                mask = 0;
             }
         }
-        if (ANY) {   // a lane with a hit is done (traverseOct<true>: next = DONE)
-            alive &= ~__ballot(hit >= 0);
-            if (alive == 0) break;
-        }
-        while (ANY && nextMask == 0 && sp > 0) {   // skip deferred children whose lanes are all done
+        if (ANY && alive == 0) break;
+        if (mask == 0) {
+            if (sp == 0) break;
             --sp;
-            nextNode = __builtin_amdgcn_readfirstlane((int)stkN[sp]);
+            node = (uint32_t)__builtin_amdgcn_readfirstlane((int)stkN[sp]);
             const uint64_t m = stkM[sp];
-            nextMask = (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m)) & alive;
+            mask = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m);
         }
-        if (!ANY && nextMask == 0 && sp > 0) {
-            --sp;
-            nextNode = __builtin_amdgcn_readfirstlane((int)stkN[sp]);
-            const uint64_t m = stkM[sp];
-            nextMask = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
-                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m);
-        }
-        node = nextNode;
-        mask = nextMask;
     }
     tHit = t;
     return hit;

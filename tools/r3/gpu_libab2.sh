@@ -1,0 +1,26 @@
+#!/bin/bash
+# In-tree library (B) against another build (A = $1): parity tests on B (-k $2), alternating
+# headline bench runs, SQ counters of B's timed call (pmc_summary rows for kernel filter $3).
+export TMPDIR=/tmp
+P=gpurun_out/libab2
+mkdir -p $P
+A=$PWD/$1
+timeout -k 10 900 python -u -m pytest -x -q --timeout 800 --timeout-method thread tests/ -m gpu -k "$2" > $P/tests.log 2>&1 || { tail -40 $P/tests.log; exit 3; }
+tail -1 $P/tests.log
+B="python3 bench.py --no-cpu-baseline --no-roofline-model --no-bdpt"
+for r in 1 2; do
+  for v in B A; do
+    if [ $v = A ]; then export MCRT_LIB_PATH=$A; else unset MCRT_LIB_PATH; fi
+    timeout -k 10 300 $B > $P/$v$r.json 2> $P/$v$r.err || { tail -20 $P/$v$r.err; exit 4; }
+    python3 -c "
+import json
+d = json.loads(open('$P/$v$r.json').read().strip().splitlines()[-1])
+print('$v$r', d['value'], d['ms_per_step'], {k: round(v['ms_per_frame'], 4) for k, v in d.get('kernels', {}).items()})"
+  done
+done
+unset MCRT_LIB_PATH
+if [ -n "$3" ]; then
+C="python3 bench.py --no-kernel-timing --no-bdpt --no-cpu-baseline --no-roofline-model"
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY -d $P/sq -o s -- $C > $P/sq.log 2>&1 || { tail -5 $P/sq.log; exit 5; }
+python3 tools/pmc_summary.py $(find $P/sq -name "*.db" | head -1) $3 | tail -2
+fi
