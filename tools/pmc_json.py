@@ -87,6 +87,8 @@ def main():
                    "wave_time_issue_stalled": round(c["SQ_WAIT_INST_ANY"] / wc, 3),
                    "valu_busy": round(c["SQ_INSTS_VALU"] * 2 / (1024 * cyc), 3),
                    "clock_ghz": round(cyc / (ms[k] * 1e-3) / 1e9, 3)}
+            if "SQ_INSTS_SALU" in c:   # one scalar unit per CU issues one SALU instruction per cycle
+                lim["salu_busy"] = round(c["SQ_INSTS_SALU"] / (256 * cyc), 3)
             if "SQ_ACTIVE_INST_ANY" in c:
                 lim["wave_time_issuing"] = round(c["SQ_ACTIVE_INST_ANY"] / wc, 3)
             if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
@@ -103,6 +105,7 @@ def main():
             mem, iss = lim["wave_time_waiting_on_memory"], lim["wave_time_issue_stalled"]
             bw = lim.get("memory_side_tb_s_bounds", [0.0, 0.0])[1]
             lim["binding"] = ("HBM bandwidth" if bw >= 5.0 else
+                              "scalar issue (SALU)" if lim.get("salu_busy", 0.0) >= 0.7 else
                               "vector-memory pipeline (TA busy) + memory latency"
                               if lim.get("ta_busy", 0.0) >= 0.85 and mem >= 0.4 else
                               "memory latency" if mem >= 0.4 and lim["valu_busy"] < 0.6 else
