@@ -207,7 +207,6 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
     const int lane = (int)__lane_id();
     const bool leader = lane == __builtin_amdgcn_readfirstlane(lane);
     const uint64_t laneBit = 1ull << lane;
-    bool overflow = false;
     float t = r.tmax;
     int hit = -1;
     uint64_t mask = __ballot(valid);
@@ -265,17 +264,6 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                 const uint32_t cF = (uint32_t)(goR ? c1 : c0), cS = (uint32_t)(goR ? c0 : c1);
                 // deferred entries, bottom to top: F for the late lanes, then S
                 const int nPush = (late != 0 ? 1 : 0) + (mS != 0 ? 1 : 0);
-#if MCRT_PK_ALLWRITE
-                if (nPush != 0) {   // every lane writes the same words to the same addresses
-                    const int sp0 = min(sp, PK_STACK - 2);
-                    stkN[sp0] = late != 0 ? cF : cS;
-                    stkM[sp0] = late != 0 ? late : mS;
-                    stkN[sp0 + 1] = cS;
-                    stkM[sp0 + 1] = mS;
-                    overflow |= sp + nPush > PK_STACK;
-                    sp = min(sp + nPush, PK_STACK);
-                }
-#else
                 if (nPush != 0) {
                     if (sp + nPush <= PK_STACK) {
                         if (leader) {
@@ -289,7 +277,6 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                         *overflowFlag = 1;   // deeper than the wave stack: reported by the host
                     }
                 }
-#endif
                 node = cF;
                 mask = mF & ~late;
             } else {
@@ -312,7 +299,6 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m);
         }
     }
-    if (overflow && leader) *overflowFlag = 1;   // deeper than the wave stack: reported by the host
     tHit = t;
     return hit;
 }
