@@ -15,3 +15,7 @@ d = json.loads(open('$P/c${c}_$r.json').read().strip().splitlines()[-1])
 print('chunks $c run $r', d['value'], d['ms_per_step'])"
   done
 done
+for c in 20 10; do
+  timeout -k 10 400 python tools/scale_emulate.py --ns 1,8 --steps 20 --chunks $c > $P/scale_c$c.json 2> $P/scale_c$c.err || { tail -5 $P/scale_c$c.err; exit 5; }
+  python -c "import json; d=json.load(open('$P/scale_c$c.json')); print('scale chunks $c', {n: (v['max_ms'], v['compute_eff']) for n, v in d['per_n'].items()})"
+done
