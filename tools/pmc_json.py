@@ -105,7 +105,7 @@ def main():
             mem, iss = lim["wave_time_waiting_on_memory"], lim["wave_time_issue_stalled"]
             bw = lim.get("memory_side_tb_s_bounds", [0.0, 0.0])[1]
             lim["binding"] = ("HBM bandwidth" if bw >= 5.0 else
-                              "scalar issue (SALU)" if lim.get("salu_busy", 0.0) >= 0.7 else
+                              "dependent-fetch latency, scalar unit busy (wave packets)" if lim.get("salu_busy", 0.0) >= 0.7 else
                               "vector-memory pipeline (TA busy) + memory latency"
                               if lim.get("ta_busy", 0.0) >= 0.85 and mem >= 0.4 else
                               "memory latency" if mem >= 0.4 and lim["valu_busy"] < 0.6 else
