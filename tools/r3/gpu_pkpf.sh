@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 P=gpurun_out/pkpf
 mkdir -p $P
-V=$PWD/monte-carlo-raytracer_amd/libmcrt_pkpf.so
+V=$PWD/monte-carlo-raytracer_amd/${VLIB:-libmcrt_pkpf.so}
 MCRT_LIB_PATH=$V timeout -k 10 900 python -u -m pytest -x -q --timeout 800 --timeout-method thread tests/ -m gpu -k "packets or sm_pt_1080p" > $P/tests.log 2>&1 || { tail -40 $P/tests.log; exit 3; }
 tail -1 $P/tests.log
 B="python3 bench.py --no-cpu-baseline --no-roofline-model --no-bdpt"
