@@ -690,10 +690,14 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
     int code = 0;
     if (live) {
         BVertex cv, samp;   // samp: the sampled vertex of a t = 1 / s = 1 strategy (pt / qs in the MIS)
-        if (CLS != CONN_LIGHT) cv = loadVertex(b.camV, t - 1, pix, N);
+        if (CLS != CONN_LIGHT && CLS != CONN_EMIT) cv = loadVertex(b.camV, t - 1, pix, N);
         if (CLS == CONN_EMIT) {
-            // ConnectVertices (BDPT.cl:723-731): emission of a camera vertex that is a light
-            if (cv.type == RT_BDPT_LIGHT_VERTEX || cv.lightIdx != -1) {
+            // ConnectVertices (BDPT.cl:723-731): emission of a camera vertex that is a light.  Only
+            // the type word is read first: for the (many) vertices that are not lights the strategy
+            // contributes nothing and the other 7 planes are never needed.
+            const int4 h = *reinterpret_cast<const int4*>(&vplane(b.camV, t - 1, 7, N)[pix]);
+            if (h.x == RT_BDPT_LIGHT_VERTEX || h.z != -1) {
+                cv = loadVertex(b.camV, t - 1, pix, N);
                 const f3 Le = evalLightLe(s.lights[cv.lightIdx], cv.fr.gn, cv.wo);
                 L = Le * cv.throughput;
             }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # every BASELINE config on one MI355X with this round's build (1 spp per step)
-P=gpurun_out/cfg3
+P=gpurun_out/${CFG_DIR:-cfg3}
 mkdir -p $P
 F="--no-cpu-baseline --no-roofline-model --no-bdpt"
 run() { n=$1; shift; timeout -k 10 400 python3 bench.py $F "$@" > $P/$n.json 2> $P/$n.err || { tail -20 $P/$n.err; exit 4; }
