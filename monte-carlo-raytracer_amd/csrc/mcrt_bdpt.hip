@@ -3,8 +3,8 @@
 // One frame (1 sample per pixel, maxDepth D) is, per rank band:
 //   k_bdpt_start          camera vertex 0 + light vertex 0 of every pixel (GenerateStartVertices,
 //                         BDPT.cl:240-312); the first camera rays and light rays go to two queues
-//                         (d = 1: k_extend + k_bdpt_vertex once per queue, the camera rays over
-//                         the descent-compact records)
+//                         (d = 1: one k_extend_pair launch, the camera rays as wave packets,
+//                         then k_bdpt_vertex once per queue)
 //   for d in 1..D+1:
 //     k_extend            closest hit over the queue (camera and light rays together)
 //     k_bdpt_vertex       GenerateSecondaryVertices (BDPT.cl:317-458) for every queued ray: the

@@ -120,8 +120,6 @@ void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStrea
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st);
 void launch_chase_init(void* rec, uint32_t n, hipStream_t st);
 void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* sink, hipStream_t st);
-// descent-compact traversal records (mcrt_traverse.h traverseOct2); *bad = 1 if the tree lacks
-// the exact-union property or an index does not fit the 27-bit child word
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& camQ, const BdptQueue& lightQ, hipStream_t st);
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,

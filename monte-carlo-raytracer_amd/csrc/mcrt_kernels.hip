@@ -293,8 +293,8 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
     }
 }
 
-// Closest hit over two queues in ONE launch, each over its own records: BDPT's first camera rays
-// (coherent: descent-compact records, cc) and first light rays (plain records, c).  The camera
+// Closest hit over two queues in ONE launch: BDPT's first camera rays (coherent: wave packets when
+// cc.packet) and first light rays (per ray, c).  The camera
 // workgroups come first; the light workgroups fill their tail (as k_shadow_extend).
 template <int LAY0, int LAY1>
 __global__ __launch_bounds__(64) void k_extend_pair(TraceCtx cc, TraceCtx c, const int* __restrict__ count0,
