@@ -502,10 +502,10 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
 __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameArgs f, BdptArgs b, int depth,
                                                             BdptQueue qIn, const float4* __restrict__ hits,
                                                             BdptQueue qOut) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = *qIn.count;
     __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
     if ((int)blockIdx.x * BDPT_BLOCK >= n) return;
+    const int i = xcdRemap(blockIdx.x, (n + BDPT_BLOCK - 1) / BDPT_BLOCK) * BDPT_BLOCK + threadIdx.x;
     const int N = (int)(f.W * f.H) * f.batch;   // plane stride (NB)
     const int D = f.maxDepth;
     bool push = false;

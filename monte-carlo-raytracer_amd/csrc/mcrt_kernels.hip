@@ -455,7 +455,9 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade0(SceneArgs s, FrameArgs f
                                                 const float4* __restrict__ hits, float4* __restrict__ radiance,
                                                 QueueArgs q) {
     const int lane = threadIdx.x & 63;
-    const int tileAll = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // XCD-aware block order: an XCD shades contiguous runs of tiles (their hits share surface
+    // records, materials and textures in its L2): k_shade0 -4 %
+    const int tileAll = xcdRemap(blockIdx.x, gridDim.x) * (SHADE_BLOCK / 64) + (int)(threadIdx.x >> 6);
     int k, tile, pi = lane;   // batch frame k
     if (f.shadePack && f.batch > 1) {
         // as k_primary's packed waves; the bounce-0 shadow rays of a wave (one light direction,
@@ -493,11 +495,13 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shadeN(SceneArgs s, FrameArgs f
                                                 const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                 const float4* __restrict__ qT, const float4* __restrict__ hits,
                                                 float4* __restrict__ radiance, QueueArgs q) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = *countIn;
     __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
     __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];
     if ((int)blockIdx.x * SHADE_BLOCK >= n) return;   // whole block past the queue: uniform exit
+    // XCD-aware block order (xcdRemap): each XCD shades contiguous runs of the queue, whose paths
+    // share triangles, materials and textures in that XCD's L2
+    const int i = xcdRemap(blockIdx.x, (n + SHADE_BLOCK - 1) / SHADE_BLOCK) * SHADE_BLOCK + threadIdx.x;
     ShadeOut o;
     o.pushS = o.pushE = false;
     o.eD = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
