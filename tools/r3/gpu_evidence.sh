@@ -3,7 +3,7 @@
 # bench.py reads, profiles/pmc_latest.json), then per-rank scaling emulation (PT 20 steps as one call
 # per rank; BDPT band split, 8 frames per call).
 export TMPDIR=/tmp
-P=gpurun_out/ev
+P=gpurun_out/${EV_DIR:-ev}
 mkdir -p $P
 B="python3 bench.py --no-kernel-timing --no-bdpt --no-cpu-baseline --no-roofline-model"
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $P/trace -o k -- $B > $P/trace.log 2>&1 || { tail -5 $P/trace.log; exit 7; }
@@ -17,6 +17,7 @@ echo "passes done"
 python3 tools/pmc_json.py $P "$B" 1 pmc_ $P/pmc_latest.json > $P/pmc_json.log 2>&1 || { tail -5 $P/pmc_json.log; exit 9; }
 python3 tools/timed_call_trace.py $(find $P/trace -name "*.db" | head -1) > $P/timed_call_trace.txt 2>&1 || { tail -5 $P/timed_call_trace.txt; exit 9; }
 cat $P/timed_call_trace.txt | head -12
+[ -n "$NO_SCALE" ] && exit 0
 timeout -k 10 400 python tools/scale_emulate.py --ns 1,2,4,8 --steps 20 --chunks 20 --kernels > $P/pt_scale.json 2> $P/pt_scale.err || { tail -5 $P/pt_scale.err; exit 4; }
 python -c "import json; d=json.load(open('$P/pt_scale.json')); print('PT', {n: (v['max_ms'], v['compute_eff']) for n, v in d['per_n'].items()})"
 timeout -k 10 500 python tools/scale_emulate.py --integrator bdpt --ns 1,2,4,8 --steps 16 --batch 8 > $P/bdpt_scale.json 2> $P/bdpt_scale.err || { tail -5 $P/bdpt_scale.err; exit 4; }
