@@ -530,26 +530,30 @@ def main():
 
     ctx.reset_stats()
     if world > 1:
-        acc_buf, acc_s, acc_w = mdist.packed_accumulators(W * H, "cuda")   # one buffer -> one reduce
         if args.end_collective == "gather" and dist.get_backend() not in ("nccl", "gloo"):
             args.end_collective = "reduce"   # decided from the backend, identically on every rank
+        if args.end_collective == "gather":   # packed own rows -> one gather (no full-frame copies)
+            band_send, band_recv = mdist.band_buffers(H, W, args.band_rows, world, "cuda")
+        else:
+            acc_buf, acc_s, acc_w = mdist.packed_accumulators(W * H, "cuda")   # one buffer -> one reduce
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     run(frame0, args.steps)
     if world > 1:   # one collective: each rank's own band rows gathered to rank 0 (north star)
-        fb.copy_device(1, acc_s.data_ptr())
-        fb.copy_device(3, acc_w.data_ptr())
-        ctx.sync()
         # no try/except here: a fallback taken by one rank while the others sit in the gather would
         # hang the job; an error exits this rank and torch.distributed.run stops the others
         if args.end_collective == "gather":
-            mdist.gather_bands(acc_s, acc_w, H, W, args.band_rows, dst=0)
+            # rows packed straight from the frame buffer, unpacked in place on rank 0 (+ image)
+            mdist.gather_bands_fb(ctx, fb, H, W, args.band_rows, band_send, band_recv, dst=0)
         else:
+            fb.copy_device(1, acc_s.data_ptr())
+            fb.copy_device(3, acc_w.data_ptr())
+            ctx.sync()
             mdist.reduce_packed(acc_buf, dst=0)
-        if rank == 0:
-            torch.cuda.synchronize()
-            fb.set_accumulation(acc_s.data_ptr(), acc_w.data_ptr())
+            if rank == 0:
+                torch.cuda.synchronize()
+                fb.set_accumulation(acc_s.data_ptr(), acc_w.data_ptr())
     ctx.sync()
     torch.cuda.synchronize()
     if world > 1:

@@ -263,6 +263,9 @@ MCRT_API const char* mcrt_last_error(mcrt_ctx ctx);   /* ctx may be NULL: last g
 MCRT_API mcrt_status mcrt_ctx_synchronize(mcrt_ctx ctx);
 /* stream: a hipStream_t (as void*) all work of this context is enqueued on; NULL = the context's own stream. */
 MCRT_API mcrt_status mcrt_ctx_set_stream(mcrt_ctx ctx, void* stream);
+/* The context stream (hipStream_t) that accumulation and the frame-buffer copies are enqueued on:
+ * a caller orders its own work (e.g. an RCCL collective) after them with it. */
+MCRT_API mcrt_status mcrt_ctx_get_stream(mcrt_ctx ctx, void** stream);
 /* Per-kernel HIP-event timing (replaces QueryManager GPU timers, source/engine/util/QueryManager.h:141-164). */
 MCRT_API mcrt_status mcrt_ctx_set_profiling(mcrt_ctx ctx, int enable);
 /* Synchronizes, then fills up to max entries: kernel name, summed HIP-event time (ms),
@@ -469,6 +472,19 @@ MCRT_API mcrt_status mcrt_framebuffer_copy_device(mcrt_framebuffer fb, int which
 /* Inverse for multi-GPU: overwrite the weighted sums (float4) and weights (float) from device
  * memory (after a reduce) and recompute the image = sum / weight on the device. */
 MCRT_API mcrt_status mcrt_framebuffer_set_accumulation(mcrt_framebuffer fb, const void* d_wsum, const void* d_wts);
+/* Tile split (mcrt_frame_params.num_bands > 1), end of job, without full-frame copies: pack this
+ * rank's own rows of the accumulators (its bands of the last render, local 8-row block tb at rows
+ * 8 tb .. 8 tb + 7) into d_dst, one row = W x float4 weighted sum then W x float weight (5 W
+ * floats), straight from the frame buffer.  Rows past the rank's last row are left untouched.
+ * Enqueued on the context stream after the last accumulate.  Replaces the all-reduce of the two
+ * accumulation buffers the reference would need (RTPathTracingPass.cpp:99-117 accumulates on one
+ * device) with the gather of mcrt.dist.gather_bands_fb. */
+MCRT_API mcrt_status mcrt_framebuffer_bands_pack(mcrt_framebuffer fb, void* d_dst);
+/* On the gathering rank: d_recv = num_bands chunks of max_rows packed rows (chunk r = rank r's
+ * mcrt_framebuffer_bands_pack output); every other rank's rows are written into this frame
+ * buffer's accumulators in place and the image = sum / weight is recomputed (the same division
+ * as mcrt_framebuffer_set_accumulation).  Enqueued on the context stream. */
+MCRT_API mcrt_status mcrt_framebuffer_bands_unpack(mcrt_framebuffer fb, const void* d_recv, int32_t max_rows);
 /* Per-frame path statistics of the last render (paths, closest rays, any rays, ...). */
 MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closest_rays, int64_t* any_rays,
                                             int64_t* shaded_paths);

@@ -405,6 +405,12 @@ MCRT_API mcrt_status mcrt_ctx_set_stream(mcrt_ctx ctx, void* stream) {
     return MCRT_OK;
 }
 
+MCRT_API mcrt_status mcrt_ctx_get_stream(mcrt_ctx ctx, void** stream) {
+    if (!ctx || !stream) return fail(ctx, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    *stream = (void*)ctx->stream;
+    return MCRT_OK;
+}
+
 MCRT_API mcrt_status mcrt_ctx_set_profiling(mcrt_ctx ctx, int enable) {
     if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
     ctx->profiling = enable != 0;
@@ -1749,6 +1755,34 @@ MCRT_API mcrt_status mcrt_framebuffer_set_accumulation(mcrt_framebuffer fb, cons
     HIPCHK(ctx, hipMemcpyAsync(fb->wsum, d_wsum, 16 * fb->N, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(fb->wts, d_wts, 4 * fb->N, hipMemcpyDeviceToDevice, ctx->stream));
     mcrt::launch_resolve(fb->W, fb->H, fb->wsum, fb->wts, fb->image, ctx->stream);
+    HIPCHK(ctx, hipGetLastError());
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_bands_pack(mcrt_framebuffer fb, void* d_dst) {
+    if (!fb || !d_dst) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    if (!fb->haveBands) return fail(fb->ctx, MCRT_ERROR_NOT_READY, "no frame rendered");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    mcrt::launch_band_pack(fb->bands, fb->wsum, fb->wts, static_cast<float*>(d_dst), ctx->stream);
+    HIPCHK(ctx, hipGetLastError());
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_bands_unpack(mcrt_framebuffer fb, const void* d_recv, int32_t max_rows) {
+    if (!fb || !d_recv) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    if (!fb->haveBands) return fail(fb->ctx, MCRT_ERROR_NOT_READY, "no frame rendered");
+    const FrameArgs& f = fb->bands;
+    // the largest rank's row count (whole 8-row blocks): every chunk of d_recv must hold it
+    const int blocks = (int)((f.H + 7) / 8), bpb = f.bandRows / 8;
+    const int perCycle = bpb * f.numBands;
+    const int maxBlocks = (blocks / perCycle) * bpb + std::min(blocks % perCycle, bpb);
+    if (max_rows < maxBlocks * 8)
+        return fail(fb->ctx, MCRT_ERROR_INVALID_ARG, "max_rows below the largest rank's row count");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    mcrt::launch_band_unpack(f, max_rows, static_cast<const float*>(d_recv), fb->wsum, fb->wts, fb->image,
+                             ctx->stream);
     HIPCHK(ctx, hipGetLastError());
     return MCRT_OK;
 }

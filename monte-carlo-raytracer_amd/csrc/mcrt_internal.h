@@ -115,6 +115,9 @@ void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, 
 void launch_accumulate(const FrameArgs& f, int frame, const BatchFilters& w, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st);
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st);
+void launch_band_pack(const FrameArgs& f, const float4* wsum, const float* wts, float* out, hipStream_t st);
+void launch_band_unpack(const FrameArgs& f, int maxRows, const float* recv, float4* wsum, float* wts, float4* image,
+                        hipStream_t st);
 void launch_denoise(int W, int H, int r, float ss, float sr, const float4* in, float4* out, hipStream_t st);
 void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStream_t st);
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st);

@@ -663,6 +663,59 @@ __global__ __launch_bounds__(256) void k_resolve(int n, const float4* __restrict
     image[i] = make_float4(cl_div(s.x, w), cl_div(s.y, w), cl_div(s.z, w), cl_div(s.w, w));
 }
 
+// Tile split, end of job: a rank's own rows of the accumulators in its band order (local 8-row
+// block tb at rows 8 tb .. 8 tb + 7, tilePixel's numbering; mcrt.dist.band_rows_of), one packed row
+// = W x (sum w*L as 4 floats) then W x sum w, straight from the frame buffer: no full-frame copy
+// before the gather.  bpb = band_rows / 8.
+__device__ __forceinline__ void bandOwner(int y, int bpb, int numBands, int& r, int& row) {
+    const int gb = y >> 3;
+    r = (gb / bpb) % numBands;
+    row = ((gb / (bpb * numBands)) * bpb + gb % bpb) * 8 + (y & 7);
+}
+
+__global__ __launch_bounds__(256) void k_band_pack(int W, int H, int bpb, int numBands, int band,
+                                                   const float4* __restrict__ wsum, const float* __restrict__ wts,
+                                                   float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= W * H) return;
+    const int y = i / W, x = i - y * W;
+    int r, row;
+    bandOwner(y, bpb, numBands, r, row);
+    if (r != band) return;
+    float* o = out + (size_t)row * 5 * W;
+    const float4 v = wsum[i];
+    o[4 * x] = v.x;
+    o[4 * x + 1] = v.y;
+    o[4 * x + 2] = v.z;
+    o[4 * x + 3] = v.w;
+    o[4 * W + x] = wts[i];
+}
+
+// Rank dst after the gather: every other rank's rows (recv = numBands x maxRows packed rows) into
+// the accumulators in place, then the image (k_resolve's division) in the same pass.
+__global__ __launch_bounds__(256) void k_band_unpack(int W, int H, int bpb, int numBands, int band, int maxRows,
+                                                     const float* __restrict__ recv, float4* __restrict__ wsum,
+                                                     float* __restrict__ wts, float4* __restrict__ image) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= W * H) return;
+    const int y = i / W, x = i - y * W;
+    int r, row;
+    bandOwner(y, bpb, numBands, r, row);
+    float4 s;
+    float w;
+    if (r == band) {
+        s = wsum[i];
+        w = wts[i];
+    } else {
+        const float* p = recv + ((size_t)r * maxRows + row) * 5 * W;
+        s = make_float4(p[4 * x], p[4 * x + 1], p[4 * x + 2], p[4 * x + 3]);
+        w = p[4 * W + x];
+        wsum[i] = s;
+        wts[i] = w;
+    }
+    image[i] = make_float4(cl_div(s.x, w), cl_div(s.y, w), cl_div(s.z, w), cl_div(s.w, w));
+}
+
 // ---------------------------------------------------------------------------
 // Post-process (the reference's RTDenoisePass + RTToneMappingPass after reconstruction)
 // ---------------------------------------------------------------------------
@@ -869,6 +922,17 @@ void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, h
 }
 
 
+void launch_band_pack(const FrameArgs& f, const float4* wsum, const float* wts, float* out, hipStream_t st) {
+    const int n = (int)(f.W * f.H);
+    hipLaunchKernelGGL(k_band_pack, dim3((n + 255) / 256), dim3(256), 0, st, (int)f.W, (int)f.H, f.bandRows >> 3,
+                       f.numBands, f.bandIndex, wsum, wts, out);
+}
+void launch_band_unpack(const FrameArgs& f, int maxRows, const float* recv, float4* wsum, float* wts, float4* image,
+                        hipStream_t st) {
+    const int n = (int)(f.W * f.H);
+    hipLaunchKernelGGL(k_band_unpack, dim3((n + 255) / 256), dim3(256), 0, st, (int)f.W, (int)f.H, f.bandRows >> 3,
+                       f.numBands, f.bandIndex, maxRows, recv, wsum, wts, image);
+}
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st) {
     const int n = (int)(W * H);
     hipLaunchKernelGGL(k_resolve, dim3((n + 255) / 256), dim3(256), 0, st, n, wsum, wts, image);

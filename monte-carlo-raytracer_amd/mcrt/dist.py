@@ -182,6 +182,48 @@ def gather_bands(wsum, wts, height, width, band_rows, dst=0, group=None):
             wts.copy_(w.reshape(-1))
 
 
+def band_buffers(height, width, band_rows, world, device):
+    """(send, recv) for gather_bands_fb: one rank's packed rows (largest share) and world of them."""
+    import torch
+    maxr = splat_chunk_rows(height, band_rows, world)
+    return (torch.empty(maxr * 5 * width, dtype=torch.float32, device=device),
+            torch.empty(world * maxr * 5 * width, dtype=torch.float32, device=device))
+
+
+def gather_bands_fb(ctx, fb, height, width, band_rows, send, recv, dst=0, group=None):
+    """gather_bands without the full-frame copies: the rank's own rows are packed straight from
+    its frame buffer (mcrt_framebuffer_bands_pack, on the context stream after the last
+    accumulate: ONE kernel instead of two full-frame copies plus row gathers), ONE gather brings
+    every rank's rows to `dst`, and dst writes the others' rows into its accumulators in place and
+    recomputes the image (mcrt_framebuffer_bands_unpack: one kernel instead of a scatter per rank
+    and a copy back).  The collective runs on torch's current stream between two host
+    synchronisations, as gather_bands.  send / recv: band_buffers (recv is only used on dst).
+    Same bits as gather_bands and as one GPU rendering the whole image."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    maxr = splat_chunk_rows(height, band_rows, world)
+    n = maxr * 5 * width
+    if send.numel() < n or (rank == dst and recv.numel() < world * n):
+        raise ValueError("band buffers smaller than the band layout (mcrt.dist.band_buffers)")
+    send = send[:n]
+    fb.bands_pack(send.data_ptr())
+    ctx.sync()
+    if send.is_cuda and dist.get_backend(group) == "gloo":   # gloo rehearsal: through the host
+        h = send.cpu()
+        parts = [torch.empty_like(h) for _ in range(world)] if rank == dst else None
+        dist.gather(h, parts, dst=dst, group=group)
+        if rank == dst:
+            recv[:world * n].copy_(torch.cat(parts))
+    else:
+        dist.gather(send, list(recv[:world * n].view(world, n).unbind(0)) if rank == dst else None,
+                    dst=dst, group=group)
+    if rank == dst:
+        if recv.is_cuda:
+            torch.cuda.synchronize(recv.device)
+        fb.bands_unpack(recv.data_ptr(), maxr)
+
+
 def reduce_accumulators(wsum, wts, dst=0, group=None):
     """Sum separate per-rank accumulator tensors into rank `dst` (two collectives; the bench
     packs both into one buffer with packed_accumulators and calls reduce_packed once)."""

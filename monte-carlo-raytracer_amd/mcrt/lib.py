@@ -33,6 +33,7 @@ SIGNATURES = {
     "mcrt_ctx_kernel_stats": (_c.c_int, [_vp, _c.c_int, _vp, _vp, _vp, _vp, _c.POINTER(_c.c_int)]),
     "mcrt_ctx_reset_stats": (_c.c_int, [_vp]),
     "mcrt_ctx_stream_copy": (_c.c_int, [_vp, _c.c_uint64, _c.c_int, _c.POINTER(_c.c_double)]),
+    "mcrt_ctx_get_stream": (_c.c_int, [_vp, _c.POINTER(_vp)]),
     "mcrt_ctx_gather_chase": (_c.c_int, [_vp, _c.c_uint64, _c.c_int, _c.c_int, _c.POINTER(_c.c_double)]),
     "mcrt_scene_create": (_c.c_int, [_vp, _vp, _c.POINTER(_vp)]),
     "mcrt_scene_destroy": (_c.c_int, [_vp]),
@@ -74,6 +75,8 @@ SIGNATURES = {
     "mcrt_framebuffer_stats": (_c.c_int, [_vp, _vp, _vp, _vp]),
     "mcrt_framebuffer_copy_device": (_c.c_int, [_vp, _c.c_int, _vp]),
     "mcrt_framebuffer_set_accumulation": (_c.c_int, [_vp, _vp, _vp]),
+    "mcrt_framebuffer_bands_pack": (_c.c_int, [_vp, _vp]),
+    "mcrt_framebuffer_bands_unpack": (_c.c_int, [_vp, _vp, _c.c_int32]),
     "mcrt_framebuffer_read_queue": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int32)]),
     "mcrt_framebuffer_queue_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.POINTER(_c.c_int32), _c.c_int]),
     "mcrt_postprocess": (_c.c_int, [_vp, _c.POINTER(T.PostprocessParams)]),
@@ -158,6 +161,12 @@ class Context:
 
     def set_stream(self, stream_ptr):
         _check(lib().mcrt_ctx_set_stream(self.h, stream_ptr), self.h)
+
+    def stream(self):
+        """hipStream_t (int) of the context stream (mcrt_ctx_get_stream)."""
+        st = _vp()
+        _check(lib().mcrt_ctx_get_stream(self.h, _c.byref(st)), self.h)
+        return st.value or 0
 
     def set_profiling(self, on=True):
         _check(lib().mcrt_ctx_set_profiling(self.h, 1 if on else 0), self.h)
@@ -406,6 +415,14 @@ class FrameBuffer:
 
     def set_accumulation(self, wsum_ptr, wts_ptr):
         _check(lib().mcrt_framebuffer_set_accumulation(self.h, wsum_ptr, wts_ptr), self.ctx.h)
+
+    def bands_pack(self, dst_ptr):
+        """mcrt_framebuffer_bands_pack: this rank's rows of the accumulators, packed (5 W floats a row)."""
+        _check(lib().mcrt_framebuffer_bands_pack(self.h, dst_ptr), self.ctx.h)
+
+    def bands_unpack(self, recv_ptr, max_rows):
+        """mcrt_framebuffer_bands_unpack: the other ranks' packed rows into the accumulators + image."""
+        _check(lib().mcrt_framebuffer_bands_unpack(self.h, recv_ptr, max_rows), self.ctx.h)
 
     def stats(self):
         a, b, c = _c.c_int64(), _c.c_int64(), _c.c_int64()

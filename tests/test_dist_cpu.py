@@ -110,6 +110,79 @@ def test_band_gather_equals_reduce(tmp_path, world, height, band_rows):
     assert np.array_equal(z["gs"], z["fs"]) and np.array_equal(z["gw"], z["fw"])
 
 
+class _FakeBandsFB:
+    """Host model of mcrt_framebuffer_bands_pack / _unpack (the kernels' row layout: a rank's
+    local 8-row block tb at rows 8 tb .. 8 tb + 7, i.e. band_rows_of order; 5 W floats a row)
+    over torch CPU tensors, so gather_bands_fb's orchestration runs under gloo without a GPU.
+    The kernels themselves are checked against a whole-image render in
+    tests/test_gpu_render.py::test_band_pack_unpack_through_product."""
+
+    def __init__(self, s, w, height, width, band_rows, world, rank):
+        self.s, self.w = s, w   # (H, W, 4), (H, W) float32 numpy, zero outside the rank's rows
+        self.H, self.W, self.br, self.world, self.rank = height, width, band_rows, world, rank
+
+    def _rows(self, r):
+        return mdist.band_rows_of(self.H, self.br, self.world, r)
+
+    def bands_pack(self, ptr):
+        rows = self._rows(self.rank)
+        dst = _BUFS[ptr]
+        v = dst[:len(rows) * 5 * self.W].view(len(rows), 5 * self.W)
+        v[:, :4 * self.W] = torch.from_numpy(self.s[rows].reshape(len(rows), -1))
+        v[:, 4 * self.W:] = torch.from_numpy(self.w[rows])
+
+    def bands_unpack(self, ptr, maxr):
+        src = _BUFS[ptr].view(self.world, maxr, 5 * self.W)
+        for r in range(self.world):
+            if r == self.rank:
+                continue
+            rows = self._rows(r)
+            self.s[rows] = src[r, :len(rows), :4 * self.W].numpy().reshape(len(rows), self.W, 4)
+            self.w[rows] = src[r, :len(rows), 4 * self.W:].numpy()
+
+
+_BUFS = {}
+
+
+class _NoCtx:
+    def sync(self):
+        pass
+
+
+def _gather_fb_worker(rank, world, port, out_path, height, width, band_rows):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(11)
+    full_s = rng.random((height, width, 4), dtype=np.float32) * 3.0
+    full_w = rng.random((height, width), dtype=np.float32) + 0.5
+    rows = mdist.band_rows_of(height, band_rows, world, rank)
+    s = np.zeros_like(full_s)
+    w = np.zeros_like(full_w)
+    s[rows], w[rows] = full_s[rows], full_w[rows]
+    fb = _FakeBandsFB(s, w, height, width, band_rows, world, rank)
+    send, recv = mdist.band_buffers(height, width, band_rows, world, "cpu")
+    send.fill_(float("nan"))   # rows past the rank's last row are never read
+    _BUFS[send.data_ptr()], _BUFS[recv.data_ptr()] = send, recv
+    mdist.gather_bands_fb(_NoCtx(), fb, height, width, band_rows, send, recv, dst=0)
+    if rank == 0:
+        np.savez(out_path, s=fb.s, w=fb.w, fs=full_s, fw=full_w)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,height,band_rows", [(2, 36, 8), (3, 1080 // 8, 16), (4, 43, 8)])
+def test_band_gather_fb_whole_image(tmp_path, world, height, band_rows):
+    """bench.py's end-of-job path (gather_bands_fb): packed own rows, ONE gather, unpack on rank
+    0 -> rank 0 holds the whole image's accumulators bit for bit."""
+    out = str(tmp_path / "gfb.npz")
+    mp.start_processes(_gather_fb_worker, args=(world, _free_port(), out, height, 24, band_rows), nprocs=world,
+                       join=True, start_method="spawn")
+    z = np.load(out)
+    assert np.array_equal(z["s"].view(np.uint32), z["fs"].view(np.uint32))
+    assert np.array_equal(z["w"].view(np.uint32), z["fw"].view(np.uint32))
+
+
 def test_two_rank_reduce_matches_single_process(tmp_path):
     out = str(tmp_path / "reduced.npz")
     mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")

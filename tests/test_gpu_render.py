@@ -288,6 +288,61 @@ def test_batched_no_lights_after_lit_batch(hip_ctx, mixed):
     ds.close()
 
 
+@pytest.mark.parametrize("ranks,W,H", [(2, 96, 80), (3, 96, 84), (8, 64, 140)])
+def test_band_pack_unpack_through_product(hip_ctx, mixed, ranks, W, H):
+    """bench.py's end of job (mcrt.dist.gather_bands_fb), every rank emulated by its own frame
+    buffer on this GPU: each renders and accumulates its 8-row bands, packs its own rows straight
+    from the frame buffer (mcrt_framebuffer_bands_pack) into its chunk of the gather buffer, and
+    rank 0 unpacks the other chunks into its accumulators (mcrt_framebuffer_bands_unpack, image
+    recomputed).  Accumulators and image must equal one frame buffer rendering the whole image,
+    bit for bit (H = 84, 140: a partial last 8-row block)."""
+    import torch
+    from mcrt import dist as mdist
+    from mcrt import lib
+    sc, _ = mixed
+    D, frames, batch = 2, 4, 2
+    cams = [scene_camera("mixed", W, H, frame=f, jitter=True) for f in range(frames)]
+    filt = T.make_filter(T.BOX)
+    ds = lib.DeviceScene(hip_ctx, sc)
+    full = lib.FrameBuffer(hip_ctx, W, H)
+    for f0 in range(0, frames, batch):
+        full.render_frames(ds, cams[f0:f0 + batch], frame=f0, max_depth=D)
+        full.accumulate(filt, f0)
+    wsum = torch.empty(W * H * 4, dtype=torch.float32, device="cuda")
+    wts = torch.empty(W * H, dtype=torch.float32, device="cuda")
+    full.copy_device(1, wsum.data_ptr())
+    full.copy_device(3, wts.data_ptr())
+    hip_ctx.sync()
+    want = (full.read(1), full.read(2), wts.cpu().numpy())
+    send, recv = mdist.band_buffers(H, W, 8, ranks, "cuda")
+    maxr = mdist.splat_chunk_rows(H, 8, ranks)
+    n = maxr * 5 * W
+    recv.fill_(float("nan"))   # rows a chunk does not hold are never read
+    fbs = []
+    for r in range(ranks):
+        fb = lib.FrameBuffer(hip_ctx, W, H)
+        for f0 in range(0, frames, batch):
+            fb.render_frames(ds, cams[f0:f0 + batch], frame=f0, max_depth=D, band_rows=8, num_bands=ranks,
+                             band_index=r)
+            fb.accumulate(filt, f0)
+        fb.bands_pack(recv[r * n:].data_ptr())   # rank r's chunk of the gather
+        hip_ctx.sync()
+        fbs.append(fb)
+    with pytest.raises(RuntimeError):
+        fbs[0].bands_unpack(recv.data_ptr(), maxr - 8)   # chunk too small for the largest share
+    fbs[0].bands_unpack(recv.data_ptr(), maxr)
+    fbs[0].copy_device(3, wts.data_ptr())
+    hip_ctx.sync()
+    np.testing.assert_array_equal(fbs[0].read(1).view(np.uint32), want[0].view(np.uint32))
+    np.testing.assert_array_equal(fbs[0].read(2).view(np.uint32), want[1].view(np.uint32))
+    np.testing.assert_array_equal(wts.cpu().numpy().view(np.uint32), want[2].view(np.uint32))
+    assert want[1][..., :3].max() > 0
+    for fb in fbs:
+        fb.close()
+    full.close()
+    ds.close()
+
+
 @pytest.mark.parametrize("ranks", [2, 3])
 def test_multi_gpu_reduce_through_product(hip_ctx, mixed, ranks):
     """The multi-GPU path of bench.py, every rank emulated by its own frame buffer on this GPU:
