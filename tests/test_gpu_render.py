@@ -288,8 +288,9 @@ def test_batched_no_lights_after_lit_batch(hip_ctx, mixed):
     ds.close()
 
 
-@pytest.mark.parametrize("ranks,W,H", [(2, 96, 80), (3, 96, 84), (8, 64, 140)])
-def test_band_pack_unpack_through_product(hip_ctx, mixed, ranks, W, H):
+@pytest.mark.parametrize("ranks,W,H,BR", [(1, 64, 40, 8), (2, 96, 80, 8), (3, 96, 84, 8), (3, 96, 84, 16),
+                                         (8, 64, 140, 8)])
+def test_band_pack_unpack_through_product(hip_ctx, mixed, ranks, W, H, BR):
     """bench.py's end of job (mcrt.dist.gather_bands_fb), every rank emulated by its own frame
     buffer on this GPU: each renders and accumulates its 8-row bands, packs its own rows straight
     from the frame buffer (mcrt_framebuffer_bands_pack) into its chunk of the gather buffer, and
@@ -314,22 +315,26 @@ def test_band_pack_unpack_through_product(hip_ctx, mixed, ranks, W, H):
     full.copy_device(3, wts.data_ptr())
     hip_ctx.sync()
     want = (full.read(1), full.read(2), wts.cpu().numpy())
-    send, recv = mdist.band_buffers(H, W, 8, ranks, "cuda")
-    maxr = mdist.splat_chunk_rows(H, 8, ranks)
+    send, recv = mdist.band_buffers(H, W, BR, ranks, "cuda")
+    maxr = mdist.splat_chunk_rows(H, BR, ranks)
     n = maxr * 5 * W
     recv.fill_(float("nan"))   # rows a chunk does not hold are never read
     fbs = []
     for r in range(ranks):
         fb = lib.FrameBuffer(hip_ctx, W, H)
+        if r == 0:
+            with pytest.raises(RuntimeError):   # nothing rendered yet
+                fb.bands_pack(send.data_ptr())
         for f0 in range(0, frames, batch):
-            fb.render_frames(ds, cams[f0:f0 + batch], frame=f0, max_depth=D, band_rows=8, num_bands=ranks,
+            fb.render_frames(ds, cams[f0:f0 + batch], frame=f0, max_depth=D, band_rows=BR, num_bands=ranks,
                              band_index=r)
             fb.accumulate(filt, f0)
         fb.bands_pack(recv[r * n:].data_ptr())   # rank r's chunk of the gather
         hip_ctx.sync()
         fbs.append(fb)
-    with pytest.raises(RuntimeError):
-        fbs[0].bands_unpack(recv.data_ptr(), maxr - 8)   # chunk too small for the largest share
+    if ranks > 1:
+        with pytest.raises(RuntimeError):
+            fbs[0].bands_unpack(recv.data_ptr(), maxr - 8)   # chunk too small for the largest share
     fbs[0].bands_unpack(recv.data_ptr(), maxr)
     fbs[0].copy_device(3, wts.data_ptr())
     hip_ctx.sync()
