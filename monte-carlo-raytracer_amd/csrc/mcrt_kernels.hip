@@ -19,8 +19,15 @@
 #include "mcrt_traverse.h"
 #include "mcrt_shading.h"
 
-// Shading workgroup size (threads; one queue atomic per workgroup and queue).
-#define SHADE_BLOCK 256
+// Shading workgroup sizes (threads; one queue atomic per workgroup and queue).  The extension rays
+// a workgroup appends are grouped by direction octant inside its queue slice, so a larger first-
+// shading workgroup hands the incoherent launch longer single-octant runs.
+#ifndef SHADE0_BLOCK
+#define SHADE0_BLOCK 512
+#endif
+#ifndef SHADEN_BLOCK
+#define SHADEN_BLOCK 256
+#endif
 
 // ---------------------------------------------------------------------------
 // RadeonRays-compatible queries on AoS rays (mcrt_trace_closest / mcrt_trace_any).
@@ -451,13 +458,13 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
 
 // Bounce 0: every pixel of the band (tile order); writes radiance[pix] (= `=` of ShadowPass).
 template <bool LOD>
-__global__ __launch_bounds__(SHADE_BLOCK) void k_shade0(SceneArgs s, FrameArgs f, const mcrt_camera* __restrict__ camp,
+__global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 const float4* __restrict__ hits, float4* __restrict__ radiance,
                                                 QueueArgs q) {
     const int lane = threadIdx.x & 63;
     // XCD-aware block order: an XCD shades contiguous runs of tiles (their hits share surface
     // records, materials and textures in its L2): k_shade0 -4 %
-    const int tileAll = xcdRemap(blockIdx.x, gridDim.x) * (SHADE_BLOCK / 64) + (int)(threadIdx.x >> 6);
+    const int tileAll = xcdRemap(blockIdx.x, gridDim.x) * (SHADE0_BLOCK / 64) + (int)(threadIdx.x >> 6);
     int k, tile, pi = lane;   // batch frame k
     if (f.shadePack && f.batch > 1) {
         // as k_primary's packed waves; the bounce-0 shadow rays of a wave (one light direction,
@@ -468,8 +475,8 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade0(SceneArgs s, FrameArgs f
     }
     int x = 0, y = 0;
     bool valid = k < f.batch && tile < f.numTiles && tilePixel(f, tile, pi, x, y);
-    __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
-    __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];
+    __shared__ int ldsWave[SHADE0_BLOCK / 64 + 1];
+    __shared__ int ldsGroup[(SHADE0_BLOCK / 64) * 8 + 1];
     ShadeOut o;
     o.pushS = o.pushE = false;
     o.eD = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -482,26 +489,26 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade0(SceneArgs s, FrameArgs f
         const f3 add = shadePath<LOD>(s, f, 0, pix, hits[pix], dir, splat3(1.0f), 0, o, ld3(cam.pos), dx, dy);
         radiance[pix] = make_float4(add.x, add.y, add.z, 0.0f);
     }
-    const int ss = blockAppend<SHADE_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
+    const int ss = blockAppend<SHADE0_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
     // extension rays grouped by direction octant inside the block's queue slice
     const int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
-    const int es = blockAppendGrouped<SHADE_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
+    const int es = blockAppendGrouped<SHADE0_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 
 // Bounce >= 1: the compacted extension queue of the previous bounce.
-__global__ __launch_bounds__(SHADE_BLOCK) void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
+__global__ __launch_bounds__(SHADEN_BLOCK) void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
                                                 const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                 const float4* __restrict__ qT, const float4* __restrict__ hits,
                                                 float4* __restrict__ radiance, QueueArgs q) {
     const int n = *countIn;
-    __shared__ int ldsWave[SHADE_BLOCK / 64 + 1];
-    __shared__ int ldsGroup[(SHADE_BLOCK / 64) * 8 + 1];
-    if ((int)blockIdx.x * SHADE_BLOCK >= n) return;   // whole block past the queue: uniform exit
+    __shared__ int ldsWave[SHADEN_BLOCK / 64 + 1];
+    __shared__ int ldsGroup[(SHADEN_BLOCK / 64) * 8 + 1];
+    if ((int)blockIdx.x * SHADEN_BLOCK >= n) return;   // whole block past the queue: uniform exit
     // XCD-aware block order (xcdRemap): each XCD shades contiguous runs of the queue, whose paths
     // share triangles, materials and textures in that XCD's L2
-    const int i = xcdRemap(blockIdx.x, (n + SHADE_BLOCK - 1) / SHADE_BLOCK) * SHADE_BLOCK + threadIdx.x;
+    const int i = xcdRemap(blockIdx.x, (n + SHADEN_BLOCK - 1) / SHADEN_BLOCK) * SHADEN_BLOCK + threadIdx.x;
     ShadeOut o;
     o.pushS = o.pushE = false;
     o.eD = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -515,11 +522,11 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shadeN(SceneArgs s, FrameArgs f
             radiance[pix] = r;
         }
     }
-    const int ss = blockAppend<SHADE_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
+    const int ss = blockAppend<SHADEN_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
     // extension rays grouped by direction octant inside the block's queue slice
     const int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
-    const int es = blockAppendGrouped<SHADE_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
+    const int es = blockAppendGrouped<SHADEN_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 
@@ -878,15 +885,15 @@ void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* 
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {
-    const int blocks = (f.numTiles * f.batch * 64 + SHADE_BLOCK - 1) / SHADE_BLOCK;
-    hipLaunchKernelGGL(f.textureLod ? k_shade0<true> : k_shade0<false>, dim3(blocks), dim3(SHADE_BLOCK), 0, st, s, f,
+    const int blocks = (f.numTiles * f.batch * 64 + SHADE0_BLOCK - 1) / SHADE0_BLOCK;
+    hipLaunchKernelGGL(f.textureLod ? k_shade0<true> : k_shade0<false>, dim3(blocks), dim3(SHADE0_BLOCK), 0, st, s, f,
                        cam, hits, radiance, q);
 }
 void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,
                    const float4* qD, const float4* qT, const float4* hits, float4* radiance, const QueueArgs& q,
                    int maxCount, hipStream_t st) {
-    const int blocks = (maxCount + SHADE_BLOCK - 1) / SHADE_BLOCK;
-    hipLaunchKernelGGL(k_shadeN, dim3(blocks > 0 ? blocks : 1), dim3(SHADE_BLOCK), 0, st, s, f, bounce, countIn, qO, qD,
+    const int blocks = (maxCount + SHADEN_BLOCK - 1) / SHADEN_BLOCK;
+    hipLaunchKernelGGL(k_shadeN, dim3(blocks > 0 ? blocks : 1), dim3(SHADEN_BLOCK), 0, st, s, f, bounce, countIn, qO, qD,
                        qT, hits, radiance, q);
 }
 void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits, int which,
