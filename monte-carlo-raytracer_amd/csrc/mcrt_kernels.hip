@@ -28,6 +28,10 @@
 #ifndef SHADEN_BLOCK
 #define SHADEN_BLOCK 256
 #endif
+// direction groups of the first shading's extension rays (8 = octants; 24 = octant x dominant axis)
+#ifndef MCRT_EXT_GROUPS
+#define MCRT_EXT_GROUPS 24
+#endif
 
 // ---------------------------------------------------------------------------
 // RadeonRays-compatible queries on AoS rays (mcrt_trace_closest / mcrt_trace_any).
@@ -476,7 +480,7 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
     int x = 0, y = 0;
     bool valid = k < f.batch && tile < f.numTiles && tilePixel(f, tile, pi, x, y);
     __shared__ int ldsWave[SHADE0_BLOCK / 64 + 1];
-    __shared__ int ldsGroup[(SHADE0_BLOCK / 64) * 8 + 1];
+    __shared__ int ldsGroup[(SHADE0_BLOCK / 64) * MCRT_EXT_GROUPS + 1];
     ShadeOut o;
     o.pushS = o.pushE = false;
     o.eD = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -492,8 +496,14 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
     const int ss = blockAppend<SHADE0_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
     // extension rays grouped by direction octant inside the block's queue slice
-    const int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
-    const int es = blockAppendGrouped<SHADE0_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
+    int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
+#if MCRT_EXT_GROUPS == 24   // octant x dominant axis
+    {
+        const float ax = fabsf(o.eD.x), ay = fabsf(o.eD.y), az = fabsf(o.eD.z);
+        oct = oct * 3 + (ax >= ay && ax >= az ? 0 : ay >= az ? 1 : 2);
+    }
+#endif
+    const int es = blockAppendGrouped<SHADE0_BLOCK / 64, MCRT_EXT_GROUPS>(q.extCountOut, o.pushE, oct, ldsGroup);
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 
