@@ -32,6 +32,9 @@
 #ifndef MCRT_EXT_GROUPS
 #define MCRT_EXT_GROUPS 24
 #endif
+#ifndef MCRT_EXT_LDS_APPEND   // 1: one LDS atomic per record instead of a ballot per group and wave
+#define MCRT_EXT_LDS_APPEND 1
+#endif
 
 // ---------------------------------------------------------------------------
 // RadeonRays-compatible queries on AoS rays (mcrt_trace_closest / mcrt_trace_any).
@@ -503,7 +506,11 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
         oct = oct * 3 + (ax >= ay && ax >= az ? 0 : ay >= az ? 1 : 2);
     }
 #endif
+#if MCRT_EXT_LDS_APPEND
+    const int es = blockAppendGroupedLds<MCRT_EXT_GROUPS>(q.extCountOut, o.pushE, oct, ldsGroup);
+#else
     const int es = blockAppendGrouped<SHADE0_BLOCK / 64, MCRT_EXT_GROUPS>(q.extCountOut, o.pushE, oct, ldsGroup);
+#endif
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 

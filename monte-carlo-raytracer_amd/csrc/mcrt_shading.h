@@ -242,6 +242,31 @@ MCRT_DEV int blockAppendGrouped(int* counter, bool pred, int group, int* lds) {
     return slot;
 }
 
+// The same grouping with one LDS atomic per record instead of G ballots per wave (for many
+// groups): records of a group are contiguous in the block's slice, their order inside the group
+// is the LDS atomics' order (queue order never changes a result: every record carries its path).
+// Every thread of the block must call.  lds: G + 1 ints.
+template <int G>
+MCRT_DEV int blockAppendGroupedLds(int* counter, bool pred, int group, int* lds) {
+    for (int g = threadIdx.x; g < G; g += blockDim.x) lds[g] = 0;
+    __syncthreads();
+    const int local = pred ? atomicAdd(&lds[group], 1) : 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int sum = 0;
+        for (int g = 0; g < G; ++g) {
+            const int c = lds[g];
+            lds[g] = sum;
+            sum += c;
+        }
+        lds[G] = sum ? atomicAdd(counter, sum) : 0;
+    }
+    __syncthreads();
+    const int slot = lds[G] + (pred ? lds[group] : 0) + local;
+    __syncthreads();
+    return slot;
+}
+
 // May be called under divergent control flow: only active lanes take part.
 MCRT_DEV int waveAppend(int* counter, bool pred) {
     const unsigned long long m = __ballot(pred);
