@@ -220,9 +220,9 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     first = [True]
     band = split == "band" and world > 1
     if band:   # rank-major splats (chunks of this rank count x 8-row blocks x batch frames) + own chunk
-        cr = mdist.splat_chunk_rows(H, 8, world)
-        splat_full = torch.zeros(4 * W * cr * batch * world, dtype=torch.float32, device="cuda")
-        splat_own = torch.zeros(4 * W * cr * batch, dtype=torch.float32, device="cuda")
+        cr = mdist.splat_chunk_rows(H, 8, world)   # uninitialised: mcrt_bdpt_splats_copy zeroes on its stream
+        splat_full = torch.empty(4 * W * cr * batch * world, dtype=torch.float32, device="cuda")
+        splat_own = torch.empty(4 * W * cr * batch, dtype=torch.float32, device="cuda")
 
     last = [1]   # frames of the last call (fb.stats() counts that call's queues)
 
@@ -354,6 +354,22 @@ def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s):
     return out
 
 
+def launch_ranks(n):
+    """Runs this script under `python -m torch.distributed.run --nproc-per-node n` (one process
+    per GPU, rendezvous on 127.0.0.1 at a free port) as a child process with the same arguments,
+    and returns its exit status.  Called before torch is imported: this process never initialises
+    a GPU, and it waits for the child instead of replacing itself."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -409,12 +425,30 @@ def main():
                          "0 = auto (32 up to 1080p, 16 above)")
     args = ap.parse_args()
 
+    # --gpus N is the job's world size.  A plain `python bench.py --gpus N` (no launcher) starts
+    # torch.distributed.run with N ranks as a CHILD process -- before torch is imported or any GPU
+    # is touched here -- and exits with its status; rank 0 of the child prints the JSON line on
+    # the inherited stdout.  Under a launcher, WORLD_SIZE must equal --gpus.  (The reference is
+    # single-device: PlatformManager.cpp:59-79 picks one OpenCL device.)
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={env_world} from the launcher but --gpus {args.gpus}; they must agree")
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.dist_backend == "nccl" and torch.cuda.device_count() < world:
+        # RCCL needs one GPU per rank (it refuses two ranks on one device); --dist-backend gloo
+        # rehearses N ranks on one GPU
+        sys.exit(f"bench.py: {world} ranks over nccl need {world} GPUs, {torch.cuda.device_count()} visible "
+                 f"(use --dist-backend gloo to rehearse on one GPU)")
     if world > 1:
         if args.dist_backend == "gloo":   # rehearsal: every rank on cuda:0 of a 1-GPU box
             local = local % max(torch.cuda.device_count(), 1)
@@ -467,9 +501,9 @@ def main():
     band_bdpt = bdpt and args.bdpt_split == "band" and world > 1
     if band_bdpt:   # band split: every rank renders every frame's rows of its bands
         band = dict(band_rows=8, num_bands=world, band_index=rank, integrator=T.INTEGRATOR_BDPT)
-        cr = mdist.splat_chunk_rows(H, 8, world)
-        splat_full = torch.zeros(4 * W * cr * args.bdpt_batch * world, dtype=torch.float32, device="cuda")
-        splat_own = torch.zeros(4 * W * cr * args.bdpt_batch, dtype=torch.float32, device="cuda")
+        cr = mdist.splat_chunk_rows(H, 8, world)   # uninitialised: mcrt_bdpt_splats_copy zeroes on its stream
+        splat_full = torch.empty(4 * W * cr * args.bdpt_batch * world, dtype=torch.float32, device="cuda")
+        splat_own = torch.empty(4 * W * cr * args.bdpt_batch, dtype=torch.float32, device="cuda")
     elif bdpt:   # frame split: whole frames per rank
         band = dict(band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_BDPT)
     else:

@@ -485,6 +485,12 @@ MCRT_API mcrt_status mcrt_framebuffer_bands_pack(mcrt_framebuffer fb, void* d_ds
  * buffer's accumulators in place and the image = sum / weight is recomputed (the same division
  * as mcrt_framebuffer_set_accumulation).  Enqueued on the context stream. */
 MCRT_API mcrt_status mcrt_framebuffer_bands_unpack(mcrt_framebuffer fb, const void* d_recv, int32_t max_rows);
+/* Band geometry of the last render, for a C++ host sizing the gather of the packed rows:
+ * max_rows = the largest rank's row count (whole 8-row blocks; one packed chunk = max_rows x 5 W
+ * floats, the max_rows argument of mcrt_framebuffer_bands_unpack), and the num_bands / band_index
+ * the frame was rendered with.  Any output pointer may be NULL. */
+MCRT_API mcrt_status mcrt_framebuffer_band_layout(mcrt_framebuffer fb, int32_t* max_rows, int32_t* num_bands,
+                                                  int32_t* band_index);
 /* Per-frame path statistics of the last render (paths, closest rays, any rays, ...). */
 MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closest_rays, int64_t* any_rays,
                                             int64_t* shaded_paths);
@@ -496,7 +502,11 @@ MCRT_API mcrt_status mcrt_framebuffer_queue_counts(mcrt_framebuffer fb, int32_t*
  *   which 0: shadow queue of the last bounce    -- origin.xyz|tmax, dir.xyz|pixel(int bits), throughput*L
  *   which 1: last extension queue (bounce D-2)  -- origin.xyz|pixel(int bits), dir.xyz|bsdf flags, throughput
  * Writes min(count, max_records) records as three float4 arrays back to back
- * (dst = [a0..a(n-1) | b0.. | c0..], 48 * max_records bytes) and the full count. */
+ * (dst = [a0..a(n-1) | b0.. | c0..], 48 * max_records bytes) and the full count.
+ * The ORDER of the records is not deterministic: the shading kernels append them per workgroup
+ * through LDS atomics (grouped by octant x dominant axis), so two runs hold the same set of
+ * records in different orders.  Every record carries its pixel, and the radiance does not depend
+ * on the order; compare queues as sets (e.g. sorted by pixel). */
 MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which, void* host_dst,
                                                  int64_t max_records, int32_t* count);
 /* Host copy of the BDPT state of the last BDPT frame (the reference keeps it in RTBDPTPass's

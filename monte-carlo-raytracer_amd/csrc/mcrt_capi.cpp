@@ -1099,14 +1099,14 @@ static hipError_t slot_alloc(FrameSlot& k, size_t N, int frames = 1, size_t Q = 
     A(&k.counters, SLOT_COUNTER_BYTES);
     k.frames = frames;
     k.queueCap = Q;
-    if (e == hipSuccess) e = hipMemset(k.radiance, 0, 16 * N * frames);
-    if (e == hipSuccess) e = hipMemset(k.counters, 0, SLOT_COUNTER_BYTES);
-    // hipMemset runs on the null stream, which the non-blocking slot streams do not wait for: finish
-    // it before any slot launch can touch these buffers
-    if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&k.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&k.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&k.free, hipEventDisableTiming);
+    // zero-fills on the slot's own stream, ahead of its first launch; `done` covers them for
+    // readers on other streams (ctx_wait_slots) before the slot's first frame records it
+    if (e == hipSuccess) e = hipMemsetAsync(k.radiance, 0, 16 * N * frames, k.stream);
+    if (e == hipSuccess) e = hipMemsetAsync(k.counters, 0, SLOT_COUNTER_BYTES, k.stream);
+    if (e == hipSuccess) e = hipEventRecord(k.done, k.stream);
     if (e != hipSuccess) slot_free(k);
     return e;
 }
@@ -1145,7 +1145,7 @@ static void ctx_wait_slots(mcrt_framebuffer fb) {
 
 // NQ = the pixels of the whole 8x8 tiles covering the image (>= N): the start queues hold one slot
 // per lane of the tile walk.  Ray queues and hits hold 2 x NQ (the depth-1 camera and light halves).
-static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D, int frames) {
+static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D, int frames, hipStream_t st) {
     const size_t C = (size_t)bdpt_max_connections(D);
     N *= frames;    // every per-frame array holds the batch's frames
     NQ *= frames;
@@ -1165,12 +1165,12 @@ static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D, int frames)
     A(&b.cO, 16 * N * C);
     A(&b.cD, 16 * N * C);
     A(&b.cL, 16 * N * C);
-    if (e == hipSuccess) e = hipMemset(b.splat, 0, 16 * N);
-    if (e == hipSuccess) e = hipMemset(b.camV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 2));
-    if (e == hipSuccess) e = hipMemset(b.lightV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 1));
-    // the null-stream memsets must land before the set's first launch on a (non-blocking) slot
-    // stream: a 3 GB vertex-plane memset still running under k_bdpt_start zeroes its vertices
-    if (e == hipSuccess) e = hipDeviceSynchronize();
+    // zero-fills on the stream of the set's frames (st, its slot's), ahead of the first launch
+    // that writes the set: a 3 GB vertex-plane memset on another stream could still be running
+    // under k_bdpt_start and zero its vertices
+    if (e == hipSuccess) e = hipMemsetAsync(b.splat, 0, 16 * N, st);
+    if (e == hipSuccess) e = hipMemsetAsync(b.camV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 2), st);
+    if (e == hipSuccess) e = hipMemsetAsync(b.lightV, 0, 16 * N * BDPT_VERTEX_PLANES * (D + 1), st);
     if (e != hipSuccess) bset_free(b);
     else b.frames = frames;
     return e;
@@ -1191,7 +1191,7 @@ static void fb_bind_bdpt(mcrt_framebuffer fb, int k) {
 static size_t bdpt_queue_cap(mcrt_framebuffer fb) {
     return (size_t)((fb->W + 7) / 8) * ((fb->H + 7) / 8) * 64;
 }
-static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k, int frames) {
+static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k, int frames, hipStream_t st) {
     const size_t N = fb->N;
     if (fb->bdptDepth != D) {
         for (auto& sl : fb->slot)
@@ -1199,9 +1199,11 @@ static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k, int frames) 
         hipStreamSynchronize(fb->ctx->stream);
         fb_free_bdpt(fb);
         hipError_t e = hipMalloc(&fb->sampLight, 16 * N * D);
-        if (e == hipSuccess) e = hipMemset(fb->sampLight, 0, 16 * N * D);
-        if (e == hipSuccess) e = hipDeviceSynchronize();   // before the slot streams read it
         if (e == hipSuccess) e = hipEventCreateWithFlags(&fb->bdptConnect, hipEventDisableTiming);
+        // zeroed on this frame's stream; every connect launch (the planes' only reader and writer)
+        // waits for bdptConnect, recorded here first
+        if (e == hipSuccess) e = hipMemsetAsync(fb->sampLight, 0, 16 * N * D, st);
+        if (e == hipSuccess) e = hipEventRecord(fb->bdptConnect, st);
         if (e != hipSuccess) { fb_free_bdpt(fb); return e; }
         fb->bdptDepth = D;
     }
@@ -1213,7 +1215,7 @@ static hipError_t fb_ensure_bdpt(mcrt_framebuffer fb, int D, int k, int frames) 
         bset_free(bs);
         bs = BdptSet{};
     }
-    if (!bs.camV) return bset_alloc(bs, N, bdpt_queue_cap(fb), D, frames);
+    if (!bs.camV) return bset_alloc(bs, N, bdpt_queue_cap(fb), D, frames, st);
     return hipSuccess;
 }
 
@@ -1239,12 +1241,14 @@ MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint3
     fb->slot.resize(MCRT_MAX_FRAMES_IN_FLIGHT);
     if (e == hipSuccess) e = slot_alloc(fb->slot[0], N);
     if (e == hipSuccess) fb_bind(fb, 0);
-    if (e == hipSuccess) e = hipMemset(fb->wsum, 0, 16 * N);
-    if (e == hipSuccess) e = hipMemset(fb->wts, 0, 4 * N);
-    if (e == hipSuccess) e = hipMemset(fb->image, 0, 16 * N);
-    if (e == hipSuccess) e = hipMemset(fb->denoised, 0, 16 * N);
-    if (e == hipSuccess) e = hipMemset(fb->display, 0, 16 * N);
-    if (e == hipSuccess) e = hipDeviceSynchronize();   // null-stream memsets before any slot-stream launch
+    // zero-fills on slot 0's (private) stream, finished before the frame buffer is handed out:
+    // only this buffer's work is waited for, not the device (other contexts, a captured caller stream)
+    if (e == hipSuccess) e = hipMemsetAsync(fb->wsum, 0, 16 * N, fb->slot[0].stream);
+    if (e == hipSuccess) e = hipMemsetAsync(fb->wts, 0, 4 * N, fb->slot[0].stream);
+    if (e == hipSuccess) e = hipMemsetAsync(fb->image, 0, 16 * N, fb->slot[0].stream);
+    if (e == hipSuccess) e = hipMemsetAsync(fb->denoised, 0, 16 * N, fb->slot[0].stream);
+    if (e == hipSuccess) e = hipMemsetAsync(fb->display, 0, 16 * N, fb->slot[0].stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(fb->slot[0].stream);
     if (e != hipSuccess) {
         fb_free(fb);
         delete fb;
@@ -1325,7 +1329,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     mcrt_ctx ctx = s->ctx;
     const int D = p->max_depth;
     const int B = f.batch;   // frames of this call (mcrt_render_frames): path = k * W*H + pixel
-    HIPCHK(ctx, fb_ensure_bdpt(fb, D, k, B));
+    HIPCHK(ctx, fb_ensure_bdpt(fb, D, k, B, st));
     fb_bind_bdpt(fb, k);
     fb->lastMaxDepth = D;
     fb->lastPixels = 0;
@@ -1480,7 +1484,11 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     if (bdpt && ks != 0 && fb->bdptDepth == p->max_depth && !fb->bset[ks].camV) {
         // each BDPT set holds ~C x N x 48 B of connection rays (2.5 GB at 1080p, D = 2): when a
         // second one does not fit, fall back to one frame in flight instead of failing the frame
-        const hipError_t e = bset_alloc(fb->bset[ks], fb->N, bdpt_queue_cap(fb), p->max_depth, count);
+        // (zero-filled on slot ks's stream when it exists, else on slot 0's and finished here: set ks
+        // is then first written on slot ks's stream)
+        hipStream_t zs = fb->slot[ks].stream ? fb->slot[ks].stream : fb->slot[0].stream;
+        hipError_t e = bset_alloc(fb->bset[ks], fb->N, bdpt_queue_cap(fb), p->max_depth, count, zs);
+        if (e == hipSuccess && zs != fb->slot[ks].stream) e = hipStreamSynchronize(zs);
         if (e == hipErrorOutOfMemory) {
             hipGetLastError();
             fb->bdptOneSet = true;
@@ -1769,15 +1777,29 @@ MCRT_API mcrt_status mcrt_framebuffer_bands_pack(mcrt_framebuffer fb, void* d_ds
     return MCRT_OK;
 }
 
+// The largest rank's row count of a band split (whole 8-row blocks): the rows of one packed chunk.
+static int band_max_rows(const FrameArgs& f) {
+    const int blocks = (int)((f.H + 7) / 8), bpb = f.bandRows / 8;
+    const int perCycle = bpb * f.numBands;
+    return 8 * ((blocks / perCycle) * bpb + std::min(blocks % perCycle, bpb));
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_band_layout(mcrt_framebuffer fb, int32_t* max_rows, int32_t* num_bands,
+                                                  int32_t* band_index) {
+    if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
+    if (!fb->haveBands) return fail(fb->ctx, MCRT_ERROR_NOT_READY, "no frame rendered");
+    if (max_rows) *max_rows = band_max_rows(fb->bands);
+    if (num_bands) *num_bands = fb->bands.numBands;
+    if (band_index) *band_index = fb->bands.bandIndex;
+    return MCRT_OK;
+}
+
 MCRT_API mcrt_status mcrt_framebuffer_bands_unpack(mcrt_framebuffer fb, const void* d_recv, int32_t max_rows) {
     if (!fb || !d_recv) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
     if (!fb->haveBands) return fail(fb->ctx, MCRT_ERROR_NOT_READY, "no frame rendered");
     const FrameArgs& f = fb->bands;
-    // the largest rank's row count (whole 8-row blocks): every chunk of d_recv must hold it
-    const int blocks = (int)((f.H + 7) / 8), bpb = f.bandRows / 8;
-    const int perCycle = bpb * f.numBands;
-    const int maxBlocks = (blocks / perCycle) * bpb + std::min(blocks % perCycle, bpb);
-    if (max_rows < maxBlocks * 8)
+    // every chunk of d_recv must hold the largest rank's rows
+    if (max_rows < band_max_rows(f))
         return fail(fb->ctx, MCRT_ERROR_INVALID_ARG, "max_rows below the largest rank's row count");
     mcrt_ctx ctx = fb->ctx;
     hipSetDevice(ctx->device);

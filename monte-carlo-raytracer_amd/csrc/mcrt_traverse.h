@@ -269,8 +269,10 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                         if (leader) {
                             stkN[sp] = late != 0 ? cF : cS;
                             stkM[sp] = late != 0 ? late : mS;
-                            stkN[sp + 1] = cS;
-                            stkM[sp + 1] = mS;
+                            if (nPush == 2) {   // (sp + 1 < PK_STACK only holds then)
+                                stkN[sp + 1] = cS;
+                                stkM[sp + 1] = mS;
+                            }
                         }
                         sp += nPush;
                     } else if (leader) {

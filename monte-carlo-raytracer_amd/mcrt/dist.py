@@ -79,11 +79,13 @@ def reduce_scatter_chunks(full, chunk, group=None):
 
 def splat_buffers(fb, device="cuda"):
     """The two device buffers of exchange_splats for frame buffer fb after a band-split frame:
-    (full rank-major buffer, own chunk), float32."""
+    (full rank-major buffer, own chunk), float32.  Left uninitialised: mcrt_bdpt_splats_copy
+    zeroes `full` on the frame's stream and the collective writes all of `chunk` (a zero-fill on
+    torch's stream would race with that pack, which runs on another stream)."""
     import torch
     cp, chunks = fb.bdpt_splat_layout()
-    return (torch.zeros(4 * cp * chunks, dtype=torch.float32, device=device),
-            torch.zeros(4 * cp, dtype=torch.float32, device=device))
+    return (torch.empty(4 * cp * chunks, dtype=torch.float32, device=device),
+            torch.empty(4 * cp, dtype=torch.float32, device=device))
 
 
 def exchange_splats(fb, full, chunk, group=None):
@@ -114,6 +116,8 @@ def exchange_splats(fb, full, chunk, group=None):
         if full.is_cuda:
             torch.cuda.synchronize(full.device)
         reduce_scatter_chunks(full, chunk, group)
+        if chunk.is_cuda:   # the copy into chunk ran on torch's stream; the gather reads it on the frame's
+            torch.cuda.current_stream(chunk.device).synchronize()
     fb.bdpt_gather(chunk.data_ptr())
 
 

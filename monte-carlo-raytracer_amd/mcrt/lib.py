@@ -77,6 +77,8 @@ SIGNATURES = {
     "mcrt_framebuffer_set_accumulation": (_c.c_int, [_vp, _vp, _vp]),
     "mcrt_framebuffer_bands_pack": (_c.c_int, [_vp, _vp]),
     "mcrt_framebuffer_bands_unpack": (_c.c_int, [_vp, _vp, _c.c_int32]),
+    "mcrt_framebuffer_band_layout": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.POINTER(_c.c_int32),
+                                                _c.POINTER(_c.c_int32)]),
     "mcrt_framebuffer_read_queue": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int32)]),
     "mcrt_framebuffer_queue_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.POINTER(_c.c_int32), _c.c_int]),
     "mcrt_postprocess": (_c.c_int, [_vp, _c.POINTER(T.PostprocessParams)]),
@@ -423,6 +425,12 @@ class FrameBuffer:
     def bands_unpack(self, recv_ptr, max_rows):
         """mcrt_framebuffer_bands_unpack: the other ranks' packed rows into the accumulators + image."""
         _check(lib().mcrt_framebuffer_bands_unpack(self.h, recv_ptr, max_rows), self.ctx.h)
+
+    def band_layout(self):
+        """(max_rows, num_bands, band_index) of the last render (mcrt_framebuffer_band_layout)."""
+        a, b, c = _c.c_int32(), _c.c_int32(), _c.c_int32()
+        _check(lib().mcrt_framebuffer_band_layout(self.h, _c.byref(a), _c.byref(b), _c.byref(c)), self.ctx.h)
+        return a.value, b.value, c.value
 
     def stats(self):
         a, b, c = _c.c_int64(), _c.c_int64(), _c.c_int64()

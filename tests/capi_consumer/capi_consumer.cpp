@@ -15,37 +15,19 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
-#include <fstream>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "consumer_util.h"
 #include "mcrt_capi.h"
 
 namespace {
 
-inline void check(mcrt_status s, mcrt_ctx c) {   // MCRTBridge.h
-    if (s != MCRT_OK) throw std::runtime_error(mcrt_last_error(c));
-}
-inline void hipCheck(hipError_t e) {
-    if (e != hipSuccess) throw std::runtime_error(hipGetErrorString(e));
-}
-
-template <class T>
-std::vector<T> load(const std::string& path) {
-    std::ifstream f(path, std::ios::binary | std::ios::ate);
-    if (!f) return {};
-    const size_t n = (size_t)f.tellg();
-    std::vector<T> v(n / sizeof(T));
-    f.seekg(0);
-    f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
-    return v;
-}
-template <class T>
-void save(const std::string& path, const T* p, size_t n) {
-    std::ofstream f(path, std::ios::binary);
-    f.write(reinterpret_cast<const char*>(p), (std::streamsize)(n * sizeof(T)));
-}
+using consumer::check;
+using consumer::hipCheck;
+using consumer::load;
+using consumer::save;
 
 // GeneratePerspectiveRays (PathTracing.cl:13-35) on the host: d = normalize(mix(mix(r00, r10, u),
 // mix(r01, r11, u), v)), u = x / W, v = y / H; tmax 1000; active, mask -1
@@ -91,37 +73,14 @@ int main(int argc, char** argv) {
             if (sun.size() == 6) check(mcrt_obj_add_directional_light(objScene, &sun[0], &sun[3]), ctx);
         }
         // ---- RTScene::commit ------------------------------------------------------------------
-        auto shapes = load<mcrt_shape>(in + "/shapes.bin");
-        auto indices = load<uint32_t>(in + "/indices.bin");
-        auto positions = load<mcrt_float4>(in + "/positions.bin");
-        auto uvs = load<mcrt_float2>(in + "/uvs.bin");
-        auto normals = load<mcrt_float4>(in + "/normals.bin");
-        auto tangents = load<mcrt_float4>(in + "/tangents.bin");
-        auto binormals = load<mcrt_float4>(in + "/binormals.bin");
-        auto texDescs = load<mcrt_texture_desc>(in + "/textures.bin");
-        auto texData = load<uint8_t>(in + "/texdata.bin");
-        auto sobol = load<uint32_t>(in + "/sobol.bin");
-        auto lights = load<mcrt_light>(in + "/lights.bin");
-        auto materials = load<mcrt_material>(in + "/materials.bin");
-        auto camv = load<mcrt_camera>(in + "/camera.bin");
-        if (camv.size() != 1 || (shapes.empty() && !objScene)) throw std::runtime_error("bad scene directory");
-        mcrt_scene_desc d = {};
-        d.shapes = shapes.data();                 d.num_shapes = (uint32_t)shapes.size();
-        d.indices = indices.data();               d.num_indices = (uint32_t)indices.size();
-        d.positions = positions.data();           d.num_vertices = (uint32_t)positions.size();
-        d.uvs = uvs.data();
-        d.normals = normals.data();
-        d.tangents = tangents.data();
-        d.binormals = binormals.data();
-        d.textures = texDescs.data();             d.num_textures = (uint32_t)texDescs.size();
-        d.tex_data = texData.data();              d.tex_data_bytes = texData.size();
-        d.sobol_matrices = sobol.data();          d.num_sobol_words = (uint32_t)sobol.size();
-        d.lights = lights.data();                 d.num_lights = (uint32_t)lights.size();
-        d.materials = materials.data();           d.num_materials = (uint32_t)materials.size();
+        const consumer::SceneFiles files(in);
+        const auto& camv = files.camera;
+        if (camv.size() != 1 || (files.shapes.empty() && !objScene)) throw std::runtime_error("bad scene directory");
+        mcrt_scene_desc d = files.desc();
         if (objScene) {
             check(mcrt_obj_scene_desc(objScene, &d), ctx);
-            d.sobol_matrices = sobol.empty() ? nullptr : sobol.data();
-            d.num_sobol_words = (uint32_t)sobol.size();
+            d.sobol_matrices = files.sobol.empty() ? nullptr : files.sobol.data();
+            d.num_sobol_words = (uint32_t)files.sobol.size();
         }
         mcrt_scene scene = nullptr;
         check(mcrt_scene_create(ctx, &d, &scene), ctx);

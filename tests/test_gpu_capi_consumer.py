@@ -105,3 +105,44 @@ def test_cpp_consumer_obj_scene(hip_ctx, tmp_path):
     np.testing.assert_array_equal(out("image", np.uint32).reshape(H, W, 4), img.view(np.uint32))
     fb.close()
     ds.close()
+
+
+RCCL_EXE = os.path.join(HERE, "capi_consumer", "capi_rccl")
+
+
+def test_cpp_rccl_end_of_job(hip_ctx, tmp_path):
+    """The multi-GPU end of job from C++ (capi_rccl.cpp; INTEGRATION.md "Multi-GPU"): 3 bands on one
+    GPU with a 1-rank RCCL communicator -- each band's accumulators packed on the context stream, ONE
+    ncclGroupStart/ncclSend/ncclRecv gather, mcrt_framebuffer_bands_unpack; BDPT adds a per-frame
+    mcrt_bdpt_splats_copy -> ncclReduceScatter -> mcrt_bdpt_gather.  PT: the whole-image frame bit
+    for bit; BDPT: up to the order of the splat sums (rtol 2e-5, as the band-split BDPT tests)."""
+    from mcrt import lib
+    if not os.path.exists(RCCL_EXE):
+        pytest.skip("tests/capi_consumer/capi_rccl not built (make -C tests/capi_consumer)")
+    sc = scenes.test_scene()
+    W, H, frames, D, bands = 96, 72, 3, 2, 3
+    cam = scene_camera("mixed", W, H)
+    write_scene(sc, cam, str(tmp_path / "scene"))
+    os.makedirs(tmp_path / "out")
+    env = dict(os.environ, NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"))
+    r = subprocess.run([RCCL_EXE, str(tmp_path / "scene"), str(tmp_path / "out"), str(frames), str(D), str(bands)],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["world"] == 1 and info["bands"] == bands and info["pixels"] == W * H, info
+    assert info["pt_identical"] == 1, info
+    assert 0 <= info["bdpt_max_rel"] <= 2e-5, info
+    out = lambda n: np.fromfile(str(tmp_path / "out" / f"{n}.bin"), np.float32).reshape(H, W, 4)   # noqa: E731
+    np.testing.assert_array_equal(out("pt_split").view(np.uint32), out("pt_plain").view(np.uint32))
+    bd = out("bdpt_split")
+    assert np.isfinite(bd).all() and bd[..., :3].max() > 0
+    np.testing.assert_allclose(bd, out("bdpt_plain"), rtol=2e-5, atol=2e-5)
+    # the C++ host's whole-image frames = the ctypes path's
+    ds = lib.DeviceScene(hip_ctx, sc)
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    for f in range(frames):
+        fb.render(ds, cam, frame=f, max_depth=D)
+        fb.accumulate(T.make_filter(T.BOX), f)
+    np.testing.assert_array_equal(out("pt_plain").view(np.uint32), fb.read(2).view(np.uint32))
+    fb.close()
+    ds.close()
