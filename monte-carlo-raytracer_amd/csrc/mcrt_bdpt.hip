@@ -39,6 +39,7 @@
 #include "mcrt_shading.h"
 
 #define BDPT_BLOCK 256
+#define BDPT_EXT_GROUPS 24   // direction octant x dominant axis of the subpath rays a vertex launch queues
 
 // RTBDPTVertexType / RTBDPTVertexFlag (kernel_data.h:202-218)
 enum { RT_BDPT_CAMERA_VERTEX = 0, RT_BDPT_LIGHT_VERTEX = 1, RT_BDPT_SURFACE_VERTEX = 2 };
@@ -469,7 +470,15 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
         const f2 uv = f2{(float)x * r.x, (float)y * r.y};
         camDir = lerpDirection(ld3(cam.r00), ld3(cam.r10), ld3(cam.r11), ld3(cam.r01), uv.x, uv.y);
         camPos = ld3(cam.pos);
-        storeVertex(b.camV, 0, pix, NB, createCameraVertex(camPos, splat3(1.0f)));
+        // camera vertex 0 (createCameraVertex): only its position and pdfRev (reset; the depth-1
+        // vertex launch may set it) change from frame to frame -- the other 6 planes are constants
+        // written once per plane stride
+        if (b.depth0Const) {
+            vplane(b.camV, 0, 0, NB)[pix] = make_float4(camPos.x, camPos.y, camPos.z, 0.0f);
+            vplane(b.camV, 0, 2, NB)[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        } else {
+            storeVertex(b.camV, 0, pix, NB, createCameraVertex(camPos, splat3(1.0f)));
+        }
         camPdf = evalPinholeCameraPdfWe(cam, camPos, camDir);
         // light (BDPT.cl:294-311)
         Sampler sampler = makeSampler(f.sampler, (uint32_t)px, f.frame + k, 0, f.W, f.H, s.sobol);
@@ -481,7 +490,17 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
         const LightLe le = sampleLightLe(s, light, u1, u2);
         BVertex lv = createLightVertex(chosen, le.origin, le.normal, le.Le, le.pdfPos * lightPdf, light.flags);
         lv.pdfPos = le.pdfPos;
-        storeVertex(b.lightV, 0, pix, NB, lv);
+        if (b.depth0Const) {   // planes 4-5 (sdpdu|uv.x, sdpdv|uv.y) of a light vertex are always zero
+            vplane(b.lightV, 0, 0, NB)[pix] = make_float4(lv.fr.p.x, lv.fr.p.y, lv.fr.p.z, lv.traceErrorOffset);
+            vplane(b.lightV, 0, 1, NB)[pix] = make_float4(lv.fr.gn.x, lv.fr.gn.y, lv.fr.gn.z, lv.pdfFwd);
+            vplane(b.lightV, 0, 2, NB)[pix] = make_float4(lv.fr.sn.x, lv.fr.sn.y, lv.fr.sn.z, lv.pdfRev);
+            vplane(b.lightV, 0, 3, NB)[pix] = make_float4(lv.wo.x, lv.wo.y, lv.wo.z, lv.pdfPos);
+            vplane(b.lightV, 0, 6, NB)[pix] = make_float4(lv.throughput.x, lv.throughput.y, lv.throughput.z, 0.0f);
+            *reinterpret_cast<int4*>(&vplane(b.lightV, 0, 7, NB)[pix]) =
+                make_int4(lv.type, lv.flags, lv.lightIdx, lv.materialIdx);
+        } else {
+            storeVertex(b.lightV, 0, pix, NB, lv);
+        }
         lo = le.origin;
         ld = le.dir;
         lt = cl_div(le.Le * absDot(le.normal, le.dir), (lightPdf * le.pdfPos * le.pdfDir));
@@ -503,7 +522,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                                                             BdptQueue qIn, const float4* __restrict__ hits,
                                                             BdptQueue qOut) {
     const int n = *qIn.count;
-    __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
+    __shared__ int ldsGroup[BDPT_EXT_GROUPS + 1];
     if ((int)blockIdx.x * BDPT_BLOCK >= n) return;
     const int i = xcdRemap(blockIdx.x, (n + BDPT_BLOCK - 1) / BDPT_BLOCK) * BDPT_BLOCK + threadIdx.x;
     const int N = (int)(f.W * f.H) * f.batch;   // plane stride (NB)
@@ -603,7 +622,14 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
             }
         }
     }
-    const int slot = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
+    // the next rays grouped by direction octant x dominant axis inside the block's queue slice (as
+    // the PT first shading's), so more k_extend waves run the octant-specialised traversal
+    int grp = (nd.x < 0.0f ? 1 : 0) | (nd.y < 0.0f ? 2 : 0) | (nd.z < 0.0f ? 4 : 0);
+    {
+        const float ax = fabsf(nd.x), ay = fabsf(nd.y), az = fabsf(nd.z);
+        grp = grp * 3 + (ax >= ay && ax >= az ? 0 : ay >= az ? 1 : 2);
+    }
+    const int slot = blockAppendGroupedLds<BDPT_EXT_GROUPS>(qOut.count, push, grp, ldsGroup);
     if (push) pushRay(qOut, slot, no, tag, nd, nPdf, ntp);
 }
 

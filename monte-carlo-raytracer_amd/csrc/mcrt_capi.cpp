@@ -147,6 +147,10 @@ struct BdptSet {
     uint32_t* spill = nullptr;   // traversal spill columns of this set's launches
     int frames = 0;              // batch frames the per-frame arrays hold (plane stride N x frames)
     size_t spillWords = 0;
+    // plane stride and band (rows, count, index) whose depth-0 frame-invariant planes k_bdpt_start
+    // wrote for every path of the band
+    size_t constStride = 0;
+    int constBand[3] = {0, 0, -1};
 };   // [0..127] ints: counters; cameras (176 B each, <= MCRT_MAX_BATCH_FRAMES) from byte 512
 
 struct mcrt_framebuffer_s {
@@ -1370,6 +1374,13 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     b.slots = fb->slots;
     b.splat = fb->splat;
     b.ownSlots = (int)C - D;
+    // (planes at another stride hold other data; another band's paths were never written)
+    b.depth0Const = bs.constStride == N && bs.constBand[0] == f.bandRows && bs.constBand[1] == f.numBands &&
+                    bs.constBand[2] == f.bandIndex ? 1 : 0;
+    bs.constStride = N;
+    bs.constBand[0] = f.bandRows;
+    bs.constBand[1] = f.numBands;
+    bs.constBand[2] = f.bandIndex;
     int* cnt = fb->bdptCounters;   // [d] ray queue of depth d (d <= D + 1 <= 33), BDPT_CNT_* below
     auto queue = [&](int d) {
         BdptQueue q;

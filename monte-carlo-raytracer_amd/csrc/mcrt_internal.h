@@ -67,6 +67,8 @@ struct BdptArgs {
     float4* slots;       // ownSlots planes x N
     float4* splat;       // N
     int ownSlots;        // strategies with t >= 2 = maxConnections - D
+    int depth0Const;     // 1: the frame-invariant planes of the depth-0 vertices are already in place
+                         // at this plane stride (k_bdpt_start writes only the per-frame ones)
 };
 struct BdptQueue {
     int* count;

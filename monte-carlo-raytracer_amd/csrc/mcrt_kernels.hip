@@ -20,21 +20,14 @@
 #include "mcrt_shading.h"
 
 // Shading workgroup sizes (threads; one queue atomic per workgroup and queue).  The extension rays
-// a workgroup appends are grouped by direction octant inside its queue slice, so a larger first-
-// shading workgroup hands the incoherent launch longer single-octant runs.
-#ifndef SHADE0_BLOCK
+// a workgroup appends are grouped by direction inside its queue slice, so a larger first-shading
+// workgroup hands the incoherent launch longer single-group runs (512 / 256 measured best,
+// profiles/r03/ab item 17; the sweep's knobs: tools/experiments/r3_knobs.patch).
 #define SHADE0_BLOCK 512
-#endif
-#ifndef SHADEN_BLOCK
 #define SHADEN_BLOCK 256
-#endif
-// direction groups of the first shading's extension rays (8 = octants; 24 = octant x dominant axis)
-#ifndef MCRT_EXT_GROUPS
+// direction groups of the first shading's extension rays: octant x dominant axis, appended with
+// one LDS atomic per record (profiles/r03/ab items 18-19)
 #define MCRT_EXT_GROUPS 24
-#endif
-#ifndef MCRT_EXT_LDS_APPEND   // 1: one LDS atomic per record instead of a ballot per group and wave
-#define MCRT_EXT_LDS_APPEND 1
-#endif
 
 // ---------------------------------------------------------------------------
 // RadeonRays-compatible queries on AoS rays (mcrt_trace_closest / mcrt_trace_any).
@@ -483,7 +476,7 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
     int x = 0, y = 0;
     bool valid = k < f.batch && tile < f.numTiles && tilePixel(f, tile, pi, x, y);
     __shared__ int ldsWave[SHADE0_BLOCK / 64 + 1];
-    __shared__ int ldsGroup[(SHADE0_BLOCK / 64) * MCRT_EXT_GROUPS + 1];
+    __shared__ int ldsGroup[MCRT_EXT_GROUPS + 1];
     ShadeOut o;
     o.pushS = o.pushE = false;
     o.eD = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -498,19 +491,13 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
     }
     const int ss = blockAppend<SHADE0_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
-    // extension rays grouped by direction octant inside the block's queue slice
+    // extension rays grouped by direction octant x dominant axis inside the block's queue slice
     int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
-#if MCRT_EXT_GROUPS == 24   // octant x dominant axis
     {
         const float ax = fabsf(o.eD.x), ay = fabsf(o.eD.y), az = fabsf(o.eD.z);
         oct = oct * 3 + (ax >= ay && ax >= az ? 0 : ay >= az ? 1 : 2);
     }
-#endif
-#if MCRT_EXT_LDS_APPEND
     const int es = blockAppendGroupedLds<MCRT_EXT_GROUPS>(q.extCountOut, o.pushE, oct, ldsGroup);
-#else
-    const int es = blockAppendGrouped<SHADE0_BLOCK / 64, MCRT_EXT_GROUPS>(q.extCountOut, o.pushE, oct, ldsGroup);
-#endif
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 

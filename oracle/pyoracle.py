@@ -434,6 +434,7 @@ def clref(variant="ieee"):
         L.clref_bdpt_read.argtypes = [_vp, _c.c_int, _vp]
         L.clref_probe_lod.argtypes = [_vp, _c.c_char_p, _vp, _vp, _c.c_int, _c.c_int, _vp]
         L.clref_probe_filters.argtypes = [_c.c_char_p, _vp, _c.c_int, _vp]
+        L.clref_probe_tonemap.argtypes = [_c.c_char_p, _vp, _c.c_int, _c.c_float, _vp]
         L.clref_scene_set_two_level.argtypes = [_vp, _vp, _c.c_int64, _vp, _c.c_int64, _vp, _c.c_int64, _vp,
                                                 _c.c_int64, _c.c_int]
         st = L.clref_init(os.path.join(HERE, "_ref").encode(), variant.encode())
@@ -452,6 +453,21 @@ def clref_filter_weights(filters, variant="ieee"):
     st = L.clref_probe_filters(os.path.join(HERE, "_ref", "clref_probe_filters.hsaco").encode(), _p(f), len(f), _p(out))
     if st != 0:
         raise RuntimeError(f"clref_probe_filters {st}: {L.clref_error().decode()}")
+    return out
+
+
+def clref_tonemap(img, Lwhite, variant="ieee"):
+    """The reference's Reinhard tone mapping (computeLuminanceFromRGB + toneMapControlled of
+    ToneMapping.cl / colors.cl via oracle/refbuild/clprobe_tonemap.cl, run live) of a float32
+    (..., 4) image."""
+    L = clref(variant)
+    a = np.ascontiguousarray(img, np.float32)
+    out = np.zeros_like(a)
+    n = a.size // 4
+    st = L.clref_probe_tonemap(os.path.join(HERE, "_ref", "clref_probe_tonemap.hsaco").encode(), _p(a), n,
+                               float(Lwhite), _p(out))
+    if st != 0:
+        raise RuntimeError(f"clref_probe_tonemap {st}: {L.clref_error().decode()}")
     return out
 
 

@@ -522,6 +522,35 @@ __attribute__((visibility("default"))) int clref_probe_filters(const char* hsaco
     return good ? 0 : -5;
 }
 
+// Tone-mapping probe (clprobe_tonemap.cl, test infrastructure): the reference's Reinhard operator
+// (computeLuminanceFromRGB + toneMapControlled) on n float4 pixels.
+__attribute__((visibility("default"))) int clref_probe_tonemap(const char* hsaco, const float* in, int n, float Lwhite,
+                                                               float* out) {
+    static cl_program prog = nullptr;
+    static cl_kernel k = nullptr;
+    cl_int e = 0;
+    if (!k) {
+        prog = loadProgram(hsaco);
+        if (!prog) return -1;
+        k = clCreateKernel(prog, "ProbeToneMap", &e);
+        if (!ok(e, "kernel ProbeToneMap")) return -2;
+    }
+    cl_mem bi = buf(16 * (size_t)n, in);
+    cl_mem bo = buf(16 * (size_t)n, nullptr);
+    e = 0;
+    e |= arg(k, 0, bi);
+    e |= arg(k, 1, n);
+    e |= arg(k, 2, Lwhite);
+    e |= arg(k, 3, bo);
+    if (!ok(e, "probe tonemap args")) return -4;
+    size_t gs = ((size_t)n + 63) / 64 * 64, ls = 64;
+    bool good = ok(clEnqueueNDRangeKernel(R.q, k, 1, nullptr, &gs, &ls, 0, nullptr, nullptr), "probe tonemap launch") &&
+                ok(clEnqueueReadBuffer(R.q, bo, CL_TRUE, 0, 16 * (size_t)n, out, 0, nullptr, nullptr), "probe tonemap read");
+    clReleaseMemObject(bi);
+    clReleaseMemObject(bo);
+    return good ? 0 : -5;
+}
+
 // ---------------------------------------------------------------------------
 // BDPT (RTBDPTPass::update, RTBDPTPass.cpp:67-128; kernels BDPT.cl:240-932)
 // ---------------------------------------------------------------------------

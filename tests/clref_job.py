@@ -152,6 +152,26 @@ def taa_camera(name, W, H, f):
     return scene_camera(name, W, H, frame=f % 64, jitter=True)
 
 
+# BASELINE.json config 1 (the reference's CPU-device plumbing case): Dragon proxy 512x512, 4 spp
+# (frames 0..3 accumulated with the box filter), PT, maxDepth 2.  "pt_acc": the frames are
+# compared bit for bit and the product's accumulated image against the oracle's accumulation of
+# the reference's frames (test_gpu_reference_scale.py); CONFIG1_ROWS of the reference frames are
+# committed as tests/golden/config1_dragon512.npz (config1_job) for the CPU oracle test.
+CONFIG1 = ("dragon_pt_512_4spp", "dragon_proxy", 512, 512, "pt_acc", (0, 1, 2, 3), 2)
+CONFIG1_ROWS = tuple(range(3, 512, 64))
+
+
+def config1_job(out_path, variant):
+    key, name, W, H, _, frames, D = CONFIG1
+    cs = po.CLRefScene(scale_scene(name), variant)
+    cam = scene_camera(name, W, H)
+    rows = np.asarray(CONFIG1_ROWS, np.int32)
+    res = {"rows": rows}
+    for f in frames:
+        res[f"f{f}"] = np.ascontiguousarray(cs.render(cam, frame=f, max_depth=D)[rows, :, :3])
+    np.savez_compressed(out_path, **res)
+
+
 # BASELINE.json configs at full size against the reference kernels run live
 # (tests/test_gpu_reference_scale.py): (key, scene, W, H, integrator, frames, max_depth).
 # The sampler is the job's variant: "ieee" = random (the reference default), "sobol_ieee" = the
@@ -165,6 +185,8 @@ SCALE_CASES = {
         ("sponza_pt_1080p", "sponza_proxy", 1920, 1080, "pt", (0, 1), 2),           # config 3
         ("dragon_pt_1080p", "dragon_proxy", 1920, 1080, "pt", (0, 1), 2),           # config 2
         ("sm_bdpt_1080p", "san_miguel_proxy", 1920, 1080, "bdpt", (0, 1), 2),       # config 4 integrator (bench size)
+        # config 1: the Dragon proxy at 512x512, 4 spp accumulated (frames 0..3, box filter)
+        CONFIG1,
     ],
     "sobol_ieee": [
         ("sm_sobol_4k", "san_miguel_proxy", 3840, 2160, "pt", (0, 600), 2),        # config 5; frame 600: Q6 wrap
@@ -310,6 +332,9 @@ def main():
         return
     if len(sys.argv) > 3 and sys.argv[3] == "filters":
         filters_job(out_path, variant)
+        return
+    if len(sys.argv) > 3 and sys.argv[3] == "config1":
+        config1_job(out_path, variant)
         return
     if len(sys.argv) > 3 and sys.argv[3] == "scale":
         scale_job(out_path, variant)

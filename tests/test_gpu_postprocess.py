@@ -1,9 +1,13 @@
-"""GPU post-process passes (mcrt_postprocess) against the oracle's restatements of the
-reference's BilateralDenoise (KRN/Denoise.cl:6-47) and ReinhardToneMapping
-(KRN/ToneMapping.cl:42-63).  The reference kernels read and write image2d_t objects, which the
-MI355X OpenCL runtime does not support, so they cannot run here; the oracle (IEEE C) is the
-pin, at a tolerance that covers exp/division rounding (device: 2.5-ulp OpenCL division and the
-device-library exp, as the reference's own build) -- rtol 2e-5."""
+"""GPU post-process passes (mcrt_postprocess) against the reference and the oracle.
+
+* ReinhardToneMapping (KRN/ToneMapping.cl:42-63): its two functions, computeLuminanceFromRGB
+  (colors.cl:19-22) and toneMapControlled (ToneMapping.cl:37-40), run live from the reference
+  sources through oracle/refbuild/clprobe_tonemap.cl; k_tonemap must match them BIT FOR BIT.
+* BilateralDenoise (KRN/Denoise.cl:6-47) reads its window through image2d_t inline (no function to
+  call), and the MI355X OpenCL runtime has no image support, so it cannot run here: the oracle's
+  IEEE C restatement is the pin (parity unpinned against reference code), at a tolerance that
+  covers exp/division rounding (device: 2.5-ulp OpenCL division and the device-library exp, as the
+  reference's own build) -- rtol 2e-5."""
 import numpy as np
 import pytest
 
@@ -47,6 +51,42 @@ def test_tonemap_matches_oracle(rendered):
     ok = np.isfinite(ref)
     np.testing.assert_array_equal(np.isfinite(got), ok)   # L = 0 -> 0/0, as the reference
     np.testing.assert_allclose(got[ok], ref[ok], rtol=2e-5, atol=1e-7)
+
+
+def _tonemap_product(hip_ctx, img, Lwhite):
+    """k_tonemap over an arbitrary float4 image: installed as the accumulation with unit weights
+    (image = sum / 1, exact), then mcrt_postprocess."""
+    import torch
+    from mcrt import lib
+    H, W = img.shape[:2]
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    s = torch.from_numpy(np.ascontiguousarray(img, np.float32).reshape(-1)).cuda()
+    w = torch.ones(H * W, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    fb.set_accumulation(s.data_ptr(), w.data_ptr())
+    hip_ctx.sync()
+    np.testing.assert_array_equal(fb.read(2), img)   # the installed image is the input, bit for bit
+    fb.postprocess(tonemap=True, min_luminance=Lwhite)
+    out = fb.read(3)
+    fb.close()
+    return out
+
+
+@pytest.mark.parametrize("Lwhite", [2.0, 0.37, 11.5])
+def test_tonemap_bit_exact_vs_reference_functions(hip_ctx, rendered, Lwhite):
+    """k_tonemap == the reference's computeLuminanceFromRGB + toneMapControlled run live, on the
+    rendered image and on HDR values over 12 decades (zeros, single-channel, huge, tiny)."""
+    _, img = rendered
+    rng = np.random.default_rng(7)
+    hdr = (10.0 ** rng.uniform(-6, 6, size=(48, 64, 4))).astype(np.float32)
+    hdr[rng.random((48, 64)) < 0.05] = 0.0                      # L = 0: 0/0 as the reference
+    hdr[..., 0][rng.random((48, 64)) < 0.1] = 0.0                # one channel off
+    hdr[..., 3] = rng.uniform(0, 1, size=(48, 64)).astype(np.float32)   # alpha passes through
+    for src in (img, hdr):
+        got = _tonemap_product(hip_ctx, src, Lwhite)
+        ref = po.clref_tonemap(src, Lwhite)
+        np.testing.assert_array_equal(got.view(np.uint32)[np.isfinite(ref)], ref.view(np.uint32)[np.isfinite(ref)])
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
 
 
 def test_denoise_then_tonemap_and_passthrough(rendered):

@@ -7,6 +7,10 @@
     (129 .. 148) on that scene -- frames 1, 7 and 19 of the batch bit-exact against the reference
     run live with the same cameras, and the accumulators and image after the call bit-identical
     to 20 x (mcrt_render_frame + mcrt_accumulate);
+  * config 1: Dragon proxy 512x512, 4 spp: the four frames bit-exact, and the accumulated image
+    (4 x mcrt_render_frame + mcrt_accumulate, box filter) bit-identical to the oracle's
+    ReconstructionPass restatement over the REFERENCE's four frames (the reference's own
+    ReconstructionPass writes an image2d_t, which this GPU's OpenCL cannot run);
   * config 3: Sponza proxy (16 x 1024^2 mip-mapped textures) 1920x1080, PT -- bit-exact;
   * config 4: San-Miguel proxy BDPT at 1920x1080 (the bench's BDPT object), frames 0 and 1 in sequence from fresh buffers
     (BDPT.cl) -- vertex counts bit-exact, every defined field of the vertices of every 17th pixel
@@ -71,6 +75,8 @@ def test_full_size_config_matches_reference(hip_ctx, clref_scale, variant, case)
     ds = device_scene(hip_ctx, name)
     if integ == "pt_taa":
         return timed_call_matches(hip_ctx, ds, ref, key, name, W, H, frames, D)
+    if integ == "pt_acc":
+        return accumulated_matches(hip_ctx, ds, ref, key, name, W, H, frames, D)
     fb = lib.FrameBuffer(hip_ctx, W, H)
     cam = scene_camera(name, W, H)
     bad = []
@@ -143,5 +149,32 @@ def timed_call_matches(ctx, ds, ref, key, name, W, H, frames, D):
         ex = _exact(a, b)
         if not ex.all():
             bad.append(f"{nm} after the batched call differs from 20 single frames at {int((~ex.all(-1)).sum())} px")
+    fb.close()
+    assert not bad, (key, bad)
+
+
+def accumulated_matches(ctx, ds, ref, key, name, W, H, frames, D):
+    """Config 1: frames bit-exact against the reference, and the product's accumulation of them
+    bit-identical to the oracle's accumulation (orc_accumulate) of the reference's frames."""
+    from mcrt import lib
+    box = T.make_filter(T.BOX)
+    cam = scene_camera(name, W, H)
+    fb = lib.FrameBuffer(ctx, W, H)
+    bad = []
+    wsum = wts = None
+    for f in frames:
+        fb.render(ds, cam, frame=f, max_depth=D)
+        fb.accumulate(box, f)
+        r = ref[f"{key}_f{f}"]
+        assert r[..., :3].max() > 0, (key, f, "empty reference frame")
+        ex = _exact(fb.read(0)[..., :3], r[..., :3])
+        if not ex.all():
+            bad.append(f"frame {f}: {int((~ex.all(-1)).sum())} of {W * H} pixels differ")
+        wsum, wts, img = po.accumulate(np.ascontiguousarray(r, np.float32), f, box, wsum, wts)
+    for nm, a, b in (("weighted sum", fb.read(1), wsum), ("image", fb.read(2), img)):
+        ex = _exact(a, b)
+        if not ex.all():
+            bad.append(f"{nm} after {len(frames)} spp differs from the oracle's accumulation of the reference "
+                       f"frames at {int((~ex.all(-1)).sum())} px")
     fb.close()
     assert not bad, (key, bad)

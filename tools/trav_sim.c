@@ -126,3 +126,103 @@ void sim(const Node* nodes, const Ray* rays, int n, int any, int32_t* out, float
         hit_node[i] = best == INV ? -1 : (int32_t)best;
     }
 }
+
+/* Leaf-pair schemes.  out per ray: [0] visits (= loop iterations now),
+ * [1] iterations when an internal node whose two children are both leaves and whose two boxes
+ * the ray hits tests both triangles in ONE iteration (their records fetched together, nearer
+ * first; the far leaf is not pushed), [2] iterations when such a leaf-pair parent's record
+ * carries both triangles (one iteration covers the parent and whichever leaves it hits),
+ * [3] leaf-pair parents visited, [4] of them with both boxes hit. */
+void sim_pairs(const Node* nodes, const Ray* rays, int n, int any, int32_t* out) {
+    static uint32_t stack[1 << 16];
+    for (int i = 0; i < n; ++i) {
+        const Ray* r = &rays[i];
+        int32_t* o = out + (size_t)i * 5;
+        memset(o, 0, sizeof(int32_t) * 5);
+        if (r->extra[1] == 0) continue;
+        float inv[3], oxi[3];
+        for (int k = 0; k < 3; ++k) { inv[k] = sinv(r->d[k]); oxi[k] = -r->o[k] * inv[k]; }
+        float ct = r->o[3];
+        uint32_t addr = 0;
+        int sp = 0, nv = 0, p1 = 0, p2 = 0, pp = 0, pb = 0;
+        stack[sp++] = INV;
+        while (addr != INV) {
+            const Node* nd = &nodes[addr];
+            ++nv; ++p1; ++p2;
+            if (nd->left != INV) {
+                float a0, a1, b0, b1;
+                bbox(nd->lmin, nd->lmax, inv, oxi, ct, &a0, &a1);
+                bbox(nd->rmin, nd->rmax, inv, oxi, ct, &b0, &b1);
+                int h0 = a0 <= a1, h1 = b0 <= b1, c1 = h1 && (a0 > b0);
+                int pair = nodes[nd->left].left == INV && nodes[nd->right].left == INV;
+                if (pair) {
+                    ++pp;
+                    if (h0 && h1) ++pb;
+                    /* the leaves this node reaches: nearer first, each tested against the t so far */
+                    uint32_t first = (c1 || !h0) ? nd->right : nd->left, second = (c1 || !h0) ? nd->left : nd->right;
+                    int nl = (h0 ? 1 : 0) + (h1 ? 1 : 0);
+                    int done = 0;
+                    for (int k = 0; k < nl && !done; ++k) {
+                        const Node* lf = &nodes[k == 0 ? first : second];
+                        ++nv;
+                        if (r->extra[0] != (int)lf->mesh) {
+                            float t = tri(r, lf, ct);
+                            if (t < ct) { ct = t; if (any) done = 1; }
+                        }
+                    }
+                    p1 += nl ? 1 : 0;   /* both hit: one iteration for the two; one hit: its own */
+                    if (done) break;
+                    addr = stack[--sp];
+                    continue;
+                }
+                if (h0 || h1) {
+                    uint32_t def;
+                    if (c1 || !h0) { addr = nd->right; def = nd->left; } else { addr = nd->left; def = nd->right; }
+                    if (h0 && h1) stack[sp++] = def;
+                    continue;
+                }
+            } else if (r->extra[0] != (int)nd->mesh) {
+                float t = tri(r, nd, ct);
+                if (t < ct) { ct = t; if (any) break; }
+            }
+            addr = stack[--sp];
+        }
+        o[0] = nv; o[1] = p1; o[2] = p2; o[3] = pp; o[4] = pb;
+    }
+}
+
+/* Visits by tree level (analysis of an LDS-resident top of the tree): hist[min(level, 63)] +=
+ * visits of nodes at that level (root = 0), over the closest / any traversal of n rays. */
+void sim_levels(const Node* nodes, const uint8_t* level, const Ray* rays, int n, int any, int64_t* hist) {
+    static uint32_t stack[1 << 16];
+    for (int i = 0; i < n; ++i) {
+        const Ray* r = &rays[i];
+        if (r->extra[1] == 0) continue;
+        float inv[3], oxi[3];
+        for (int k = 0; k < 3; ++k) { inv[k] = sinv(r->d[k]); oxi[k] = -r->o[k] * inv[k]; }
+        float ct = r->o[3];
+        uint32_t addr = 0;
+        int sp = 0;
+        stack[sp++] = INV;
+        while (addr != INV) {
+            const Node* nd = &nodes[addr];
+            hist[level[addr] < 63 ? level[addr] : 63] += 1;
+            if (nd->left != INV) {
+                float a0, a1, b0, b1;
+                bbox(nd->lmin, nd->lmax, inv, oxi, ct, &a0, &a1);
+                bbox(nd->rmin, nd->rmax, inv, oxi, ct, &b0, &b1);
+                int h0 = a0 <= a1, h1 = b0 <= b1, c1 = h1 && (a0 > b0);
+                if (h0 || h1) {
+                    uint32_t def;
+                    if (c1 || !h0) { addr = nd->right; def = nd->left; } else { addr = nd->left; def = nd->right; }
+                    if (h0 && h1) stack[sp++] = def;
+                    continue;
+                }
+            } else if (r->extra[0] != (int)nd->mesh) {
+                float t = tri(r, nd, ct);
+                if (t < ct) { ct = t; if (any) break; }
+            }
+            addr = stack[--sp];
+        }
+    }
+}
