@@ -39,7 +39,6 @@
 #include "mcrt_shading.h"
 
 #define BDPT_BLOCK 256
-#define BDPT_EXT_GROUPS 24   // direction octant x dominant axis of the subpath rays a vertex launch queues
 
 // RTBDPTVertexType / RTBDPTVertexFlag (kernel_data.h:202-218)
 enum { RT_BDPT_CAMERA_VERTEX = 0, RT_BDPT_LIGHT_VERTEX = 1, RT_BDPT_SURFACE_VERTEX = 2 };
@@ -522,7 +521,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                                                             BdptQueue qIn, const float4* __restrict__ hits,
                                                             BdptQueue qOut) {
     const int n = *qIn.count;
-    __shared__ int ldsGroup[BDPT_EXT_GROUPS + 1];
+    __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
     if ((int)blockIdx.x * BDPT_BLOCK >= n) return;
     const int i = xcdRemap(blockIdx.x, (n + BDPT_BLOCK - 1) / BDPT_BLOCK) * BDPT_BLOCK + threadIdx.x;
     const int N = (int)(f.W * f.H) * f.batch;   // plane stride (NB)
@@ -622,14 +621,10 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
             }
         }
     }
-    // the next rays grouped by direction octant x dominant axis inside the block's queue slice (as
-    // the PT first shading's), so more k_extend waves run the octant-specialised traversal
-    int grp = (nd.x < 0.0f ? 1 : 0) | (nd.y < 0.0f ? 2 : 0) | (nd.z < 0.0f ? 4 : 0);
-    {
-        const float ax = fabsf(nd.x), ay = fabsf(nd.y), az = fabsf(nd.z);
-        grp = grp * 3 + (ax >= ay && ax >= az ? 0 : ay >= az ? 1 : 2);
-    }
-    const int slot = blockAppendGroupedLds<BDPT_EXT_GROUPS>(qOut.count, push, grp, ldsGroup);
+    // (queue order = the block's ray order: grouping the next rays by direction as the PT first
+    // shading does made this kernel 11 % slower -- its plane reads and writes follow the queue --
+    // for 1 % on k_extend; profiles/r04/ab/README.txt)
+    const int slot = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
     if (push) pushRay(qOut, slot, no, tag, nd, nPdf, ntp);
 }
 

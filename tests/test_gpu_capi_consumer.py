@@ -120,6 +120,7 @@ def test_cpp_rccl_end_of_job(hip_ctx, tmp_path):
     if not os.path.exists(RCCL_EXE):
         pytest.skip("tests/capi_consumer/capi_rccl not built (make -C tests/capi_consumer)")
     sc = scenes.test_scene()
+    sc.sobol = sobol_matrices()
     W, H, frames, D, bands = 96, 72, 3, 2, 3
     cam = scene_camera("mixed", W, H)
     write_scene(sc, cam, str(tmp_path / "scene"))

@@ -3,7 +3,8 @@
 * A 1-rank `nccl` (= RCCL) process group in this process runs the end-of-job band gather
   (mcrt.dist.gather_bands_fb: pack -> dist.gather -> unpack) and the BDPT splat exchange
   (mcrt.dist.exchange_splats: splats_copy -> reduce_scatter_tensor on the frame's stream ->
-  bdpt_gather) on real RCCL kernels; the result must be the no-collective frame bit for bit.
+  bdpt_gather) on real RCCL kernels; the result must be the no-collective frame: PT bit for bit,
+  BDPT up to the order of its float-atomic light-tracing splats (rtol 4e-6, tests/test_gpu_bdpt.py).
 * `python bench.py --gpus 2 --dist-backend gloo` with NO launcher starts its own 2 ranks
   (torch.distributed.run as a child process) and reports n_gpus 2; its image equals the
   1-rank image bit for bit (RCCL refuses two ranks on one GPU, so the 2-rank rehearsal uses gloo;
@@ -66,8 +67,12 @@ def test_rccl_band_gather_and_splat_exchange(hip_ctx, nccl_one_rank):
         mdist.gather_bands_fb(hip_ctx, fb, H, W, 8, send, recv, dst=0)   # dist.gather over RCCL
         hip_ctx.sync()
         torch.cuda.synchronize()
-        np.testing.assert_array_equal(fb.read(2).view(np.uint32), plain.read(2).view(np.uint32))
-        np.testing.assert_array_equal(fb.read(1).view(np.uint32), plain.read(1).view(np.uint32))
+        if integ == T.INTEGRATOR_PT:   # the same paths, the same sums: bit for bit
+            np.testing.assert_array_equal(fb.read(2).view(np.uint32), plain.read(2).view(np.uint32))
+            np.testing.assert_array_equal(fb.read(1).view(np.uint32), plain.read(1).view(np.uint32))
+        else:   # light-tracing splats are float atomics: two renders differ by their order only
+            np.testing.assert_allclose(fb.read(2), plain.read(2), rtol=4e-6, atol=1e-30)
+            np.testing.assert_allclose(fb.read(1), plain.read(1), rtol=4e-6, atol=1e-30)
         plain.close()
         fb.close()
     # one more collective on the same group: the timing reduction bench.py ends with

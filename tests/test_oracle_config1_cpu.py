@@ -10,7 +10,6 @@ import os
 import time
 
 import numpy as np
-import pytest
 
 from clref_job import CONFIG1, scale_scene
 from mcrt import types as T
@@ -27,8 +26,6 @@ def frac_within(a, b, rtol=1e-4):
 
 def test_config1_dragon_512_4spp():
     key, name, W, H, _, frames, D = CONFIG1
-    if not os.path.exists(GOLD):
-        pytest.skip("tests/golden/config1_dragon512.npz not generated yet (clref_job.py ... config1 on the GPU box)")
     z = np.load(GOLD, allow_pickle=False)
     rows = z["rows"]
     o = po.OracleScene(scale_scene(name))
