@@ -102,8 +102,6 @@ struct mcrt_scene_s {
     bool twoLevel = false;          // instanced scene: two-level records (mcrt_bvh2l.cpp)
     int numMeshes = 0, numInstances = 0;
     // traversal scratch
-    void* dTop = nullptr;           // LDS-resident top of a flat tree (TraceCtx::top)
-    int topNodes = 0;
     uint32_t* dSpill = nullptr;
     int spillCap = 0;
     size_t spillRays = 0;           // rays the spill buffer covers (spillCap words each)
@@ -309,8 +307,6 @@ static TraceCtx trace_ctx(mcrt_scene s) {
     c.spillCap = s->spillCap;
     c.overflow = s->ctx->dFlags;
     c.twoLevel = s->twoLevel ? 1 : 0;
-    c.top = (const float4*)s->dTop;
-    c.topNodes = s->twoLevel ? 0 : s->topNodes;
     return c;
 }
 
@@ -518,7 +514,7 @@ MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx) {
 static void scene_free_device(mcrt_scene s) {
     void** ptrs[] = {&s->dShapes, &s->dIndices, &s->dPositions, &s->dUvs, &s->dNormals, &s->dTextures,
                      &s->dTexData, &s->dSobol, &s->dLights, &s->dMaterials, &s->dNodes, &s->dTris,
-                     &s->dSurf, &s->dSurfBase, &s->dSurfMeshes, &s->dTop};
+                     &s->dSurf, &s->dSurfBase, &s->dSurfMeshes};
     for (void** p : ptrs) {
         if (*p) hipFree(*p);
         *p = nullptr;
@@ -833,14 +829,6 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
     s->packets = !s->twoLevel && 2 * (s->bvhDepth + 1) <= MCRT_PK_STACK && !(pe && std::atoi(pe) == 0);
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
-    s->topNodes = 0;
-    if (!s->twoLevel) {   // the top records the traversal launches stage in LDS
-        if (!s->dTop) HIPCHK(ctx, hipMalloc(&s->dTop, 64 * MCRT_TOP_NODES));
-        mcrt::launch_build_top((const float4*)s->dNodes, (float4*)s->dTop, s->dScratch + 255, ctx->stream);
-        HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipMemcpyAsync(&s->topNodes, s->dScratch + 255, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    }
     int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries
     // test hook: MCRT_TEST_SPILL_CAP=k caps the spill columns at k entries (0 = LDS stack only) so a
     // test can drive a traversal past its capacity and check that the overflow is reported
@@ -1551,8 +1539,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
         HIPCHK(ctx, slot_alloc(slot, fb->N, count, qNeed));
     }
     const int cap = s->spillCap;
-    // (+ 512: the 4-wave traversal workgroups round each of a launch's two sections up to 256 rays)
-    const size_t spillRays = (std::max((size_t)bandPaths, 2 * qNeed + 512) + 63) / 64 * 64;
+    const size_t spillRays = (std::max((size_t)bandPaths, 2 * qNeed + 64) + 63) / 64 * 64;
     if (!slot.spill || slot.spillWords < spillRays * cap) {
         HIPCHK(ctx, hipStreamSynchronize(slot.stream));
         if (slot.spill) hipFree(slot.spill);

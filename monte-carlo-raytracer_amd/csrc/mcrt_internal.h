@@ -86,13 +86,7 @@ struct TraceCtx {
     uint32_t* spill;
     int spillCap;           // spill entries per ray (a multiple of STACK_LDS)
     int* overflow;
-    // the first topNodes internal records in breadth-first order, children remapped (MCRT_TOP_BASE +
-    // slot for a child in this set): the traversal launches stage them in LDS (mcrt_traverse.h)
-    const float4* top;
-    int topNodes;
 };
-#define MCRT_TOP_NODES 64          // records of the LDS-resident top of a flat tree (4 KB)
-#define MCRT_TOP_BASE (1 << 30)    // node words >= this address the LDS copy
 
 namespace mcrt {
 // n rays, or with countDev (device memory) min(*countDev, n) of them
@@ -110,7 +104,6 @@ void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const 
                    hipStream_t st);
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st);
-void launch_build_top(const float4* nodes, float4* top, int* count, hipStream_t st);
 void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
                           const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
                           float4* radiance, int maxExt, int maxShadow, hipStream_t st);

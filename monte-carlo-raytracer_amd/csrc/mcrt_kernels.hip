@@ -300,126 +300,6 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
     }
 }
 
-// The LDS-resident top of a flat tree (TraceCtx::top): the first MCRT_TOP_NODES internal records in
-// breadth-first order, child words of children inside the set remapped to MCRT_TOP_BASE + slot.
-// One thread (a few hundred records read once per accel build).
-__global__ void k_build_top(const float4* __restrict__ nodes, float4* __restrict__ top, int* __restrict__ count) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    int idx[MCRT_TOP_NODES];
-    int n = 0;
-    auto internal = [&](int i) { return reinterpret_cast<const int4*>(&nodes[4 * i + 3])->x >= 0; };
-    if (internal(0)) idx[n++] = 0;
-    for (int i = 0; i < n; ++i) {
-        const int4 c = *reinterpret_cast<const int4*>(&nodes[4 * idx[i] + 3]);
-        if (n < MCRT_TOP_NODES && internal(c.x)) idx[n++] = c.x;
-        if (n < MCRT_TOP_NODES && internal(c.y)) idx[n++] = c.y;
-    }
-    for (int i = 0; i < n; ++i) {
-        for (int k = 0; k < 3; ++k) top[4 * i + k] = nodes[4 * idx[i] + k];
-        int4 c = *reinterpret_cast<const int4*>(&nodes[4 * idx[i] + 3]);
-        for (int j = 0; j < n; ++j) {
-            if (idx[j] == c.x) c.x = MCRT_TOP_BASE + j;
-            if (idx[j] == c.y) c.y = MCRT_TOP_BASE + j;
-        }
-        *reinterpret_cast<int4*>(&top[4 * i + 3]) = c;
-    }
-    *count = n;
-}
-
-#if MCRT_LDS_TOP
-// k_shadow_extend / k_extend / k_shadow with 4-wave workgroups sharing one LDS copy of the top of
-// the tree (4 KB) next to their 4 per-wave stacks (16 KB).
-#define TOP_BLOCK 256
-template <int LAY>
-__global__ __launch_bounds__(TOP_BLOCK) void k_shadow_extend_top(TraceCtx c, const int* __restrict__ extCount,
-                                                                 const float4* __restrict__ qO, const float4* __restrict__ qD,
-                                                                 float4* __restrict__ hitOut, const int* __restrict__ shadowCount,
-                                                                 const float4* __restrict__ sO, const float4* __restrict__ sD,
-                                                                 const float4* __restrict__ sL, float4* __restrict__ radiance) {
-    __shared__ __attribute__((aligned(16))) uint32_t ldsAll[TOP_BLOCK / 64][STACK_LDS * 64];
-    __shared__ float4 top[4 * MCRT_TOP_NODES];
-    const int ne = *extCount;
-    const int eb = (ne + TOP_BLOCK - 1) / TOP_BLOCK;
-    const int ns = *shadowCount;
-    const int sb = (ns + TOP_BLOCK - 1) / TOP_BLOCK;
-    if ((int)blockIdx.x >= eb + sb) return;   // whole block past both queues: uniform exit
-    loadTop(c, top);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t* lds = ldsAll[wv];
-    if ((int)blockIdx.x < eb) {
-        const int blk = xcdRemap(blockIdx.x, eb);
-        const int i = blk * TOP_BLOCK + (int)threadIdx.x;
-        if (i >= ne) return;
-        const float4 o = qO[i], d = qD[i];
-        TraceRay r;
-        r.o = ld3(o);
-        r.d = ld3(d);
-        r.tmax = RT_MAX_TRACE_F;
-        r.mask = -1;
-        float t;
-#if MCRT_TOP_OFF   // A/B: the 4-wave workgroups without the LDS copy
-        const int tri = traverse<false, LAY_PLAIN>(c, r, lds + lane, raySpill(c, blk * (TOP_BLOCK / 64) + wv, lane), t);
-#else
-        const int tri = traverseTop<false>(c, r, lds + lane, raySpill(c, blk * (TOP_BLOCK / 64) + wv, lane), top, t);
-#endif
-        hitOut[i] = closestRecord(c.nodes, r, tri, t);
-    } else {
-        const int sblk = xcdRemap((int)blockIdx.x - eb, sb);
-        const int i = sblk * TOP_BLOCK + (int)threadIdx.x;
-        if (c.packet) {   // bounce-0 shadow rays: wave packets, as k_shadow_extend
-            const bool valid = i < ns;
-            TraceRay r;
-            r.o = splat3(0.0f);
-            r.d = f3{0.0f, 0.0f, 1.0f};
-            r.tmax = 0.0f;
-            float4 d = make_float4(0.f, 0.f, 1.f, 0.f);
-            if (valid) {
-                const float4 o = sO[i];
-                d = sD[i];
-                r.o = ld3(o);
-                r.d = ld3(d);
-                r.tmax = o.w;
-            }
-            r.mask = -1;
-            float tt;
-            const bool occ = traversePacket<true>(c.nodes, r, valid, lds, pkMasks(lds), c.overflow, tt) >= 0;
-            if (valid) {
-                const float V = occ ? 0.0f : 1.0f;
-                const float4 L = sL[i];
-                const int pix = __float_as_int(d.w);
-                float4 acc = radiance[pix];
-                acc.x += L.x * V;
-                acc.y += L.y * V;
-                acc.z += L.z * V;
-                radiance[pix] = acc;
-            }
-            return;
-        }
-        if (i >= ns) return;
-        const float4 o = sO[i], d = sD[i], L = sL[i];
-        TraceRay r;
-        r.o = ld3(o);
-        r.d = ld3(d);
-        r.tmax = o.w;
-        r.mask = -1;
-        float tt;
-#if MCRT_TOP_OFF
-        const float V = traverse<true, LAY_PLAIN>(c, r, lds + lane, raySpill(c, blockIdx.x * (TOP_BLOCK / 64) + wv, lane),
-                                                  tt) >= 0 ? 0.0f : 1.0f;
-#else
-        const float V = traverseTop<true>(c, r, lds + lane, raySpill(c, blockIdx.x * (TOP_BLOCK / 64) + wv, lane), top,
-                                          tt) >= 0 ? 0.0f : 1.0f;
-#endif
-        const int pix = __float_as_int(d.w);
-        float4 acc = radiance[pix];
-        acc.x += L.x * V;
-        acc.y += L.y * V;
-        acc.z += L.z * V;
-        radiance[pix] = acc;
-    }
-}
-#endif
-
 // Closest hit over two queues in ONE launch: BDPT's first camera rays (coherent: wave packets when
 // cc.packet) and first light rays (per ray, c).  The camera
 // workgroups come first; the light workgroups fill their tail (as k_shadow_extend).
@@ -999,20 +879,9 @@ void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const 
     hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, sO, sD, sL, radiance);
 }
-void launch_build_top(const float4* nodes, float4* top, int* count, hipStream_t st) {
-    hipLaunchKernelGGL(k_build_top, dim3(1), dim3(64), 0, st, nodes, top, count);
-}
 void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
                           const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
                           float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
-#if MCRT_LDS_TOP
-    if (!c.twoLevel) {
-        const int tb = (maxExt + TOP_BLOCK - 1) / TOP_BLOCK + (maxShadow + TOP_BLOCK - 1) / TOP_BLOCK;
-        hipLaunchKernelGGL(k_shadow_extend_top<LAY_PLAIN>, dim3(tb > 0 ? tb : 1), dim3(TOP_BLOCK), 0, st, c, extCount,
-                           qO, qD, hits, shadowCount, sO, sD, sL, radiance);
-        return;
-    }
-#endif
     const int blocks = (maxExt + 63) / 64 + (maxShadow + 63) / 64;
     hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_PLAIN>),
                        dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, extCount, qO, qD, hits, shadowCount, sO, sD,

@@ -65,36 +65,23 @@ MCRT_DEV float triHit(const TraceRay& r, float4 A, float4 E1, float4 E2, float t
 // tests its triangle.  Returns the hit leaf's node index or -1; tHit = hit distance.
 // stk: this lane's LDS stack column ([entry][lane], conflict free); spill: global overflow.
 // OCT: the wave's common ray-direction octant (bit k = sign of 1/d along axis k), -1 = mixed.
-// TOP: the first internal records (breadth first) sit in LDS (ldsTop, TraceCtx::top): a node word
-// >= MCRT_TOP_BASE addresses that copy, whose child words point back into it where they can; the
-// visit order, and so every result, is that of the plain walk.
-template <bool ANY, int OCT, bool TOP = false>
+template <bool ANY, int OCT>
 MCRT_DEV int traverseOct(const float4* __restrict__ nodes, const TraceRay& r, f3 inv, uint32_t* stk, uint32_t* spill,
-                         int spillCap, int* overflowFlag, float& tHit, const float4* ldsTop = nullptr, int top0 = 0) {
+                         int spillCap, int* overflowFlag, float& tHit) {
     // One flat loop with a single exit (node == DONE): stack entry 0 is a DONE sentinel, so a
     // pop is one LDS read and no lane idles at a nested loop boundary waiting for the others.
     constexpr int DONE = -1, POP = -2;
     const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
     float t = r.tmax;
     int hit = -1;
-    int node = TOP ? top0 : 0;
+    int node = 0;
     stk[0] = (uint32_t)DONE;
     int sp = 1, spillTop = 0;
     while (node != DONE) {
-        float4 n0, n1, n2;
-        int4 n3;
-        if (TOP && node >= MCRT_TOP_BASE) {
-            const float4* q = ldsTop + 4 * (node - MCRT_TOP_BASE);
-            n0 = q[0];
-            n1 = q[1];
-            n2 = q[2];
-            n3 = *reinterpret_cast<const int4*>(&q[3]);
-        } else {
-            n0 = nodes[4 * node + 0];
-            n1 = nodes[4 * node + 1];
-            n2 = nodes[4 * node + 2];
-            n3 = *reinterpret_cast<const int4*>(&nodes[4 * node + 3]);
-        }
+        const float4 n0 = nodes[4 * node + 0];
+        const float4 n1 = nodes[4 * node + 1];
+        const float4 n2 = nodes[4 * node + 2];
+        const int4 n3 = *reinterpret_cast<const int4*>(&nodes[4 * node + 3]);
         // keep the whole 64-B record in one round trip: without this the compiler defers the
         // two words only internal nodes use into a second, dependent load after the branch
         asm volatile("" ::"v"(n1.w), "v"(n2.w));
@@ -367,40 +354,6 @@ MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint3
     }
     MCRT_TRAV_CALL(-1);
 #undef MCRT_TRAV_CALL
-}
-
-// traverse<ANY, LAY_PLAIN> with the top of the tree staged in LDS (ldsTop: c.topNodes records).
-template <bool ANY>
-MCRT_DEV int traverseTop(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, const float4* ldsTop,
-                         float& tHit) {
-    const f3 inv = safeInvDir(r.d);
-    const int top0 = c.topNodes > 0 ? MCRT_TOP_BASE : 0;
-#define MCRT_TRAV_CALL(OCT) \
-    return traverseOct<ANY, OCT, true>(c.nodes, r, inv, stk, spill, c.spillCap, c.overflow, tHit, ldsTop, top0)
-    const int oct = (int)(__float_as_uint(inv.x) >> 31) | (int)((__float_as_uint(inv.y) >> 31) << 1) |
-                    (int)((__float_as_uint(inv.z) >> 31) << 2);
-    const int oct0 = __builtin_amdgcn_readfirstlane(oct);
-    if (__all(oct == oct0)) {
-        switch (oct0) {
-            case 0: MCRT_TRAV_CALL(0);
-            case 1: MCRT_TRAV_CALL(1);
-            case 2: MCRT_TRAV_CALL(2);
-            case 3: MCRT_TRAV_CALL(3);
-            case 4: MCRT_TRAV_CALL(4);
-            case 5: MCRT_TRAV_CALL(5);
-            case 6: MCRT_TRAV_CALL(6);
-            case 7: MCRT_TRAV_CALL(7);
-            default: break;
-        }
-    }
-    MCRT_TRAV_CALL(-1);
-#undef MCRT_TRAV_CALL
-}
-
-// Stages the top records in LDS (every thread of the block calls; ends with a barrier).
-MCRT_DEV void loadTop(const TraceCtx& c, float4* ldsTop) {
-    for (int i = threadIdx.x; i < 4 * c.topNodes; i += blockDim.x) ldsTop[i] = c.top[i];
-    __syncthreads();
 }
 
 // RR common.cl:249-277 (triangle_calculate_barycentrics)
