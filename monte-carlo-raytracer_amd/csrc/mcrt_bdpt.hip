@@ -33,12 +33,16 @@
 //
 // Arithmetic mirrors the reference expressions (mcrt_device.h conventions: cl_div = the 2.5-ulp
 // OpenCL division, contraction as ROCm clang does at -O3 with FP_CONTRACT ON).
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "mcrt_device.h"
 #include "mcrt_internal.h"
 #include "mcrt_traverse.h"
 #include "mcrt_shading.h"
 
 #define BDPT_BLOCK 256
+#define BDPT_LIGHT_KEY_BITS 13
+#define BDPT_LIGHT_KEY_NONE ((1u << BDPT_LIGHT_KEY_BITS) - 1)
 
 // RTBDPTVertexType / RTBDPTVertexFlag (kernel_data.h:202-218)
 enum { RT_BDPT_CAMERA_VERTEX = 0, RT_BDPT_LIGHT_VERTEX = 1, RT_BDPT_SURFACE_VERTEX = 2 };
@@ -459,6 +463,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
     const int px = y * (int)f.W + x, pix = k * N + px;   // pix: the path (plane index)
     f3 camDir = splat3(0.0f), camPos = splat3(0.0f), lo = splat3(0.0f), ld = splat3(0.0f), lt = splat3(0.0f);
     float camPdf = 0.0f, lightPdfDir = 0.0f;
+    uint32_t key = BDPT_LIGHT_KEY_NONE;   // the light ray's cell (b.lightKey): invalid slots sort last
     if (valid) {
         const mcrt_camera& cam = camp[k];
         b.splat[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -487,6 +492,15 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
         const f2 u1 = getSample2D(sampler);
         const f2 u2 = getSample2D(sampler);
         const LightLe le = sampleLightLe(s, light, u1, u2);
+        // cell of the ray for the light-queue sort: a directional light's rays are parallel, so
+        // the 64 x 64 grid of its disk sample u1 (concentricSampleDisc keeps cells compact) groups
+        // rays that walk the same nodes; other lights by light and a 4 x 4 grid of the direction
+        // sample u2
+        if (light.type == MCRT_DIRECTIONAL_LIGHT)
+            key = (uint32_t)min((int)(u1.y * 64.0f), 63) * 64u + (uint32_t)min((int)(u1.x * 64.0f), 63);
+        else
+            key = 4096u + (((uint32_t)chosen * 16u + (uint32_t)min((int)(u2.y * 4.0f), 3) * 4u +
+                            (uint32_t)min((int)(u2.x * 4.0f), 3)) & 1023u);
         BVertex lv = createLightVertex(chosen, le.origin, le.normal, le.Le, le.pdfPos * lightPdf, light.flags);
         lv.pdfPos = le.pdfPos;
         if (b.depth0Const) {   // planes 4-5 (sdpdu|uv.x, sdpdv|uv.y) of a light vertex are always zero
@@ -512,25 +526,33 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
         const f3 up = f3{0.0f, 1.0f, 0.0f};
         pushRay(camQ, slot, camPos, valid ? 2 * pix : -1, valid ? camDir : up, camPdf, splat3(1.0f));
         pushRay(lightQ, slot, lo, valid ? 2 * pix + 1 : -1, valid ? ld : up, lightPdfDir, lt);
+        if (b.lightKey) {
+            b.lightKey[slot] = key;
+            b.lightSlot[slot] = (uint32_t)slot;
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) camQ.count[0] = lightQ.count[0] = f.numTiles * f.batch * 64;
 }
 
 // GenerateSecondaryVertices (BDPT.cl:317-458) for every queued subpath ray at depth d.
+// perm (optional): qIn walked in this order (the sorted light-start rays): the j-th thread takes
+// slot perm[j], so the next rays are appended in the sorted order too -- the light paths' second
+// segments leave neighbouring points.
 __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameArgs f, BdptArgs b, int depth,
                                                             BdptQueue qIn, const float4* __restrict__ hits,
-                                                            BdptQueue qOut) {
+                                                            BdptQueue qOut, const uint32_t* __restrict__ perm) {
     const int n = *qIn.count;
     __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
     if ((int)blockIdx.x * BDPT_BLOCK >= n) return;
-    const int i = xcdRemap(blockIdx.x, (n + BDPT_BLOCK - 1) / BDPT_BLOCK) * BDPT_BLOCK + threadIdx.x;
+    const int j = xcdRemap(blockIdx.x, (n + BDPT_BLOCK - 1) / BDPT_BLOCK) * BDPT_BLOCK + threadIdx.x;
+    const int i = perm && j < n ? (int)perm[j] : j;
     const int N = (int)(f.W * f.H) * f.batch;   // plane stride (NB)
     const int D = f.maxDepth;
     bool push = false;
     f3 no = splat3(0.0f), nd = splat3(0.0f), ntp = splat3(0.0f);
     float nPdf = 0.0f;
     int tag = 0;
-    const float4 O = i < n ? qIn.o[i] : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+    const float4 O = j < n ? qIn.o[i] : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
     tag = __float_as_int(O.w);
     if (tag >= 0) {   // tag -1: a start-queue slot outside the image
         const float4 Dd = qIn.d[i], Tp = qIn.t[i];
@@ -991,16 +1013,30 @@ __global__ __launch_bounds__(256) void k_bdpt_clear_splat(int n, float4* __restr
 }
 
 namespace mcrt {
+// The light-start queue in cell order (k_bdpt_start's keys): rocPRIM radix sort of (key, slot)
+// over the key's 13 bits; perm[j] = the slot traced j-th.  The queue itself stays in slot (tile)
+// order for the vertex launch; only the traversal walks it sorted (k_extend_pair).
+size_t bdpt_light_sort_temp_bytes(int n) {
+    size_t bytes = 0;
+    uint32_t* k = nullptr;
+    rocprim::radix_sort_pairs(nullptr, bytes, k, k, k, k, (size_t)n, 0, BDPT_LIGHT_KEY_BITS, (hipStream_t)0);
+    return bytes;
+}
+hipError_t bdpt_light_sort(uint32_t* keys, uint32_t* keys2, uint32_t* slots, uint32_t* perm, int n, void* tmp,
+                           size_t tmpBytes, hipStream_t st) {
+    return rocprim::radix_sort_pairs(tmp, tmpBytes, keys, keys2, slots, perm, (size_t)n, 0, BDPT_LIGHT_KEY_BITS, st);
+}
+
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& camQ, const BdptQueue& lightQ, hipStream_t st) {
     const int blocks = (f.numTiles * f.batch * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK;
     hipLaunchKernelGGL(k_bdpt_start, dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, camQ, lightQ);
 }
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
-                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st) {
+                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st, const uint32_t* perm) {
     const int blocks = (maxCount + BDPT_BLOCK - 1) / BDPT_BLOCK;
     hipLaunchKernelGGL(k_bdpt_vertex, dim3(blocks > 0 ? blocks : 1), dim3(BDPT_BLOCK), 0, st, s, f, b, depth, qIn, hits,
-                       qOut);
+                       qOut, perm);
 }
 void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                          const BdptQueue& q, hipStream_t st) {

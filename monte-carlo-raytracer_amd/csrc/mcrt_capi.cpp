@@ -145,6 +145,10 @@ struct BdptSet {
     float4 *bqO[2] = {}, *bqD[2] = {}, *bqT[2] = {}, *bHits = nullptr;
     float4 *cO = nullptr, *cD = nullptr, *cL = nullptr;
     uint32_t* spill = nullptr;   // traversal spill columns of this set's launches
+    // the light-start queue's sort (mcrt::bdpt_light_sort): keys, sorted keys, slots, permutation
+    uint32_t *lkey = nullptr, *lkey2 = nullptr, *lslot = nullptr, *lperm = nullptr;
+    void* sortTmp = nullptr;
+    size_t sortTmpBytes = 0;
     int frames = 0;              // batch frames the per-frame arrays hold (plane stride N x frames)
     size_t spillWords = 0;
     // plane stride and band (rows, count, index) whose depth-0 frame-invariant planes k_bdpt_start
@@ -1049,7 +1053,8 @@ MCRT_API mcrt_status mcrt_event_destroy(mcrt_event ev) {
 // ---------------------------------------------------------------------------
 static void bset_free(BdptSet& b) {
     void* ptrs[] = {b.camV,   b.lightV, b.slots,  b.splat,  b.camCount, b.lightCount, b.bdptCounters,
-                    b.bqO[0], b.bqO[1], b.bqD[0], b.bqD[1], b.bqT[0], b.bqT[1], b.bHits, b.cO, b.cD, b.cL, b.spill};
+                    b.bqO[0], b.bqO[1], b.bqD[0], b.bqD[1], b.bqT[0], b.bqT[1], b.bHits, b.cO, b.cD, b.cL, b.spill,
+                    b.lkey, b.lkey2, b.lslot, b.lperm, b.sortTmp};
     for (void* p : ptrs)
         if (p) hipFree(p);
     b = BdptSet();
@@ -1169,6 +1174,12 @@ static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D, int frames,
     A(&b.cO, 16 * N * C);
     A(&b.cD, 16 * N * C);
     A(&b.cL, 16 * N * C);
+    A(&b.lkey, 4 * NQ);
+    A(&b.lkey2, 4 * NQ);
+    A(&b.lslot, 4 * NQ);
+    A(&b.lperm, 4 * NQ);
+    b.sortTmpBytes = mcrt::bdpt_light_sort_temp_bytes((int)NQ);
+    A(&b.sortTmp, b.sortTmpBytes);
     // zero-fills on the stream of the set's frames (st, its slot's), ahead of the first launch
     // that writes the set: a 3 GB vertex-plane memset on another stream could still be running
     // under k_bdpt_start and zero its vertices
@@ -1375,6 +1386,13 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     b.splat = fb->splat;
     b.ownSlots = (int)C - D;
     // (planes at another stride hold other data; another band's paths were never written)
+    // light-start rays traced in cell order (MCRT_BDPT_LIGHT_SORT: 0 off, 1 sorted, 2 sorted + packets)
+    static const int lightSort = [] {
+        const char* e = std::getenv("MCRT_BDPT_LIGHT_SORT");
+        return e ? std::atoi(e) : 0;
+    }();
+    b.lightKey = lightSort ? bs.lkey : nullptr;
+    b.lightSlot = bs.lslot;
     b.depth0Const = bs.constStride == N && bs.constBand[0] == f.bandRows && bs.constBand[1] == f.numBands &&
                     bs.constBand[2] == f.bandIndex ? 1 : 0;
     bs.constStride = N;
@@ -1410,8 +1428,12 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         TraceCtx tcc = packet_ctx(s);
         tcc.spill = bs.spill;
         Timed t(ctx, K_EXTEND, camQ.count, 0, st);
+        if (b.lightKey)
+            // exactly the slots k_bdpt_start wrote (the light queue's count, f.numTiles x 64 x B <= NQ)
+            HIPCHK(ctx, mcrt::bdpt_light_sort(bs.lkey, bs.lkey2, bs.lslot, bs.lperm, f.numTiles * 64 * B, bs.sortTmp,
+                                              bs.sortTmpBytes, st));
         mcrt::launch_extend_pair(tcc, tcs, camQ.count, camQ.o, camQ.d, fb->bHits, lightQ.count, lightQ.o, lightQ.d,
-                                 fb->bHits + NQ, (int)NQ, (int)NQ, st);
+                                 fb->bHits + NQ, (int)NQ, (int)NQ, st, b.lightKey ? bs.lperm : nullptr);
     }
     {
         Timed t(ctx, K_BDPT_VERTEX, camQ.count, 0, st);
@@ -1419,7 +1441,8 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     }
     {
         Timed t(ctx, K_BDPT_VERTEX, lightQ.count, 0, st);
-        mcrt::launch_bdpt_vertex(sa, f, b, 1, lightQ, fb->bHits + NQ, queue(1), (int)NQ, st);
+        mcrt::launch_bdpt_vertex(sa, f, b, 1, lightQ, fb->bHits + NQ, queue(1), (int)NQ, st,
+                                 b.lightKey && lightSort >= 3 ? bs.lperm : nullptr);
     }
     for (int d = 2; d <= D + 1; ++d) {
         const BdptQueue qIn = queue(d - 1), qOut = queue(d);

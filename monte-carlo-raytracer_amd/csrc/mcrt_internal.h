@@ -69,6 +69,8 @@ struct BdptArgs {
     int ownSlots;        // strategies with t >= 2 = maxConnections - D
     int depth0Const;     // 1: the frame-invariant planes of the depth-0 vertices are already in place
                          // at this plane stride (k_bdpt_start writes only the per-frame ones)
+    uint32_t* lightKey;  // per start-queue slot: the light ray's origin / direction cell (NULL: no sort)
+    uint32_t* lightSlot; //   and its slot (the radix sort's values)
 };
 struct BdptQueue {
     int* count;
@@ -97,9 +99,13 @@ void launch_surface_records(const uint32_t* meshStartIdx, const uint32_t* meshSt
                             const float2* uvs, const float4* normals, float4* surf, hipStream_t st);
 void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* cam, float4* hits, hipStream_t st);
 // closest hit over two queues in one launch: queue 0 over cc's records, queue 1 over c's
+// the light-start queue of a BDPT call sorted by cell (keys, slots from k_bdpt_start) -> perm
+size_t bdpt_light_sort_temp_bytes(int n);
+hipError_t bdpt_light_sort(uint32_t* keys, uint32_t* keys2, uint32_t* slots, uint32_t* perm, int n, void* tmp,
+                           size_t tmpBytes, hipStream_t st);
 void launch_extend_pair(const TraceCtx& cc, const TraceCtx& c, const int* count0, const float4* qO0, const float4* qD0,
                         float4* hit0, const int* count1, const float4* qO1, const float4* qD1, float4* hit1,
-                        int maxCount0, int maxCount1, hipStream_t st);
+                        int maxCount0, int maxCount1, hipStream_t st, const uint32_t* perm1 = nullptr);
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
                    hipStream_t st);
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
@@ -128,7 +134,8 @@ void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* s
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& camQ, const BdptQueue& lightQ, hipStream_t st);
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
-                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st);
+                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st,
+                        const uint32_t* perm = nullptr);
 void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                          const BdptQueue& q, hipStream_t st);
 // k_bdpt_vis is a grid-stride launch of at most this many one-wave workgroups (spill columns per wave)

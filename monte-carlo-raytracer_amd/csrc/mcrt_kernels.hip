@@ -303,12 +303,16 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
 // Closest hit over two queues in ONE launch: BDPT's first camera rays (coherent: wave packets when
 // cc.packet) and first light rays (per ray, c).  The camera
 // workgroups come first; the light workgroups fill their tail (as k_shadow_extend).
+// perm1 (optional): queue 1 walked in this order (BDPT's light rays sorted by origin / direction
+// cell, mcrt::bdpt_light_sort): the j-th ray traced is slot perm1[j], its hit record goes back to
+// that slot.  (As wave packets, the sorted parallel rays of a directional light ran 16 % slower
+// than per ray: profiles/r04/ab/README.txt.)
 template <int LAY0, int LAY1>
 __global__ __launch_bounds__(64) void k_extend_pair(TraceCtx cc, TraceCtx c, const int* __restrict__ count0,
                                                     const float4* __restrict__ qO0, const float4* __restrict__ qD0,
                                                     float4* __restrict__ hit0, const int* __restrict__ count1,
                                                     const float4* __restrict__ qO1, const float4* __restrict__ qD1,
-                                                    float4* __restrict__ hit1) {
+                                                    float4* __restrict__ hit1, const uint32_t* __restrict__ perm1) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[STACK_LDS * 64];
     const int n0 = *count0;
     const int b0 = (n0 + 63) >> 6;
@@ -336,8 +340,16 @@ __global__ __launch_bounds__(64) void k_extend_pair(TraceCtx cc, TraceCtx c, con
         const int n1 = *count1;
         const int b1 = (n1 + 63) >> 6;
         if ((int)blockIdx.x - b0 >= b1) return;
-        const int i = xcdRemap((int)blockIdx.x - b0, b1) * 64 + lane;
-        if (i >= n1) return;
+        const int j = xcdRemap((int)blockIdx.x - b0, b1) * 64 + lane;
+        if (perm1 == nullptr) {
+            if (j >= n1) return;
+            r.o = ld3(qO1[j]);
+            r.d = ld3(qD1[j]);
+            hit1[j] = traceClosest<LAY1>(c, r, lds + lane, raySpill(c, blockIdx.x, lane), t);
+            return;
+        }
+        if (j >= n1) return;
+        const int i = (int)perm1[j];
         r.o = ld3(qO1[i]);
         r.d = ld3(qD1[i]);
         hit1[i] = traceClosest<LAY1>(c, r, lds + lane, raySpill(c, blockIdx.x, lane), t);
@@ -868,11 +880,11 @@ void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const 
 }
 void launch_extend_pair(const TraceCtx& cc, const TraceCtx& c, const int* count0, const float4* qO0, const float4* qD0,
                         float4* hit0, const int* count1, const float4* qO1, const float4* qD1, float4* hit1,
-                        int maxCount0, int maxCount1, hipStream_t st) {
+                        int maxCount0, int maxCount1, hipStream_t st, const uint32_t* perm1) {
     auto k = c.twoLevel ? k_extend_pair<LAY_TWO_LEVEL, LAY_TWO_LEVEL> : k_extend_pair<LAY_PLAIN, LAY_PLAIN>;
     const int blocks = (maxCount0 + 63) / 64 + (maxCount1 + 63) / 64;
     hipLaunchKernelGGL(k, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, cc, c, count0, qO0, qD0, hit0, count1, qO1,
-                       qD1, hit1);
+                       qD1, hit1, perm1);
 }
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st) {
