@@ -273,18 +273,46 @@ MCRT_DEV LightLe sampleLightLe(const SceneArgs& s, const mcrt_light& light, f2 u
 }
 
 // --- materials.cl with transport modes ----------------------------------------------------
-// evaluateMaterial / evaluateMaterialPdf (materials.cl:120-142) of a stored surface vertex: the
-// uber properties come from the vertex's planes 8-12 (the same getUberMaterialProperties values
-// the reference recomputes from the textures at every call).  Non-uber materials evaluate to 0.
-MCRT_DEV f3 evaluateMaterialV(const BVertex& v, int pix, int N, f3 wo, f3 wi, int mode) {
+// A material whose uber properties do not depend on the hit (not an uber material, or no texture
+// behind any property) gives getUberMaterialProperties' values from the material alone: the vertex
+// launch stores no material planes for it and the connections recompute them from the material
+// record (cached; the same floats: uberProps without a texture read is a function of the
+// material only), instead of streaming 80 B per vertex through HBM twice.
+MCRT_DEV bool uberFromMaterial(const mcrt_material& m) {
+    return m.type != 0 || (m.uber_diffuseTexId == -1 && m.uber_glossyTexId == -1 && m.uber_specReflectionTexId == -1 &&
+                           m.uber_transmissionTexId == -1 && m.uber_opacityTexId == -1 &&
+                           m.uber_roughnessTexId == -1 && m.uber_iorTexId == -1);
+}
+// getUberMaterialProperties of a stored surface vertex: from its material when uberFromMaterial,
+// else from the vertex's planes 8-12 (written by k_bdpt_vertex at its uv)
+MCRT_DEV Uber vertexUber(const SceneArgs& s, const BVertex& v, int pix, int N, int* matType) {
+    const mcrt_material& m = s.materials[v.materialIdx];
+    if (uberFromMaterial(m)) {
+        *matType = m.type;
+        if (m.type != 0) {
+            Uber z;
+            z.Kd = z.Ks = z.Kr = z.opacity = splat3(0.0f);
+            z.Kt = f4{0.0f, 0.0f, 0.0f, 0.0f};
+            z.roughness = f2{0.0f, 0.0f};
+            z.eta = 0.0f;
+            return z;
+        }
+        return uberProps(s, m, v.fr.uv);
+    }
+    return loadUber(v.planes, v.depth, pix, N, matType);
+}
+// evaluateMaterial / evaluateMaterialPdf (materials.cl:120-142) of a stored surface vertex with
+// the uber properties of vertexUber (the same getUberMaterialProperties values the reference
+// recomputes from the textures at every call).  Non-uber materials evaluate to 0.
+MCRT_DEV f3 evaluateMaterialV(const SceneArgs& s, const BVertex& v, int pix, int N, f3 wo, f3 wi, int mode) {
     int type;
-    const Uber um = loadUber(v.planes, v.depth, pix, N, &type);
+    const Uber um = vertexUber(s, v, pix, N, &type);
     if (type != 0) return splat3(0.0f);
     return evaluateUberBSDF(um, v.fr, wo, wi, mode);
 }
-MCRT_DEV float evaluateMaterialPdfV(const BVertex& v, int pix, int N, f3 wo, f3 wi) {
+MCRT_DEV float evaluateMaterialPdfV(const SceneArgs& s, const BVertex& v, int pix, int N, f3 wo, f3 wi) {
     int type;
-    const Uber um = loadUber(v.planes, v.depth, pix, N, &type);
+    const Uber um = vertexUber(s, v, pix, N, &type);
     if (type != 0) return 0.0f;
     return evaluateUberBSDF_Pdf(um, v.fr, wo, wi);
 }
@@ -373,18 +401,18 @@ MCRT_DEV float evalVertexPdf(const SceneArgs& s, const mcrt_camera& cam, const B
             if (isNearZero(lenSq)) return 0.0f;
             wp = cl_div(wp, cl_sqrt(lenSq));
         }
-        pdf = evaluateMaterialPdfV(v, pix, N, wp, wn);
+        pdf = evaluateMaterialPdfV(s, v, pix, N, wp, wn);
     }
     return convertVertexDensity(pdf, v.fr.p, next);
 }
 // evalVertex_f(this, next, mode) (BDPT.cl:215-235)
-MCRT_DEV f3 evalVertex_f(const BVertex& v, int pix, int N, f3 nextP, int mode) {
+MCRT_DEV f3 evalVertex_f(const SceneArgs& s, const BVertex& v, int pix, int N, f3 nextP, int mode) {
     f3 wi = nextP - v.fr.p;
     const float lenSq = cl_dot(wi, wi);
     if (isNearZero(lenSq)) return splat3(0.0f);
     wi = cl_div(wi, cl_sqrt(lenSq));
     if (v.type == RT_BDPT_SURFACE_VERTEX) {
-        const f3 f = evaluateMaterialV(v, pix, N, v.wo, wi, mode);
+        const f3 f = evaluateMaterialV(s, v, pix, N, v.wo, wi, mode);
         return f * shadingNormalCorrection(v.fr, v.wo, wi, mode);
     }
     return f3{1.0f, 0.0784f, 0.5765f};
@@ -583,7 +611,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                 um.roughness = f2{0.0f, 0.0f};
                 um.eta = 0.0f;
             }
-            storeUber(V, depth, pix, N, um, mat.type);
+            if (!uberFromMaterial(mat)) storeUber(V, depth, pix, N, um, mat.type);   // else: vertexUber
             const int mode = isCamera ? TRANSPORT_MODE_RADIANCE : TRANSPORT_MODE_IMPORTANCE;
             const BVertexPos prev = loadVertexPos(V, depth - 1, pix, N);
             float pdfFwd = Dd.w;
@@ -761,7 +789,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                     ix = min(max(ix, 0), (int)f.W - 1);
                     iy = min(max(iy, 0), (int)f.H - 1);
                     code = ~(k * N0 + ix + iy * (int)f.W);   // frame k's splat plane
-                    L = lv.throughput * samp.throughput * evalVertex_f(lv, pix, N, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                    L = lv.throughput * samp.throughput * evalVertex_f(s, lv, pix, N, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
                     if (isVertexOnSurface(lv.fr.gn)) L *= absDot(wi, lv.fr.sn);
                     rayO = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
                     rayT = cl_distance(rayO, ld3(cam.pos));
@@ -797,7 +825,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                                              pdfFwdS, light.flags);
                     *stale = make_float4(samp.fr.p.x, samp.fr.p.y, samp.fr.p.z,
                                          __int_as_float((samp.flags << 16) | (chosen & 0xffff)));
-                    const f3 fm = evaluateMaterialV(cv, pix, N, cv.wo, ls.wi, TRANSPORT_MODE_RADIANCE);
+                    const f3 fm = evaluateMaterialV(s, cv, pix, N, cv.wo, ls.wi, TRANSPORT_MODE_RADIANCE);
                     L = cv.throughput * samp.throughput * fm;
                     if (isVertexOnSurface(cv.fr.gn)) L *= absDot(ls.wi, cv.fr.sn);
                     if (ls.shadowSet) {
@@ -811,8 +839,8 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
         } else {
             const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
             if (isConnectible(cv.flags) && isConnectible(lv.flags)) {
-                const f3 lvf = evalVertex_f(lv, pix, N, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
-                const f3 cvf = evalVertex_f(cv, pix, N, lv.fr.p, TRANSPORT_MODE_RADIANCE);
+                const f3 lvf = evalVertex_f(s, lv, pix, N, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                const f3 cvf = evalVertex_f(s, cv, pix, N, lv.fr.p, TRANSPORT_MODE_RADIANCE);
                 const f3 lp = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
                 const f3 cp = cv.fr.p + cv.fr.gn * cv.traceErrorOffset;
                 f3 w = cp - lp;

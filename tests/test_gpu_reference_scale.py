@@ -178,3 +178,29 @@ def accumulated_matches(ctx, ds, ref, key, name, W, H, frames, D):
                        f"frames at {int((~ex.all(-1)).sum())} px")
     fb.close()
     assert not bad, (key, bad)
+
+
+def test_perf_tree_full_size_vs_reference(hip_ctx, clref_scale):
+    """The perf-mode tree (mcrt_accel_opts.device_build 4: the host 3-axis binned SAH, a different
+    tree from the reference's Bvh2) on the headline scene at 1080p against the reference's kernels
+    run live (frames 0 and 1 of sm_pt_1080p).  Another tree visits leaves in another order, so only
+    triangles at exactly equal t could resolve differently: the frames must be bit-exact on >= 99.99 %
+    of pixels and within SURVEY App. A's tolerance (|dL| <= 1e-4 max(1, |L|)) on >= 99.5 %."""
+    from mcrt import lib
+    key, name, W, H, integ, frames, D = next(c for c in SCALE_CASES["ieee"] if c[0] == "sm_pt_1080p")
+    ref = clref_scale["ieee"]
+    for k in list(_scenes):   # one 10 M-triangle scene on the device at a time
+        _scenes.pop(k).close()
+    ds = lib.DeviceScene(hip_ctx, scale_scene(name), device_build=4)
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    cam = scene_camera(name, W, H)
+    for f in frames:
+        fb.render(ds, cam, frame=f, max_depth=D)
+        g = fb.read(0)[..., :3]
+        r = ref[f"{key}_f{f}"][..., :3]
+        exact = _exact(g, r).all(-1)
+        d = np.abs(g.astype(np.float64) - r)
+        close = (d <= 1e-4 * np.maximum(1.0, np.abs(r))).all(-1)
+        assert exact.mean() >= 0.9999 and close.mean() >= 0.995, (f, float(exact.mean()), float(close.mean()))
+    fb.close()
+    ds.close()
