@@ -273,46 +273,18 @@ MCRT_DEV LightLe sampleLightLe(const SceneArgs& s, const mcrt_light& light, f2 u
 }
 
 // --- materials.cl with transport modes ----------------------------------------------------
-// A material whose uber properties do not depend on the hit (not an uber material, or no texture
-// behind any property) gives getUberMaterialProperties' values from the material alone: the vertex
-// launch stores no material planes for it and the connections recompute them from the material
-// record (cached; the same floats: uberProps without a texture read is a function of the
-// material only), instead of streaming 80 B per vertex through HBM twice.
-MCRT_DEV bool uberFromMaterial(const mcrt_material& m) {
-    return m.type != 0 || (m.uber_diffuseTexId == -1 && m.uber_glossyTexId == -1 && m.uber_specReflectionTexId == -1 &&
-                           m.uber_transmissionTexId == -1 && m.uber_opacityTexId == -1 &&
-                           m.uber_roughnessTexId == -1 && m.uber_iorTexId == -1);
-}
-// getUberMaterialProperties of a stored surface vertex: from its material when uberFromMaterial,
-// else from the vertex's planes 8-12 (written by k_bdpt_vertex at its uv)
-MCRT_DEV Uber vertexUber(const SceneArgs& s, const BVertex& v, int pix, int N, int* matType) {
-    const mcrt_material& m = s.materials[v.materialIdx];
-    if (uberFromMaterial(m)) {
-        *matType = m.type;
-        if (m.type != 0) {
-            Uber z;
-            z.Kd = z.Ks = z.Kr = z.opacity = splat3(0.0f);
-            z.Kt = f4{0.0f, 0.0f, 0.0f, 0.0f};
-            z.roughness = f2{0.0f, 0.0f};
-            z.eta = 0.0f;
-            return z;
-        }
-        return uberProps(s, m, v.fr.uv);
-    }
-    return loadUber(v.planes, v.depth, pix, N, matType);
-}
-// evaluateMaterial / evaluateMaterialPdf (materials.cl:120-142) of a stored surface vertex with
-// the uber properties of vertexUber (the same getUberMaterialProperties values the reference
-// recomputes from the textures at every call).  Non-uber materials evaluate to 0.
-MCRT_DEV f3 evaluateMaterialV(const SceneArgs& s, const BVertex& v, int pix, int N, f3 wo, f3 wi, int mode) {
+// evaluateMaterial / evaluateMaterialPdf (materials.cl:120-142) of a stored surface vertex: the
+// uber properties come from the vertex's planes 8-12 (the same getUberMaterialProperties values
+// the reference recomputes from the textures at every call).  Non-uber materials evaluate to 0.
+MCRT_DEV f3 evaluateMaterialV(const BVertex& v, int pix, int N, f3 wo, f3 wi, int mode) {
     int type;
-    const Uber um = vertexUber(s, v, pix, N, &type);
+    const Uber um = loadUber(v.planes, v.depth, pix, N, &type);
     if (type != 0) return splat3(0.0f);
     return evaluateUberBSDF(um, v.fr, wo, wi, mode);
 }
-MCRT_DEV float evaluateMaterialPdfV(const SceneArgs& s, const BVertex& v, int pix, int N, f3 wo, f3 wi) {
+MCRT_DEV float evaluateMaterialPdfV(const BVertex& v, int pix, int N, f3 wo, f3 wi) {
     int type;
-    const Uber um = vertexUber(s, v, pix, N, &type);
+    const Uber um = loadUber(v.planes, v.depth, pix, N, &type);
     if (type != 0) return 0.0f;
     return evaluateUberBSDF_Pdf(um, v.fr, wo, wi);
 }
@@ -401,18 +373,18 @@ MCRT_DEV float evalVertexPdf(const SceneArgs& s, const mcrt_camera& cam, const B
             if (isNearZero(lenSq)) return 0.0f;
             wp = cl_div(wp, cl_sqrt(lenSq));
         }
-        pdf = evaluateMaterialPdfV(s, v, pix, N, wp, wn);
+        pdf = evaluateMaterialPdfV(v, pix, N, wp, wn);
     }
     return convertVertexDensity(pdf, v.fr.p, next);
 }
 // evalVertex_f(this, next, mode) (BDPT.cl:215-235)
-MCRT_DEV f3 evalVertex_f(const SceneArgs& s, const BVertex& v, int pix, int N, f3 nextP, int mode) {
+MCRT_DEV f3 evalVertex_f(const BVertex& v, int pix, int N, f3 nextP, int mode) {
     f3 wi = nextP - v.fr.p;
     const float lenSq = cl_dot(wi, wi);
     if (isNearZero(lenSq)) return splat3(0.0f);
     wi = cl_div(wi, cl_sqrt(lenSq));
     if (v.type == RT_BDPT_SURFACE_VERTEX) {
-        const f3 f = evaluateMaterialV(s, v, pix, N, v.wo, wi, mode);
+        const f3 f = evaluateMaterialV(v, pix, N, v.wo, wi, mode);
         return f * shadingNormalCorrection(v.fr, v.wo, wi, mode);
     }
     return f3{1.0f, 0.0784f, 0.5765f};
@@ -563,24 +535,23 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
 }
 
 // GenerateSecondaryVertices (BDPT.cl:317-458) for every queued subpath ray at depth d.
-// perm (optional): qIn walked in this order (the sorted light-start rays): the j-th thread takes
-// slot perm[j], so the next rays are appended in the sorted order too -- the light paths' second
-// segments leave neighbouring points.
 __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameArgs f, BdptArgs b, int depth,
                                                             BdptQueue qIn, const float4* __restrict__ hits,
-                                                            BdptQueue qOut, const uint32_t* __restrict__ perm) {
+                                                            BdptQueue qOut) {
     const int n = *qIn.count;
     __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
     if ((int)blockIdx.x * BDPT_BLOCK >= n) return;
-    const int j = xcdRemap(blockIdx.x, (n + BDPT_BLOCK - 1) / BDPT_BLOCK) * BDPT_BLOCK + threadIdx.x;
-    const int i = perm && j < n ? (int)perm[j] : j;
+    // (queue = slot order: walking the light-start rays in their sorted order here made this launch
+    // 37 % slower for 1 % on the next traversal -- its plane writes follow the pixel order;
+    // profiles/r04/ab/README.txt)
+    const int i = xcdRemap(blockIdx.x, (n + BDPT_BLOCK - 1) / BDPT_BLOCK) * BDPT_BLOCK + threadIdx.x;
     const int N = (int)(f.W * f.H) * f.batch;   // plane stride (NB)
     const int D = f.maxDepth;
     bool push = false;
     f3 no = splat3(0.0f), nd = splat3(0.0f), ntp = splat3(0.0f);
     float nPdf = 0.0f;
     int tag = 0;
-    const float4 O = j < n ? qIn.o[i] : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+    const float4 O = i < n ? qIn.o[i] : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
     tag = __float_as_int(O.w);
     if (tag >= 0) {   // tag -1: a start-queue slot outside the image
         const float4 Dd = qIn.d[i], Tp = qIn.t[i];
@@ -611,7 +582,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                 um.roughness = f2{0.0f, 0.0f};
                 um.eta = 0.0f;
             }
-            if (!uberFromMaterial(mat)) storeUber(V, depth, pix, N, um, mat.type);   // else: vertexUber
+            storeUber(V, depth, pix, N, um, mat.type);
             const int mode = isCamera ? TRANSPORT_MODE_RADIANCE : TRANSPORT_MODE_IMPORTANCE;
             const BVertexPos prev = loadVertexPos(V, depth - 1, pix, N);
             float pdfFwd = Dd.w;
@@ -789,7 +760,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                     ix = min(max(ix, 0), (int)f.W - 1);
                     iy = min(max(iy, 0), (int)f.H - 1);
                     code = ~(k * N0 + ix + iy * (int)f.W);   // frame k's splat plane
-                    L = lv.throughput * samp.throughput * evalVertex_f(s, lv, pix, N, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                    L = lv.throughput * samp.throughput * evalVertex_f(lv, pix, N, samp.fr.p, TRANSPORT_MODE_IMPORTANCE);
                     if (isVertexOnSurface(lv.fr.gn)) L *= absDot(wi, lv.fr.sn);
                     rayO = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
                     rayT = cl_distance(rayO, ld3(cam.pos));
@@ -825,7 +796,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                                              pdfFwdS, light.flags);
                     *stale = make_float4(samp.fr.p.x, samp.fr.p.y, samp.fr.p.z,
                                          __int_as_float((samp.flags << 16) | (chosen & 0xffff)));
-                    const f3 fm = evaluateMaterialV(s, cv, pix, N, cv.wo, ls.wi, TRANSPORT_MODE_RADIANCE);
+                    const f3 fm = evaluateMaterialV(cv, pix, N, cv.wo, ls.wi, TRANSPORT_MODE_RADIANCE);
                     L = cv.throughput * samp.throughput * fm;
                     if (isVertexOnSurface(cv.fr.gn)) L *= absDot(ls.wi, cv.fr.sn);
                     if (ls.shadowSet) {
@@ -839,8 +810,8 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
         } else {
             const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
             if (isConnectible(cv.flags) && isConnectible(lv.flags)) {
-                const f3 lvf = evalVertex_f(s, lv, pix, N, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
-                const f3 cvf = evalVertex_f(s, cv, pix, N, lv.fr.p, TRANSPORT_MODE_RADIANCE);
+                const f3 lvf = evalVertex_f(lv, pix, N, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
+                const f3 cvf = evalVertex_f(cv, pix, N, lv.fr.p, TRANSPORT_MODE_RADIANCE);
                 const f3 lp = lv.fr.p + lv.fr.gn * lv.traceErrorOffset;
                 const f3 cp = cv.fr.p + cv.fr.gn * cv.traceErrorOffset;
                 f3 w = cp - lp;
@@ -1061,10 +1032,10 @@ void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b
     hipLaunchKernelGGL(k_bdpt_start, dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, camQ, lightQ);
 }
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
-                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st, const uint32_t* perm) {
+                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st) {
     const int blocks = (maxCount + BDPT_BLOCK - 1) / BDPT_BLOCK;
     hipLaunchKernelGGL(k_bdpt_vertex, dim3(blocks > 0 ? blocks : 1), dim3(BDPT_BLOCK), 0, st, s, f, b, depth, qIn, hits,
-                       qOut, perm);
+                       qOut);
 }
 void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                          const BdptQueue& q, hipStream_t st) {

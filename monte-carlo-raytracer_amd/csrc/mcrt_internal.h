@@ -134,8 +134,7 @@ void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* s
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& camQ, const BdptQueue& lightQ, hipStream_t st);
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
-                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st,
-                        const uint32_t* perm = nullptr);
+                        const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st);
 void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                          const BdptQueue& q, hipStream_t st);
 // k_bdpt_vis is a grid-stride launch of at most this many one-wave workgroups (spill columns per wave)

@@ -329,6 +329,8 @@ def test_band_pack_unpack_through_product(hip_ctx, mixed, ranks, W, H, BR):
             fb.render_frames(ds, cams[f0:f0 + batch], frame=f0, max_depth=D, band_rows=BR, num_bands=ranks,
                              band_index=r)
             fb.accumulate(filt, f0)
+        # the chunk geometry a C++ host reads (mcrt_framebuffer_band_layout) = mcrt.dist's
+        assert fb.band_layout() == (maxr, ranks, r)
         fb.bands_pack(recv[r * n:].data_ptr())   # rank r's chunk of the gather
         hip_ctx.sync()
         fbs.append(fb)
