@@ -827,10 +827,12 @@ MCRT_API mcrt_status mcrt_accel_build(mcrt_scene s, const mcrt_accel_opts* opts)
 static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_point t0, const float* box6) {
     mcrt_ctx ctx = s->ctx;
     // wave packets for the coherent launches (mcrt_traverse.h traversePacket): flat trees whose
-    // depth fits the packet stack (2 entries per level).  MCRT_CAMERA_PACKETS=0 walks them per ray
-    // (A/B and tests: the results are the same bit for bit).
+    // depth fits the packet stack (at most 2 entries per internal level: 2 x depth, the leaves'
+    // level).  MCRT_CAMERA_PACKETS=0 walks them per ray (A/B and tests: the results are the same bit
+    // for bit).
     const char* pe = std::getenv("MCRT_CAMERA_PACKETS");
-    s->packets = !s->twoLevel && 2 * (s->bvhDepth + 1) <= MCRT_PK_STACK && !(pe && std::atoi(pe) == 0);
+    s->packets = !s->twoLevel && 2 * s->bvhDepth <= MCRT_PK_STACK && s->numNodes < (1u << 26) &&   // 32-bit offsets
+                 !(pe && std::atoi(pe) == 0);
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
     int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries

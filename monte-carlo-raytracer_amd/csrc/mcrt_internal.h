@@ -77,14 +77,15 @@ struct BdptQueue {
     float4 *o, *d, *t;
 };
 
-// entries of a wave packet's LDS stack (node word + 64-bit lane mask); a level pushes at most 2
-#define MCRT_PK_STACK 128
+// entries of a wave packet's stack (one VGPR lane each: node word + 64-bit lane mask); a level
+// pushes at most 2, so trees of depth <= MCRT_PK_STACK / 2 take the packets
+#define MCRT_PK_STACK 64
 struct TraceCtx {
     const float4* nodes;   // 4 float4 per node (mcrt_bvh.cpp): internal = child boxes + indices, leaf = triangle
                            // two-level (mcrt_bvh2l.cpp): + instance records (world->object rows, bottom root)
     int twoLevel;          // selects the kernels' two-level instantiation (launch-time, not per lane)
     int packet;            // coherent launches (camera rays, bounce-0 shadow rays) walk the tree as wave
-                           // packets (mcrt_traverse.h traversePacket); flat trees of depth <= MCRT_PK_STACK/2 - 1
+                           // packets (mcrt_traverse.h traversePacket); flat trees of depth <= MCRT_PK_STACK / 2
     uint32_t* spill;
     int spillCap;           // spill entries per ray (a multiple of STACK_LDS)
     int* overflow;

@@ -145,8 +145,6 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
 // and hit records as k_primary.
 __global__ __launch_bounds__(64) void k_primary_pk(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                    float4* __restrict__ hitOut) {
-    __shared__ uint32_t stkN[PK_STACK];
-    __shared__ uint64_t stkM[PK_STACK];
     const int lane = threadIdx.x;
     const int tileAll = xcdRemap(blockIdx.x, gridDim.x);
     int k, tile, pi = lane;
@@ -168,7 +166,7 @@ __global__ __launch_bounds__(64) void k_primary_pk(TraceCtx c, FrameArgs f, cons
     r.tmax = 1000.0f;
     r.mask = -1;
     float t;
-    const int tri = traversePacket<false>(c.nodes, r, valid, stkN, stkM, c.overflow, t);
+    const int tri = traversePacket<false>(c.nodes, r, valid, t);
     if (valid) hitOut[(size_t)k * f.W * f.H + (size_t)y * f.W + x] = closestRecord(c.nodes, r, tri, t);
 }
 
@@ -270,7 +268,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
             }
             r.mask = -1;
             float tt;
-            const bool occ = traversePacket<true>(c.nodes, r, valid, lds, pkMasks(lds), c.overflow, tt) >= 0;
+            const bool occ = traversePacket<true>(c.nodes, r, valid, tt) >= 0;
             if (valid) {
                 const float V = occ ? 0.0f : 1.0f;
                 const float4 L = sL[i];
@@ -328,7 +326,7 @@ __global__ __launch_bounds__(64) void k_extend_pair(TraceCtx cc, TraceCtx c, con
             const bool valid = i < n0;
             r.o = valid ? ld3(qO0[i]) : splat3(0.0f);
             r.d = valid ? ld3(qD0[i]) : f3{0.0f, 0.0f, 1.0f};
-            const int tri = traversePacket<false>(cc.nodes, r, valid, lds, pkMasks(lds), cc.overflow, t);
+            const int tri = traversePacket<false>(cc.nodes, r, valid, t);
             if (valid) hit0[i] = closestRecord(cc.nodes, r, tri, t);
             return;
         }

@@ -170,13 +170,14 @@ MCRT_DEV int traverseOct(const float4* __restrict__ nodes, const TraceRay& r, f3
 // rule -- and the closest hit is the same; only the ORDER of a lane's leaves can differ from
 // nearer-first, which matters for exactly-equal t (a tie) alone, as for any other visit order.
 // ---------------------------------------------------------------------------
-#define PK_STACK MCRT_PK_STACK
+// The wave's stack lives in three VGPRs, entry k in lane k (node word, mask low and high halves):
+// a push is a lane compare + selects, a pop three v_readlane with the wave-uniform stack pointer,
+// so neither costs an LDS access, a wait or an exec-mask change for a leader lane.  A level pushes at most 2 entries,
+// so a tree of depth D (leaves at level D) needs 2 D entries and writes at most entry 2 D - 1: the
+// host takes this path for 2 D <= MCRT_PK_STACK = 64 (mcrt_capi.cpp finish_accel).
 typedef float __attribute__((ext_vector_type(4))) PkV4;
 typedef const __attribute__((address_space(4))) PkV4* PkNodes;   // uniform loads -> s_load
-// A kernel that also runs per-ray traversals keeps the packet stack in its per-ray LDS stack array
-// (STACK_LDS x 64 words): node words in the first PK_STACK words, lane masks after them.
-static_assert(PK_STACK * 3 <= STACK_LDS * 64, "packet stack must fit the per-ray LDS stack");
-MCRT_DEV uint64_t* pkMasks(uint32_t* lds) { return reinterpret_cast<uint64_t*>(lds + PK_STACK); }
+static_assert(MCRT_PK_STACK == 64, "the packet stack is one VGPR lane per entry");
 MCRT_DEV float4 pkLoad(PkNodes p, int i) {
     const PkV4 v = p[i];
     return make_float4(v.x, v.y, v.z, v.w);
@@ -194,19 +195,20 @@ MCRT_DEV float triHitSel(const TraceRay& r, float4 A, float4 E1, float4 E2, floa
     const float b1 = cl_dot(d, s1) * invd;
     const f3 s2 = cl_cross(d, e1);
     const float b2 = cl_dot(r.d, s2) * invd;
-    const float temp = cl_dot(e2, s2) * invd;
+    float temp = cl_dot(e2, s2) * invd;
+    __asm__ volatile("" : "+v"(temp));   // computed by every lane: no exec-mask branch around it
     const bool miss = denom == 0.f || b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || temp < 0.f || temp > tmax;
     return miss ? tmax : temp;
 }
 
 template <bool ANY, int OCT>
 MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay& r, f3 inv, bool valid,
-                               uint32_t* stkN, uint64_t* stkM, int* overflowFlag, float& tHit) {
+                               float& tHit) {
     const PkNodes cn = (PkNodes)(const void*)nodes;
     const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
     const int lane = (int)__lane_id();
-    const bool leader = lane == __builtin_amdgcn_readfirstlane(lane);
     const uint64_t laneBit = 1ull << lane;
+    int stN = 0, stLo = 0, stHi = 0;   // the stack: entry k in lane k
     float t = r.tmax;
     int hit = -1;
     uint64_t mask = __ballot(valid);
@@ -216,7 +218,8 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
     while (true) {
         if (ANY) mask &= alive;
         if (mask != 0) {
-            const PkNodes q = (PkNodes)((const char __attribute__((address_space(4)))*)cn + ((size_t)node << 6));
+            // 32-bit byte offset (s_load's SGPR offset, no 64-bit add): < 2^26 nodes (finish_accel)
+            const PkNodes q = (PkNodes)((const char __attribute__((address_space(4)))*)cn + (uint32_t)(node << 6));
             const float4 n0 = pkLoad(q, 0), n1 = pkLoad(q, 1), n2 = pkLoad(q, 2), n3f = pkLoad(q, 3);
             const int c0 = __builtin_amdgcn_readfirstlane(__float_as_int(n3f.x));
             const int c1 = __builtin_amdgcn_readfirstlane(__float_as_int(n3f.y));
@@ -258,27 +261,23 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                 // answer does not depend on the order, so no third pass.)
                 const uint64_t both = mL & mR;
                 const uint64_t pr = __ballot(a0 > b0) & both;   // lanes preferring the right child
-                const bool goR = mL == 0 || 2 * __popcll(pr) > __popcll(both);
+                const bool goR = (mL == 0) | (2 * __popcll(pr) > __popcll(both));   // no branch
                 const uint64_t late = ANY ? 0ull : (goR ? both & ~pr : pr);   // first child, visited later
                 const uint64_t mF = goR ? mR : mL, mS = goR ? mL : mR;
                 const uint32_t cF = (uint32_t)(goR ? c1 : c0), cS = (uint32_t)(goR ? c0 : c1);
-                // deferred entries, bottom to top: F for the late lanes, then S
-                const int nPush = (late != 0 ? 1 : 0) + (mS != 0 ? 1 : 0);
-                if (nPush != 0) {
-                    if (sp + nPush <= PK_STACK) {
-                        if (leader) {
-                            stkN[sp] = late != 0 ? cF : cS;
-                            stkM[sp] = late != 0 ? late : mS;
-                            if (nPush == 2) {   // (sp + 1 < PK_STACK only holds then)
-                                stkN[sp + 1] = cS;
-                                stkM[sp + 1] = mS;
-                            }
-                        }
-                        sp += nPush;
-                    } else if (leader) {
-                        *overflowFlag = 1;   // deeper than the wave stack: reported by the host
-                    }
-                }
+                // deferred entries, bottom to top: F for the late lanes, then S.  Each slot is
+                // written whether or not it is pushed (the pointer only advances for a push), which
+                // stays below entry 2 D (see above)
+                const bool at0 = lane == sp;
+                stN = at0 ? (int)cF : stN;
+                stLo = at0 ? (int)(uint32_t)late : stLo;
+                stHi = at0 ? (int)(uint32_t)(late >> 32) : stHi;
+                sp += late != 0 ? 1 : 0;
+                const bool at1 = lane == sp;
+                stN = at1 ? (int)cS : stN;
+                stLo = at1 ? (int)(uint32_t)mS : stLo;
+                stHi = at1 ? (int)(uint32_t)(mS >> 32) : stHi;
+                sp += mS != 0 ? 1 : 0;
                 node = cF;
                 mask = mF & ~late;
             } else {
@@ -295,10 +294,9 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
         if (mask == 0) {
             if (sp == 0) break;
             --sp;
-            node = (uint32_t)__builtin_amdgcn_readfirstlane((int)stkN[sp]);
-            const uint64_t m = stkM[sp];
-            mask = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
-                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m);
+            node = (uint32_t)__builtin_amdgcn_readlane(stN, sp);
+            mask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(stHi, sp) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane(stLo, sp);
         }
     }
     tHit = t;
@@ -308,8 +306,7 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
 // Closest (ANY = false) or any hit of the wave's rays over plain records; lanes with valid = false take
 // no part.  Returns the hit leaf's node index or -1 per lane.
 template <bool ANY>
-MCRT_DEV int traversePacket(const float4* __restrict__ nodes, const TraceRay& r, bool valid, uint32_t* stkN,
-                            uint64_t* stkM, int* overflowFlag, float& tHit) {
+MCRT_DEV int traversePacket(const float4* __restrict__ nodes, const TraceRay& r, bool valid, float& tHit) {
     const f3 inv = safeInvDir(r.d);
     const int oct = (int)(__float_as_uint(inv.x) >> 31) | (int)((__float_as_uint(inv.y) >> 31) << 1) |
                     (int)((__float_as_uint(inv.z) >> 31) << 2);
@@ -318,18 +315,18 @@ MCRT_DEV int traversePacket(const float4* __restrict__ nodes, const TraceRay& r,
     const int oct0 = __builtin_amdgcn_readfirstlane(__shfl(oct, first));
     if (__all(!valid || oct == oct0)) {
         switch (oct0) {
-            case 0: return traversePacketOct<ANY, 0>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
-            case 1: return traversePacketOct<ANY, 1>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
-            case 2: return traversePacketOct<ANY, 2>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
-            case 3: return traversePacketOct<ANY, 3>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
-            case 4: return traversePacketOct<ANY, 4>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
-            case 5: return traversePacketOct<ANY, 5>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
-            case 6: return traversePacketOct<ANY, 6>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
-            case 7: return traversePacketOct<ANY, 7>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+            case 0: return traversePacketOct<ANY, 0>(nodes, r, inv, valid, tHit);
+            case 1: return traversePacketOct<ANY, 1>(nodes, r, inv, valid, tHit);
+            case 2: return traversePacketOct<ANY, 2>(nodes, r, inv, valid, tHit);
+            case 3: return traversePacketOct<ANY, 3>(nodes, r, inv, valid, tHit);
+            case 4: return traversePacketOct<ANY, 4>(nodes, r, inv, valid, tHit);
+            case 5: return traversePacketOct<ANY, 5>(nodes, r, inv, valid, tHit);
+            case 6: return traversePacketOct<ANY, 6>(nodes, r, inv, valid, tHit);
+            case 7: return traversePacketOct<ANY, 7>(nodes, r, inv, valid, tHit);
             default: break;
         }
     }
-    return traversePacketOct<ANY, -1>(nodes, r, inv, valid, stkN, stkM, overflowFlag, tHit);
+    return traversePacketOct<ANY, -1>(nodes, r, inv, valid, tHit);
 }
 
 template <bool ANY, int LAY>
