@@ -87,6 +87,8 @@ bdpt-prof)
   B="python3 bench.py --integrator bdpt --steps 16 --warmup 2 --no-kernel-timing --no-cpu-baseline --no-roofline-model"
   pmc_passes $P $B
   python3 tools/pmc_json.py $P "$B" 1 pmc_ $P/pmc_bdpt.json > $P/pmc_json.log 2>&1 || fail pmc_json $P/pmc_json.log 9
+  # the raw per-dispatch rocprofv3 output of 8-frame BDPT calls exceeds what gpurun copies back
+  find $P/trace -name "*kernel_stats.csv" -exec cp {} $P/ \; ; rm -rf $P/trace $P/pmc_fetch $P/pmc_write $P/pmc_sq1 $P/pmc_sq2 $P/pmc_grbm $P/pmc_ta
   ;;
 configs)
   P=gpurun_out/${1:-configs}; mkdir -p $P
