@@ -43,6 +43,7 @@
 #define BDPT_BLOCK 256
 #define BDPT_LIGHT_KEY_BITS 13
 #define BDPT_LIGHT_KEY_NONE ((1u << BDPT_LIGHT_KEY_BITS) - 1)
+#define BDPT_BOUNCE_KEY_BITS 16
 
 // RTBDPTVertexType / RTBDPTVertexFlag (kernel_data.h:202-218)
 enum { RT_BDPT_CAMERA_VERTEX = 0, RT_BDPT_LIGHT_VERTEX = 1, RT_BDPT_SURFACE_VERTEX = 2 };
@@ -535,6 +536,19 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_start(SceneArgs s, FrameArg
 }
 
 // GenerateSecondaryVertices (BDPT.cl:317-458) for every queued subpath ray at depth d.
+// Sort key of a bounce ray (BDPT_BOUNCE_KEY_BITS = 16, the same two 8-bit radix passes as 13): direction
+// octant, then a 32 x 8 x 32 grid cell of its origin over the scene bounds (y is up), so a wave of
+// the sorted queue holds rays that leave one region in one octant: they share nodes and take the
+// octant-specialised loop.
+MCRT_DEV uint32_t bounceKey(const BdptArgs& b, f3 o, f3 d) {
+    const uint32_t oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
+                         ((__float_as_uint(d.z) >> 31) << 2);
+    const int cx = min(max((int)((o.x - b.keyLo[0]) * b.keyScale[0]), 0), 31);
+    const int cy = min(max((int)((o.y - b.keyLo[1]) * b.keyScale[1]), 0), 7);
+    const int cz = min(max((int)((o.z - b.keyLo[2]) * b.keyScale[2]), 0), 31);
+    return (oct << 13) | (uint32_t)((cx << 8) | (cy << 5) | cz);
+}
+
 __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameArgs f, BdptArgs b, int depth,
                                                             BdptQueue qIn, const float4* __restrict__ hits,
                                                             BdptQueue qOut) {
@@ -646,7 +660,13 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
     // shading does made this kernel 11 % slower -- its plane reads and writes follow the queue --
     // for 1 % on k_extend; profiles/r04/ab/README.txt)
     const int slot = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
-    if (push) pushRay(qOut, slot, no, tag, nd, nPdf, ntp);
+    if (push) {
+        pushRay(qOut, slot, no, tag, nd, nPdf, ntp);
+        if (b.extKey) {   // the traversal walks the queue sorted by this key (render_bdpt)
+            b.extKey[slot] = bounceKey(b, no, nd);
+            b.extSlot[slot] = (uint32_t)slot;
+        }
+    }
 }
 
 // Connection-ray record (3 float4): (o.xyz, tmax), (d.xyz, code), (c.xyz, 0) where code >= 0 is an
@@ -1018,12 +1038,12 @@ namespace mcrt {
 size_t bdpt_light_sort_temp_bytes(int n) {
     size_t bytes = 0;
     uint32_t* k = nullptr;
-    rocprim::radix_sort_pairs(nullptr, bytes, k, k, k, k, (size_t)n, 0, BDPT_LIGHT_KEY_BITS, (hipStream_t)0);
+    rocprim::radix_sort_pairs(nullptr, bytes, k, k, k, k, (size_t)n, 0, BDPT_BOUNCE_KEY_BITS, (hipStream_t)0);
     return bytes;
 }
 hipError_t bdpt_light_sort(uint32_t* keys, uint32_t* keys2, uint32_t* slots, uint32_t* perm, int n, void* tmp,
-                           size_t tmpBytes, hipStream_t st) {
-    return rocprim::radix_sort_pairs(tmp, tmpBytes, keys, keys2, slots, perm, (size_t)n, 0, BDPT_LIGHT_KEY_BITS, st);
+                           size_t tmpBytes, hipStream_t st, int bits) {
+    return rocprim::radix_sort_pairs(tmp, tmpBytes, keys, keys2, slots, perm, (size_t)n, 0, bits, st);
 }
 
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,

@@ -147,6 +147,8 @@ struct BdptSet {
     uint32_t* spill = nullptr;   // traversal spill columns of this set's launches
     // the light-start queue's sort (mcrt::bdpt_light_sort): keys, sorted keys, slots, permutation
     uint32_t *lkey = nullptr, *lkey2 = nullptr, *lslot = nullptr, *lperm = nullptr;
+    // the traced bounce queues' sort (same routine; k_bdpt_vertex's keys over 2 N slots)
+    uint32_t *ekey = nullptr, *ekey2 = nullptr, *eslot = nullptr, *eperm = nullptr;
     void* sortTmp = nullptr;
     size_t sortTmpBytes = 0;
     int frames = 0;              // batch frames the per-frame arrays hold (plane stride N x frames)
@@ -1056,7 +1058,7 @@ MCRT_API mcrt_status mcrt_event_destroy(mcrt_event ev) {
 static void bset_free(BdptSet& b) {
     void* ptrs[] = {b.camV,   b.lightV, b.slots,  b.splat,  b.camCount, b.lightCount, b.bdptCounters,
                     b.bqO[0], b.bqO[1], b.bqD[0], b.bqD[1], b.bqT[0], b.bqT[1], b.bHits, b.cO, b.cD, b.cL, b.spill,
-                    b.lkey, b.lkey2, b.lslot, b.lperm, b.sortTmp};
+                    b.lkey, b.lkey2, b.lslot, b.lperm, b.ekey, b.ekey2, b.eslot, b.eperm, b.sortTmp};
     for (void* p : ptrs)
         if (p) hipFree(p);
     b = BdptSet();
@@ -1180,7 +1182,11 @@ static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D, int frames,
     A(&b.lkey2, 4 * NQ);
     A(&b.lslot, 4 * NQ);
     A(&b.lperm, 4 * NQ);
-    b.sortTmpBytes = mcrt::bdpt_light_sort_temp_bytes((int)NQ);
+    A(&b.ekey, 8 * N);
+    A(&b.ekey2, 8 * N);
+    A(&b.eslot, 8 * N);
+    A(&b.eperm, 8 * N);
+    b.sortTmpBytes = mcrt::bdpt_light_sort_temp_bytes((int)std::max(NQ, 2 * N));
     A(&b.sortTmp, b.sortTmpBytes);
     // zero-fills on the stream of the set's frames (st, its slot's), ahead of the first launch
     // that writes the set: a 3 GB vertex-plane memset on another stream could still be running
@@ -1392,6 +1398,22 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     // k_extend 3.07 -> 2.82 ms per frame at 1080p (profiles/r04/ab/README.txt)
     b.lightKey = bs.lkey;
     b.lightSlot = bs.lslot;
+    // the bounce queues that are traced (depths 1..D) in octant / origin-cell order: keys written by
+    // k_bdpt_vertex, sorted below, walked through the permutation by k_extend
+    b.extKey = nullptr;
+    b.extSlot = nullptr;
+    for (int a = 0; a < 3; ++a) {
+        const float ext = s->bbHi[a] - s->bbLo[a];
+        b.keyLo[a] = s->bbLo[a];
+        b.keyScale[a] = ext > 0.0f ? (a == 1 ? 8.0f : 32.0f) / ext : 0.0f;
+    }
+    BdptArgs bk = b;   // the vertex launches whose output queue is traced
+    bk.extKey = bs.ekey;
+    bk.extSlot = bs.eslot;
+    const int nSort = (int)(2 * N);
+    auto clearKeys = [&]() {   // unwritten slots sort last (stable sort: after the written ones)
+        return hipMemsetAsync(bs.ekey, 0xFF, 4 * (size_t)nSort, st);
+    };
     b.depth0Const = bs.constStride == N && bs.constBand[0] == f.bandRows && bs.constBand[1] == f.numBands &&
                     bs.constBand[2] == f.bandIndex ? 1 : 0;
     bs.constStride = N;
@@ -1433,22 +1455,27 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         mcrt::launch_extend_pair(tcc, tcs, camQ.count, camQ.o, camQ.d, fb->bHits, lightQ.count, lightQ.o, lightQ.d,
                                  fb->bHits + NQ, (int)NQ, (int)NQ, st, bs.lperm);
     }
+    HIPCHK(ctx, clearKeys());   // queue 1 is traced (D >= 1)
     {
         Timed t(ctx, K_BDPT_VERTEX, camQ.count, 0, st);
-        mcrt::launch_bdpt_vertex(sa, f, b, 1, camQ, fb->bHits, queue(1), (int)NQ, st);
+        mcrt::launch_bdpt_vertex(sa, f, bk, 1, camQ, fb->bHits, queue(1), (int)NQ, st);
     }
     {
         Timed t(ctx, K_BDPT_VERTEX, lightQ.count, 0, st);
-        mcrt::launch_bdpt_vertex(sa, f, b, 1, lightQ, fb->bHits + NQ, queue(1), (int)NQ, st);
+        mcrt::launch_bdpt_vertex(sa, f, bk, 1, lightQ, fb->bHits + NQ, queue(1), (int)NQ, st);
     }
     for (int d = 2; d <= D + 1; ++d) {
         const BdptQueue qIn = queue(d - 1), qOut = queue(d);
         {
             Timed t(ctx, K_EXTEND, qIn.count, 0, st);
-            mcrt::launch_extend(tcs, qIn.count, qIn.o, qIn.d, fb->bHits, (int)(2 * N), st);
+            HIPCHK(ctx, mcrt::bdpt_light_sort(bs.ekey, bs.ekey2, bs.eslot, bs.eperm, nSort, bs.sortTmp,
+                                              bs.sortTmpBytes, st, 16));
+            mcrt::launch_extend(tcs, qIn.count, qIn.o, qIn.d, fb->bHits, (int)(2 * N), st, bs.eperm);
         }
+        const bool traced = d <= D;   // queue d is traced by the next round
+        if (traced) HIPCHK(ctx, clearKeys());
         Timed t(ctx, K_BDPT_VERTEX, qIn.count, 0, st);
-        mcrt::launch_bdpt_vertex(sa, f, b, d, qIn, fb->bHits, qOut, (int)(2 * N), st);
+        mcrt::launch_bdpt_vertex(sa, f, traced ? bk : b, d, qIn, fb->bHits, qOut, (int)(2 * N), st);
     }
     BdptQueue cq;
     cq.count = cnt + BDPT_CNT_CONN;

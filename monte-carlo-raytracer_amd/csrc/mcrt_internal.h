@@ -71,6 +71,9 @@ struct BdptArgs {
                          // at this plane stride (k_bdpt_start writes only the per-frame ones)
     uint32_t* lightKey;  // per start-queue slot: the light ray's origin / direction cell (NULL: no sort)
     uint32_t* lightSlot; //   and its slot (the radix sort's values)
+    uint32_t* extKey;    // per slot of a bounce queue that will be traced: the ray's direction octant and
+    uint32_t* extSlot;   //   origin cell (NULL: no sort), and its slot
+    float keyLo[3], keyScale[3];   // origin cell = (o - keyLo) * keyScale, 32 x 8 x 32 cells
 };
 struct BdptQueue {
     int* count;
@@ -103,12 +106,12 @@ void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* ca
 // the light-start queue of a BDPT call sorted by cell (keys, slots from k_bdpt_start) -> perm
 size_t bdpt_light_sort_temp_bytes(int n);
 hipError_t bdpt_light_sort(uint32_t* keys, uint32_t* keys2, uint32_t* slots, uint32_t* perm, int n, void* tmp,
-                           size_t tmpBytes, hipStream_t st);
+                           size_t tmpBytes, hipStream_t st, int bits = 13);
 void launch_extend_pair(const TraceCtx& cc, const TraceCtx& c, const int* count0, const float4* qO0, const float4* qD0,
                         float4* hit0, const int* count1, const float4* qO1, const float4* qD1, float4* hit1,
                         int maxCount0, int maxCount1, hipStream_t st, const uint32_t* perm1 = nullptr);
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
-                   hipStream_t st);
+                   hipStream_t st, const uint32_t* perm = nullptr);
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st);
 void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,

@@ -173,15 +173,19 @@ __global__ __launch_bounds__(64) void k_primary_pk(TraceCtx c, FrameArgs f, cons
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
 // The grid covers the queue's capacity; workgroups past the device-side count exit at once.
 template <int LAY>
+// perm (optional): the queue walked in this order (BDPT's bounce rays sorted by direction octant and
+// origin cell, mcrt::bdpt_light_sort over k_bdpt_vertex's keys); hit records go back to their slots.
 __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict__ count, const float4* __restrict__ qO,
-                                               const float4* __restrict__ qD, float4* __restrict__ hitOut) {
+                                               const float4* __restrict__ qD, float4* __restrict__ hitOut,
+                                               const uint32_t* __restrict__ perm) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[STACK_LDS * 64];
     const int n = *count;
     if ((int)blockIdx.x * 64 >= n) return;
     const int lane = threadIdx.x;
     const int blk = xcdRemap(blockIdx.x, (n + 63) >> 6);
-    const int i = blk * 64 + lane;
-    if (i >= n) return;
+    const int j = blk * 64 + lane;
+    if (j >= n) return;
+    const int i = perm ? (int)perm[j] : j;
     const float4 o = qO[i], d = qD[i];
     TraceRay r;
     r.o = ld3(o);
@@ -872,9 +876,9 @@ void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* ca
                        hits);
 }
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
-                   hipStream_t st) {
+                   hipStream_t st, const uint32_t* perm) {
     hipLaunchKernelGGL(pickLayout(c, k_extend<LAY_TWO_LEVEL>, k_extend<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
-                       count, qO, qD, hits);
+                       count, qO, qD, hits, perm);
 }
 void launch_extend_pair(const TraceCtx& cc, const TraceCtx& c, const int* count0, const float4* qO0, const float4* qD0,
                         float4* hit0, const int* count1, const float4* qO1, const float4* qD1, float4* hit1,
