@@ -107,6 +107,8 @@ struct mcrt_scene_s {
     size_t spillRays = 0;           // rays the spill buffer covers (spillCap words each)
     int* dScratch = nullptr;   // work counters for API queries
     float bbLo[3] = {0, 0, 0}, bbHi[3] = {0, 0, 0};   // world bounds (root record of the BVH)
+    // occluder hints of the shadow rays after bounce 0, by origin cell (TraceCtx::hint, flat trees)
+    uint32_t* dHintCell = nullptr;
 };
 
 // One frame in flight (PT): the per-frame buffers of mcrt_render_frame, its own stream and
@@ -173,6 +175,7 @@ struct mcrt_framebuffer_s {
     float4* image = nullptr;
     float4* denoised = nullptr;  // RTDenoisePass output (persistent: the reference keeps its image)
     float4* display = nullptr;   // post-processed image (mcrt_postprocess)
+    uint32_t* hintPix = nullptr; // occluder hint of each pixel's bounce-0 shadow ray (TraceCtx::hint)
     float4* hitsP = nullptr;     // primary hits by pixel
     float4* hitsE = nullptr;     // extension hits by queue slot
     float4* eO[2] = {};
@@ -306,14 +309,57 @@ static bool ensure_spill(mcrt_scene s, size_t rays) {
 }
 
 static TraceCtx trace_ctx(mcrt_scene s) {
-    TraceCtx c;
+    TraceCtx c = {};
     c.nodes = (const float4*)s->dNodes;
     c.packet = 0;
     c.spill = s->dSpill;
     c.spillCap = s->spillCap;
     c.overflow = s->ctx->dFlags;
     c.twoLevel = s->twoLevel ? 1 : 0;
+    c.numNodes = (uint32_t)s->numNodes;
     return c;
+}
+
+// Occluder hints for a shadow launch (mcrt_traverse.h hintOccludes; flat trees only -- the leaf test
+// of a two-level record would need the instance transform): bounce-0 rays by pixel (table `pix`,
+// n pixels), later ones by origin cell.  The answers are the walk's with or without them;
+// MCRT_SHADOW_HINTS=0 turns them off (A/B, tests).
+static bool hints_enabled() {
+    const char* e = std::getenv("MCRT_SHADOW_HINTS");
+    return !(e && std::atoi(e) == 0);
+}
+// test hook: MCRT_TEST_HINT_FILL=seed fills a new hint table with pseudo-random words below
+// `range` instead of "no hint", so a test can check that arbitrary hints change no answer
+static hipError_t fill_hints(uint32_t* d, size_t n, uint32_t range, hipStream_t st) {
+    const char* e = std::getenv("MCRT_TEST_HINT_FILL");
+    if (!e) return hipMemsetAsync(d, 0xff, 4 * n, st);
+    std::vector<uint32_t> h(n);
+    uint32_t x = 2463534242u + (uint32_t)std::atoi(e);
+    for (auto& v : h) {
+        x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+        v = x % range;
+    }
+    hipError_t r = hipMemcpyAsync(d, h.data(), 4 * n, hipMemcpyHostToDevice, st);
+    if (r == hipSuccess) r = hipStreamSynchronize(st);
+    return r;
+}
+static void with_hints(TraceCtx& c, mcrt_scene s, uint32_t* pix, uint32_t n) {
+    if (s->twoLevel || !hints_enabled()) return;
+    if (pix) {
+        c.hint = pix;
+        c.hintMode = MCRT_HINT_PIXEL;
+        c.hintPixels = n;
+        return;
+    }
+    if (!s->dHintCell) return;
+    c.hint = s->dHintCell;
+    c.hintMode = MCRT_HINT_CELL;
+    c.hintMask = (1u << MCRT_HINT_CELL_BITS) - 1;
+    for (int a = 0; a < 3; ++a) {
+        const float ext = s->bbHi[a] - s->bbLo[a];
+        c.hintLo[a] = s->bbLo[a];
+        c.hintScale[a] = ext > 0.0f ? (float)MCRT_HINT_GRID / ext : 0.0f;
+    }
 }
 
 // the coherent launches' view (camera rays, bounce-0 shadow rays): wave packets when the tree allows
@@ -527,6 +573,8 @@ static void scene_free_device(mcrt_scene s) {
     }
     if (s->dSpill) hipFree(s->dSpill);
     if (s->dScratch) hipFree(s->dScratch);
+    if (s->dHintCell) hipFree(s->dHintCell);
+    s->dHintCell = nullptr;
     s->dSpill = nullptr;
     s->spillRays = 0;
     s->dScratch = nullptr;
@@ -837,6 +885,13 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
                  !(pe && std::atoi(pe) == 0);
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
+    if (!s->twoLevel) {
+        // parent links of the leaves (occluder hints), and the origin-cell hint table (16 MB)
+        mcrt::launch_leaf_parents((float4*)s->dNodes, (uint32_t)s->numNodes, ctx->stream);
+        if (!s->dHintCell) HIPCHK(ctx, hipMalloc(&s->dHintCell, sizeof(uint32_t) << MCRT_HINT_CELL_BITS));
+        HIPCHK(ctx, fill_hints(s->dHintCell, (size_t)1 << MCRT_HINT_CELL_BITS, (uint32_t)s->numNodes + 64, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    }
     int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries
     // test hook: MCRT_TEST_SPILL_CAP=k caps the spill columns at k entries (0 = LDS stack only) so a
     // test can drive a traversal past its capacity and check that the overflow is reported
@@ -1089,7 +1144,7 @@ static void slot_free(FrameSlot& k) {
 
 static void fb_free(mcrt_framebuffer fb) {
     for (auto& k : fb->slot) slot_free(k);
-    void* ptrs[] = {fb->wsum, fb->wts, fb->image, fb->denoised, fb->display};
+    void* ptrs[] = {fb->wsum, fb->wts, fb->image, fb->denoised, fb->display, fb->hintPix};
     for (void* p : ptrs)
         if (p) hipFree(p);
     fb_free_bdpt(fb);
@@ -1261,6 +1316,7 @@ MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint3
     A(&fb->image, 16 * N);
     A(&fb->denoised, 16 * N);
     A(&fb->display, 16 * N);
+    A(&fb->hintPix, 4 * N);
     fb->slot.resize(MCRT_MAX_FRAMES_IN_FLIGHT);
     if (e == hipSuccess) e = slot_alloc(fb->slot[0], N);
     if (e == hipSuccess) fb_bind(fb, 0);
@@ -1271,6 +1327,7 @@ MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint3
     if (e == hipSuccess) e = hipMemsetAsync(fb->image, 0, 16 * N, fb->slot[0].stream);
     if (e == hipSuccess) e = hipMemsetAsync(fb->denoised, 0, 16 * N, fb->slot[0].stream);
     if (e == hipSuccess) e = hipMemsetAsync(fb->display, 0, 16 * N, fb->slot[0].stream);
+    if (e == hipSuccess) e = fill_hints(fb->hintPix, N, 1u << 22, fb->slot[0].stream);   // no hints
     if (e == hipSuccess) e = hipStreamSynchronize(fb->slot[0].stream);
     if (e != hipSuccess) {
         fb_free(fb);
@@ -1647,11 +1704,14 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
             // bounce-0 shadow rays are coherent (a packed wave's paths share a pixel): wave packets
             TraceCtx tse = b == 0 ? packet_ctx(s) : tcs;
             tse.spill = slot.spill;
+            with_hints(tse, s, b == 0 ? fb->hintPix : nullptr, (uint32_t)fb->N);
             mcrt::launch_shadow_extend(tse, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
                                        fb->sO, fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
             Timed t(ctx, K_SHADOW, shadowCnt + b, 0, st);
-            mcrt::launch_shadow(tcs, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, qCap, st);
+            TraceCtx tsh = tcs;
+            with_hints(tsh, s, b == 0 ? fb->hintPix : nullptr, (uint32_t)fb->N);
+            mcrt::launch_shadow(tsh, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, qCap, st);
         }
     }
     HIPCHK(ctx, hipGetLastError());

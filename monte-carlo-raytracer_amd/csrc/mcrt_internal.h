@@ -92,7 +92,20 @@ struct TraceCtx {
     uint32_t* spill;
     int spillCap;           // spill entries per ray (a multiple of STACK_LDS)
     int* overflow;
+    // Occluder hints of the any-hit launches over plain records (mcrt_traverse.h hintOccludes):
+    // a table of leaf indices that shadow rays test before walking the tree.  NULL = off.
+    uint32_t* hint;
+    int hintMode;           // MCRT_HINT_PIXEL: slot = path id % hintPixels; MCRT_HINT_CELL: hash of the
+                            // ray's origin cell (hintLo / hintScale, 512^3 over the scene bounds) and octant
+    uint32_t hintPixels;
+    uint32_t hintMask;      // cell table entries - 1 (a power of two)
+    float hintLo[3], hintScale[3];
+    uint32_t numNodes;      // records in `nodes` (hints are range-checked against it)
 };
+#define MCRT_HINT_PIXEL 1
+#define MCRT_HINT_CELL 2
+#define MCRT_HINT_CELL_BITS 22
+#define MCRT_HINT_GRID 512
 
 namespace mcrt {
 // n rays, or with countDev (device memory) min(*countDev, n) of them
@@ -133,6 +146,8 @@ void launch_band_unpack(const FrameArgs& f, int maxRows, const float* recv, floa
 void launch_denoise(int W, int H, int r, float ss, float sr, const float4* in, float4* out, hipStream_t st);
 void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStream_t st);
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st);
+// parent index of each triangle leaf into its record's word 13 (flat trees, finish_accel)
+void launch_leaf_parents(float4* nodes, uint32_t n, hipStream_t st);
 void launch_chase_init(void* rec, uint32_t n, hipStream_t st);
 void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* sink, hipStream_t st);
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,

@@ -196,6 +196,21 @@ __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict
     hitOut[i] = traceClosest<LAY>(c, r, lds + lane, raySpill(c, blk, lane), t);
 }
 
+// Any hit of one shadow ray: first the occluder hint of its slot (c.hint, plain records), then the
+// walk, whose occluder becomes the slot's next hint.
+template <int LAY>
+MCRT_DEV bool shadowOccluded(const TraceCtx& c, const TraceRay& r, int path, uint32_t* stk, uint32_t* spill) {
+    if (LAY == LAY_PLAIN && c.hint) {
+        const uint32_t h = hintSlot(c, r, path);
+        if (hintOccludes(c, r, c.hint[h])) return true;
+        float t;
+        const int leaf = traverse<true, LAY>(c, r, stk, spill, t);
+        if (leaf >= 0) c.hint[h] = (uint32_t)leaf;
+        return leaf >= 0;
+    }
+    return traceAny<LAY>(c, r, stk, spill);
+}
+
 // Any hit over the shadow queue + ShadowPass (PathTracing.cl:186-217):
 // sO = (o.xyz, tmax), sD = (d.xyz, pix), sL = throughput * L; radiance[pix] += L * V.
 template <int LAY>
@@ -215,8 +230,8 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     r.d = ld3(d);
     r.tmax = o.w;
     r.mask = -1;
-    const float V = traceAny<LAY>(c, r, lds + lane, raySpill(c, blk, lane)) ? 0.0f : 1.0f;
     const int pix = __float_as_int(d.w);
+    const float V = shadowOccluded<LAY>(c, r, pix, lds + lane, raySpill(c, blk, lane)) ? 0.0f : 1.0f;
     float4 acc = radiance[pix];
     acc.x += L.x * V;
     acc.y += L.y * V;
@@ -271,12 +286,23 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
                 r.tmax = o.w;
             }
             r.mask = -1;
+            // lanes whose occluder hint holds leave the packet before it starts
+            const int pix = __float_as_int(d.w);
+            uint32_t h = 0;
+            bool occ = false;
+            if (valid && c.hint) {
+                h = hintSlot(c, r, pix);
+                occ = hintOccludes(c, r, c.hint[h]);
+            }
             float tt;
-            const bool occ = traversePacket<true>(c.nodes, r, valid, tt) >= 0;
+            const int leaf = traversePacket<true>(c.nodes, r, valid && !occ, tt);
+            if (leaf >= 0) {
+                occ = true;
+                if (c.hint) c.hint[h] = (uint32_t)leaf;
+            }
             if (valid) {
                 const float V = occ ? 0.0f : 1.0f;
                 const float4 L = sL[i];
-                const int pix = __float_as_int(d.w);
                 float4 acc = radiance[pix];
                 acc.x += L.x * V;
                 acc.y += L.y * V;
@@ -292,8 +318,8 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.d = ld3(d);
         r.tmax = o.w;
         r.mask = -1;
-        const float V = traceAny<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane)) ? 0.0f : 1.0f;
         const int pix = __float_as_int(d.w);
+        const float V = shadowOccluded<LAY>(c, r, pix, lds + lane, raySpill(c, blockIdx.x, lane)) ? 0.0f : 1.0f;
         float4 acc = radiance[pix];
         acc.x += L.x * V;
         acc.y += L.y * V;
@@ -826,6 +852,22 @@ __global__ __launch_bounds__(64) void k_chase(const int4* __restrict__ rec, uint
     if (acc == 0xdeadbeefu) sink[0] = idx;   // never true: keeps the loads live
 }
 
+// Parent links of the flat tree's leaves (the occluder hints' box test, mcrt_traverse.h
+// hintOccludes): every internal record writes its index into word 13 of each child that is a
+// triangle leaf (mcrt_bvh.cpp leaves carry -1 there; the traversal never reads it for a leaf).
+__global__ __launch_bounds__(256) void k_leaf_parents(float4* __restrict__ nodes, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int4 w = *reinterpret_cast<const int4*>(&nodes[4 * (size_t)i + 3]);
+    if (w.x < 0) return;
+    const int ch[2] = {w.x, w.y};
+    for (int k = 0; k < 2; ++k) {
+        if ((uint32_t)ch[k] >= n) continue;
+        int* cw = reinterpret_cast<int*>(&nodes[4 * (size_t)ch[k] + 3]);
+        if (cw[0] == -1) cw[1] = (int)i;
+    }
+}
+
 // Attainable-bandwidth probe (mcrt_ctx_stream_copy): a persistent grid (8 workgroups per CU)
 // strides over the array; each lane keeps 4 independent 16-B nontemporal loads in flight.
 __global__ __launch_bounds__(256) void k_stream_copy(const f4* __restrict__ src, f4* __restrict__ dst, size_t n) {
@@ -937,6 +979,11 @@ void launch_chase_init(void* rec, uint32_t n, hipStream_t st) {
 }
 void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* sink, hipStream_t st) {
     hipLaunchKernelGGL(k_chase, dim3(waves), dim3(64), 0, st, reinterpret_cast<const int4*>(rec), n, steps, sink);
+}
+
+void launch_leaf_parents(float4* nodes, uint32_t n, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_leaf_parents, dim3((n + 255) / 256), dim3(256), 0, st, nodes, n);
 }
 
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st) {

@@ -382,6 +382,58 @@ MCRT_DEV float4 closestRecord(const float4* __restrict__ nodes, const TraceRay& 
 }
 
 // ---------------------------------------------------------------------------
+// Occluder hints for any-hit queries (plain records).  Before walking the tree a shadow ray tests
+// ONE leaf named by a hint table -- the occluder the same pixel's bounce-0 shadow ray found in an
+// earlier frame, or the last one found from the ray's origin cell -- and is occluded without a walk
+// when both tests below pass, with the walk's own arithmetic:
+//   * the leaf's triangle (triHit, t < tmax, RR_RAY_MASK);
+//   * the leaf's box as its parent record stores it (fast_intersect_bbox2 with t = tmax).
+// That answer is the reference's: every box on the root-to-leaf path contains the leaf's box
+// (a node's box is the exact min/max union of its subtree's triangle boxes), and for a superset box
+// each slab's fma(bound, 1/d, -o/d) interval contains the subset's (fma rounds monotonically), so
+// the entry/exit test passes at every ancestor too.  The any-hit walk therefore reaches this leaf
+// unless it stops earlier at another hit: occluded either way (intersect_bvh2_lds.cl:229-363 reports
+// only hit / no hit).  Any table content is safe: the leaf and its parent link (k_leaf_parents:
+// leaf record word 13) are checked against the current tree, a stale or empty entry is a miss.
+// ---------------------------------------------------------------------------
+MCRT_DEV bool hintOccludes(const TraceCtx& c, const TraceRay& r, uint32_t leaf) {
+    if (leaf >= c.numNodes) return false;   // empty (0xffffffff) or stale
+    const float4 A = c.nodes[4 * leaf], E1 = c.nodes[4 * leaf + 1], E2 = c.nodes[4 * leaf + 2];
+    const int4 n3 = *reinterpret_cast<const int4*>(&c.nodes[4 * leaf + 3]);
+    if (n3.x != -1 || r.mask == __float_as_int(A.w)) return false;
+    if (!(triHit(r, A, E1, E2, r.tmax) < r.tmax)) return false;
+    const int par = n3.y;
+    if (par < 0) return leaf == 0;   // the root itself: the walk tests it without a box
+    if ((uint32_t)par >= c.numNodes) return false;
+    const float4 p0 = c.nodes[4 * par], p1 = c.nodes[4 * par + 1], p2 = c.nodes[4 * par + 2];
+    const int4 p3 = *reinterpret_cast<const int4*>(&c.nodes[4 * par + 3]);
+    const bool right = p3.y == (int)leaf;
+    if (p3.x < 0 || (!right && p3.x != (int)leaf)) return false;
+    const f3 inv = safeInvDir(r.d);
+    const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
+    const float x0 = fmaf(right ? p1.x : p0.x, inv.x, oxi.x), x1 = fmaf(right ? p1.y : p0.y, inv.x, oxi.x);
+    const float y0 = fmaf(right ? p1.z : p0.z, inv.y, oxi.y), y1 = fmaf(right ? p1.w : p0.w, inv.y, oxi.y);
+    const float z0 = fmaf(right ? p2.z : p2.x, inv.z, oxi.z), z1 = fmaf(right ? p2.w : p2.y, inv.z, oxi.z);
+    const float b0 = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), 0.0f);
+    const float b1 = fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), r.tmax);
+    return b0 <= b1;
+}
+
+// The hint table slot of a shadow ray: its path's pixel (bounce-0 rays of a TAA-jittered camera
+// start on nearly the same surface point every frame) or its origin cell and direction octant
+// (rays toward the same directional light from one cell are parallel and close).
+MCRT_DEV uint32_t hintSlot(const TraceCtx& c, const TraceRay& r, int path) {
+    if (c.hintMode == MCRT_HINT_PIXEL) return (uint32_t)path % c.hintPixels;
+    const float g = (float)(MCRT_HINT_GRID - 1);
+    const uint32_t cx = (uint32_t)fminf(fmaxf((r.o.x - c.hintLo[0]) * c.hintScale[0], 0.0f), g);
+    const uint32_t cy = (uint32_t)fminf(fmaxf((r.o.y - c.hintLo[1]) * c.hintScale[1], 0.0f), g);
+    const uint32_t cz = (uint32_t)fminf(fmaxf((r.o.z - c.hintLo[2]) * c.hintScale[2], 0.0f), g);
+    const uint32_t oct = (r.d.x < 0.f ? 1u : 0u) | (r.d.y < 0.f ? 2u : 0u) | (r.d.z < 0.f ? 4u : 0u);
+    const uint32_t key = ((cz * MCRT_HINT_GRID + cy) * MCRT_HINT_GRID + cx) * 8u + oct;
+    return (key * 2654435761u) >> (32 - MCRT_HINT_CELL_BITS) & c.hintMask;
+}
+
+// ---------------------------------------------------------------------------
 // Two-level (instanced) traversal over the mcrt_bvh2l.cpp records: RadeonRays'
 // IntersectorTwoLevel semantics (intersect_bvh2level_skiplinks.cl:112-318) -- at a top-level
 // leaf the ray moves into the shape's object space (world-to-local rows), the shape's own

@@ -1,0 +1,67 @@
+"""Occluder hints of the shadow rays (mcrt_traverse.h hintOccludes): a shadow ray first tests the
+leaf its pixel's bounce-0 ray (or its origin cell's rays) last found occluding, with the walk's own
+triangle and box arithmetic, and skips the walk when both pass.  The answer must be the walk's for
+ANY hint content, so every frame is compared bit for bit with hints off (MCRT_SHADOW_HINTS=0):
+the pixel hints (bounce 0, wave packets and per ray), the cell hints (later bounces, D = 2 and 3),
+hints carried over from earlier calls, and tables filled with random leaf indices
+(MCRT_TEST_HINT_FILL)."""
+import os
+
+import numpy as np
+import pytest
+
+from mcrt import scenes
+from mcrt.camera import scene_camera
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(hip_ctx, sc, name, W, H, max_depth, calls=3, batch=4):
+    from mcrt import lib
+    ds = lib.DeviceScene(hip_ctx, sc)
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    out = []
+    for c in range(calls):   # TAA-jittered cameras, as the bench
+        cams = [scene_camera(name, W, H, frame=c * batch + k, jitter=True) for k in range(batch)]
+        fb.render_frames(ds, cams, frame=c * batch, max_depth=max_depth)
+        hip_ctx.sync()
+        out.append(np.stack([fb.read_frame(k) for k in range(batch)]))
+    fb.close()
+    ds.close()
+    return np.stack(out)
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def sm_small():
+    return scenes.san_miguel_proxy(tris=1_000_000)
+
+
+CASES = [("mixed", 2, {}), ("mixed", 3, {}), ("sm", 2, {}), ("sm", 3, {}),
+         ("sm", 2, {"MCRT_CAMERA_PACKETS": "0"}),          # bounce-0 shadow rays walked per ray
+         ("sm", 2, {"MCRT_TEST_HINT_FILL": "7"}),          # tables full of random leaf indices
+         ("mixed", 3, {"MCRT_TEST_HINT_FILL": "11"})]
+
+
+@pytest.mark.parametrize("name,max_depth,env", CASES)
+def test_hints_change_no_answer(hip_ctx, sm_small, name, max_depth, env):
+    sc, cam_name, W, H = ((scenes.test_scene(), "mixed", 96, 64) if name == "mixed" else
+                          (sm_small, "san_miguel_proxy", 256, 144))
+    on = _with_env(dict(env, MCRT_SHADOW_HINTS="1"), lambda: _frames(hip_ctx, sc, cam_name, W, H, max_depth))
+    off = _with_env(dict(env, MCRT_SHADOW_HINTS="0"), lambda: _frames(hip_ctx, sc, cam_name, W, H, max_depth))
+    assert np.isfinite(on).all()
+    assert on[..., :3].max() > 0
+    diff = on.view(np.uint32) != off.view(np.uint32)
+    assert not diff.any(), f"{int(diff.any(-1).sum())} pixels differ"

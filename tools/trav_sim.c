@@ -226,3 +226,54 @@ void sim_levels(const Node* nodes, const uint8_t* level, const Ray* rays, int n,
         }
     }
 }
+
+/* Wave-packet cost model: per group of 64 consecutive rays, the number of DISTINCT nodes the
+ * group's active rays (skip[i] == 0) visit in their own traversals -- a lower bound of the
+ * packet walk's records (tools/shadow_cache_model.py). */
+static int cmp_u32(const void* a, const void* b) {
+    uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return x < y ? -1 : x > y;
+}
+#include <stdlib.h>
+void sim_union(const Node* nodes, const Ray* rays, int n, int any, const uint8_t* skip, int32_t* out_waves) {
+    static uint32_t stack[1 << 16];
+    uint32_t* buf = (uint32_t*)malloc(sizeof(uint32_t) * (64u << 12));
+    for (int w = 0; w * 64 < n; ++w) {
+        int cnt = 0;
+        for (int i = w * 64; i < n && i < w * 64 + 64; ++i) {
+            const Ray* r = &rays[i];
+            if (r->extra[1] == 0 || skip[i]) continue;
+            float inv[3], oxi[3];
+            for (int k = 0; k < 3; ++k) { inv[k] = sinv(r->d[k]); oxi[k] = -r->o[k] * inv[k]; }
+            float ct = r->o[3];
+            uint32_t addr = 0;
+            int sp = 0;
+            stack[sp++] = INV;
+            while (addr != INV) {
+                const Node* nd = &nodes[addr];
+                if (cnt < (64 << 12)) buf[cnt++] = addr;
+                if (nd->left != INV) {
+                    float a0, a1, b0, b1;
+                    bbox(nd->lmin, nd->lmax, inv, oxi, ct, &a0, &a1);
+                    bbox(nd->rmin, nd->rmax, inv, oxi, ct, &b0, &b1);
+                    int h0 = a0 <= a1, h1 = b0 <= b1, c1 = h1 && (a0 > b0);
+                    if (h0 || h1) {
+                        uint32_t def;
+                        if (c1 || !h0) { addr = nd->right; def = nd->left; } else { addr = nd->left; def = nd->right; }
+                        if (h0 && h1) stack[sp++] = def;
+                        continue;
+                    }
+                } else if (r->extra[0] != (int)nd->mesh) {
+                    float t = tri(r, nd, ct);
+                    if (t < ct) { ct = t; if (any) break; }
+                }
+                addr = stack[--sp];
+            }
+        }
+        qsort(buf, cnt, sizeof(uint32_t), cmp_u32);
+        int u = cnt ? 1 : 0;
+        for (int j = 1; j < cnt; ++j) u += buf[j] != buf[j - 1];
+        out_waves[w] = u;
+    }
+    free(buf);
+}
