@@ -964,7 +964,9 @@ __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const i
         r.d = ld3(d);
         r.tmax = o.w;
         r.mask = -1;
-        const bool occluded = traceAny<LAY>(c, r, lds + lane, raySpill(c, blockIdx.x, lane));
+        // occluder hints by origin cell (c.hint when on): the NEE rays to a directional light and the
+        // light-tracing rays toward the camera leave one cell nearly parallel
+        const bool occluded = shadowOccluded<LAY>(c, r, 0, lds + lane, raySpill(c, blockIdx.x, lane));
         const int code = __float_as_int(d.w);
         if (code >= 0) {
             if (occluded) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);

@@ -344,22 +344,17 @@ static hipError_t fill_hints(uint32_t* d, size_t n, uint32_t range, hipStream_t 
     return r;
 }
 static void with_hints(TraceCtx& c, mcrt_scene s, uint32_t* pix, uint32_t n) {
-    if (s->twoLevel || !hints_enabled()) return;
-    if (pix) {
-        c.hint = pix;
-        c.hintMode = MCRT_HINT_PIXEL;
-        c.hintPixels = n;
-        return;
-    }
-    if (!s->dHintCell) return;
-    c.hint = s->dHintCell;
-    c.hintMode = MCRT_HINT_CELL;
+    if (s->twoLevel || !hints_enabled() || !s->dHintCell) return;
+    c.hintCell = s->dHintCell;
     c.hintMask = (1u << MCRT_HINT_CELL_BITS) - 1;
     for (int a = 0; a < 3; ++a) {
         const float ext = s->bbHi[a] - s->bbLo[a];
         c.hintLo[a] = s->bbLo[a];
-        c.hintScale[a] = ext > 0.0f ? (float)MCRT_HINT_GRID / ext : 0.0f;
+        c.hintInvExt[a] = ext > 0.0f ? 1.0f / ext : 0.0f;
     }
+    c.hint = pix ? pix : s->dHintCell;
+    c.hintMode = pix ? MCRT_HINT_PIXEL : MCRT_HINT_CELL;
+    c.hintPixels = n;
 }
 
 // the coherent launches' view (camera rays, bounce-0 shadow rays): wave packets when the tree allows
@@ -1547,7 +1542,9 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     HIPCHK(ctx, hipEventRecord(fb->bdptConnect, st));
     {
         Timed t(ctx, K_BDPT_VIS, cq.count, 0, st);
-        mcrt::launch_bdpt_vis(tcs, b, cq, (int)(C * N), st);
+        TraceCtx tvis = tcs;
+        with_hints(tvis, s, nullptr, 0);   // occluder hints by origin cell
+        mcrt::launch_bdpt_vis(tvis, b, cq, (int)(C * N), st);
     }
     if (bandSplit) {   // completed by mcrt_bdpt_gather once the ranks' splats are summed
         fb->bdptPendingGather = true;

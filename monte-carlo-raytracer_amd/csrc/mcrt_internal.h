@@ -96,16 +96,19 @@ struct TraceCtx {
     // a table of leaf indices that shadow rays test before walking the tree.  NULL = off.
     uint32_t* hint;
     int hintMode;           // MCRT_HINT_PIXEL: slot = path id % hintPixels; MCRT_HINT_CELL: hash of the
-                            // ray's origin cell (hintLo / hintScale, 512^3 over the scene bounds) and octant
+                            // ray's origin cell (MCRT_HINT_GRID^3 over the scene bounds) and octant
     uint32_t hintPixels;
+    uint32_t* hintCell;     // the origin-cell table (also given to pixel-mode launches)
     uint32_t hintMask;      // cell table entries - 1 (a power of two)
-    float hintLo[3], hintScale[3];
+    float hintLo[3], hintInvExt[3];   // cell = (o - hintLo) * hintInvExt * MCRT_HINT_GRID
     uint32_t numNodes;      // records in `nodes` (hints are range-checked against it)
 };
 #define MCRT_HINT_PIXEL 1
 #define MCRT_HINT_CELL 2
 #define MCRT_HINT_CELL_BITS 22
+#ifndef MCRT_HINT_GRID
 #define MCRT_HINT_GRID 512
+#endif
 
 namespace mcrt {
 // n rays, or with countDev (device memory) min(*countDev, n) of them

@@ -28,6 +28,11 @@
 // direction groups of the first shading's extension rays: octant x dominant axis, appended with
 // one LDS atomic per record (profiles/r03/ab items 18-19)
 #define MCRT_EXT_GROUPS 24
+// occluder hints of the bounce-0 shadow packets: 1 = the origin cell's occluder as a second
+// candidate after the pixel's, and the cell table updated too (profiles/r04/ab item 12)
+#ifndef MCRT_HINT_BOTH
+#define MCRT_HINT_BOTH 1
+#endif
 
 // ---------------------------------------------------------------------------
 // RadeonRays-compatible queries on AoS rays (mcrt_trace_closest / mcrt_trace_any).
@@ -196,21 +201,6 @@ __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict
     hitOut[i] = traceClosest<LAY>(c, r, lds + lane, raySpill(c, blk, lane), t);
 }
 
-// Any hit of one shadow ray: first the occluder hint of its slot (c.hint, plain records), then the
-// walk, whose occluder becomes the slot's next hint.
-template <int LAY>
-MCRT_DEV bool shadowOccluded(const TraceCtx& c, const TraceRay& r, int path, uint32_t* stk, uint32_t* spill) {
-    if (LAY == LAY_PLAIN && c.hint) {
-        const uint32_t h = hintSlot(c, r, path);
-        if (hintOccludes(c, r, c.hint[h])) return true;
-        float t;
-        const int leaf = traverse<true, LAY>(c, r, stk, spill, t);
-        if (leaf >= 0) c.hint[h] = (uint32_t)leaf;
-        return leaf >= 0;
-    }
-    return traceAny<LAY>(c, r, stk, spill);
-}
-
 // Any hit over the shadow queue + ShadowPass (PathTracing.cl:186-217):
 // sO = (o.xyz, tmax), sD = (d.xyz, pix), sL = throughput * L; radiance[pix] += L * V.
 template <int LAY>
@@ -288,17 +278,29 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
             r.mask = -1;
             // lanes whose occluder hint holds leave the packet before it starts
             const int pix = __float_as_int(d.w);
-            uint32_t h = 0;
+            uint32_t h = 0, h2 = 0;
             bool occ = false;
             if (valid && c.hint) {
                 h = hintSlot(c, r, pix);
+#if MCRT_HINT_BOTH
+                h2 = hintCellSlot(c, r);   // the origin cell's occluder as a second candidate
+                const uint32_t l1 = c.hint[h], l2 = c.hintCell[h2];
+                const bool o1 = hintOccludes(c, r, l1), o2 = l2 != l1 && hintOccludes(c, r, l2);
+                occ = o1 || o2;
+#else
                 occ = hintOccludes(c, r, c.hint[h]);
+#endif
             }
             float tt;
             const int leaf = traversePacket<true>(c.nodes, r, valid && !occ, tt);
             if (leaf >= 0) {
                 occ = true;
-                if (c.hint) c.hint[h] = (uint32_t)leaf;
+                if (c.hint) {
+                    c.hint[h] = (uint32_t)leaf;
+#if MCRT_HINT_BOTH
+                    c.hintCell[h2] = (uint32_t)leaf;
+#endif
+                }
             }
             if (valid) {
                 const float V = occ ? 0.0f : 1.0f;

@@ -422,15 +422,17 @@ MCRT_DEV bool hintOccludes(const TraceCtx& c, const TraceRay& r, uint32_t leaf) 
 // The hint table slot of a shadow ray: its path's pixel (bounce-0 rays of a TAA-jittered camera
 // start on nearly the same surface point every frame) or its origin cell and direction octant
 // (rays toward the same directional light from one cell are parallel and close).
-MCRT_DEV uint32_t hintSlot(const TraceCtx& c, const TraceRay& r, int path) {
-    if (c.hintMode == MCRT_HINT_PIXEL) return (uint32_t)path % c.hintPixels;
-    const float g = (float)(MCRT_HINT_GRID - 1);
-    const uint32_t cx = (uint32_t)fminf(fmaxf((r.o.x - c.hintLo[0]) * c.hintScale[0], 0.0f), g);
-    const uint32_t cy = (uint32_t)fminf(fmaxf((r.o.y - c.hintLo[1]) * c.hintScale[1], 0.0f), g);
-    const uint32_t cz = (uint32_t)fminf(fmaxf((r.o.z - c.hintLo[2]) * c.hintScale[2], 0.0f), g);
+MCRT_DEV uint32_t hintCellSlot(const TraceCtx& c, const TraceRay& r) {
+    constexpr float G = (float)MCRT_HINT_GRID, g = G - 1.0f;
+    const uint32_t cx = (uint32_t)fminf(fmaxf((r.o.x - c.hintLo[0]) * c.hintInvExt[0] * G, 0.0f), g);
+    const uint32_t cy = (uint32_t)fminf(fmaxf((r.o.y - c.hintLo[1]) * c.hintInvExt[1] * G, 0.0f), g);
+    const uint32_t cz = (uint32_t)fminf(fmaxf((r.o.z - c.hintLo[2]) * c.hintInvExt[2] * G, 0.0f), g);
     const uint32_t oct = (r.d.x < 0.f ? 1u : 0u) | (r.d.y < 0.f ? 2u : 0u) | (r.d.z < 0.f ? 4u : 0u);
     const uint32_t key = ((cz * MCRT_HINT_GRID + cy) * MCRT_HINT_GRID + cx) * 8u + oct;
     return (key * 2654435761u) >> (32 - MCRT_HINT_CELL_BITS) & c.hintMask;
+}
+MCRT_DEV uint32_t hintSlot(const TraceCtx& c, const TraceRay& r, int path) {
+    return c.hintMode == MCRT_HINT_PIXEL ? (uint32_t)path % c.hintPixels : hintCellSlot(c, r);
 }
 
 // ---------------------------------------------------------------------------
@@ -594,6 +596,21 @@ MCRT_DEV bool traceAny(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint
     } else {
         return traverse<true, LAY>(c, r, stk, spill, t) >= 0;
     }
+}
+
+// Any hit of one shadow / connection ray: first the occluder hint of its slot (c.hint, plain
+// records; mcrt_traverse.h hintOccludes), then the walk, whose occluder becomes the slot's next hint.
+template <int LAY>
+MCRT_DEV bool shadowOccluded(const TraceCtx& c, const TraceRay& r, int path, uint32_t* stk, uint32_t* spill) {
+    if (LAY == LAY_PLAIN && c.hint) {
+        const uint32_t h = hintSlot(c, r, path);
+        if (hintOccludes(c, r, c.hint[h])) return true;
+        float t;
+        const int leaf = traverse<true, LAY>(c, r, stk, spill, t);
+        if (leaf >= 0) c.hint[h] = (uint32_t)leaf;
+        return leaf >= 0;
+    }
+    return traceAny<LAY>(c, r, stk, spill);
 }
 
 // XCD-aware workgroup order for the traversal launches.  Workgroups are dealt round-robin to the

@@ -4,7 +4,7 @@ triangle and box arithmetic, and skips the walk when both pass.  The answer must
 ANY hint content, so every frame is compared bit for bit with hints off (MCRT_SHADOW_HINTS=0):
 the pixel hints (bounce 0, wave packets and per ray), the cell hints (later bounces, D = 2 and 3),
 hints carried over from earlier calls, and tables filled with random leaf indices
-(MCRT_TEST_HINT_FILL)."""
+(MCRT_TEST_HINT_FILL); BDPT's connection rays take the cell hints too."""
 import os
 
 import numpy as np
@@ -16,14 +16,15 @@ from mcrt.camera import scene_camera
 pytestmark = pytest.mark.gpu
 
 
-def _frames(hip_ctx, sc, name, W, H, max_depth, calls=3, batch=4):
+def _frames(hip_ctx, sc, name, W, H, max_depth, calls=3, batch=4, integrator=None):
     from mcrt import lib
     ds = lib.DeviceScene(hip_ctx, sc)
     fb = lib.FrameBuffer(hip_ctx, W, H)
     out = []
     for c in range(calls):   # TAA-jittered cameras, as the bench
         cams = [scene_camera(name, W, H, frame=c * batch + k, jitter=True) for k in range(batch)]
-        fb.render_frames(ds, cams, frame=c * batch, max_depth=max_depth)
+        kw = {} if integrator is None else {"integrator": integrator}
+        fb.render_frames(ds, cams, frame=c * batch, max_depth=max_depth, **kw)
         hip_ctx.sync()
         out.append(np.stack([fb.read_frame(k) for k in range(batch)]))
     fb.close()
@@ -65,3 +66,14 @@ def test_hints_change_no_answer(hip_ctx, sm_small, name, max_depth, env):
     assert on[..., :3].max() > 0
     diff = on.view(np.uint32) != off.view(np.uint32)
     assert not diff.any(), f"{int(diff.any(-1).sum())} pixels differ"
+
+
+def test_bdpt_visibility_hints(hip_ctx, sm_small):
+    """k_bdpt_vis takes the origin-cell hints: the same visibility answers, so the frames agree up to
+    the order of the light-tracing splats' float atomics (test_gpu_bdpt.py's 4e-6)."""
+    from mcrt import types as T
+    args = (hip_ctx, sm_small, "san_miguel_proxy", 256, 144, 2)
+    on = _with_env({"MCRT_SHADOW_HINTS": "1"}, lambda: _frames(*args, integrator=T.INTEGRATOR_BDPT))
+    off = _with_env({"MCRT_SHADOW_HINTS": "0"}, lambda: _frames(*args, integrator=T.INTEGRATOR_BDPT))
+    assert np.isfinite(on).all() and on[..., :3].max() > 0
+    np.testing.assert_allclose(on[..., :3], off[..., :3], rtol=4e-6, atol=4e-6)

@@ -6,6 +6,8 @@
 #   tools/gpu_task.sh bench     [DIR] [bench args...]     the driver's default bench (+ extra args)
 #   tools/gpu_task.sh ab        LIB_A [RUNS] [bench args] alternating bench runs: in-tree library (B)
 #                                                         vs LIB_A (MCRT_LIB_PATH), per-kernel times
+#   tools/gpu_task.sh sweep     R "bench args" V...       R rounds of the in-tree library, then each
+#                                                         variant libmcrt_<V>.so (MCRT_LIB_PATH)
 #   tools/gpu_task.sh evidence  [DIR]                     kernel trace + PMC passes of the PT timed call
 #                                                         (-> pmc_latest.json, timed_call_trace.txt);
 #                                                         SCALE=1 adds the per-rank scaling emulation
@@ -67,6 +69,18 @@ ab)
   done
   summary $P/A*.json $P/B*.json
   ;;
+sweep)
+  # rounds of: the in-tree library, then each variant libmcrt_<V>.so (tools/build_variant.sh)
+  R=$1; ARGS=$2; shift 2; P=gpurun_out/sweep; mkdir -p $P
+  B="python3 bench.py --no-cpu-baseline --no-roofline-model $ARGS"
+  for r in $(seq 1 $R); do
+    timeout -k 10 400 $B > $P/base_$r.json 2> $P/base_$r.err || fail base$r $P/base_$r.err 4
+    for v in "$@"; do
+      MCRT_LIB_PATH=$PWD/monte-carlo-raytracer_amd/libmcrt_$v.so timeout -k 10 400 $B > $P/${v}_$r.json 2> $P/${v}_$r.err || fail $v$r $P/${v}_$r.err 4
+    done
+  done
+  summary $P/*.json
+  ;;
 evidence)
   P=gpurun_out/${1:-evidence}; mkdir -p $P
   pmc_passes $P python3 bench.py --no-kernel-timing --no-bdpt --no-cpu-baseline --no-roofline-model
@@ -112,6 +126,6 @@ print('images bit-identical:', a.shape == b.shape and np.array_equal(a.view(np.u
   summary $P/n1.json $P/nN.json
   ;;
 *)
-  echo "unknown task '$task' (suite | bench | ab | evidence | bdpt-prof | configs | rehearse)"; exit 2
+  echo "unknown task '$task' (suite | bench | ab | sweep | evidence | bdpt-prof | configs | rehearse)"; exit 2
   ;;
 esac

@@ -277,3 +277,41 @@ void sim_union(const Node* nodes, const Ray* rays, int n, int any, const uint8_t
     }
     free(buf);
 }
+
+/* Closest-hit visits when the walk starts with closest = seed[i] (a known hit distance, e.g.
+ * hit_t * (1 + 1e-4)): an upper bound of what a hit-distance hint could save. out: visits. */
+void sim_seeded(const Node* nodes, const Ray* rays, int n, const float* seed, int32_t* out) {
+    static uint32_t stack[1 << 16];
+    for (int i = 0; i < n; ++i) {
+        const Ray* r = &rays[i];
+        out[i] = 0;
+        if (r->extra[1] == 0) continue;
+        float inv[3], oxi[3];
+        for (int k = 0; k < 3; ++k) { inv[k] = sinv(r->d[k]); oxi[k] = -r->o[k] * inv[k]; }
+        float ct = seed[i] < r->o[3] ? seed[i] : r->o[3];
+        uint32_t addr = 0;
+        int sp = 0, nv = 0;
+        stack[sp++] = INV;
+        while (addr != INV) {
+            const Node* nd = &nodes[addr];
+            ++nv;
+            if (nd->left != INV) {
+                float a0, a1, b0, b1;
+                bbox(nd->lmin, nd->lmax, inv, oxi, ct, &a0, &a1);
+                bbox(nd->rmin, nd->rmax, inv, oxi, ct, &b0, &b1);
+                int h0 = a0 <= a1, h1 = b0 <= b1, c1 = h1 && (a0 > b0);
+                if (h0 || h1) {
+                    uint32_t def;
+                    if (c1 || !h0) { addr = nd->right; def = nd->left; } else { addr = nd->left; def = nd->right; }
+                    if (h0 && h1) stack[sp++] = def;
+                    continue;
+                }
+            } else if (r->extra[0] != (int)nd->mesh) {
+                float t = tri(r, nd, ct);
+                if (t < ct) ct = t;
+            }
+            addr = stack[--sp];
+        }
+        out[i] = nv;
+    }
+}
