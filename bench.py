@@ -145,18 +145,20 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
     return out
 
 
-def gather_ceiling(ctx, rl, vq, avg_ms):
+def gather_ceiling(ctx, rl, vq, avg_ms, hint_frac=0.0):
     """The latency roofline of the traversal launch: its node-visit rate (the launch's rays x the
     oracle's visits per query, over its HIP-event time) against the rate of a pure dependent-gather
     probe with the same access pattern (mcrt_ctx_gather_chase: chains of 64-B records fetched as
     four 16-B loads, links read from the record just fetched, 32 waves per CU) with its records
     resident in L2, in the Infinity Cache, or (the tree's own size) in HBM.  A node visit also
-    does the slab / triangle arithmetic and stack work the probe leaves out."""
+    does the slab / triangle arithmetic and stack work the probe leaves out.  hint_frac: the share of
+    the launch's shadow rays answered by their occluder hint (two record fetches instead of a walk)."""
     rays = rl["rays_per_launch"]
-    visits = rays["extension"] * vq["k_extend"] + rays["shadow"] * vq["k_shadow"]
+    hinted = rays["shadow"] * hint_frac
+    visits = rays["extension"] * vq["k_extend"] + (rays["shadow"] - hinted) * vq["k_shadow"] + 2 * hinted
     rate = visits / (avg_ms * 1e-3) / 1e9
     out = {"unit": "G dependent 64-B record fetches / s", "node_visits_per_launch": int(visits),
-           "node_visits_per_s": round(rate, 1), "ceilings": {}}
+           "node_visits_per_s": round(rate, 1), "shadow_rays_hinted": round(hint_frac, 4), "ceilings": {}}
     try:
         for name, recs in (("l2_resident_2MiB", 32768), ("infinity_cache_resident_122MiB", 2_000_000),
                            ("hbm_tree_size", int(rl["nodes_total"]))):
@@ -560,6 +562,7 @@ def main():
     ctx.sync()
     fstats = fb.stats()
     qcounts = fb.queue_counts() if not bdpt else None
+    hcounts = fb.hint_counts() if not bdpt else None   # shadow rays answered by their occluder hint
     frame0 = warm + 1
 
     ctx.reset_stats()
@@ -647,6 +650,8 @@ def main():
         rays = {"closest": fstats["closest_rays"] / (W * H / world), "any": fstats["any_rays"] / (W * H / world),
                 "shaded": fstats["shaded_paths"] / (W * H / world)}
         out["rays_per_path"] = {k: round(v, 4) for k, v in rays.items()}
+        if hcounts is not None and qcounts is not None:   # occluder hints
+            out["shadow_hints"] = {f"bounce{b}": round(hcounts[b] / max(qcounts[0][b], 1), 4) for b in range(D)}
         # (the CPU oracle and the roofline's node counts price the flat structure)
         oracle_ok = world == 1 and not bdpt and sampler == T.SAMPLER_RANDOM and not two_level
         cpu = None
@@ -681,8 +686,9 @@ def main():
                 out["roofline"] = roofline_shadow_extend(scene, cam_of, W, H, D, stats_batch, avg_ms, qcounts, ctx,
                                                          cpu["_oracle"] if cpu else None)
                 if "visits_per_query" in out:
+                    hf = hcounts[0] / max(qcounts[0][0], 1) if hcounts else 0.0
                     out["roofline"]["gather_ceiling"] = gather_ceiling(ctx, out["roofline"], out["visits_per_query"],
-                                                                       avg_ms)
+                                                                       avg_ms, hf)
         if bd is not None:
             bdo = {k: v for k, v in bd.items() if not k.startswith("_")}
             if oracle_ok and sampler == T.SAMPLER_RANDOM and not args.no_cpu_baseline:

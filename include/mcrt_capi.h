@@ -497,6 +497,10 @@ MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closes
 /* Queue sizes of the last PT render, per bounce b < max: shadow[b] = shadow rays queued by
  * bounce b's shading, extension[b] = extension rays queued for bounce b+1. */
 MCRT_API mcrt_status mcrt_framebuffer_queue_counts(mcrt_framebuffer fb, int32_t* shadow, int32_t* extension, int max);
+/* Shadow rays of the last PT render answered by their occluder hint, per bounce b < max (the rest
+ * walked the tree; the reference walks every one, intersect_bvh2_lds.cl:229-363, with the same
+ * answers).  All zero when the hints are off (MCRT_SHADOW_HINTS=0) or the structure is two-level. */
+MCRT_API mcrt_status mcrt_framebuffer_hint_counts(mcrt_framebuffer fb, int32_t* hits, int max);
 /* Host copy of a ray queue of the last render (the state the reference keeps in its
  * per-pixel trace_shadowRays / trace_rays / throughput buffers):
  *   which 0: shadow queue of the last bounce    -- origin.xyz|tmax, dir.xyz|pixel(int bits), throughput*L

@@ -1702,12 +1702,14 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
             TraceCtx tse = b == 0 ? packet_ctx(s) : tcs;
             tse.spill = slot.spill;
             with_hints(tse, s, b == 0 ? fb->hintPix : nullptr, (uint32_t)fb->N);
+            if (tse.hint) tse.hintHits = fb->counters + 64 + b;
             mcrt::launch_shadow_extend(tse, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
                                        fb->sO, fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
             Timed t(ctx, K_SHADOW, shadowCnt + b, 0, st);
             TraceCtx tsh = tcs;
             with_hints(tsh, s, b == 0 ? fb->hintPix : nullptr, (uint32_t)fb->N);
+            if (tsh.hint) tsh.hintHits = fb->counters + 64 + b;
             mcrt::launch_shadow(tsh, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, qCap, st);
         }
     }
@@ -1964,6 +1966,20 @@ MCRT_API mcrt_status mcrt_framebuffer_queue_counts(mcrt_framebuffer fb, int32_t*
         const bool live = b < fb->lastMaxDepth && fb->lastIntegrator == MCRT_INTEGRATOR_PT;
         if (shadow) shadow[b] = live ? c[b] : 0;
         if (extension) extension[b] = live && b + 1 < fb->lastMaxDepth ? c[32 + b] : 0;
+    }
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_hint_counts(mcrt_framebuffer fb, int32_t* hits, int max) {
+    if (!fb || max < 0) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, fb_sync(fb));
+    int c[128];
+    HIPCHK(ctx, hipMemcpy(c, fb->counters, sizeof(c), hipMemcpyDeviceToHost));
+    for (int b = 0; b < max && b < 32; ++b) {
+        const bool live = b < fb->lastMaxDepth && fb->lastIntegrator == MCRT_INTEGRATOR_PT;
+        if (hits) hits[b] = live ? c[64 + b] : 0;
     }
     return MCRT_OK;
 }

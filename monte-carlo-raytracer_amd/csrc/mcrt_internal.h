@@ -102,6 +102,7 @@ struct TraceCtx {
     uint32_t hintMask;      // cell table entries - 1 (a power of two)
     float hintLo[3], hintInvExt[3];   // cell = (o - hintLo) * hintInvExt * MCRT_HINT_GRID
     uint32_t numNodes;      // records in `nodes` (hints are range-checked against it)
+    int* hintHits;          // rays answered by their hint are counted here (NULL: not counted)
 };
 #define MCRT_HINT_PIXEL 1
 #define MCRT_HINT_CELL 2

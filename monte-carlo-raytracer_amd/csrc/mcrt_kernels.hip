@@ -291,6 +291,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
                 occ = hintOccludes(c, r, c.hint[h]);
 #endif
             }
+            countHintHits(c, occ);
             float tt;
             const int leaf = traversePacket<true>(c.nodes, r, valid && !occ, tt);
             if (leaf >= 0) {

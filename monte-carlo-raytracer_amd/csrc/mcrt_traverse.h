@@ -598,13 +598,22 @@ MCRT_DEV bool traceAny(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint
     }
 }
 
+// One atomic per wave: the lanes whose hint answered (mcrt_framebuffer_hint_counts).
+MCRT_DEV void countHintHits(const TraceCtx& c, bool ok) {
+    if (!c.hintHits) return;
+    const uint64_t m = __ballot(ok), act = __ballot(true);
+    if (m != 0 && (int)__lane_id() == (int)__builtin_ctzll(act)) atomicAdd(c.hintHits, (int)__popcll(m));
+}
+
 // Any hit of one shadow / connection ray: first the occluder hint of its slot (c.hint, plain
 // records; mcrt_traverse.h hintOccludes), then the walk, whose occluder becomes the slot's next hint.
 template <int LAY>
 MCRT_DEV bool shadowOccluded(const TraceCtx& c, const TraceRay& r, int path, uint32_t* stk, uint32_t* spill) {
     if (LAY == LAY_PLAIN && c.hint) {
         const uint32_t h = hintSlot(c, r, path);
-        if (hintOccludes(c, r, c.hint[h])) return true;
+        const bool ok = hintOccludes(c, r, c.hint[h]);
+        countHintHits(c, ok);
+        if (ok) return true;
         float t;
         const int leaf = traverse<true, LAY>(c, r, stk, spill, t);
         if (leaf >= 0) c.hint[h] = (uint32_t)leaf;

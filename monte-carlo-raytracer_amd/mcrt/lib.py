@@ -81,6 +81,7 @@ SIGNATURES = {
                                                 _c.POINTER(_c.c_int32)]),
     "mcrt_framebuffer_read_queue": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int32)]),
     "mcrt_framebuffer_queue_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.POINTER(_c.c_int32), _c.c_int]),
+    "mcrt_framebuffer_hint_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.c_int]),
     "mcrt_postprocess": (_c.c_int, [_vp, _c.POINTER(T.PostprocessParams)]),
     "mcrt_render_aov": (_c.c_int, [_vp, _vp, _vp, _vp, _c.c_int, _vp]),
     "mcrt_framebuffer_read_bdpt": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64)]),
@@ -443,6 +444,12 @@ class FrameBuffer:
         ex = (_c.c_int32 * max_bounces)()
         _check(lib().mcrt_framebuffer_queue_counts(self.h, sh, ex, max_bounces), self.ctx.h)
         return list(sh), list(ex)
+
+    def hint_counts(self, max_bounces=8):
+        """hits[b]: shadow rays of bounce b answered by their occluder hint in the last PT render."""
+        h = (_c.c_int32 * max_bounces)()
+        _check(lib().mcrt_framebuffer_hint_counts(self.h, h, max_bounces), self.ctx.h)
+        return list(h)
 
     def read_queue(self, which):
         """(a, b, c) float4 arrays of the last bounce's shadow (0) / extension (1) queue."""

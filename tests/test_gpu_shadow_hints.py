@@ -77,3 +77,29 @@ def test_bdpt_visibility_hints(hip_ctx, sm_small):
     off = _with_env({"MCRT_SHADOW_HINTS": "0"}, lambda: _frames(*args, integrator=T.INTEGRATOR_BDPT))
     assert np.isfinite(on).all() and on[..., :3].max() > 0
     np.testing.assert_allclose(on[..., :3], off[..., :3], rtol=4e-6, atol=4e-6)
+
+
+def test_hint_counts(hip_ctx, sm_small):
+    """mcrt_framebuffer_hint_counts: the hints answer a large share of the occluded bounce-0 shadow
+    rays from the second call on (the pixel table holds the first call's occluders), none when off."""
+    from mcrt import lib
+
+    def run():
+        ds = lib.DeviceScene(hip_ctx, sm_small)
+        fb = lib.FrameBuffer(hip_ctx, 256, 144)
+        got = []
+        for c in range(2):
+            cams = [scene_camera("san_miguel_proxy", 256, 144, frame=4 * c + k, jitter=True) for k in range(4)]
+            fb.render_frames(ds, cams, frame=4 * c, max_depth=2)
+            got.append((fb.hint_counts(2), fb.queue_counts(2)[0]))
+        fb.close()
+        ds.close()
+        return got
+
+    on = _with_env({"MCRT_SHADOW_HINTS": "1"}, run)
+    off = _with_env({"MCRT_SHADOW_HINTS": "0"}, run)
+    (h1, q1), (h2, q2) = on
+    assert all(0 <= h <= q for h, q in zip(h2, q2))
+    assert h2[0] > 0.2 * q2[0], (h2, q2)     # bounce 0: pixel + cell hints of the first call
+    assert h2[1] > 0, (h2, q2)                # bounce 1: cell hints
+    assert all(h == 0 for h, _ in [(x, None) for x in off[1][0]])
