@@ -557,9 +557,11 @@ def main():
     run(0, warm)
     ctx.sync()
     warm_frames = warm + 1   # + the untimed statistics frame below (the driver's W is a minimum)
-    # per-frame path statistics (device queue sizes) from one untimed frame
+    # per-frame path statistics (device queue sizes, occluder-hint counts) from one untimed frame
+    ctx.set_profiling(2)
     step(warm)
     ctx.sync()
+    ctx.set_profiling(False)
     fstats = fb.stats()
     qcounts = fb.queue_counts() if not bdpt else None
     hcounts = fb.hint_counts() if not bdpt else None   # shadow rays answered by their occluder hint

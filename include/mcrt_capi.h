@@ -266,7 +266,9 @@ MCRT_API mcrt_status mcrt_ctx_set_stream(mcrt_ctx ctx, void* stream);
 /* The context stream (hipStream_t) that accumulation and the frame-buffer copies are enqueued on:
  * a caller orders its own work (e.g. an RCCL collective) after them with it. */
 MCRT_API mcrt_status mcrt_ctx_get_stream(mcrt_ctx ctx, void** stream);
-/* Per-kernel HIP-event timing (replaces QueryManager GPU timers, source/engine/util/QueryManager.h:141-164). */
+/* Per-kernel HIP-event timing (replaces QueryManager GPU timers, source/engine/util/QueryManager.h:141-164).
+ * enable = 2 also counts the shadow rays answered by their occluder hint (mcrt_framebuffer_hint_counts);
+ * those counters are device atomics that slow the shadow launches by a few per cent, so timing runs use 1. */
 MCRT_API mcrt_status mcrt_ctx_set_profiling(mcrt_ctx ctx, int enable);
 /* Synchronizes, then fills up to max entries: kernel name, summed HIP-event time (ms),
  * launch count and items processed (pixels / rays / paths); *count = kernels with stats. */
@@ -499,7 +501,8 @@ MCRT_API mcrt_status mcrt_framebuffer_stats(mcrt_framebuffer fb, int64_t* closes
 MCRT_API mcrt_status mcrt_framebuffer_queue_counts(mcrt_framebuffer fb, int32_t* shadow, int32_t* extension, int max);
 /* Shadow rays of the last PT render answered by their occluder hint, per bounce b < max (the rest
  * walked the tree; the reference walks every one, intersect_bvh2_lds.cl:229-363, with the same
- * answers).  All zero when the hints are off (MCRT_SHADOW_HINTS=0) or the structure is two-level. */
+ * answers).  Counted while mcrt_ctx_set_profiling(ctx, 2) is on; zero otherwise, when the hints are
+ * off (MCRT_SHADOW_HINTS=0) or the structure is two-level. */
 MCRT_API mcrt_status mcrt_framebuffer_hint_counts(mcrt_framebuffer fb, int32_t* hits, int max);
 /* Host copy of a ray queue of the last render (the state the reference keeps in its
  * per-pixel trace_shadowRays / trace_rays / throughput buffers):

@@ -53,6 +53,7 @@ struct mcrt_ctx_s {
     hipStream_t stream = nullptr;
     int numCUs = 256;
     bool profiling = false;
+    bool countHints = false;   // mcrt_ctx_set_profiling(2): occluder-hint counters (one atomic per wave)
     int* dFlags = nullptr;          // device flags: [0] traversal-stack overflow (mcrt_traverse.h), set by any launch
     std::string error;
     struct Pending {
@@ -465,6 +466,7 @@ MCRT_API mcrt_status mcrt_ctx_get_stream(mcrt_ctx ctx, void** stream) {
 MCRT_API mcrt_status mcrt_ctx_set_profiling(mcrt_ctx ctx, int enable) {
     if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
     ctx->profiling = enable != 0;
+    ctx->countHints = enable >= 2;
     return MCRT_OK;
 }
 
@@ -1702,14 +1704,14 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
             TraceCtx tse = b == 0 ? packet_ctx(s) : tcs;
             tse.spill = slot.spill;
             with_hints(tse, s, b == 0 ? fb->hintPix : nullptr, (uint32_t)fb->N);
-            if (tse.hint) tse.hintHits = fb->counters + 64 + b;
+            if (tse.hint && ctx->countHints) tse.hintHits = fb->counters + 64 + b;
             mcrt::launch_shadow_extend(tse, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
                                        fb->sO, fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
             Timed t(ctx, K_SHADOW, shadowCnt + b, 0, st);
             TraceCtx tsh = tcs;
             with_hints(tsh, s, b == 0 ? fb->hintPix : nullptr, (uint32_t)fb->N);
-            if (tsh.hint) tsh.hintHits = fb->counters + 64 + b;
+            if (tsh.hint && ctx->countHints) tsh.hintHits = fb->counters + 64 + b;
             mcrt::launch_shadow(tsh, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, qCap, st);
         }
     }

@@ -599,8 +599,11 @@ MCRT_DEV bool traceAny(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint
 }
 
 // One atomic per wave: the lanes whose hint answered (mcrt_framebuffer_hint_counts).
+#ifndef MCRT_HINT_COUNT
+#define MCRT_HINT_COUNT 1
+#endif
 MCRT_DEV void countHintHits(const TraceCtx& c, bool ok) {
-    if (!c.hintHits) return;
+    if (!MCRT_HINT_COUNT || !c.hintHits) return;
     const uint64_t m = __ballot(ok), act = __ballot(true);
     if (m != 0 && (int)__lane_id() == (int)__builtin_ctzll(act)) atomicAdd(c.hintHits, (int)__popcll(m));
 }

@@ -172,7 +172,8 @@ class Context:
         return st.value or 0
 
     def set_profiling(self, on=True):
-        _check(lib().mcrt_ctx_set_profiling(self.h, 1 if on else 0), self.h)
+        """on: True / 1 = per-kernel HIP events; 2 = also the occluder-hint counters."""
+        _check(lib().mcrt_ctx_set_profiling(self.h, int(on)), self.h)
 
     def reset_stats(self):
         _check(lib().mcrt_ctx_reset_stats(self.h), self.h)

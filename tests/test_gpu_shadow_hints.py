@@ -87,11 +87,13 @@ def test_hint_counts(hip_ctx, sm_small):
     def run():
         ds = lib.DeviceScene(hip_ctx, sm_small)
         fb = lib.FrameBuffer(hip_ctx, 256, 144)
+        hip_ctx.set_profiling(2)   # counters on
         got = []
         for c in range(2):
             cams = [scene_camera("san_miguel_proxy", 256, 144, frame=4 * c + k, jitter=True) for k in range(4)]
             fb.render_frames(ds, cams, frame=4 * c, max_depth=2)
             got.append((fb.hint_counts(2), fb.queue_counts(2)[0]))
+        hip_ctx.set_profiling(False)
         fb.close()
         ds.close()
         return got
