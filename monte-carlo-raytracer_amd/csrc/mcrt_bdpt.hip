@@ -549,6 +549,9 @@ MCRT_DEV uint32_t bounceKey(const BdptArgs& b, f3 o, f3 d) {
     return (oct << 13) | (uint32_t)((cx << 8) | (cy << 5) | cz);
 }
 
+// FINAL: the launch of depth D + 1, whose queue holds camera rays only and whose vertices all end
+// their subpath -- no BSDF sampling, so its instantiation carries far fewer registers.
+template <bool FINAL>
 __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameArgs f, BdptArgs b, int depth,
                                                             BdptQueue qIn, const float4* __restrict__ hits,
                                                             BdptQueue qOut) {
@@ -617,7 +620,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                 if (isVertexOnSurface(cur.fr.gn)) cur.pdfFwd *= absDot(rayD, cur.fr.gn);
                 storePdfFwd(V, 0, pix, N, 0.0f);
             }
-            if (depth == D + (isCamera ? 1 : 0)) {   // subpath complete (BDPT.cl:395-403)
+            if (FINAL || depth == D + (isCamera ? 1 : 0)) {   // subpath complete (BDPT.cl:395-403)
                 if (hasMaterialNonDeltaComponents(s, materialIdx, cur.fr)) cur.flags |= VF_CONNECTIBLE;
                 storeVertex(V, depth, pix, N, cur);
             } else {
@@ -659,6 +662,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
     // (queue order = the block's ray order: grouping the next rays by direction as the PT first
     // shading does made this kernel 11 % slower -- its plane reads and writes follow the queue --
     // for 1 % on k_extend; profiles/r04/ab/README.txt)
+    if (FINAL) return;
     const int slot = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
     if (push) {
         pushRay(qOut, slot, no, tag, nd, nPdf, ntp);
@@ -1056,8 +1060,10 @@ void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,
                         const float4* hits, const BdptQueue& qOut, int maxCount, hipStream_t st) {
     const int blocks = (maxCount + BDPT_BLOCK - 1) / BDPT_BLOCK;
-    hipLaunchKernelGGL(k_bdpt_vertex, dim3(blocks > 0 ? blocks : 1), dim3(BDPT_BLOCK), 0, st, s, f, b, depth, qIn, hits,
-                       qOut);
+    // depth D + 1 (the round after the light subpaths ended at depth D): camera vertices that all end
+    const bool fin = depth >= 2 && depth == f.maxDepth + 1;
+    hipLaunchKernelGGL(fin ? k_bdpt_vertex<true> : k_bdpt_vertex<false>, dim3(blocks > 0 ? blocks : 1),
+                       dim3(BDPT_BLOCK), 0, st, s, f, b, depth, qIn, hits, qOut);
 }
 void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                          const BdptQueue& q, hipStream_t st) {

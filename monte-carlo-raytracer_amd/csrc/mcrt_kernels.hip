@@ -25,6 +25,10 @@
 // profiles/r03/ab item 17; the sweep's knobs: tools/experiments/r3_knobs.patch).
 #define SHADE0_BLOCK 512
 #define SHADEN_BLOCK 256
+// the last bounce's shading (no extension ray, 83 VGPRs unconstrained): waves per SIMD it is built for
+#ifndef MCRT_SHADEN_LAST_WAVES
+#define MCRT_SHADEN_LAST_WAVES 1
+#endif
 // direction groups of the first shading's extension rays: octant x dominant axis, appended with
 // one LDS atomic per record (profiles/r03/ab items 18-19)
 #define MCRT_EXT_GROUPS 24
@@ -398,7 +402,9 @@ struct ShadeOut {
 
 // LOD (k_shade0 with mcrt_frame_params.texture_lod): textures at this camera-ray hit are read
 // mip-mapped over the pixel footprint given by the ray differentials (ro, dxDir, dyDir).
-template <bool LOD = false>
+// EXT = false: the last bounce's instantiation (no extension ray; its sampling code and registers
+// are left out, so the launch keeps more waves resident).
+template <bool LOD = false, bool EXT = true>
 MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pix, float4 hit, f3 dir, f3 throughput,
                       int prevFlags, ShadeOut& o, f3 ro = f3{0, 0, 0}, f3 dxDir = f3{0, 0, 0}, f3 dyDir = f3{0, 0, 0}) {
     f3 add = splat3(0.0f);
@@ -465,7 +471,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
         }
     }
     // extension (PathTracing.cl:138-175)
-    if (bounce + 1 < f.maxDepth) {
+    if (EXT && bounce + 1 < f.maxDepth) {
         const f2 bsdfSample = getSample2D(sampler);
         if (isUber) {
             f3 wi;
@@ -544,8 +550,9 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
     if (o.pushE) { q.eOout[es] = o.eO; q.eDout[es] = o.eD; q.eTout[es] = o.eT; }
 }
 
-// Bounce >= 1: the compacted extension queue of the previous bounce.
-__global__ __launch_bounds__(SHADEN_BLOCK) void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
+// Bounce >= 1: the compacted extension queue of the previous bounce.  LAST: bounce maxDepth - 1.
+template <bool LAST>
+__global__ __launch_bounds__(SHADEN_BLOCK, LAST ? MCRT_SHADEN_LAST_WAVES : 1) void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
                                                 const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                 const float4* __restrict__ qT, const float4* __restrict__ hits,
                                                 float4* __restrict__ radiance, QueueArgs q) {
@@ -562,7 +569,7 @@ __global__ __launch_bounds__(SHADEN_BLOCK) void k_shadeN(SceneArgs s, FrameArgs 
     if (i < n) {
         const float4 O = qO[i], D = qD[i], Tp = qT[i];
         const int pix = __float_as_int(O.w);
-        const f3 add = shadePath(s, f, bounce, pix, hits[i], ld3(D), ld3(Tp), __float_as_int(D.w), o);
+        const f3 add = shadePath<false, !LAST>(s, f, bounce, pix, hits[i], ld3(D), ld3(Tp), __float_as_int(D.w), o);
         if (add.x != 0.0f || add.y != 0.0f || add.z != 0.0f || add.x != add.x) {
             float4 r = radiance[pix];
             r.x += add.x; r.y += add.y; r.z += add.z;
@@ -571,6 +578,7 @@ __global__ __launch_bounds__(SHADEN_BLOCK) void k_shadeN(SceneArgs s, FrameArgs 
     }
     const int ss = blockAppend<SHADEN_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
     if (o.pushS) { q.sO[ss] = o.sO; q.sD[ss] = o.sD; q.sL[ss] = o.sL; }
+    if (LAST) return;
     // extension rays grouped by direction octant inside the block's queue slice
     const int oct = (o.eD.x < 0.0f ? 1 : 0) | (o.eD.y < 0.0f ? 2 : 0) | (o.eD.z < 0.0f ? 4 : 0);
     const int es = blockAppendGrouped<SHADEN_BLOCK / 64, 8>(q.extCountOut, o.pushE, oct, ldsGroup);
@@ -956,8 +964,8 @@ void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int
                    const float4* qD, const float4* qT, const float4* hits, float4* radiance, const QueueArgs& q,
                    int maxCount, hipStream_t st) {
     const int blocks = (maxCount + SHADEN_BLOCK - 1) / SHADEN_BLOCK;
-    hipLaunchKernelGGL(k_shadeN, dim3(blocks > 0 ? blocks : 1), dim3(SHADEN_BLOCK), 0, st, s, f, bounce, countIn, qO, qD,
-                       qT, hits, radiance, q);
+    hipLaunchKernelGGL(bounce + 1 >= f.maxDepth ? k_shadeN<true> : k_shadeN<false>, dim3(blocks > 0 ? blocks : 1),
+                       dim3(SHADEN_BLOCK), 0, st, s, f, bounce, countIn, qO, qD, qT, hits, radiance, q);
 }
 void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits, int which,
                 float4* out, hipStream_t st) {
