@@ -41,6 +41,8 @@
 #include "mcrt_shading.h"
 
 #define BDPT_BLOCK 256
+// (register caps for more resident waves spill and lose: k_bdpt_vertex at 5 waves +8 %,
+// k_bdpt_connect's GENERAL / NEE classes at 4 waves +20 %; profiles/r04/ab/README.txt item 15)
 #define BDPT_LIGHT_KEY_BITS 13
 #define BDPT_LIGHT_KEY_NONE ((1u << BDPT_LIGHT_KEY_BITS) - 1)
 #define BDPT_BOUNCE_KEY_BITS 16
@@ -1044,7 +1046,8 @@ namespace mcrt {
 size_t bdpt_light_sort_temp_bytes(int n) {
     size_t bytes = 0;
     uint32_t* k = nullptr;
-    rocprim::radix_sort_pairs(nullptr, bytes, k, k, k, k, (size_t)n, 0, BDPT_BOUNCE_KEY_BITS, (hipStream_t)0);
+    // a size query: no launch, and a failure leaves bytes = 0 (the caller's allocation then fails loudly)
+    (void)rocprim::radix_sort_pairs(nullptr, bytes, k, k, k, k, (size_t)n, 0, BDPT_BOUNCE_KEY_BITS, (hipStream_t)0);
     return bytes;
 }
 hipError_t bdpt_light_sort(uint32_t* keys, uint32_t* keys2, uint32_t* slots, uint32_t* perm, int n, void* tmp,

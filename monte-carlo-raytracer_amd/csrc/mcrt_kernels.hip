@@ -25,10 +25,8 @@
 // profiles/r03/ab item 17; the sweep's knobs: tools/experiments/r3_knobs.patch).
 #define SHADE0_BLOCK 512
 #define SHADEN_BLOCK 256
-// the last bounce's shading (no extension ray, 83 VGPRs unconstrained): waves per SIMD it is built for
-#ifndef MCRT_SHADEN_LAST_WAVES
-#define MCRT_SHADEN_LAST_WAVES 1
-#endif
+// (register caps for more resident waves spill and lose: k_shade0 at 5 waves +7 %, the last-bounce
+// k_shadeN at 6 waves +33 %; profiles/r04/ab/README.txt items 14-15)
 // direction groups of the first shading's extension rays: octant x dominant axis, appended with
 // one LDS atomic per record (profiles/r03/ab items 18-19)
 #define MCRT_EXT_GROUPS 24
@@ -552,7 +550,7 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
 
 // Bounce >= 1: the compacted extension queue of the previous bounce.  LAST: bounce maxDepth - 1.
 template <bool LAST>
-__global__ __launch_bounds__(SHADEN_BLOCK, LAST ? MCRT_SHADEN_LAST_WAVES : 1) void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
+__global__ __launch_bounds__(SHADEN_BLOCK) void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
                                                 const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                 const float4* __restrict__ qT, const float4* __restrict__ hits,
                                                 float4* __restrict__ radiance, QueueArgs q) {
