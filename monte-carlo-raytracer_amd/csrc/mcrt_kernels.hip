@@ -30,11 +30,6 @@
 // direction groups of the first shading's extension rays: octant x dominant axis, appended with
 // one LDS atomic per record (profiles/r03/ab items 18-19)
 #define MCRT_EXT_GROUPS 24
-// occluder hints of the bounce-0 shadow packets: 1 = the origin cell's occluder as a second
-// candidate after the pixel's, and the cell table updated too (profiles/r04/ab item 12)
-#ifndef MCRT_HINT_BOTH
-#define MCRT_HINT_BOTH 1
-#endif
 
 // ---------------------------------------------------------------------------
 // RadeonRays-compatible queries on AoS rays (mcrt_trace_closest / mcrt_trace_any).
@@ -284,25 +279,20 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
             bool occ = false;
             if (valid && c.hint) {
                 h = hintSlot(c, r, pix);
-#if MCRT_HINT_BOTH
-                h2 = hintCellSlot(c, r);   // the origin cell's occluder as a second candidate
+                // the origin cell's occluder as a second candidate (profiles/r04/ab/README.txt item 12)
+                h2 = hintCellSlot(c, r);
                 const uint32_t l1 = c.hint[h], l2 = c.hintCell[h2];
                 const bool o1 = hintOccludes(c, r, l1), o2 = l2 != l1 && hintOccludes(c, r, l2);
                 occ = o1 || o2;
-#else
-                occ = hintOccludes(c, r, c.hint[h]);
-#endif
             }
             countHintHits(c, occ);
             float tt;
             const int leaf = traversePacket<true>(c.nodes, r, valid && !occ, tt);
             if (leaf >= 0) {
                 occ = true;
-                if (c.hint) {
+                if (c.hint) {   // the next hint of the pixel and of the origin cell
                     c.hint[h] = (uint32_t)leaf;
-#if MCRT_HINT_BOTH
                     c.hintCell[h2] = (uint32_t)leaf;
-#endif
                 }
             }
             if (valid) {
