@@ -178,23 +178,6 @@ MCRT_DEV int traverseOct(const float4* __restrict__ nodes, const TraceRay& r, f3
 typedef float __attribute__((ext_vector_type(4))) PkV4;
 typedef const __attribute__((address_space(4))) PkV4* PkNodes;   // uniform loads -> s_load
 static_assert(MCRT_PK_STACK == 64, "the packet stack is one VGPR lane per entry");
-#ifndef MCRT_PK_WRITELANE
-#define MCRT_PK_WRITELANE 0
-#endif
-// Lane `lane` of the three stack VGPRs takes the wave-uniform values (a, b, c): v_writelane with the
-// lane select in M0 (gfx9 reads one SGPR per VALU instruction; M0 is the lane-select exception),
-// one s_nop after the M0 write.
-MCRT_DEV void pkPush3(int& vN, int& vLo, int& vHi, int lane, int a, int b, int c) {
-    __asm__ volatile(
-        "s_mov_b32 m0, %3\n\t"
-        "s_nop 1\n\t"
-        "v_writelane_b32 %0, %4, m0\n\t"
-        "v_writelane_b32 %1, %5, m0\n\t"
-        "v_writelane_b32 %2, %6, m0"
-        : "+v"(vN), "+v"(vLo), "+v"(vHi)
-        : "s"(lane), "s"(a), "s"(b), "s"(c)
-        : "m0");
-}
 MCRT_DEV float4 pkLoad(PkNodes p, int i) {
     const PkV4 v = p[i];
     return make_float4(v.x, v.y, v.z, v.w);
@@ -285,13 +268,6 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                 // deferred entries, bottom to top: F for the late lanes, then S.  Each slot is
                 // written whether or not it is pushed (the pointer only advances for a push), which
                 // stays below entry 2 D (see above)
-#if MCRT_PK_WRITELANE
-                // v_writelane: each value straight into lane sp (no lane compare + select)
-                pkPush3(stN, stLo, stHi, sp, (int)cF, (int)(uint32_t)late, (int)(uint32_t)(late >> 32));
-                sp += late != 0 ? 1 : 0;
-                pkPush3(stN, stLo, stHi, sp, (int)cS, (int)(uint32_t)mS, (int)(uint32_t)(mS >> 32));
-                sp += mS != 0 ? 1 : 0;
-#else
                 const bool at0 = lane == sp;
                 stN = at0 ? (int)cF : stN;
                 stLo = at0 ? (int)(uint32_t)late : stLo;
@@ -302,7 +278,6 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                 stLo = at1 ? (int)(uint32_t)mS : stLo;
                 stHi = at1 ? (int)(uint32_t)(mS >> 32) : stHi;
                 sp += mS != 0 ? 1 : 0;
-#endif
                 node = cF;
                 mask = mF & ~late;
             } else {
