@@ -23,7 +23,9 @@
 // a workgroup appends are grouped by direction inside its queue slice, so a larger first-shading
 // workgroup hands the incoherent launch longer single-group runs (512 / 256 measured best,
 // profiles/r03/ab item 17; the sweep's knobs: tools/experiments/r3_knobs.patch).
+#ifndef SHADE0_BLOCK
 #define SHADE0_BLOCK 512
+#endif
 #define SHADEN_BLOCK 256
 // (register caps for more resident waves spill and lose: k_shade0 at 5 waves +7 %, the last-bounce
 // k_shadeN at 6 waves +33 %; profiles/r04/ab/README.txt items 14-15)
@@ -391,8 +393,10 @@ struct ShadeOut {
 // LOD (k_shade0 with mcrt_frame_params.texture_lod): textures at this camera-ray hit are read
 // mip-mapped over the pixel footprint given by the ray differentials (ro, dxDir, dyDir).
 // EXT = false: the last bounce's instantiation (no extension ray; its sampling code and registers
-// are left out, so the launch keeps more waves resident).
-template <bool LOD = false, bool EXT = true>
+// are left out, so the launch keeps more waves resident).  RR: the opt-in Russian roulette has its
+// own instantiation, so the default one carries none of its registers (k_shade0: 95 VGPRs, 5 waves
+// per SIMD, instead of 97 and 4).
+template <bool LOD = false, bool EXT = true, bool RR = false>
 MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pix, float4 hit, f3 dir, f3 throughput,
                       int prevFlags, ShadeOut& o, f3 ro = f3{0, 0, 0}, f3 dxDir = f3{0, 0, 0}, f3 dyDir = f3{0, 0, 0}) {
     f3 add = splat3(0.0f);
@@ -475,7 +479,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
                 const f3 no = si.p + si.gn * off;
                 bool alive = true;
                 f3 tp1 = nt;
-                if (f.russianRoulette && bounce + 1 >= f.rrStartDepth) {   // opt-in perf mode
+                if (RR && bounce + 1 >= f.rrStartDepth) {   // opt-in perf mode
                     const float qr = fmaxf(0.05f, 1.0f - fmaxf(nt.x, fmaxf(nt.y, nt.z)));
                     const float ur = (float)wangHash((uint32_t)px * 9781u + (uint32_t)frame * 6271u + (uint32_t)bounce) * 0x1p-32f;
                     alive = ur >= qr;
@@ -494,7 +498,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
 }
 
 // Bounce 0: every pixel of the band (tile order); writes radiance[pix] (= `=` of ShadowPass).
-template <bool LOD>
+template <bool LOD, bool RR>
 __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                 const float4* __restrict__ hits, float4* __restrict__ radiance,
                                                 QueueArgs q) {
@@ -523,7 +527,7 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
         const f3 dir = cameraDir(cam, x, y);
         f3 dx = splat3(0.0f), dy = splat3(0.0f);
         if (LOD) cameraDiffDirs(cam, x, y, dx, dy);
-        const f3 add = shadePath<LOD>(s, f, 0, pix, hits[pix], dir, splat3(1.0f), 0, o, ld3(cam.pos), dx, dy);
+        const f3 add = shadePath<LOD, true, RR>(s, f, 0, pix, hits[pix], dir, splat3(1.0f), 0, o, ld3(cam.pos), dx, dy);
         radiance[pix] = make_float4(add.x, add.y, add.z, 0.0f);
     }
     const int ss = blockAppend<SHADE0_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
@@ -539,7 +543,7 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
 }
 
 // Bounce >= 1: the compacted extension queue of the previous bounce.  LAST: bounce maxDepth - 1.
-template <bool LAST>
+template <bool LAST, bool RR>
 __global__ __launch_bounds__(SHADEN_BLOCK) void k_shadeN(SceneArgs s, FrameArgs f, int bounce, const int* __restrict__ countIn,
                                                 const float4* __restrict__ qO, const float4* __restrict__ qD,
                                                 const float4* __restrict__ qT, const float4* __restrict__ hits,
@@ -557,7 +561,7 @@ __global__ __launch_bounds__(SHADEN_BLOCK) void k_shadeN(SceneArgs s, FrameArgs 
     if (i < n) {
         const float4 O = qO[i], D = qD[i], Tp = qT[i];
         const int pix = __float_as_int(O.w);
-        const f3 add = shadePath<false, !LAST>(s, f, bounce, pix, hits[i], ld3(D), ld3(Tp), __float_as_int(D.w), o);
+        const f3 add = shadePath<false, !LAST, RR>(s, f, bounce, pix, hits[i], ld3(D), ld3(Tp), __float_as_int(D.w), o);
         if (add.x != 0.0f || add.y != 0.0f || add.z != 0.0f || add.x != add.x) {
             float4 r = radiance[pix];
             r.x += add.x; r.y += add.y; r.z += add.z;
@@ -945,15 +949,19 @@ void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* 
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {
     const int blocks = (f.numTiles * f.batch * 64 + SHADE0_BLOCK - 1) / SHADE0_BLOCK;
-    hipLaunchKernelGGL(f.textureLod ? k_shade0<true> : k_shade0<false>, dim3(blocks), dim3(SHADE0_BLOCK), 0, st, s, f,
-                       cam, hits, radiance, q);
+    auto k = f.russianRoulette ? (f.textureLod ? k_shade0<true, true> : k_shade0<false, true>)
+                               : (f.textureLod ? k_shade0<true, false> : k_shade0<false, false>);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(SHADE0_BLOCK), 0, st, s, f, cam, hits, radiance, q);
 }
 void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,
                    const float4* qD, const float4* qT, const float4* hits, float4* radiance, const QueueArgs& q,
                    int maxCount, hipStream_t st) {
     const int blocks = (maxCount + SHADEN_BLOCK - 1) / SHADEN_BLOCK;
-    hipLaunchKernelGGL(bounce + 1 >= f.maxDepth ? k_shadeN<true> : k_shadeN<false>, dim3(blocks > 0 ? blocks : 1),
-                       dim3(SHADEN_BLOCK), 0, st, s, f, bounce, countIn, qO, qD, qT, hits, radiance, q);
+    const bool last = bounce + 1 >= f.maxDepth;
+    auto k = f.russianRoulette ? (last ? k_shadeN<true, true> : k_shadeN<false, true>)
+                               : (last ? k_shadeN<true, false> : k_shadeN<false, false>);
+    hipLaunchKernelGGL(k, dim3(blocks > 0 ? blocks : 1), dim3(SHADEN_BLOCK), 0, st, s, f, bounce, countIn, qO, qD, qT,
+                       hits, radiance, q);
 }
 void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits, int which,
                 float4* out, hipStream_t st) {
