@@ -197,6 +197,17 @@ SCALE_CASES = {
 BDPT_VERTEX_STRIDE = 17   # vertex records kept for every 17th pixel (the full arrays are ~0.5 GB at 960x540)
 
 
+def bdpt_vertex_sel(W, H):
+    """Pixels whose BDPT vertex records the full-size comparison keeps: every 17th pixel, plus every
+    pixel of three full rows (top, middle, bottom) and of a 64 x 64 block at the image centre, so
+    neighbouring pixels (shared tiles, waves, splat targets) are compared without gaps too."""
+    N = W * H
+    rows = [np.arange(r * W, (r + 1) * W) for r in (0, H // 2, H - 1)]
+    y0, x0 = H // 2 - 32, W // 2 - 32
+    block = (np.arange(y0, y0 + 64)[:, None] * W + np.arange(x0, x0 + 64)[None, :]).ravel()
+    return np.unique(np.concatenate([np.arange(0, N, BDPT_VERTEX_STRIDE), *rows, block]))
+
+
 def scale_scene(name):
     from mcrt import sobol_matrices
     full = {"san_miguel_proxy": scenes.san_miguel_proxy, "sponza_proxy": scenes.sponza_proxy,
@@ -225,7 +236,7 @@ def scale_job(out_path, variant):
             res[f"{key}_f{f}"] = (cs.render_bdpt if integ == "bdpt" else cs.render)(cam, frame=f, max_depth=D)
         if integ == "bdpt":
             N = W * H
-            sel = np.arange(0, N, BDPT_VERTEX_STRIDE)
+            sel = bdpt_vertex_sel(W, H)
             for which, depths in (("camera_vertices", D + 2), ("light_vertices", D + 1)):
                 v = cs.read_bdpt(which).view(po.REF_VERTEX_DTYPE).reshape(N, depths)
                 res[f"{key}_{which}"] = np.ascontiguousarray(v[sel])

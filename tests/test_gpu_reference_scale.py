@@ -13,8 +13,8 @@
     ReconstructionPass writes an image2d_t, which this GPU's OpenCL cannot run);
   * config 3: Sponza proxy (16 x 1024^2 mip-mapped textures) 1920x1080, PT -- bit-exact;
   * config 4: San-Miguel proxy BDPT at 1920x1080 (the bench's BDPT object), frames 0 and 1 in sequence from fresh buffers
-    (BDPT.cl) -- vertex counts bit-exact, every defined field of the vertices of every 17th pixel
-    bit-exact, radiance within 4e-6 relative (splat atomics, tests/test_gpu_bdpt.py) and
+    (BDPT.cl) -- vertex counts bit-exact, every defined field of the vertices bit-exact for every
+    17th pixel plus every pixel of three full rows and a 64 x 64 block (clref_job.bdpt_vertex_sel), radiance within 4e-6 relative (splat atomics, tests/test_gpu_bdpt.py) and
     bit-exact where no light-tracing splat landed;
   * config 5: San-Miguel proxy 3840x2160 with the Sobol sampler (the reference rebuilt with
     RT_SAMPLER_SOBOL, samplers.cl:18), frames 0 and 600 -- frame 600's sample index
@@ -27,7 +27,7 @@ import sys
 import numpy as np
 import pytest
 
-from clref_job import BDPT_VERTEX_STRIDE, SCALE_CASES, TIMED_F0, TIMED_STEPS, scale_scene, taa_camera
+from clref_job import SCALE_CASES, TIMED_F0, TIMED_STEPS, bdpt_vertex_sel, scale_scene, taa_camera
 from mcrt import types as T
 from mcrt.camera import scene_camera
 from oracle import pyoracle as po
@@ -99,7 +99,7 @@ def test_full_size_config_matches_reference(hip_ctx, clref_scale, variant, case)
             bad.append(f"frame {f}: {int((~exact.all(-1)[nosplat]).sum())} no-splat pixels not bit-exact")
     if integ == "bdpt":
         N = W * H
-        sel = np.arange(0, N, BDPT_VERTEX_STRIDE)
+        sel = bdpt_vertex_sel(W, H)
         cc = fb.read_bdpt("camera_counts").view(np.int32)
         lc = fb.read_bdpt("light_counts").view(np.int32)
         for nm, a, b in (("camera", cc, ref[f"{key}_camera_counts"]), ("light", lc, ref[f"{key}_light_counts"])):
