@@ -313,7 +313,9 @@ MCRT_API mcrt_status mcrt_accel_info(mcrt_scene scene, uint64_t* num_nodes, uint
 MCRT_API mcrt_status mcrt_accel_layout(mcrt_scene scene, int32_t* two_level, uint32_t* num_meshes,
                                        uint32_t* num_instances, int32_t* depth);
 /* Copy of the device records (64 B each, the mcrt_accel_build_host_records layout) into out
- * (up to max_records; out may be NULL to query *num_records). */
+ * (up to max_records; out may be NULL to query *num_records).  In a flat structure a triangle
+ * leaf's int word 13 holds its parent record's index on the device (the occluder hints' box test)
+ * where the host build leaves -1. */
 MCRT_API mcrt_status mcrt_accel_read_records(mcrt_scene scene, float* out, uint64_t max_records,
                                              uint64_t* num_records);
 /* ------------------------------------------------------------------------ */

@@ -17,7 +17,8 @@
 //             float4 (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
 //             int4   (child0, child1, 0, 0)                 (child indices >= 1)
 //   leaf:     float4 (v0, shapeId bits), float4 (v1 - v0, primId bits), float4 (v2 - v0, 0),
-//             int4   (-1, -1, 0, 0)
+//             int4   (-1, -1, 0, 0); on the device word 13 becomes the parent record's index
+//             (k_leaf_parents after every flat build, for the occluder hints)
 #include <immintrin.h>
 
 #include <atomic>
