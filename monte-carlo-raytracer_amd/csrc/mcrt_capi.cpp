@@ -1464,7 +1464,11 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     BdptArgs bk = b;   // the vertex launches whose output queue is traced
     bk.extKey = bs.ekey;
     bk.extSlot = bs.eslot;
-    const int nSort = (int)(2 * N);
+    // a bounce queue holds at most the band's camera + light rays (2 per path of this rank's tiles),
+    // appended compactly from slot 0: sort (and clear) only that range, not the whole frame's -- a
+    // rank of a band split would otherwise sort 8 x its own rays at N = 8
+    const int bandQ = f.numTiles * 64 * B;   // this rank's paths: a start queue holds at most one ray each
+    const int nSort = (int)std::min((size_t)2 * N, (size_t)2 * (size_t)bandQ);
     auto clearKeys = [&]() {   // unwritten slots sort last (stable sort: after the written ones)
         return hipMemsetAsync(bs.ekey, 0xFF, 4 * (size_t)nSort, st);
     };
@@ -1507,16 +1511,16 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         HIPCHK(ctx, mcrt::bdpt_light_sort(bs.lkey, bs.lkey2, bs.lslot, bs.lperm, f.numTiles * 64 * B, bs.sortTmp,
                                           bs.sortTmpBytes, st));
         mcrt::launch_extend_pair(tcc, tcs, camQ.count, camQ.o, camQ.d, fb->bHits, lightQ.count, lightQ.o, lightQ.d,
-                                 fb->bHits + NQ, (int)NQ, (int)NQ, st, bs.lperm);
+                                 fb->bHits + NQ, bandQ, bandQ, st, bs.lperm);   // grids sized to the band
     }
     HIPCHK(ctx, clearKeys());   // queue 1 is traced (D >= 1)
     {
         Timed t(ctx, K_BDPT_VERTEX, camQ.count, 0, st);
-        mcrt::launch_bdpt_vertex(sa, f, bk, 1, camQ, fb->bHits, queue(1), (int)NQ, st);
+        mcrt::launch_bdpt_vertex(sa, f, bk, 1, camQ, fb->bHits, queue(1), bandQ, st);
     }
     {
         Timed t(ctx, K_BDPT_VERTEX, lightQ.count, 0, st);
-        mcrt::launch_bdpt_vertex(sa, f, bk, 1, lightQ, fb->bHits + NQ, queue(1), (int)NQ, st);
+        mcrt::launch_bdpt_vertex(sa, f, bk, 1, lightQ, fb->bHits + NQ, queue(1), bandQ, st);
     }
     for (int d = 2; d <= D + 1; ++d) {
         const BdptQueue qIn = queue(d - 1), qOut = queue(d);
@@ -1524,12 +1528,12 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
             Timed t(ctx, K_EXTEND, qIn.count, 0, st);
             HIPCHK(ctx, mcrt::bdpt_light_sort(bs.ekey, bs.ekey2, bs.eslot, bs.eperm, nSort, bs.sortTmp,
                                               bs.sortTmpBytes, st, 16));
-            mcrt::launch_extend(tcs, qIn.count, qIn.o, qIn.d, fb->bHits, (int)(2 * N), st, bs.eperm);
+            mcrt::launch_extend(tcs, qIn.count, qIn.o, qIn.d, fb->bHits, nSort, st, bs.eperm);
         }
         const bool traced = d <= D;   // queue d is traced by the next round
         if (traced) HIPCHK(ctx, clearKeys());
         Timed t(ctx, K_BDPT_VERTEX, qIn.count, 0, st);
-        mcrt::launch_bdpt_vertex(sa, f, traced ? bk : b, d, qIn, fb->bHits, qOut, (int)(2 * N), st);
+        mcrt::launch_bdpt_vertex(sa, f, traced ? bk : b, d, qIn, fb->bHits, qOut, nSort, st);
     }
     BdptQueue cq;
     cq.count = cnt + BDPT_CNT_CONN;
