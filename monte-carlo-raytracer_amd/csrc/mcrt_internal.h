@@ -106,7 +106,7 @@ struct TraceCtx {
 };
 #define MCRT_HINT_PIXEL 1
 #define MCRT_HINT_CELL 2
-#define MCRT_HINT_CELL_BITS 22
+#define MCRT_HINT_CELL_BITS 24
 #ifndef MCRT_HINT_GRID
 #define MCRT_HINT_GRID 512
 #endif
