@@ -108,7 +108,7 @@ struct TraceCtx {
 #define MCRT_HINT_CELL 2
 #define MCRT_HINT_CELL_BITS 24
 #ifndef MCRT_HINT_GRID
-#define MCRT_HINT_GRID 512
+#define MCRT_HINT_GRID 768
 #endif
 
 namespace mcrt {
