@@ -883,7 +883,7 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
     if (!s->twoLevel) {
-        // parent links of the leaves (occluder hints), and the origin-cell hint table (64 MB)
+        // parent links of the leaves (occluder hints), and the origin-cell hint table (128 MB)
         mcrt::launch_leaf_parents((float4*)s->dNodes, (uint32_t)s->numNodes, ctx->stream);
         if (!s->dHintCell) HIPCHK(ctx, hipMalloc(&s->dHintCell, sizeof(uint32_t) << MCRT_HINT_CELL_BITS));
         HIPCHK(ctx, fill_hints(s->dHintCell, (size_t)1 << MCRT_HINT_CELL_BITS, (uint32_t)s->numNodes + 64, ctx->stream));

@@ -106,7 +106,7 @@ struct TraceCtx {
 };
 #define MCRT_HINT_PIXEL 1
 #define MCRT_HINT_CELL 2
-#define MCRT_HINT_CELL_BITS 24
+#define MCRT_HINT_CELL_BITS 25
 #ifndef MCRT_HINT_GRID
 #define MCRT_HINT_GRID 768
 #endif
