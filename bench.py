@@ -85,6 +85,40 @@ def cpu_baseline(scene, cam_of, W, H, D, target_s=15.0):
     }
 
 
+def reference_parity(scene_name, tris, fb, ds, cam_of, W, H, D, frame, band):
+    """CHECKER, part of the cpu_baseline leg (after the timed region, rank 0, N = 1): the reference's
+    own kernels (PathTracing.cl + RadeonRays intersect_bvh2_lds.cl compiled for gfx950 from
+    /root/reference, run through ROCm OpenCL by oracle/_ref/clref_runner.so) render the first timed
+    frame with its TAA camera in a child process (oracle/clref_frame.py); the product renders the
+    same frame again (mcrt_render_frame, bit-identical to the batched call: tests/
+    test_gpu_reference_scale.py) and the share of bit-identical pixels is reported."""
+    import subprocess
+    import tempfile
+    from oracle import pyoracle as po
+    if not po.clref_available():
+        return {"skipped": "oracle/_ref/clref_runner.so not built (make -C oracle/refbuild)"}
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "clref_frame.npz")
+        t0 = time.perf_counter()
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "clref_frame.py"), path, scene_name,
+                            str(tris), str(W), str(H), str(D), str(frame)], capture_output=True, text=True, timeout=900)
+        if r.returncode != 0:
+            return {"error": (r.stdout + r.stderr)[-800:]}
+        z = np.load(path, allow_pickle=False)
+        ref, device = z[f"f{frame}"], str(z["device"])
+        el = time.perf_counter() - t0
+    fb.render(ds, cam_of(frame), frame=frame, max_depth=D, **band)
+    g = fb.read(0)
+    exact = ((g.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(g) & np.isnan(ref)))[..., :3].all(-1)
+    d = np.abs(g[..., :3].astype(np.float64) - ref[..., :3])
+    close = (d <= 1e-4 * np.maximum(1.0, np.abs(ref[..., :3]))).all(-1)
+    return {"pixels_bit_exact": round(float(exact.mean()), 6), "pixels_within_1e-4": round(float(close.mean()), 6),
+            "frame": int(frame), "pixels": int(W * H), "reference_nonzero": bool(ref[..., :3].max() > 0),
+            "checker": ("the reference's PathTracing.cl + RadeonRays intersect_bvh2_lds.cl, compiled for gfx950 from "
+                        f"the reference sources (OpenCL default fp), run live on {device} (oracle/clref_frame.py)"),
+            "checker_s": round(el, 1)}
+
+
 def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, oracle=None):
     """HBM roofline of k_shadow_extend (the dominant kernel): the shadow rays of bounce 0 and the
     extension rays for bounce 1 of `batch` frames in one launch.
@@ -273,7 +307,9 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
         el = float(t.item())
     st = fb.stats()
     out = {"value": round(W * H * steps * (1 if band else world) / el / 1e6, 3), "unit": "Mpaths/s", "steps": steps,
-           "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong" if band else "weak",
+           # the band split divides each frame (strong scaling, also its 1-rank case); --bdpt-split
+           # frame gives each rank whole frames of its own (weak)
+           "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong" if split == "band" else "weak",
            "workload": f"same scene {W}x{H}, BDPT, maxDepth {D}, 1 spp per step (SURVEY config 4's integrator), "
                        f"{batch} frames per mcrt_render_frames call, "
                        + (f"band split x {world} + 1 splat reduce-scatter per call + 1 RCCL reduce" if band else
@@ -388,6 +424,8 @@ def main():
     ap.add_argument("--end-collective", default="gather", choices=["gather", "reduce"],
                     help="tile split: gather each rank's band rows to rank 0, or sum-reduce the full frames")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-reference-parity", action="store_true",
+                    help="skip the reference-kernel render of the first timed frame (parity_vs_reference)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline-model", action="store_true",
                     help="skip the oracle pass that counts the distinct BVH nodes of one launch")
@@ -563,8 +601,8 @@ def main():
     ctx.sync()
     ctx.set_profiling(False)
     fstats = fb.stats()
-    qcounts = fb.queue_counts() if not bdpt else None
-    hcounts = fb.hint_counts() if not bdpt else None   # shadow rays answered by their occluder hint
+    qcounts = fb.queue_counts(max(D, 8)) if not bdpt else None
+    hcounts = fb.hint_counts(max(D, 8)) if not bdpt else None   # shadow rays answered by their occluder hint
     frame0 = warm + 1
 
     ctx.reset_stats()
@@ -654,26 +692,39 @@ def main():
         out["rays_per_path"] = {k: round(v, 4) for k, v in rays.items()}
         if hcounts is not None and qcounts is not None:   # occluder hints
             out["shadow_hints"] = {f"bounce{b}": round(hcounts[b] / max(qcounts[0][b], 1), 4) for b in range(D)}
+            # the wavefront's queues per bounce (one untimed frame): compaction keeps only live paths,
+            # so the launches shrink with depth (and with --russian-roulette)
+            out["queues_per_frame"] = {"shadow": [int(v) for v in qcounts[0][:D]],
+                                       "extension": [int(v) for v in qcounts[1][:max(D - 1, 0)]],
+                                       "pixels": int(W * H / world)}
         # (the CPU oracle and the roofline's node counts price the flat structure)
         oracle_ok = world == 1 and not bdpt and sampler == T.SAMPLER_RANDOM and not two_level
         cpu = None
         if oracle_ok and not args.no_cpu_baseline:
             cpu = cpu_baseline(scene, cam_of, W, H, D, args.cpu_seconds)
             st = cpu["_stats"]
-            # parity spot check: the product renders the oracle's first sampled frame again
+            # the port's fidelity: the product renders the port's first sampled frame again.  The
+            # port is an IEEE restatement (no fma contraction, exact 1/x where the reference uses
+            # native_recip), so it is NOT bit-exact at this scene size; the product's
+            # parity is measured against the reference itself (parity_vs_reference)
             f0 = cpu["_frame0"]
             fb.render(ds, cam_of(f0), frame=f0, max_depth=D, **band)
             g = fb.read(0)[cpu["_rows"]]
             r = cpu["_radiance"][cpu["_rows"]]
             dlt = np.abs(g[..., :3].astype(np.float64) - r[..., :3])
             ok = (dlt <= 1e-4 * np.maximum(1.0, np.abs(r[..., :3]))).all(-1).mean()
-            out["parity_vs_oracle"] = {"pixels_within_1e-4": round(float(ok), 5), "rows": int(len(cpu["_rows"])),
-                                       "frame": int(f0)}
             out["visits_per_query"] = {"k_primary": round(st[1] / max(st[0], 1), 2),
                                        "k_extend": round(st[3] / max(st[2], 1), 2),
                                        "k_shadow": round(st[5] / max(st[4], 1), 2)}
             out["cpu_baseline"] = {k: v for k, v in cpu.items() if not k.startswith("_")}
             out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 4)
+            out["cpu_baseline"]["fidelity"] = {
+                "pixels_within_1e-4_of_product": round(float(ok), 5), "rows": int(len(cpu["_rows"])), "frame": int(f0),
+                "note": "the port (IEEE C restatement) against the product; the product against the reference "
+                        "itself is parity_vs_reference"}
+            if not args.russian_roulette and not args.no_reference_parity:   # the reference has no RR
+                out["parity_vs_reference"] = reference_parity(args.scene, args.tris, fb, ds, cam_of, W, H, D, frame0,
+                                                              band)
         if kstats:
             out["kernels"] = {k: {"avg_ms": round(v["ms"] / max(v["launches"], 1), 4), "launches": v["launches"],
                                   "items_per_launch": round(v["items"] / max(v["launches"], 1), 1),

@@ -108,8 +108,11 @@ struct mcrt_scene_s {
     size_t spillRays = 0;           // rays the spill buffer covers (spillCap words each)
     int* dScratch = nullptr;   // work counters for API queries
     float bbLo[3] = {0, 0, 0}, bbHi[3] = {0, 0, 0};   // world bounds (root record of the BVH)
-    // occluder hints of the shadow rays after bounce 0, by origin cell (TraceCtx::hint, flat trees)
+    // occluder hints of the shadow rays after bounce 0, by origin cell (TraceCtx::hint, flat trees):
+    // allocated on the first shadow launch that uses hints (ensure_hint_cell), 2^hintBits words
     uint32_t* dHintCell = nullptr;
+    int hintBits = 0;
+    bool hintAllocFailed = false;   // no memory for the table: hints stay off for this scene
 };
 
 // One frame in flight (PT): the per-frame buffers of mcrt_render_frame, its own stream and
@@ -344,10 +347,38 @@ static hipError_t fill_hints(uint32_t* d, size_t n, uint32_t range, hipStream_t 
     if (r == hipSuccess) r = hipStreamSynchronize(st);
     return r;
 }
+// Entries of the origin-cell table: 2^25 words (128 MB) for trees of more than 2^22 nodes (the
+// headline scene: 20 M nodes), fewer for smaller trees (2 words per node, at least 2^18).  Any size
+// is safe -- a slot is a hint, never an answer.
+static int hint_bits_for(uint32_t numNodes) {
+    int b = 18;
+    while (b < MCRT_HINT_CELL_BITS && (1u << b) < 2u * numNodes) ++b;
+    return b;
+}
+// The table is allocated (and emptied) on the first launch that uses it, on the context stream,
+// which is finished before the launch's own stream reads it; if it does not fit, hints stay off.
+static bool ensure_hint_cell(mcrt_scene s) {
+    if (s->dHintCell) return true;
+    if (s->hintAllocFailed) return false;
+    mcrt_ctx ctx = s->ctx;
+    const int bits = hint_bits_for((uint32_t)s->numNodes);
+    hipError_t e = hipMalloc(&s->dHintCell, sizeof(uint32_t) << bits);
+    if (e == hipSuccess) e = fill_hints(s->dHintCell, (size_t)1 << bits, (uint32_t)s->numNodes + 64, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        hipGetLastError();
+        if (s->dHintCell) hipFree(s->dHintCell);
+        s->dHintCell = nullptr;
+        s->hintAllocFailed = true;
+        return false;
+    }
+    s->hintBits = bits;
+    return true;
+}
 static void with_hints(TraceCtx& c, mcrt_scene s, uint32_t* pix, uint32_t n) {
-    if (s->twoLevel || !hints_enabled() || !s->dHintCell) return;
+    if (s->twoLevel || !hints_enabled() || !ensure_hint_cell(s)) return;
     c.hintCell = s->dHintCell;
-    c.hintMask = (1u << MCRT_HINT_CELL_BITS) - 1;
+    c.hintMask = (1u << s->hintBits) - 1;
     for (int a = 0; a < 3; ++a) {
         const float ext = s->bbHi[a] - s->bbLo[a];
         c.hintLo[a] = s->bbLo[a];
@@ -883,11 +914,13 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
     if (!s->dScratch) HIPCHK(ctx, hipMalloc(&s->dScratch, 256 * sizeof(int)));
     HIPCHK(ctx, hipMemset(s->dScratch, 0, 256 * sizeof(int)));
     if (!s->twoLevel) {
-        // parent links of the leaves (occluder hints), and the origin-cell hint table (128 MB)
+        // parent links of the leaves (occluder hints).  The origin-cell hint table is allocated on
+        // its first use (ensure_hint_cell, sized for the tree); a rebuild drops the old one
         mcrt::launch_leaf_parents((float4*)s->dNodes, (uint32_t)s->numNodes, ctx->stream);
-        if (!s->dHintCell) HIPCHK(ctx, hipMalloc(&s->dHintCell, sizeof(uint32_t) << MCRT_HINT_CELL_BITS));
-        HIPCHK(ctx, fill_hints(s->dHintCell, (size_t)1 << MCRT_HINT_CELL_BITS, (uint32_t)s->numNodes + 64, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (s->dHintCell) hipFree(s->dHintCell);
+        s->dHintCell = nullptr;
+        s->hintAllocFailed = false;
     }
     int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries
     // test hook: MCRT_TEST_SPILL_CAP=k caps the spill columns at k entries (0 = LDS stack only) so a

@@ -185,6 +185,10 @@ SCALE_CASES = {
         ("sponza_pt_1080p", "sponza_proxy", 1920, 1080, "pt", (0, 1), 2),           # config 3
         ("dragon_pt_1080p", "dragon_proxy", 1920, 1080, "pt", (0, 1), 2),           # config 2
         ("sm_bdpt_1080p", "san_miguel_proxy", 1920, 1080, "bdpt", (0, 1), 2),       # config 4 integrator (bench size)
+        # SURVEY §8(d)'s depth-5 sensitivity case (PathTracingSettings.h:81 allows maxDepth 1..10):
+        # the regime where the wavefront's queues shrink bounce by bounce
+        ("sm_pt_1080p_d5", "san_miguel_proxy", 1920, 1080, "pt", (0, 1), 5),
+        ("sm_bdpt_540p_d5", "san_miguel_proxy", 960, 540, "bdpt", (0, 1), 5),
         # config 1: the Dragon proxy at 512x512, 4 spp accumulated (frames 0..3, box filter)
         CONFIG1,
     ],

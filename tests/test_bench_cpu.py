@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "bench.py")
 
@@ -30,7 +32,12 @@ def test_gpus_must_be_positive():
 def test_plain_command_launches_ranks():
     # no GPU here: the 2 launched nccl ranks each refuse to run on fewer GPUs than ranks, and the
     # launcher's failure is bench.py's exit status
-    r = _run(["--gpus", "2", "--steps", "1"])
+    # (no GPU visible to the ranks even on a GPU box, where 2 visible GPUs would run a real bench)
+    r = _run(["--gpus", "2", "--steps", "1"], HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    if "2 ranks over nccl need 2 GPUs" not in r.stderr:
+        import torch
+        if torch.cuda.device_count() >= 2:   # the empty device lists did not hide this box's GPUs
+            pytest.skip("2 GPUs visible to the ranks: a real 2-rank bench, not the refusal")
     assert "launching 2 ranks" in r.stderr and "torch.distributed.run" in r.stderr
     assert r.returncode != 0
     assert "2 ranks over nccl need 2 GPUs" in r.stderr, r.stderr[-3000:]

@@ -16,6 +16,8 @@
     (BDPT.cl) -- vertex counts bit-exact, every defined field of the vertices bit-exact for every
     17th pixel plus every pixel of three full rows and a 64 x 64 block (clref_job.bdpt_vertex_sel), radiance within 4e-6 relative (splat atomics, tests/test_gpu_bdpt.py) and
     bit-exact where no light-tracing splat landed;
+  * SURVEY §8(d)'s depth-5 sensitivity run on the headline scene: PT at 1920x1080 (frames 0 and 1
+    bit-exact) and BDPT at 960x540 (as config 4 above), maxDepth 5;
   * config 5: San-Miguel proxy 3840x2160 with the Sobol sampler (the reference rebuilt with
     RT_SAMPLER_SOBOL, samplers.cl:18), frames 0 and 600 -- frame 600's sample index
     pix + 600 x W x H exceeds 2^32 and wraps -- bit-exact; plus the mixed

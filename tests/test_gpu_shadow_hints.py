@@ -16,9 +16,9 @@ from mcrt.camera import scene_camera
 pytestmark = pytest.mark.gpu
 
 
-def _frames(hip_ctx, sc, name, W, H, max_depth, calls=3, batch=4, integrator=None):
+def _frames(hip_ctx, sc, name, W, H, max_depth, calls=3, batch=4, integrator=None, device_build=False):
     from mcrt import lib
-    ds = lib.DeviceScene(hip_ctx, sc)
+    ds = lib.DeviceScene(hip_ctx, sc, device_build=device_build)
     fb = lib.FrameBuffer(hip_ctx, W, H)
     out = []
     for c in range(calls):   # TAA-jittered cameras, as the bench
@@ -66,6 +66,33 @@ def test_hints_change_no_answer(hip_ctx, sm_small, name, max_depth, env):
     assert on[..., :3].max() > 0
     diff = on.view(np.uint32) != off.view(np.uint32)
     assert not diff.any(), f"{int(diff.any(-1).sum())} pixels differ"
+
+
+@pytest.mark.parametrize("build", [1, 4])
+def test_hints_change_no_answer_other_builders(hip_ctx, sm_small, build):
+    """The device LBVH (1) and the perf tree (4) take the hints too: frames bit-identical with them
+    off, with random tables, on trees other than the reference's."""
+    args = (hip_ctx, sm_small, "san_miguel_proxy", 256, 144, 3)
+    off = _with_env({"MCRT_SHADOW_HINTS": "0"}, lambda: _frames(*args, device_build=build))
+    for env in ({}, {"MCRT_TEST_HINT_FILL": "5"}):
+        on = _with_env(dict(env, MCRT_SHADOW_HINTS="1"), lambda: _frames(*args, device_build=build))
+        assert np.isfinite(on).all() and on[..., :3].max() > 0
+        diff = on.view(np.uint32) != off.view(np.uint32)
+        assert not diff.any(), (build, env, int(diff.any(-1).sum()))
+
+
+@pytest.mark.parametrize("build", [1, 2])
+def test_device_trees_nest_and_report_depth(hip_ctx, sm_small, build):
+    """The hints' premise (test_hint_premise_cpu.py) on the device-built trees, and their reported
+    depth (the packet stack's bound) against the deepest leaf."""
+    from mcrt import lib
+    from test_hint_premise_cpu import check_nesting, leaf_depth
+    ds = lib.DeviceScene(hip_ctx, sm_small, device_build=build)
+    rec = ds.records()
+    depth = ds.layout()["depth"]
+    ds.close()
+    assert check_nesting(rec) > 0
+    assert depth >= leaf_depth(rec), (build, depth, leaf_depth(rec))
 
 
 def test_bdpt_visibility_hints(hip_ctx, sm_small):
