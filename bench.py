@@ -257,8 +257,8 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     band = split == "band" and world > 1
     if band:   # rank-major splats (chunks of this rank count x 8-row blocks x batch frames) + own chunk
         cr = mdist.splat_chunk_rows(H, 8, world)   # uninitialised: mcrt_bdpt_splats_copy zeroes on its stream
-        splat_full = torch.empty(4 * W * cr * batch * world, dtype=torch.float32, device="cuda")
-        splat_own = torch.empty(4 * W * cr * batch, dtype=torch.float32, device="cuda")
+        splat_full = torch.empty(mdist.SPLAT_CHANNELS * W * cr * batch * world, dtype=torch.float32, device="cuda")
+        splat_own = torch.empty(mdist.SPLAT_CHANNELS * W * cr * batch, dtype=torch.float32, device="cuda")
 
     last = [1]   # frames of the last call (fb.stats() counts that call's queues)
 
@@ -542,8 +542,8 @@ def main():
     if band_bdpt:   # band split: every rank renders every frame's rows of its bands
         band = dict(band_rows=8, num_bands=world, band_index=rank, integrator=T.INTEGRATOR_BDPT)
         cr = mdist.splat_chunk_rows(H, 8, world)   # uninitialised: mcrt_bdpt_splats_copy zeroes on its stream
-        splat_full = torch.empty(4 * W * cr * args.bdpt_batch * world, dtype=torch.float32, device="cuda")
-        splat_own = torch.empty(4 * W * cr * args.bdpt_batch, dtype=torch.float32, device="cuda")
+        splat_full = torch.empty(mdist.SPLAT_CHANNELS * W * cr * args.bdpt_batch * world, dtype=torch.float32, device="cuda")
+        splat_own = torch.empty(mdist.SPLAT_CHANNELS * W * cr * args.bdpt_batch, dtype=torch.float32, device="cuda")
     elif bdpt:   # frame split: whole frames per rank
         band = dict(band_rows=8, num_bands=1, band_index=0, integrator=T.INTEGRATOR_BDPT)
     else:

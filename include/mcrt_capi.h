@@ -528,19 +528,21 @@ MCRT_API mcrt_status mcrt_framebuffer_read_queue(mcrt_framebuffer fb, int which,
 /* Band-split BDPT (num_bands > 1): the frame's light-tracing splats land in any pixel, so the ranks
  * exchange them once per frame (the reference's ConnectVertices atomics + CopyBuffer,
  * BDPT.cl:671-913).  The splats are laid out RANK-MAJOR: `chunks` (= num_bands) chunks of
- * `chunk_pixels` float4, chunk r holding the rows of rank r's bands in its own tile order (zero
+ * `chunk_pixels` pixels of MCRT_SPLAT_CHANNELS (3) floats -- r, g, b, as the reference's splat
+ * buffer (BDPT.cl:654-669, 888-899) -- chunk r holding the rows of rank r's bands in its own tile order (zero
  * past its last row), so ONE reduce-scatter hands each rank exactly its rows' sums:
  *   mcrt_bdpt_splat_layout   the chunk geometry of the last frame's band split;
  *   mcrt_bdpt_splats_copy    this rank's splats, rank-major, into d_dst (chunks x chunk_pixels
- *                            float4 of device memory), ENQUEUED on the frame's stream
+ *                            x 3 floats of device memory), ENQUEUED on the frame's stream
  *                            (mcrt_framebuffer_stream): order the collective after it there (no
  *                            host synchronisation, so frames in flight keep overlapping);
  *   mcrt_bdpt_gather         completes the rank's bands with d_own_chunk = chunk band_index of the
- *                            ranks' summed buffers (chunk_pixels float4; NULL: the rank's own splats
+ *                            ranks' summed buffers (chunk_pixels x 3 floats; NULL: the rank's own splats
  *                            in its natural layout -- a 1-rank check).  It reads d_own_chunk on the
  *                            frame's stream; a later mcrt_bdpt_splats_copy waits for it.
  * Rendering or accumulating in between fails with MCRT_ERROR_NOT_READY.  With no frame pending (a
  * light-less scene, a whole-image frame) the copy writes zeros and the gather does nothing. */
+#define MCRT_SPLAT_CHANNELS 3
 MCRT_API mcrt_status mcrt_bdpt_splat_layout(mcrt_framebuffer fb, uint64_t* chunk_pixels, int32_t* chunks);
 /* The HIP stream (hipStream_t) the last frame of fb was enqueued on (its frame slot's). */
 MCRT_API mcrt_status mcrt_framebuffer_stream(mcrt_framebuffer fb, void** stream);

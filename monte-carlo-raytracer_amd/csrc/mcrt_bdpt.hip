@@ -992,7 +992,7 @@ __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const i
 // the rank-major layout of k_bdpt_splat_pack (frame k's rows at k * chunkPixels, the rank's local
 // 8-row block tb at rows 8 tb .. 8 tb + 7), instead of the rank's own splat planes.
 __global__ __launch_bounds__(256) void k_bdpt_gather(FrameArgs f, BdptArgs b, float4* __restrict__ radiance,
-                                                     const float4* __restrict__ chunk, size_t chunkPixels) {
+                                                     const float* __restrict__ chunk, size_t chunkPixels) {
     const int lane = threadIdx.x & 63;
     const int tileAll = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     int tile, k;
@@ -1009,18 +1009,25 @@ __global__ __launch_bounds__(256) void k_bdpt_gather(FrameArgs f, BdptArgs b, fl
         rz += c.z;
     }
     const int tb = tile / f.tilesX;
-    const float4 sp = chunk ? chunk[(size_t)k * chunkPixels + (size_t)(tb * 8 + (lane >> 3)) * f.W + x] : b.splat[pix];
+    float4 sp;
+    if (chunk) {   // MCRT_SPLAT_CHANNELS floats per pixel
+        const float* c = chunk + 3 * ((size_t)k * chunkPixels + (size_t)(tb * 8 + (lane >> 3)) * f.W + x);
+        sp = make_float4(c[0], c[1], c[2], 0.0f);
+    } else {
+        sp = b.splat[pix];
+    }
     radiance[pix] = make_float4(rx + sp.x, ry + sp.y, rz + sp.z, 0.0f);
 }
 
 // Band split: the splat planes (W x H per batch frame, any pixel) in rank-major order -- chunk r
-// (batch x chunkPixels float4) holds, frame after frame, the rows of rank r's bands, its local 8-row
+// (batch x chunkPixels pixels of 3 floats, r g b: the reference's splat buffer, BDPT.cl:654-669;
+// the exchange moves 12 B per pixel, not the splat plane's 16) holds, frame after frame, the rows of rank r's bands, its local 8-row
 // block tb (tilePixel's numbering) at rows 8 tb .. 8 tb + 7 -- so ONE reduce-scatter hands every
 // rank the summed splats of exactly its own rows (mcrt.dist.exchange_splats).  Rows past a rank's
 // last block stay zero (memset).
 __global__ __launch_bounds__(256) void k_bdpt_splat_pack(int W, int H, int batch, int bpb, int numBands,
                                                          size_t chunkPixels, const float4* __restrict__ splat,
-                                                         float4* __restrict__ out) {
+                                                         float* __restrict__ out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t N0 = (size_t)W * H;
     if (i >= N0 * batch) return;
@@ -1029,7 +1036,11 @@ __global__ __launch_bounds__(256) void k_bdpt_splat_pack(int W, int H, int batch
     const int y = (int)(q / W), x = (int)(q - (size_t)y * W);
     const int gb = y >> 3;
     const int r = (gb / bpb) % numBands, tb = (gb / (bpb * numBands)) * bpb + gb % bpb;
-    out[(size_t)r * batch * chunkPixels + (size_t)k * chunkPixels + (size_t)(tb * 8 + (y & 7)) * W + x] = splat[i];
+    const float4 v = splat[i];
+    float* o = out + 3 * ((size_t)r * batch * chunkPixels + (size_t)k * chunkPixels + (size_t)(tb * 8 + (y & 7)) * W + x);
+    o[0] = v.x;
+    o[1] = v.y;
+    o[2] = v.z;
 }
 
 // Splats that land outside the rank's bands (multi-GPU band split): added by the rank that owns
@@ -1089,12 +1100,12 @@ void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, i
     hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks), dim3(64), 0, st, c, b, q.count,
                        q.o, q.d, q.t);
 }
-void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, const float4* chunk,
+void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, const float* chunk,
                         size_t chunkPixels, hipStream_t st) {
     const int blocks = (f.numTiles * f.batch * 64 + 255) / 256;
     hipLaunchKernelGGL(k_bdpt_gather, dim3(blocks), dim3(256), 0, st, f, b, radiance, chunk, chunkPixels);
 }
-void launch_bdpt_splat_pack(const FrameArgs& f, size_t chunkPixels, const float4* splat, float4* out, hipStream_t st) {
+void launch_bdpt_splat_pack(const FrameArgs& f, size_t chunkPixels, const float4* splat, float* out, hipStream_t st) {
     const size_t n = (size_t)f.W * f.H * f.batch;
     hipLaunchKernelGGL(k_bdpt_splat_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (int)f.W, (int)f.H,
                        f.batch, f.bandRows >> 3, f.numBands, chunkPixels, splat, out);

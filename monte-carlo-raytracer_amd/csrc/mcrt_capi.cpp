@@ -2081,9 +2081,9 @@ MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst) {
     // the caller's buffer may still be read by an earlier frame's gather on another slot's stream
     for (auto& k : fb->slot)
         if (k.stream && k.stream != st) HIPCHK(ctx, hipStreamWaitEvent(st, k.done, 0));
-    HIPCHK(ctx, hipMemsetAsync(d_dst, 0, 16 * total, st));
+    HIPCHK(ctx, hipMemsetAsync(d_dst, 0, sizeof(float) * MCRT_SPLAT_CHANNELS * total, st));
     if (fb->bdptPendingGather)   // (else, e.g. a scene without lights: the frame is complete, no splats)
-        mcrt::launch_bdpt_splat_pack(fb->bands, chunk, fb->splat, (float4*)d_dst, st);
+        mcrt::launch_bdpt_splat_pack(fb->bands, chunk, fb->splat, (float*)d_dst, st);
     HIPCHK(ctx, hipGetLastError());
     return MCRT_OK;   // enqueued on the frame's stream (mcrt_framebuffer_stream): no host sync
 }
@@ -2108,7 +2108,7 @@ MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_own_chu
     b.ownSlots = bdpt_max_connections(fb->bdptDepth) - fb->bdptDepth;
     {
         Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)fb->bands.numTiles * 64 * fb->bands.batch, st);
-        mcrt::launch_bdpt_gather(fb->bands, b, fb->radiance, (const float4*)d_own_chunk,
+        mcrt::launch_bdpt_gather(fb->bands, b, fb->radiance, (const float*)d_own_chunk,
                                  splat_chunk_pixels(fb->bands), st);
     }
     HIPCHK(ctx, hipGetLastError());

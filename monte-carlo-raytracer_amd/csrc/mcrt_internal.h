@@ -163,9 +163,9 @@ void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
 // k_bdpt_vis is a grid-stride launch of at most this many one-wave workgroups (spill columns per wave)
 constexpr int BDPT_VIS_MAX_WAVES = 65536;
 void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st);
-void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, const float4* chunk,
+void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, const float* chunk,
                         size_t chunkPixels, hipStream_t st);
-void launch_bdpt_splat_pack(const FrameArgs& f, size_t chunkPixels, const float4* splat, float4* out, hipStream_t st);
+void launch_bdpt_splat_pack(const FrameArgs& f, size_t chunkPixels, const float4* splat, float* out, hipStream_t st);
 void launch_bdpt_clear_splat(int n, float4* splat, hipStream_t st);
 }  // namespace mcrt
 

@@ -42,6 +42,11 @@ def band_rows_of(height, band_rows, num_bands, band_index):
     return rows[rows < height]
 
 
+# floats per pixel of the exchanged splats (MCRT_SPLAT_CHANNELS: r, g, b as the reference's splat
+# buffer, BDPT.cl:654-669)
+SPLAT_CHANNELS = 3
+
+
 def splat_chunk_rows(height, band_rows, num_bands):
     """Rows of one chunk of the rank-major splat layout (mcrt_bdpt_splat_layout): the largest
     rank's 8-row block count x 8."""
@@ -84,8 +89,9 @@ def splat_buffers(fb, device="cuda"):
     torch's stream would race with that pack, which runs on another stream)."""
     import torch
     cp, chunks = fb.bdpt_splat_layout()
-    return (torch.empty(4 * cp * chunks, dtype=torch.float32, device=device),
-            torch.empty(4 * cp, dtype=torch.float32, device=device))
+    c = SPLAT_CHANNELS
+    return (torch.empty(c * cp * chunks, dtype=torch.float32, device=device),
+            torch.empty(c * cp, dtype=torch.float32, device=device))
 
 
 def exchange_splats(fb, full, chunk, group=None):
@@ -102,9 +108,10 @@ def exchange_splats(fb, full, chunk, group=None):
     import torch
     import torch.distributed as dist
     cp, chunks = fb.bdpt_splat_layout()
-    if full.numel() < 4 * cp * chunks or chunk.numel() < 4 * cp:
+    c = SPLAT_CHANNELS
+    if full.numel() < c * cp * chunks or chunk.numel() < c * cp:
         raise ValueError("splat buffers smaller than the frame's layout (mcrt.dist.splat_buffers)")
-    full, chunk = full[:4 * cp * chunks], chunk[:4 * cp]
+    full, chunk = full[:c * cp * chunks], chunk[:c * cp]
     fb.bdpt_splats_copy(full.data_ptr())   # enqueued on the frame's stream
     if full.is_cuda and dist.get_backend(group) != "gloo":
         # RCCL: the collective is ordered after the pack on the frame's own stream, and the gather

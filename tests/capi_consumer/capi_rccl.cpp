@@ -169,7 +169,7 @@ int main(int argc, char** argv) {
                     check(mcrt_bdpt_splat_layout(fbs[0], &chunkPixels, &chunks), ctx);
                     if (chunks != bands) throw std::runtime_error("splat layout: chunks != bands");
                     if (!dFull) {
-                        cp4 = 4 * (size_t)chunkPixels;
+                        cp4 = MCRT_SPLAT_CHANNELS * (size_t)chunkPixels;
                         hipCheck(hipMalloc(&dFull, sizeof(float) * cp4 * bands * per));
                         hipCheck(hipMalloc(&dOwn, sizeof(float) * cp4 * per));
                     }

@@ -203,7 +203,8 @@ def test_bdpt_band_split_matches_whole_frames(hip_ctx, ranks):
     fbs = [lib.FrameBuffer(hip_ctx, W, H) for _ in range(ranks)]
     rows = [mdist.band_rows_of(H, 8, ranks, r) for r in range(ranks)]
     cr = mdist.splat_chunk_rows(H, 8, ranks)
-    bufs = [torch.zeros(4 * W * cr * ranks, dtype=torch.float32, device="cuda") for _ in range(ranks)]
+    C = mdist.SPLAT_CHANNELS
+    bufs = [torch.zeros(C * W * cr * ranks, dtype=torch.float32, device="cuda") for _ in range(ranks)]
     N = W * H
     for f in range(frames):
         full.render(ds, cam, frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT)
@@ -223,9 +224,9 @@ def test_bdpt_band_split_matches_whole_frames(hip_ctx, ranks):
             img = np.zeros((H, W, 4), np.float32)
             for fb in fbs:
                 img += fb.read_bdpt("splat").view(np.float32).reshape(H, W, 4)
-            np.testing.assert_allclose(total.cpu().numpy().reshape(ranks, cr, W, 4),
-                                       mdist.rank_major_pack(img, 8, ranks), rtol=1e-6, atol=1e-30)
-        chunks = [total[r * 4 * W * cr:(r + 1) * 4 * W * cr].clone() for r in range(ranks)]
+            np.testing.assert_allclose(total.cpu().numpy().reshape(ranks, cr, W, C),
+                                       mdist.rank_major_pack(img[..., :C], 8, ranks), rtol=1e-6, atol=1e-30)
+        chunks = [total[r * C * W * cr:(r + 1) * C * W * cr].clone() for r in range(ranks)]
         torch.cuda.synchronize()
         for r, fb in enumerate(fbs):
             fb.bdpt_gather(chunks[r].data_ptr())
