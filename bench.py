@@ -603,6 +603,7 @@ def main():
     fstats = fb.stats()
     qcounts = fb.queue_counts(max(D, 8)) if not bdpt else None
     hcounts = fb.hint_counts(max(D, 8)) if not bdpt else None   # shadow rays answered by their occluder hint
+    rcounts = fb.retrace_counts(max(D, 8)) if not bdpt else None   # compact walks repeated on exact records
     frame0 = warm + 1
 
     ctx.reset_stats()
@@ -694,6 +695,9 @@ def main():
             out["shadow_hints"] = {f"bounce{b}": round(hcounts[b] / max(qcounts[0][b], 1), 4) for b in range(D)}
             # the wavefront's queues per bounce (one untimed frame): compaction keeps only live paths,
             # so the launches shrink with depth (and with --russian-roulette)
+            # closest-hit walks over the compact records that ended on a near tie and were repeated on
+            # the exact 64-B records (mcrt_traverse.h traverseQOct), per extension bounce
+            out["near_tie_retraces"] = {f"bounce{b + 1}": int(rcounts[b]) for b in range(D - 1)}
             out["queues_per_frame"] = {"shadow": [int(v) for v in qcounts[0][:D]],
                                        "extension": [int(v) for v in qcounts[1][:max(D - 1, 0)]],
                                        "pixels": int(W * H / world)}

@@ -506,6 +506,11 @@ MCRT_API mcrt_status mcrt_framebuffer_queue_counts(mcrt_framebuffer fb, int32_t*
  * answers).  Counted while mcrt_ctx_set_profiling(ctx, 2) is on; zero otherwise, when the hints are
  * off (MCRT_SHADOW_HINTS=0) or the structure is two-level. */
 MCRT_API mcrt_status mcrt_framebuffer_hint_counts(mcrt_framebuffer fb, int32_t* hits, int max);
+/* Extension rays of the last PT render whose closest-hit walk over the compact records ended on a
+ * near tie and was repeated on the exact 64-B records (so the reference's visit order resolves it),
+ * per bounce b < max (rays traced for bounce b + 1).  Counted while mcrt_ctx_set_profiling(ctx, 2)
+ * is on; zero otherwise and with MCRT_QUANT_NODES=0. */
+MCRT_API mcrt_status mcrt_framebuffer_retrace_counts(mcrt_framebuffer fb, int32_t* retraces, int max);
 /* Host copy of a ray queue of the last render (the state the reference keeps in its
  * per-pixel trace_shadowRays / trace_rays / throughput buffers):
  *   which 0: shadow queue of the last bounce    -- origin.xyz|tmax, dir.xyz|pixel(int bits), throughput*L

@@ -1097,7 +1097,8 @@ void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
 }
 void launch_bdpt_vis(const TraceCtx& c, const BdptArgs& b, const BdptQueue& q, int maxCount, hipStream_t st) {
     const int blocks = std::max(1, std::min((maxCount + 63) / 64, BDPT_VIS_MAX_WAVES));
-    hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks), dim3(64), 0, st, c, b, q.count,
+    hipLaunchKernelGGL(pickLayout(c, k_bdpt_vis<LAY_TWO_LEVEL>, k_bdpt_vis<LAY_QUANT>, k_bdpt_vis<LAY_PLAIN>), dim3(blocks),
+                       dim3(64), 0, st, c, b, q.count,
                        q.o, q.d, q.t);
 }
 void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance, const float* chunk,

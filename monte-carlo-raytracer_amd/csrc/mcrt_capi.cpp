@@ -112,6 +112,10 @@ struct mcrt_scene_s {
     // allocated on the first shadow launch that uses hints (ensure_hint_cell), 2^hintBits words
     uint32_t* dHintCell = nullptr;
     int hintBits = 0;
+    // compact records of the flat tree (TraceCtx::qnodes; mcrt::build_qnodes), NULL when not built
+    float4* dQNodes = nullptr;
+    size_t qUnits = 0;
+    uint32_t qRoot = 0;
     bool hintAllocFailed = false;   // no memory for the table: hints stay off for this scene
 };
 
@@ -321,6 +325,8 @@ static TraceCtx trace_ctx(mcrt_scene s) {
     c.overflow = s->ctx->dFlags;
     c.twoLevel = s->twoLevel ? 1 : 0;
     c.numNodes = (uint32_t)s->numNodes;
+    c.qnodes = s->dQNodes;
+    c.qroot = s->qRoot;
     return c;
 }
 
@@ -603,6 +609,9 @@ static void scene_free_device(mcrt_scene s) {
     if (s->dScratch) hipFree(s->dScratch);
     if (s->dHintCell) hipFree(s->dHintCell);
     s->dHintCell = nullptr;
+    if (s->dQNodes) hipFree(s->dQNodes);
+    s->dQNodes = nullptr;
+    s->qUnits = 0;
     s->dSpill = nullptr;
     s->spillRays = 0;
     s->dScratch = nullptr;
@@ -922,6 +931,27 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
         s->dHintCell = nullptr;
         s->hintAllocFailed = false;
     }
+    // compact records for the per-ray walks (mcrt_traverse.h traverseQOct): depth-first flat trees;
+    // MCRT_QUANT_NODES=0 keeps the 64-B records everywhere (A/B, tests).  A tree the converter
+    // cannot take (LBVH numbering) or a device without room for it (~0.8 GB at 10 M triangles)
+    // keeps the 64-B walk: the same answers.
+    if (s->dQNodes) hipFree(s->dQNodes);
+    s->dQNodes = nullptr;
+    s->qUnits = 0;
+    const char* qe = std::getenv("MCRT_QUANT_NODES");
+    if (!s->twoLevel && !(qe && std::atoi(qe) == 0)) {
+        float4* q = nullptr;
+        size_t units = 0;
+        const hipError_t e = mcrt::build_qnodes((const float4*)s->dNodes, (uint32_t)s->numNodes, &q, &units, ctx->stream);
+        if (e == hipSuccess) {
+            s->dQNodes = q;
+            s->qUnits = units;
+        } else if (e != hipErrorNotSupported && e != hipErrorOutOfMemory) {
+            return fail(ctx, MCRT_ERROR_DEVICE, std::string("compact records: ") + hipGetErrorString(e));
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     int needCap = ((s->bvhDepth + 2 + 15) / 16) * 16;   // whole spill blocks of STACK_LDS entries
     // test hook: MCRT_TEST_SPILL_CAP=k caps the spill columns at k entries (0 = LDS stack only) so a
     // test can drive a traversal past its capacity and check that the overflow is reported
@@ -942,6 +972,7 @@ static mcrt_status finish_accel(mcrt_scene s, std::chrono::steady_clock::time_po
     HIPCHK(ctx, hipMemcpy(r, s->dNodes, 64, hipMemcpyDeviceToHost));
     int32_t mark;
     std::memcpy(&mark, &r[12], 4);
+    s->qRoot = mark >= 0 ? 0u : 1u;   // compact reference of the root: offset 0, leaf bit
     if (mark >= 0) {
         const float lo[3] = {std::min(r[0], r[4]), std::min(r[2], r[6]), std::min(r[8], r[10])};
         const float hi[3] = {std::max(r[1], r[5]), std::max(r[3], r[7]), std::max(r[9], r[11])};
@@ -961,7 +992,7 @@ MCRT_API mcrt_status mcrt_accel_info(mcrt_scene s, uint64_t* num_nodes, uint64_t
                                      uint32_t* num_triangles) {
     if (!s) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "scene is NULL");
     if (num_nodes) *num_nodes = s->numNodes;
-    if (device_bytes) *device_bytes = 64ull * s->numNodes;
+    if (device_bytes) *device_bytes = 64ull * s->numNodes + 16ull * s->qUnits;
     if (build_ms) *build_ms = s->buildMs;
     if (num_triangles) *num_triangles = s->numTris;
     return MCRT_OK;
@@ -1742,6 +1773,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
             tse.spill = slot.spill;
             with_hints(tse, s, b == 0 ? fb->hintPix : nullptr, (uint32_t)fb->N);
             if (tse.hint && ctx->countHints) tse.hintHits = fb->counters + 64 + b;
+            if (tse.qnodes && ctx->countHints) tse.retraces = fb->counters + 96 + b;
             mcrt::launch_shadow_extend(tse, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
                                        fb->sO, fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
@@ -2019,6 +2051,20 @@ MCRT_API mcrt_status mcrt_framebuffer_hint_counts(mcrt_framebuffer fb, int32_t* 
     for (int b = 0; b < max && b < 32; ++b) {
         const bool live = b < fb->lastMaxDepth && fb->lastIntegrator == MCRT_INTEGRATOR_PT;
         if (hits) hits[b] = live ? c[64 + b] : 0;
+    }
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_retrace_counts(mcrt_framebuffer fb, int32_t* retraces, int max) {
+    if (!fb || max < 0) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    mcrt_ctx ctx = fb->ctx;
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, fb_sync(fb));
+    int c[128];
+    HIPCHK(ctx, hipMemcpy(c, fb->counters, sizeof(c), hipMemcpyDeviceToHost));
+    for (int b = 0; b < max && b < 32; ++b) {
+        const bool live = b + 1 < fb->lastMaxDepth && fb->lastIntegrator == MCRT_INTEGRATOR_PT;
+        if (retraces) retraces[b] = live ? c[96 + b] : 0;
     }
     return MCRT_OK;
 }

@@ -103,6 +103,13 @@ struct TraceCtx {
     float hintLo[3], hintInvExt[3];   // cell = (o - hintLo) * hintInvExt * MCRT_HINT_GRID
     uint32_t numNodes;      // records in `nodes` (hints are range-checked against it)
     int* hintHits;          // rays answered by their hint are counted here (NULL: not counted)
+    // Compact records of the same tree (mcrt_kernels.hip k_qnodes_convert; the per-ray walks of the
+    // LAY_QUANT instantiations, mcrt_traverse.h traverseQOct): 32-B internal records with 8-bit
+    // outward-rounded child boxes, 48-B leaves; a record reference is (offset / 16) << 1 | leaf.
+    // NULL: not built (two-level, non-DFS trees, MCRT_QUANT_NODES=0).
+    const float4* qnodes;
+    uint32_t qroot;
+    int* retraces;          // closest-hit walks repeated on the exact records (near ties; NULL: not counted)
 };
 #define MCRT_HINT_PIXEL 1
 #define MCRT_HINT_CELL 2
@@ -152,6 +159,9 @@ void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStrea
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st);
 // parent index of each triangle leaf into its record's word 13 (flat trees, finish_accel)
 void launch_leaf_parents(float4* nodes, uint32_t n, hipStream_t st);
+// compact records of a flat DFS tree (after launch_leaf_parents): *qOut (16-B units, caller frees),
+// *units its size; hipErrorNotSupported when the tree is not in DFS order (left child = i + 1)
+hipError_t build_qnodes(const float4* nodes, uint32_t n, float4** qOut, size_t* units, hipStream_t st);
 void launch_chase_init(void* rec, uint32_t n, hipStream_t st);
 void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* sink, hipStream_t st);
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,

@@ -14,6 +14,8 @@
 // one wave per workgroup, the hardware dispatcher schedules the waves.
 #include <algorithm>
 
+#include <rocprim/device/device_scan.hpp>
+
 #include "mcrt_device.h"
 #include "mcrt_internal.h"
 #include "mcrt_traverse.h"
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         const int sb = (ns + 63) >> 6;
         if ((int)blockIdx.x - eb >= sb) return;
         const int i = xcdRemap((int)blockIdx.x - eb, sb) * 64 + lane;
-        if (LAY == LAY_PLAIN && c.packet) {
+        if (LAY != LAY_TWO_LEVEL && c.packet) {
             // bounce-0 shadow rays: a wave's rays leave a few pixels for one light (packed waves), so
             // they walk the tree as one packet (any hit: the answers do not depend on the order)
             const bool valid = i < ns;
@@ -871,6 +873,92 @@ __global__ __launch_bounds__(256) void k_leaf_parents(float4* __restrict__ nodes
     }
 }
 
+// Compact records (mcrt_traverse.h traverseQOct has the format and the exactness argument).
+// Sizes in 16-B units per 64-B record (internal 2, leaf 3); notDfs: a left child that is not the
+// next record (the LBVH's numbering) -- the compact walk takes the left child as the next record.
+__global__ __launch_bounds__(256) void k_qnodes_sizes(const float4* __restrict__ nodes, uint32_t n,
+                                                      uint32_t* __restrict__ units, int* __restrict__ notDfs) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int4 w = *reinterpret_cast<const int4*>(&nodes[4 * (size_t)i + 3]);
+    units[i] = w.x >= 0 ? 2u : 3u;
+    if (w.x >= 0 && w.x != (int)i + 1) atomicOr(notDfs, 1);
+}
+
+// One axis of an internal record: the two children's (lo, hi) as bytes q with fmaf(q, s, o) <= lo
+// and >= hi exactly as the traversal decodes them (s = 2^(e - 127), o = the smaller lo).  Returns
+// false when no byte reaches a bound (non-finite boxes).
+MCRT_DEV bool quantAxis(float lo0, float hi0, float lo1, float hi1, float& o, uint32_t& bytes, uint32_t& e) {
+    o = fminf(lo0, lo1);
+    const float ext = fmaxf(hi0, hi1) - o;
+    if (!(ext >= 0.0f) || ext == __builtin_inff()) return false;
+    int k = -126;
+    if (ext > 0.0f) frexpf(ext * (1.0f / 250.0f), &k);   // ext / 250 <= 2^k
+    e = (uint32_t)min(max(k + 127, 1), 254);
+    const float sc = __uint_as_float(e << 23);
+    const float b[4] = {lo0, hi0, lo1, hi1};
+    bytes = 0;
+    for (int j = 0; j < 4; ++j) {
+        const bool up = (j & 1) != 0;   // hi bounds round up, lo bounds down
+        int q = (int)(up ? ceilf((b[j] - o) / sc) : floorf((b[j] - o) / sc));
+        q = min(max(q, 0), 255);
+        if (up) {
+            while (q < 255 && fmaf((float)q, sc, o) < b[j]) ++q;
+            if (fmaf((float)q, sc, o) < b[j]) return false;
+        } else {
+            while (q > 0 && fmaf((float)q, sc, o) > b[j]) --q;
+            if (fmaf((float)q, sc, o) > b[j]) return false;
+        }
+        bytes |= (uint32_t)q << (8 * j);
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_qnodes_convert(const float4* __restrict__ nodes, uint32_t n,
+                                                        const uint32_t* __restrict__ off, float4* __restrict__ q,
+                                                        int* __restrict__ fail) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float4 n0 = nodes[4 * (size_t)i], n1 = nodes[4 * (size_t)i + 1], n2 = nodes[4 * (size_t)i + 2];
+    const int4 w = *reinterpret_cast<const int4*>(&nodes[4 * (size_t)i + 3]);
+    float4* dst = q + off[i];
+    if (w.x >= 0) {   // child 0 box (n0.x, n0.z, n2.x)-(n0.y, n0.w, n2.y), child 1 (n1.x, n1.z, n2.z)-(n1.y, n1.w, n2.w)
+        float ox, oy, oz;
+        uint32_t bx, by, bz, ex, ey, ez;
+        const bool ok = quantAxis(n0.x, n0.y, n1.x, n1.y, ox, bx, ex) && quantAxis(n0.z, n0.w, n1.z, n1.w, oy, by, ey) &&
+                        quantAxis(n2.x, n2.y, n2.z, n2.w, oz, bz, ez);
+        if (!ok || (uint32_t)w.y >= n) {
+            atomicOr(fail, 1);
+            return;
+        }
+        const uint32_t leaf0 = reinterpret_cast<const int4*>(&nodes[4 * (size_t)w.x + 3])->x < 0 ? 1u : 0u;
+        const uint32_t leaf1 = reinterpret_cast<const int4*>(&nodes[4 * (size_t)w.y + 3])->x < 0 ? 1u : 0u;
+        dst[0] = make_float4(ox, oy, oz, __uint_as_float(off[w.y]));
+        dst[1] = make_float4(__uint_as_float(bx), __uint_as_float(by), __uint_as_float(bz),
+                             __uint_as_float(ex | (ey << 8) | (ez << 16) | (leaf0 << 24) | (leaf1 << 25)));
+        return;
+    }
+    // leaf: its exact box (as the parent's record stores it) must be min / max of v0, v0 + e1, v0 + e2
+    // for the compact walk to test it from the triangle; else bit 31 sends the walk to the parent
+    bool slow = true;
+    const int par = w.y;   // k_leaf_parents
+    if (par >= 0 && (uint32_t)par < n) {
+        const float4 p0 = nodes[4 * (size_t)par], p1 = nodes[4 * (size_t)par + 1], p2 = nodes[4 * (size_t)par + 2];
+        const bool right = reinterpret_cast<const int4*>(&nodes[4 * (size_t)par + 3])->y == (int)i;
+        const f3 lo = right ? f3{p1.x, p1.z, p2.z} : f3{p0.x, p0.z, p2.x};
+        const f3 hi = right ? f3{p1.y, p1.w, p2.w} : f3{p0.y, p0.w, p2.y};
+        const f3 v0 = ld3(n0), v1 = v0 + ld3(n1), v2 = v0 + ld3(n2);
+        const f3 l = f3{fminf(fminf(v0.x, v1.x), v2.x), fminf(fminf(v0.y, v1.y), v2.y), fminf(fminf(v0.z, v1.z), v2.z)};
+        const f3 h = f3{fmaxf(fmaxf(v0.x, v1.x), v2.x), fmaxf(fmaxf(v0.y, v1.y), v2.y), fmaxf(fmaxf(v0.z, v1.z), v2.z)};
+        slow = __float_as_uint(l.x) != __float_as_uint(lo.x) || __float_as_uint(l.y) != __float_as_uint(lo.y) ||
+               __float_as_uint(l.z) != __float_as_uint(lo.z) || __float_as_uint(h.x) != __float_as_uint(hi.x) ||
+               __float_as_uint(h.y) != __float_as_uint(hi.y) || __float_as_uint(h.z) != __float_as_uint(hi.z);
+    }
+    dst[0] = n0;
+    dst[1] = n1;
+    dst[2] = make_float4(n2.x, n2.y, n2.z, __uint_as_float(i | (slow ? 0x80000000u : 0u)));
+}
+
 // Attainable-bandwidth probe (mcrt_ctx_stream_copy): a persistent grid (8 workgroups per CU)
 // strides over the array; each lane keeps 4 independent 16-B nontemporal loads in flight.
 __global__ __launch_bounds__(256) void k_stream_copy(const f4* __restrict__ src, f4* __restrict__ dst, size_t n) {
@@ -897,10 +985,12 @@ void launch_trace_rays(bool any, const TraceCtx& c, const mcrt_ray* rays, int n,
     const dim3 g((n + 63) / 64), b(64);
     {
         if (any)
-            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<true, LAY_TWO_LEVEL>, k_trace_rays<true, LAY_PLAIN>),
+            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<true, LAY_TWO_LEVEL>, k_trace_rays<true, LAY_QUANT>,
+                                          k_trace_rays<true, LAY_PLAIN>),
                                g, b, 0, st, c, rays, n, countDev, hits, occl);
         else
-            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<false, LAY_TWO_LEVEL>, k_trace_rays<false, LAY_PLAIN>),
+            hipLaunchKernelGGL(pickLayout(c, k_trace_rays<false, LAY_TWO_LEVEL>, k_trace_rays<false, LAY_QUANT>,
+                                          k_trace_rays<false, LAY_PLAIN>),
                                g, b, 0, st, c, rays, n, countDev, hits, occl);
     }
 }
@@ -922,27 +1012,31 @@ void launch_primary(const TraceCtx& c, const FrameArgs& f, const mcrt_camera* ca
 }
 void launch_extend(const TraceCtx& c, const int* count, const float4* qO, const float4* qD, float4* hits, int maxCount,
                    hipStream_t st, const uint32_t* perm) {
-    hipLaunchKernelGGL(pickLayout(c, k_extend<LAY_TWO_LEVEL>, k_extend<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+    hipLaunchKernelGGL(pickLayout(c, k_extend<LAY_TWO_LEVEL>, k_extend<LAY_QUANT>, k_extend<LAY_PLAIN>),
+                       dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, qO, qD, hits, perm);
 }
 void launch_extend_pair(const TraceCtx& cc, const TraceCtx& c, const int* count0, const float4* qO0, const float4* qD0,
                         float4* hit0, const int* count1, const float4* qO1, const float4* qD1, float4* hit1,
                         int maxCount0, int maxCount1, hipStream_t st, const uint32_t* perm1) {
-    auto k = c.twoLevel ? k_extend_pair<LAY_TWO_LEVEL, LAY_TWO_LEVEL> : k_extend_pair<LAY_PLAIN, LAY_PLAIN>;
+    auto k = c.twoLevel ? k_extend_pair<LAY_TWO_LEVEL, LAY_TWO_LEVEL>
+             : c.qnodes ? (cc.packet ? k_extend_pair<LAY_PLAIN, LAY_QUANT> : k_extend_pair<LAY_QUANT, LAY_QUANT>)
+                        : k_extend_pair<LAY_PLAIN, LAY_PLAIN>;
     const int blocks = (maxCount0 + 63) / 64 + (maxCount1 + 63) / 64;
     hipLaunchKernelGGL(k, dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, cc, c, count0, qO0, qD0, hit0, count1, qO1,
                        qD1, hit1, perm1);
 }
 void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const float4* sD, const float4* sL,
                    float4* radiance, int maxCount, hipStream_t st) {
-    hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_PLAIN>), dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
+    hipLaunchKernelGGL(pickLayout(c, k_shadow<LAY_TWO_LEVEL>, k_shadow<LAY_QUANT>, k_shadow<LAY_PLAIN>),
+                       dim3((maxCount + 63) / 64), dim3(64), 0, st, c,
                        count, sO, sD, sL, radiance);
 }
 void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
                           const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
                           float4* radiance, int maxExt, int maxShadow, hipStream_t st) {
     const int blocks = (maxExt + 63) / 64 + (maxShadow + 63) / 64;
-    hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_PLAIN>),
+    hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_QUANT>, k_shadow_extend<LAY_PLAIN>),
                        dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, extCount, qO, qD, hits, shadowCount, sO, sD,
                        sL, radiance);
 }
@@ -991,6 +1085,53 @@ void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* s
 void launch_leaf_parents(float4* nodes, uint32_t n, hipStream_t st) {
     if (n == 0) return;
     hipLaunchKernelGGL(k_leaf_parents, dim3((n + 255) / 256), dim3(256), 0, st, nodes, n);
+}
+
+hipError_t build_qnodes(const float4* nodes, uint32_t n, float4** qOut, size_t* unitsOut, hipStream_t st) {
+    *qOut = nullptr;
+    *unitsOut = 0;
+    if (n == 0 || n >= (1u << 31)) return hipErrorNotSupported;
+    uint32_t *units = nullptr, *off = nullptr;
+    int* flags = nullptr;
+    void* tmp = nullptr;
+    size_t tmpBytes = 0;
+    float4* q = nullptr;
+    int h[2] = {0, 0};
+    uint32_t lastOff = 0, lastUnits = 0;
+    hipError_t e = hipMalloc(&units, 4 * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&off, 4 * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&flags, 2 * sizeof(int));
+    if (e == hipSuccess) e = hipMemsetAsync(flags, 0, 2 * sizeof(int), st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_qnodes_sizes, dim3((n + 255) / 256), dim3(256), 0, st, nodes, n, units, flags);
+        e = rocprim::exclusive_scan(nullptr, tmpBytes, units, off, 0u, (size_t)n, rocprim::plus<uint32_t>(), st);
+    }
+    if (e == hipSuccess) e = hipMalloc(&tmp, tmpBytes);
+    if (e == hipSuccess) e = rocprim::exclusive_scan(tmp, tmpBytes, units, off, 0u, (size_t)n, rocprim::plus<uint32_t>(), st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&lastOff, off + n - 1, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&lastUnits, units + n - 1, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    const size_t total = (size_t)lastOff + lastUnits;
+    if (e == hipSuccess && h[0] != 0) e = hipErrorNotSupported;   // not depth-first
+    if (e == hipSuccess) e = hipMalloc(&q, 16 * total);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_qnodes_convert, dim3((n + 255) / 256), dim3(256), 0, st, nodes, n, off, q, flags + 1);
+        e = hipMemcpyAsync(h + 1, flags + 1, sizeof(int), hipMemcpyDeviceToHost, st);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess && h[1] != 0) e = hipErrorNotSupported;   // a box the bytes cannot bound
+    hipFree(tmp);
+    hipFree(flags);
+    hipFree(off);
+    hipFree(units);
+    if (e != hipSuccess) {
+        if (q) hipFree(q);
+        return e;
+    }
+    *qOut = q;
+    *unitsOut = total;
+    return hipSuccess;
 }
 
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st) {

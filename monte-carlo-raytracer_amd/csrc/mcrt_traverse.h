@@ -13,10 +13,15 @@
 // layout gets its own kernel instantiation, so a kernel's register budget is that of the one loop
 // it runs.
 #define LAY_PLAIN 0       // mcrt_bvh.cpp records, traverseOct (and traversePacket)
+#define LAY_QUANT 1       // the same tree's compact records (TraceCtx::qnodes), traverseQOct
 #define LAY_TWO_LEVEL 3   // mcrt_bvh2l.cpp records, traverse2L
 template <typename K>
 inline K pickLayout(const TraceCtx& c, K twoLevel, K plain) {
     return c.twoLevel ? twoLevel : plain;
+}
+template <typename K>
+inline K pickLayout(const TraceCtx& c, K twoLevel, K quant, K plain) {
+    return c.twoLevel ? twoLevel : c.qnodes ? quant : plain;
 }
 
 struct TraceRay {
@@ -353,6 +358,224 @@ MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint3
 #undef MCRT_TRAV_CALL
 }
 
+// ---------------------------------------------------------------------------
+// Compact records (TraceCtx::qnodes, built by k_qnodes_convert from the 64-B records of a
+// depth-first tree): the per-ray walks fetch 32 B per internal node and 48 B per leaf instead of
+// 64 B -- two or three 16-B loads instead of four.  The traversal launches are bound by the vector-
+// memory pipeline (TA busy 0.94, one cache access per 16-B lane load), not by arithmetic.
+//   internal (32 B): (origin.xyz, right child ref) | (x bytes, y bytes, z bytes, meta): for axis a
+//     the bytes are (child 0 lo, child 0 hi, child 1 lo, child 1 hi) and a bound decodes as
+//     fmaf(q, 2^(e_a - 127), origin_a); meta = e_x | e_y << 8 | e_z << 16 | leaf(child 0) << 24 |
+//     leaf(child 1) << 25.  The left child is the next record (depth-first order).
+//   leaf (48 B): (v0 | shape id), (v1 - v0 | prim id), (v2 - v0 | 64-B record index, bit 31 set when
+//     the leaf's exact box must come from its parent's 64-B record).
+// Why the answers are the 64-B walk's (RR intersect_bvh2_lds.cl:107-178):
+//   * every decoded bound is rounded outward (the converter checks each fmaf decode against the
+//     exact bound), and fma rounds monotonically, so a decoded box's slab interval contains the
+//     exact box's: every internal test the exact walk passes, this walk passes;
+//   * at a leaf the EXACT box test runs before the triangle test (the box is min/max of the
+//     vertices v0, v0 + e1, v0 + e2, which the converter checked against the box the parent's 64-B
+//     record stores, else bit 31 sends the lane to that record), so the triangles that can hit are
+//     exactly the exact walk's;
+//   * any hit: the answer (hit or not) is then the exact walk's;
+//   * closest hit: the nearest hit is the same, but equal distances resolve by visit order, which
+//     the outward boxes may change.  A hit within QTIE_EPS of the current closest (either side)
+//     marks a near tie; a walk whose final distance carries a near tie is repeated on the exact
+//     records (traceClosest<LAY_QUANT>), so the reference's order decides it.  The culling distance
+//     is widened by the same margin once a hit exists, so a near-tie candidate is always tested.
+// ---------------------------------------------------------------------------
+#define QREF_DONE 0xffffffffu
+#define QTIE_HI (1.0f + 0x1.0p-18f)
+#define QTIE_LO (1.0f - 0x1.0p-18f)
+
+MCRT_DEV float qScale(uint32_t meta, int axis) { return __uint_as_float(((meta >> (8 * axis)) & 0xffu) << 23); }
+MCRT_DEV float qByte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xffu); }
+
+// RR common.cl:177-218 without the tmax test: the hit distance or +inf (the caller compares)
+MCRT_DEV float triRaw(const TraceRay& r, float4 A, float4 E1, float4 E2) {
+    const f3 e1 = ld3(E1), e2 = ld3(E2);
+    const f3 s1 = cl_cross(r.d, e2);
+    const float denom = cl_dot(s1, e1);
+    if (denom == 0.f) return __builtin_inff();
+    const float invd = __builtin_amdgcn_rcpf(denom);
+    const f3 d = r.o - ld3(A);
+    const float b1 = cl_dot(d, s1) * invd;
+    const f3 s2 = cl_cross(d, e1);
+    const float b2 = cl_dot(r.d, s2) * invd;
+    const float temp = cl_dot(e2, s2) * invd;
+    if (b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || temp < 0.f) return __builtin_inff();
+    return temp;
+}
+
+// fast_intersect_bbox2 (intersect_bvh2_lds.cl:54-63) of one box, entry <= exit
+template <int OCT>
+MCRT_DEV bool slabHit(f3 lo, f3 hi, f3 inv, f3 oxi, float t) {
+    if constexpr (OCT >= 0) {
+        constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
+        const float xn = fmaf(SX ? hi.x : lo.x, inv.x, oxi.x), xf = fmaf(SX ? lo.x : hi.x, inv.x, oxi.x);
+        const float yn = fmaf(SY ? hi.y : lo.y, inv.y, oxi.y), yf = fmaf(SY ? lo.y : hi.y, inv.y, oxi.y);
+        const float zn = fmaf(SZ ? hi.z : lo.z, inv.z, oxi.z), zf = fmaf(SZ ? lo.z : hi.z, inv.z, oxi.z);
+        return fmaxf(fmaxf(xn, yn), fmaxf(zn, 0.0f)) <= fminf(fminf(xf, yf), fminf(zf, t));
+    } else {
+        const float x0 = fmaf(lo.x, inv.x, oxi.x), x1 = fmaf(hi.x, inv.x, oxi.x);
+        const float y0 = fmaf(lo.y, inv.y, oxi.y), y1 = fmaf(hi.y, inv.y, oxi.y);
+        const float z0 = fmaf(lo.z, inv.z, oxi.z), z1 = fmaf(hi.z, inv.z, oxi.z);
+        return fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), 0.0f) <=
+               fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), t);
+    }
+}
+
+// The exact box of 64-B leaf `leaf` as its parent's record stores it (the rare leaves whose box the
+// compact record cannot reproduce; the root leaf has no box test, as in the exact walk)
+MCRT_DEV bool parentBoxHit(const TraceCtx& c, uint32_t leaf, f3 inv, f3 oxi, float t) {
+    const int par = reinterpret_cast<const int4*>(&c.nodes[4 * leaf + 3])->y;
+    if (par < 0) return true;
+    const float4 p0 = c.nodes[4 * par], p1 = c.nodes[4 * par + 1], p2 = c.nodes[4 * par + 2];
+    const bool right = reinterpret_cast<const int4*>(&c.nodes[4 * par + 3])->y == (int)leaf;
+    const f3 lo = right ? f3{p1.x, p1.z, p2.z} : f3{p0.x, p0.z, p2.x};
+    const f3 hi = right ? f3{p1.y, p1.w, p2.w} : f3{p0.y, p0.w, p2.y};
+    return slabHit<-1>(lo, hi, inv, oxi, t);
+}
+
+// Returns the hit leaf's 64-B record index or -1; tie: a near tie at the final distance (closest hit).
+template <bool ANY, int OCT>
+MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t* stk, uint32_t* spill,
+                          float& tHit, bool& tie) {
+    const char* __restrict__ base = reinterpret_cast<const char*>(c.qnodes);
+    const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
+    float t = r.tmax, tc = r.tmax, tieT = -1.0f;
+    int hit = -1;
+    uint32_t ref = c.qroot;
+    stk[0] = QREF_DONE;
+    int sp = 1, spillTop = 0;
+    constexpr uint32_t POP = QREF_DONE - 1;
+    while (ref != QREF_DONE) {
+        const float4* p = reinterpret_cast<const float4*>(base + (size_t)(ref >> 1) * 16);
+        const float4 a = p[0];
+        const uint4 b = *reinterpret_cast<const uint4*>(p + 1);
+        uint32_t next;
+        if (!(ref & 1u)) {
+            const float sx = qScale(b.w, 0), sy = qScale(b.w, 1), sz = qScale(b.w, 2);
+            const f3 lo0 = f3{fmaf(qByte(b.x, 0), sx, a.x), fmaf(qByte(b.y, 0), sy, a.y), fmaf(qByte(b.z, 0), sz, a.z)};
+            const f3 hi0 = f3{fmaf(qByte(b.x, 1), sx, a.x), fmaf(qByte(b.y, 1), sy, a.y), fmaf(qByte(b.z, 1), sz, a.z)};
+            const f3 lo1 = f3{fmaf(qByte(b.x, 2), sx, a.x), fmaf(qByte(b.y, 2), sy, a.y), fmaf(qByte(b.z, 2), sz, a.z)};
+            const f3 hi1 = f3{fmaf(qByte(b.x, 3), sx, a.x), fmaf(qByte(b.y, 3), sy, a.y), fmaf(qByte(b.z, 3), sz, a.z)};
+            float a0, a1, b0, b1;
+            if constexpr (OCT >= 0) {
+                constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
+                const float axn = fmaf(SX ? hi0.x : lo0.x, inv.x, oxi.x), axf = fmaf(SX ? lo0.x : hi0.x, inv.x, oxi.x);
+                const float ayn = fmaf(SY ? hi0.y : lo0.y, inv.y, oxi.y), ayf = fmaf(SY ? lo0.y : hi0.y, inv.y, oxi.y);
+                const float azn = fmaf(SZ ? hi0.z : lo0.z, inv.z, oxi.z), azf = fmaf(SZ ? lo0.z : hi0.z, inv.z, oxi.z);
+                const float bxn = fmaf(SX ? hi1.x : lo1.x, inv.x, oxi.x), bxf = fmaf(SX ? lo1.x : hi1.x, inv.x, oxi.x);
+                const float byn = fmaf(SY ? hi1.y : lo1.y, inv.y, oxi.y), byf = fmaf(SY ? lo1.y : hi1.y, inv.y, oxi.y);
+                const float bzn = fmaf(SZ ? hi1.z : lo1.z, inv.z, oxi.z), bzf = fmaf(SZ ? lo1.z : hi1.z, inv.z, oxi.z);
+                a0 = fmaxf(fmaxf(axn, ayn), fmaxf(azn, 0.0f));
+                a1 = fminf(fminf(axf, ayf), fminf(azf, tc));
+                b0 = fmaxf(fmaxf(bxn, byn), fmaxf(bzn, 0.0f));
+                b1 = fminf(fminf(bxf, byf), fminf(bzf, tc));
+            } else {
+                const float ax0 = fmaf(lo0.x, inv.x, oxi.x), ax1 = fmaf(hi0.x, inv.x, oxi.x);
+                const float ay0 = fmaf(lo0.y, inv.y, oxi.y), ay1 = fmaf(hi0.y, inv.y, oxi.y);
+                const float az0 = fmaf(lo0.z, inv.z, oxi.z), az1 = fmaf(hi0.z, inv.z, oxi.z);
+                const float bx0 = fmaf(lo1.x, inv.x, oxi.x), bx1 = fmaf(hi1.x, inv.x, oxi.x);
+                const float by0 = fmaf(lo1.y, inv.y, oxi.y), by1 = fmaf(hi1.y, inv.y, oxi.y);
+                const float bz0 = fmaf(lo1.z, inv.z, oxi.z), bz1 = fmaf(hi1.z, inv.z, oxi.z);
+                a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
+                a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), tc);
+                b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
+                b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), tc);
+            }
+            const uint32_t cl = (((ref >> 1) + 2u) << 1) | ((b.w >> 24) & 1u);
+            const uint32_t cr = (__float_as_uint(a.w) << 1) | ((b.w >> 25) & 1u);
+            const bool h0 = a0 <= a1, h1 = b0 <= b1;
+            const bool c1first = h1 && (a0 > b0);   // intersect_bvh2_lds.cl:128-141
+            if (h0 && h1) {   // defer the far child
+                if (sp == STACK_LDS) {   // spill entries 1..15 (RR: intersect_bvh2_lds.cl:146-155)
+                    if (spillTop + STACK_LDS - 1 <= c.spillCap) {
+                        for (int k = 1; k < STACK_LDS; ++k) spill[(size_t)(spillTop + k - 1) * 64] = stk[k * 64];
+                        spillTop += STACK_LDS - 1;
+                    } else {
+                        *c.overflow = 1;
+                    }
+                    sp = 1;
+                }
+                stk[sp * 64] = c1first ? cl : cr;
+                ++sp;
+            }
+            next = (h0 || h1) ? ((c1first || !h0) ? cr : cl) : POP;
+        } else {
+            next = POP;
+            const float4 e2 = p[2];
+            const uint32_t w = __float_as_uint(e2.w);
+            if (r.mask != __float_as_int(a.w)) {   // RR_RAY_MASK
+                const float4 e1 = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), 0.0f);
+                bool boxHit;
+                if (w >> 31) {
+                    boxHit = parentBoxHit(c, w & 0x7fffffffu, inv, oxi, tc);
+                } else {
+                    const f3 v0 = ld3(a), v1 = v0 + ld3(e1), v2 = v0 + ld3(e2);
+                    const f3 lo = f3{fminf(fminf(v0.x, v1.x), v2.x), fminf(fminf(v0.y, v1.y), v2.y),
+                                     fminf(fminf(v0.z, v1.z), v2.z)};
+                    const f3 hi = f3{fmaxf(fmaxf(v0.x, v1.x), v2.x), fmaxf(fmaxf(v0.y, v1.y), v2.y),
+                                     fmaxf(fmaxf(v0.z, v1.z), v2.z)};
+                    boxHit = slabHit<OCT>(lo, hi, inv, oxi, tc);
+                }
+                if (boxHit) {
+                    const float th = triRaw(r, a, e1, e2);
+                    if (th < t) {
+                        if (!ANY && hit >= 0 && th >= t * QTIE_LO) tieT = th;
+                        t = th;
+                        tc = ANY ? th : th * QTIE_HI;
+                        hit = (int)(w & 0x7fffffffu);
+                        if (ANY) next = QREF_DONE;
+                    } else if (!ANY && hit >= 0 && th <= tc) {
+                        tieT = t;
+                    }
+                }
+            }
+        }
+        if (next == POP) {
+            --sp;
+            next = stk[sp * 64];
+            if (next == QREF_DONE && spillTop > 0) {   // refill (intersect_bvh2_lds.cl:182-191)
+                spillTop -= STACK_LDS - 1;
+                for (int k = 1; k < STACK_LDS; ++k) stk[k * 64] = spill[(size_t)(spillTop + k - 1) * 64];
+                sp = STACK_LDS - 1;
+                next = stk[sp * 64];
+            }
+        }
+        ref = next;
+    }
+    tHit = t;
+    tie = !ANY && hit >= 0 && tieT == t;
+    return hit;
+}
+
+template <bool ANY>
+MCRT_DEV int traverseQ(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, float& tHit,
+                       bool& tie) {
+    const f3 inv = safeInvDir(r.d);
+#define MCRT_TRAVQ_CALL(OCT) return traverseQOct<ANY, OCT>(c, r, inv, stk, spill, tHit, tie)
+    const int oct = (int)(__float_as_uint(inv.x) >> 31) | (int)((__float_as_uint(inv.y) >> 31) << 1) |
+                    (int)((__float_as_uint(inv.z) >> 31) << 2);
+    const int oct0 = __builtin_amdgcn_readfirstlane(oct);
+    if (__all(oct == oct0)) {
+        switch (oct0) {
+            case 0: MCRT_TRAVQ_CALL(0);
+            case 1: MCRT_TRAVQ_CALL(1);
+            case 2: MCRT_TRAVQ_CALL(2);
+            case 3: MCRT_TRAVQ_CALL(3);
+            case 4: MCRT_TRAVQ_CALL(4);
+            case 5: MCRT_TRAVQ_CALL(5);
+            case 6: MCRT_TRAVQ_CALL(6);
+            case 7: MCRT_TRAVQ_CALL(7);
+            default: break;
+        }
+    }
+    MCRT_TRAVQ_CALL(-1);
+#undef MCRT_TRAVQ_CALL
+}
+
 // RR common.cl:249-277 (triangle_calculate_barycentrics)
 MCRT_DEV f2 triBary(f3 p, float4 A, float4 E1, float4 E2) {
     const f3 e1 = ld3(E1), e2 = ld3(E2);
@@ -582,6 +805,14 @@ MCRT_DEV float4 traceClosest(const TraceCtx& c, const TraceRay& r, uint32_t* stk
         int inst;
         const int tri = traverse2L<false>(c.nodes, r, stk, spill, c.spillCap, c.overflow, t, inst);
         return closestRecord2L(c.nodes, r, tri, inst, t);
+    } else if constexpr (LAY == LAY_QUANT) {
+        bool tie;
+        int tri = traverseQ<false>(c, r, stk, spill, t, tie);
+        if (tie) {   // a near tie at the final distance: the exact walk decides it (reference order)
+            if (c.retraces) atomicAdd(c.retraces, 1);
+            tri = traverse<false, LAY_PLAIN>(c, r, stk, spill, t);
+        }
+        return closestRecord(c.nodes, r, tri, t);
     } else {
         const int tri = traverse<false, LAY>(c, r, stk, spill, t);
         return closestRecord(c.nodes, r, tri, t);
@@ -593,6 +824,9 @@ MCRT_DEV bool traceAny(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint
     if constexpr (LAY == LAY_TWO_LEVEL) {
         int inst;
         return traverse2L<true>(c.nodes, r, stk, spill, c.spillCap, c.overflow, t, inst) >= 0;
+    } else if constexpr (LAY == LAY_QUANT) {
+        bool tie;
+        return traverseQ<true>(c, r, stk, spill, t, tie) >= 0;
     } else {
         return traverse<true, LAY>(c, r, stk, spill, t) >= 0;
     }
@@ -609,13 +843,14 @@ MCRT_DEV void countHintHits(const TraceCtx& c, bool ok) {
 // records; mcrt_traverse.h hintOccludes), then the walk, whose occluder becomes the slot's next hint.
 template <int LAY>
 MCRT_DEV bool shadowOccluded(const TraceCtx& c, const TraceRay& r, int path, uint32_t* stk, uint32_t* spill) {
-    if (LAY == LAY_PLAIN && c.hint) {
+    if (LAY != LAY_TWO_LEVEL && c.hint) {
         const uint32_t h = hintSlot(c, r, path);
         const bool ok = hintOccludes(c, r, c.hint[h]);
         countHintHits(c, ok);
         if (ok) return true;
         float t;
-        const int leaf = traverse<true, LAY>(c, r, stk, spill, t);
+        bool tie;
+        const int leaf = LAY == LAY_QUANT ? traverseQ<true>(c, r, stk, spill, t, tie) : traverse<true, LAY_PLAIN>(c, r, stk, spill, t);
         if (leaf >= 0) c.hint[h] = (uint32_t)leaf;
         return leaf >= 0;
     }

@@ -82,6 +82,7 @@ SIGNATURES = {
     "mcrt_framebuffer_read_queue": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int32)]),
     "mcrt_framebuffer_queue_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.POINTER(_c.c_int32), _c.c_int]),
     "mcrt_framebuffer_hint_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.c_int]),
+    "mcrt_framebuffer_retrace_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.c_int]),
     "mcrt_postprocess": (_c.c_int, [_vp, _c.POINTER(T.PostprocessParams)]),
     "mcrt_render_aov": (_c.c_int, [_vp, _vp, _vp, _vp, _c.c_int, _vp]),
     "mcrt_framebuffer_read_bdpt": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64)]),
@@ -450,6 +451,13 @@ class FrameBuffer:
         """hits[b]: shadow rays of bounce b answered by their occluder hint in the last PT render."""
         h = (_c.c_int32 * max_bounces)()
         _check(lib().mcrt_framebuffer_hint_counts(self.h, h, max_bounces), self.ctx.h)
+        return list(h)
+
+    def retrace_counts(self, max_bounces=8):
+        """retraces[b]: rays traced for bounce b+1 whose compact-record walk ended on a near tie and
+        was repeated on the exact records, in the last PT render (counted at profiling level 2)."""
+        h = (_c.c_int32 * max_bounces)()
+        _check(lib().mcrt_framebuffer_retrace_counts(self.h, h, max_bounces), self.ctx.h)
         return list(h)
 
     def read_queue(self, which):

@@ -13,7 +13,16 @@ def dispatches(db):
     q = f"""select s.kernel_name, d.start, d.end, {qcol}, d.grid_size_x
             from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id
             order by d.start"""
-    return [(n.split("(")[0].replace("_Z", "")[:32], st, en, qu, g) for n, st, en, qu, g in c.execute(q)]
+    rows = [(n.split("(")[0].replace("_Z", "")[:32], st, en, qu, g) for n, st, en, qu, g in c.execute(q)]
+    # memory copies (rocprofv3 --memory-copy-trace), merged into the timeline
+    tables = {r[0] for r in c.execute("select name from sqlite_master where type = 'table'")}
+    if "rocpd_memory_copy" in tables:
+        mc = [r[1] for r in c.execute("pragma table_info(rocpd_memory_copy)")]
+        size = "size" if "size" in mc else "0"
+        for st, en, sz in c.execute(f"select start, end, {size} from rocpd_memory_copy"):
+            rows.append(("memcpy", st, en, -1, sz))
+        rows.sort(key=lambda r: r[1])
+    return rows
 
 
 def main():

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--kernels", action="store_true",
                     help="also report rank 0's per-kernel HIP-event ms per frame (a separate profiled pass)")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
+    ap.add_argument("--ranks", default="", help="only these ranks (comma list; profiling one rank's call)")
     ap.add_argument("--base-ms", type=float, default=None,
                     help="1-GPU ms/frame (the efficiency base) when --ns does not include 1")
     args = ap.parse_args()
@@ -55,7 +56,7 @@ def main():
         return
     for n in [int(x) for x in args.ns.split(",")]:
         per_rank = []
-        for r in range(n):
+        for r in ranks_of(args, n):
             band = dict(band_rows=args.band_rows, num_bands=n, band_index=r)
             B = args.batch if args.batch > 0 else n
 
@@ -81,7 +82,7 @@ def main():
             run(16, args.steps)
             ctx.sync()
             per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
-            if args.kernels and r == 0:
+            if args.kernels and len(per_rank) == 1:
                 ctx.set_profiling(True)
                 ctx.reset_stats()
                 run(16 + args.steps, args.steps)
@@ -105,6 +106,10 @@ def main():
     ctx.close()
 
 
+def ranks_of(args, n):
+    return [int(x) for x in args.ranks.split(",")] if args.ranks else list(range(n))
+
+
 def bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out):
     """Band-split BDPT per rank: render the rank's bands, pack its splats rank-major, complete its
     rows from its own chunk (the values do not matter for the timing), accumulate."""
@@ -116,7 +121,7 @@ def bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out):
         per_rank = []
         cr = mdist.splat_chunk_rows(H, args.band_rows, n)
         full = torch.zeros(4 * W * cr * n * B, dtype=torch.float32, device="cuda")
-        for r in range(n):
+        for r in ranks_of(args, n):
             band = dict(band_rows=args.band_rows, num_bands=n, band_index=r, integrator=T.INTEGRATOR_BDPT)
             own = full[r * 4 * W * cr * B:(r + 1) * 4 * W * cr * B]
 
