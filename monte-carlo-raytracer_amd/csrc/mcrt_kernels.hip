@@ -1121,12 +1121,12 @@ hipError_t build_qnodes(const float4* nodes, uint32_t n, float4** qOut, size_t* 
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess && h[1] != 0) e = hipErrorNotSupported;   // a box the bytes cannot bound
-    hipFree(tmp);
-    hipFree(flags);
-    hipFree(off);
-    hipFree(units);
+    (void)hipFree(tmp);
+    (void)hipFree(flags);
+    (void)hipFree(off);
+    (void)hipFree(units);
     if (e != hipSuccess) {
-        if (q) hipFree(q);
+        if (q) (void)hipFree(q);
         return e;
     }
     *qOut = q;

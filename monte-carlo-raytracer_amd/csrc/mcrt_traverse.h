@@ -453,6 +453,12 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
         const float4* p = reinterpret_cast<const float4*>(base + (size_t)(ref >> 1) * 16);
         const float4 a = p[0];
         const uint4 b = *reinterpret_cast<const uint4*>(p + 1);
+        // a leaf's third piece in the same round trip (the leaf bit is in the reference, known
+        // before the fetch): without this the compiler issues it after the branch, a second
+        // dependent fetch on every leaf visit
+        float4 e2 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (ref & 1u) e2 = p[2];
+        asm volatile("" ::"v"(e2.w), "v"(b.w));
         uint32_t next;
         if (!(ref & 1u)) {
             const float sx = qScale(b.w, 0), sy = qScale(b.w, 1), sz = qScale(b.w, 2);
@@ -505,10 +511,12 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
             next = (h0 || h1) ? ((c1first || !h0) ? cr : cl) : POP;
         } else {
             next = POP;
-            const float4 e2 = p[2];
             const uint32_t w = __float_as_uint(e2.w);
-            if (r.mask != __float_as_int(a.w)) {   // RR_RAY_MASK
-                const float4 e1 = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), 0.0f);
+            const float4 e1 = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), 0.0f);
+            // the triangle first: the exact box test (which the 64-B walk runs at the parent) only
+            // matters for a triangle that would count, and most leaf visits miss
+            const float th = r.mask != __float_as_int(a.w) ? triRaw(r, a, e1, e2) : __builtin_inff();   // RR_RAY_MASK
+            if (th <= tc) {
                 bool boxHit;
                 if (w >> 31) {
                     boxHit = parentBoxHit(c, w & 0x7fffffffu, inv, oxi, tc);
@@ -521,7 +529,6 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
                     boxHit = slabHit<OCT>(lo, hi, inv, oxi, tc);
                 }
                 if (boxHit) {
-                    const float th = triRaw(r, a, e1, e2);
                     if (th < t) {
                         if (!ANY && hit >= 0 && th >= t * QTIE_LO) tieT = th;
                         t = th;

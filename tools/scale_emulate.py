@@ -1,4 +1,4 @@
-"""Per-rank work of the N-GPU tile split, emulated on ONE GPU.
+"""Per-rank work of the N-GPU tile split, emulated on ONE GPU, plus the modelled collectives.
 
 For N in --ns, renders K frames of each rank's bands (band_index = r of num_bands = N) one rank
 at a time on cuda:0 and reports the slowest rank's ms/frame next to the 1-GPU ms/frame.  The
@@ -7,6 +7,17 @@ launch gaps of concurrent processes are not in it).  --integrator bdpt: the band
 of each rank (render, rank-major splat pack, gather of its own chunk) and the bytes of the one
 splat reduce-scatter per frame, against the full-frame all-reduce it replaced.  Prints one JSON
 line.
+
+The collectives cannot run here (one GPU; RCCL refuses two ranks on one device), so their time is
+MODELLED from the bytes each rank moves over xGMI: LINK_GBS per direction per link
+(a conservative 50 GB/s, about two thirds of one direction of the ~153 GB/s bidirectional link
+figure of the task brief) and STEP_US of latency per collective step.
+  PT:   ONE gather of every rank's own rows to rank 0 at the end of the job (mcrt.dist.gather_bands_fb):
+        rank 0 receives N - 1 shares over N - 1 links at once -> share / LINK + STEP.
+  BDPT: ONE reduce-scatter of the rank-major splats per call (mcrt.dist.exchange_splats), RCCL rings
+        striped over min(N - 1, 7) links: (N - 1) / N x buffer / (links x LINK) + 2 (N - 1) STEP.  The
+        exchange of a call runs on its frame slot's stream while the next call renders on the other
+        slot, so only the last call's exchange is exposed ("overlapped"); "serial" adds every one.
 """
 import argparse
 import json
@@ -17,6 +28,29 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "monte-carlo-raytracer_amd"))
 sys.path.insert(0, ROOT)
+
+
+LINK_GBS = 50.0   # per direction per xGMI link (model assumption, see the docstring)
+STEP_US = 10.0    # latency per collective step
+
+
+def pt_gather_ms(n, W, H, band_rows, steps):
+    """Modelled end-of-job band gather, ms per frame of the job."""
+    if n == 1:
+        return 0.0
+    from mcrt import dist as mdist
+    share = mdist.splat_chunk_rows(H, band_rows, n) * W * 5 * 4   # packed rows: sum(w L) float4 + sum(w)
+    return (share / (LINK_GBS * 1e9) * 1e3 + STEP_US * 1e-3) / steps
+
+
+def bdpt_exchange_ms(n, W, H, band_rows, batch):
+    """Modelled splat reduce-scatter of one call of `batch` frames (ms)."""
+    if n == 1:
+        return 0.0, 0
+    from mcrt import dist as mdist
+    full = mdist.SPLAT_CHANNELS * 4 * W * mdist.splat_chunk_rows(H, band_rows, n) * batch * n
+    links = min(n - 1, 7)
+    return ((n - 1) / n * full / (links * LINK_GBS * 1e9) * 1e3 + 2 * (n - 1) * STEP_US * 1e-3), full
 
 
 def main():
@@ -98,8 +132,12 @@ def main():
     # --base-ms from a separate N = 1 run (never the smallest N of the sweep, which may be > 1)
     base = out["per_n"][1]["max_ms"] if 1 in out["per_n"] else args.base_ms
     out["base_ms_n1"] = base
+    out["model"] = {"link_gbs_per_direction": LINK_GBS, "step_us": STEP_US}
     for n, v in out["per_n"].items():
         v["compute_eff"] = round(base / (n * v["max_ms"]), 4) if base else None
+        g = pt_gather_ms(n, W, H, args.band_rows, args.steps)
+        v["gather_ms_per_frame_modelled"] = round(g, 5)
+        v["eff_with_collective"] = round(base / (n * (v["max_ms"] + g)), 4) if base else None
     print(json.dumps(out), flush=True)
     fb.close()
     ds.close()
@@ -120,10 +158,11 @@ def bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out):
     for n in [int(x) for x in args.ns.split(",")]:
         per_rank = []
         cr = mdist.splat_chunk_rows(H, args.band_rows, n)
-        full = torch.zeros(4 * W * cr * n * B, dtype=torch.float32, device="cuda")
+        C = mdist.SPLAT_CHANNELS
+        full = torch.zeros(C * W * cr * n * B, dtype=torch.float32, device="cuda")
         for r in ranks_of(args, n):
             band = dict(band_rows=args.band_rows, num_bands=n, band_index=r, integrator=T.INTEGRATOR_BDPT)
-            own = full[r * 4 * W * cr * B:(r + 1) * 4 * W * cr * B]
+            own = full[r * C * W * cr * B:(r + 1) * C * W * cr * B]
 
             def run(f0, count):
                 i = 0
@@ -142,18 +181,25 @@ def bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out):
             run(16 * B, args.steps)
             ctx.sync()
             per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
-        full_bytes = 16 * W * cr * n   # per frame
+        call_ms, call_bytes = bdpt_exchange_ms(n, W, H, args.band_rows, B)
+        calls = -(-args.steps // B)
         out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
                            "min_ms": round(min(per_rank), 4),
-                           "splat_exchange": {"reduce_scatter_in_bytes_per_rank": full_bytes if n > 1 else 0,
-                                              "reduce_scatter_out_bytes_per_rank": full_bytes // n if n > 1 else 0,
-                                              "ring_bytes_per_link": (n - 1) * full_bytes // n if n > 1 else 0,
-                                              "allreduce_ring_bytes_per_link_before": 2 * (n - 1) * 16 * W * H // n
-                                              if n > 1 else 0}}
+                           "splat_exchange": {"reduce_scatter_in_bytes_per_rank_per_frame": call_bytes // B,
+                                              "reduce_scatter_ms_per_call_modelled": round(call_ms, 4),
+                                              "calls": calls,
+                                              "exposed_ms_per_frame_overlapped": round(call_ms / args.steps, 5),
+                                              "exposed_ms_per_frame_serial": round(call_ms * calls / args.steps, 5)}}
     base = out["per_n"][1]["max_ms"] if 1 in out["per_n"] else args.base_ms
     out["base_ms_n1"] = base
+    out["model"] = {"link_gbs_per_direction": LINK_GBS, "step_us": STEP_US, "frames_per_call": B}
     for n, v in out["per_n"].items():
         v["compute_eff"] = round(base / (n * v["max_ms"]), 4) if base else None
+        x = v["splat_exchange"]
+        v["eff_with_collective"] = round(base / (n * (v["max_ms"] + x["exposed_ms_per_frame_overlapped"])), 4) \
+            if base else None
+        v["eff_with_collective_serial"] = round(base / (n * (v["max_ms"] + x["exposed_ms_per_frame_serial"])), 4) \
+            if base else None
     print(json.dumps(out), flush=True)
     fb.close()
     ds.close()
