@@ -434,7 +434,7 @@ def main():
                     help="launch sequences of the untimed per-kernel timing pass (one frame slot)")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     ap.add_argument("--no-bdpt", action="store_true", help="skip the BDPT object (config 4) of the PT run")
-    ap.add_argument("--bdpt-steps", type=int, default=16, help="timed BDPT frames of the BDPT object")
+    ap.add_argument("--bdpt-steps", type=int, default=32, help="timed BDPT frames of the BDPT object")
     ap.add_argument("--bdpt-split", default="band", choices=["frame", "band"],
                     help="multi-GPU BDPT: 8-row bands per rank with one splat reduce-scatter per frame (default: "
                          "the 1-GPU image up to splat summation order; mcrt.dist.exchange_splats) or whole frames "
@@ -458,8 +458,9 @@ def main():
                     help="SAH bins (64 = RTScene::commit's setting; others are host-built A/B trees)")
     ap.add_argument("--perf-tree", action="store_true",
                     help="A/B: the host 3-axis SAH tree (device_build 4) instead of the reference's Bvh2")
-    ap.add_argument("--bdpt-batch", type=int, default=8,
-                    help="BDPT frames per mcrt_render_frames call (the BDPT object and --integrator bdpt)")
+    ap.add_argument("--bdpt-batch", type=int, default=16,
+                    help="BDPT frames per mcrt_render_frames call (the BDPT object and --integrator bdpt; 16: "
+                         "4.62 ms per frame against 4.79 at 8 and 4.74 at 32, profiles/r05/ab/bdpt_batch)")
     ap.add_argument("--batch", type=int, default=0,
                     help="PT frames per mcrt_render_frames call (one launch sequence for all of them); "
                          "0 = auto (32 up to 1080p, 16 above)")
