@@ -119,7 +119,7 @@ def reference_parity(scene_name, tris, fb, ds, cam_of, W, H, D, frame, band):
             "checker_s": round(el, 1)}
 
 
-def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, oracle=None):
+def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, oracle=None, quant=False):
     """HBM roofline of k_shadow_extend (the dominant kernel): the shadow rays of bounce 0 and the
     extension rays for bounce 1 of `batch` frames in one launch.
 
@@ -147,7 +147,15 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
     o.track_touched(False)
     n_nodes = int(((touched[1] | touched[2]) != 0).sum())
     n_ext, n_sh = qcounts[1][0], qcounts[0][0]   # extension rays for bounce 1, shadow rays of bounce 0
-    alg = batch * (n_ext * 48 + n_sh * 80) + 64 * n_nodes
+    if quant:
+        # the extension rays walk the compact records (32 B per internal node, 48 B per leaf), the
+        # bounce-0 shadow rays the 64-B records (wave packets): each distinct record once per format
+        leaf = o.nodes()["addr_left"] == 0xFFFFFFFF   # RR Bvh2 leaf (intersect_bvh2_lds.cl)
+        ext = touched[1] != 0
+        node_bytes = 32 * int((ext & ~leaf).sum()) + 48 * int((ext & leaf).sum()) + 64 * int((touched[2] != 0).sum())
+    else:
+        node_bytes = 64 * n_nodes
+    alg = batch * (n_ext * 48 + n_sh * 80) + node_bytes
     achieved = alg / (avg_ms * 1e-3) / 1e9
     tr = pmc_traffic("k_shadow_extend")
     traffic = None
@@ -157,8 +165,11 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
            "traffic": None if traffic is None else round(traffic),
            "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(avg_ms, 4),
-           "model": ("compulsory bytes per launch: 48 B per extension ray + 80 B per shadow ray + 64 B per "
-                     "DISTINCT BVH node the launch visits (oracle-counted over the launch's frames)"),
+           "model": ("compulsory bytes per launch: 48 B per extension ray + 80 B per shadow ray + each DISTINCT "
+                     "BVH record the launch visits once (oracle-counted over the launch's frames): " +
+                     ("32 B per internal / 48 B per leaf compact record for the extension rays, 64 B per record "
+                      "for the bounce-0 shadow packets" if quant else "64 B per record")),
+           "node_bytes_per_launch": int(node_bytes),
            "distinct_nodes_per_launch": n_nodes, "nodes_total": int(o.num_nodes), "frames_per_launch": batch,
            "rays_per_launch": {"extension": int(batch * n_ext), "shadow": int(batch * n_sh)},
            "node_count_pass_s": round(el, 1)}
@@ -335,7 +346,7 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     return out
 
 
-def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s):
+def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s, quant=False):
     """BDPT's dominant kernel is k_extend (the closest-hit launches over both subpaths' rays, D + 1
     per frame).  Compulsory bytes per frame: 48 B per subpath ray (read o, d; write the hit) + 64 B
     per DISTINCT BVH node the frame's subpath rays visit (counted by the oracle's BDPT on frame 0),
@@ -359,14 +370,22 @@ def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s):
     if ks:
         ms_frame = ks["ms_per_frame"]
         rays = res["rays_per_path"]["subpath"] * W * H
-        alg = rays * 48 + 64 * n_nodes
+        if quant:   # compact records: 32 B per internal node, 48 B per leaf
+            leaf = o.nodes()["addr_left"] == 0xFFFFFFFF
+            ext = touched[1] != 0
+            node_bytes = 32 * int((ext & ~leaf).sum()) + 48 * int((ext & leaf).sum())
+        else:
+            node_bytes = 64 * n_nodes
+        alg = rays * 48 + node_bytes
         ach = alg / (ms_frame * 1e-3) / 1e9
         out["roofline"] = {"bound": "hbm", "kernel": "k_extend (BDPT, D+1 launches per frame)", "achieved": round(ach, 1),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                            "alg_bytes_per_frame": int(alg), "kernel_ms_per_frame": ms_frame,
                            "distinct_nodes_per_frame": n_nodes,
-                           "model": "compulsory bytes per frame: 48 B per subpath ray + 64 B per DISTINCT BVH node the "
-                                    "frame's subpath rays visit (oracle BDPT, frame 0)"}
+                           "model": "compulsory bytes per frame: 48 B per subpath ray + each DISTINCT BVH record the "
+                                    "frame's subpath rays visit once (oracle BDPT, frame 0), " +
+                                    ("32 B per internal / 48 B per leaf compact record" if quant else "64 B per record"),
+                           "node_bytes_per_frame": int(node_bytes)}
         pm = pmc_traffic("k_extend", "pmc_bdpt.json", last_launches=2 * (D + 1))
         if pm and "fetch_raw_last" in pm:
             # the counter run's last two calls (2 x (D + 1) k_extend dispatches, interleaved by the
@@ -534,6 +553,7 @@ def main():
                          force_flat=args.force_flat, bins=args.bvh_bins)
     info = ds.info()
     two_level = ds.layout()["two_level"] == 1
+    quant = info["bytes"] > 64 * info["nodes"]   # compact records built (mcrt_traverse.h traverseQOct)
     log(f"[bench] upload+BVH {time.perf_counter() - t0:.1f}s (build {info['build_ms'] / 1e3:.1f}s, "
         f"{info['nodes']} nodes, {info['bytes'] / 1e6:.0f} MB)")
     fb = lib.FrameBuffer(ctx, W, H)
@@ -742,7 +762,7 @@ def main():
             if oracle_ok and dom == "k_shadow_extend" and not args.no_roofline_model:
                 avg_ms = kstats[dom]["ms"] / max(kstats[dom]["launches"], 1)
                 out["roofline"] = roofline_shadow_extend(scene, cam_of, W, H, D, stats_batch, avg_ms, qcounts, ctx,
-                                                         cpu["_oracle"] if cpu else None)
+                                                         cpu["_oracle"] if cpu else None, quant)
                 if "visits_per_query" in out:
                     hf = hcounts[0] / max(qcounts[0][0], 1) if hcounts else 0.0
                     out["roofline"]["gather_ceiling"] = gather_ceiling(ctx, out["roofline"], out["visits_per_query"],
@@ -751,7 +771,7 @@ def main():
             bdo = {k: v for k, v in bd.items() if not k.startswith("_")}
             if oracle_ok and sampler == T.SAMPLER_RANDOM and not args.no_cpu_baseline:
                 bdo.update(bdpt_roofline_and_cpu(scene, cpu["_oracle"] if cpu else None, cam_of, W, H, D, bdo,
-                                                 args.cpu_seconds))
+                                                 args.cpu_seconds, quant))
             out["bdpt"] = bdo
         print(json.dumps(out), flush=True)
     if bd is not None:
