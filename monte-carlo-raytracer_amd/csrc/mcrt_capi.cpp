@@ -201,6 +201,10 @@ struct mcrt_framebuffer_s {
     int bdptDepth = 0;
     BdptSet bset[MCRT_MAX_FRAMES_IN_FLIGHT];
     hipEvent_t bdptConnect = nullptr;   // recorded after the last enqueued frame's connect launch
+    // diagnostics (MCRT_WAVE_CLOCK=1): per-workgroup (start, end) clocks of the last PT call's camera,
+    // shadow+extension and last shadow launches (mcrt_framebuffer_wave_clock)
+    uint32_t* waveClk[3] = {};
+    size_t waveClkBlocks[3] = {};
     // views of the set of the last BDPT frame (read-back API)
     float4 *camV = nullptr, *lightV = nullptr, *sampLight = nullptr, *slots = nullptr, *splat = nullptr;
     int *camCount = nullptr, *lightCount = nullptr, *bdptCounters = nullptr;
@@ -1205,6 +1209,10 @@ static void slot_free(FrameSlot& k) {
 
 static void fb_free(mcrt_framebuffer fb) {
     for (auto& k : fb->slot) slot_free(k);
+    for (auto& w : fb->waveClk) {
+        if (w) hipFree(w);
+        w = nullptr;
+    }
     void* ptrs[] = {fb->wsum, fb->wts, fb->image, fb->denoised, fb->display, fb->hintPix};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -1455,6 +1463,22 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
 // tools/scale_emulate.py).  Small per-rank band shares are widened by batching frames
 // (mcrt_render_frames) rather than by more slots: 4 slots of 1/8-image frames reach 0.49 ms per
 // frame at N = 8, 2 slots of 16-frame batches 0.25.
+// MCRT_WAVE_CLOCK=1: record per-workgroup clocks of launch `which` (grid of `blocks`) on stream st
+static uint32_t* wave_clock_buf(mcrt_framebuffer fb, int which, size_t blocks, hipStream_t st) {
+    static const bool on = [] { const char* e = std::getenv("MCRT_WAVE_CLOCK"); return e && std::atoi(e) != 0; }();
+    if (!on) return nullptr;
+    if (fb->waveClkBlocks[which] < blocks) {
+        hipStreamSynchronize(st);
+        if (fb->waveClk[which]) hipFree(fb->waveClk[which]);
+        fb->waveClk[which] = nullptr;
+        fb->waveClkBlocks[which] = 0;
+        if (hipMalloc(&fb->waveClk[which], 8 * blocks) != hipSuccess) { hipGetLastError(); return nullptr; }
+        fb->waveClkBlocks[which] = blocks;
+    }
+    hipMemsetAsync(fb->waveClk[which], 0, 8 * fb->waveClkBlocks[which], st);
+    return fb->waveClk[which];
+}
+
 static int frames_in_flight(mcrt_framebuffer fb, const FrameArgs& f) {
     int n = fb->framesInFlight;
     if (n <= 0) n = 2;
@@ -1748,6 +1772,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
         Timed t(ctx, K_PRIMARY, nullptr, (int64_t)bandPaths, st);
         TraceCtx tcp = packet_ctx(s);   // coherent camera rays: wave packets
         tcp.spill = slot.spill;
+        tcp.waveClock = wave_clock_buf(fb, 0, (size_t)f.numTiles * count, st);
         mcrt::launch_primary(tcp, f, dCam, fb->hitsP, st);
     }
     for (int b = 0; b < p->max_depth; ++b) {
@@ -1774,6 +1799,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
             with_hints(tse, s, b == 0 ? fb->hintPix : nullptr, (uint32_t)fb->N);
             if (tse.hint && ctx->countHints) tse.hintHits = fb->counters + 64 + b;
             if (tse.qnodes && ctx->countHints) tse.retraces = fb->counters + 96 + b;
+            if (b == 0) tse.waveClock = wave_clock_buf(fb, 1, 2 * (((size_t)qCap + 63) / 64), st);
             mcrt::launch_shadow_extend(tse, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
                                        fb->sO, fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
         } else {
@@ -1781,6 +1807,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
             TraceCtx tsh = tcs;
             with_hints(tsh, s, b == 0 ? fb->hintPix : nullptr, (uint32_t)fb->N);
             if (tsh.hint && ctx->countHints) tsh.hintHits = fb->counters + 64 + b;
+            tsh.waveClock = wave_clock_buf(fb, 2, ((size_t)qCap + 63) / 64, st);
             mcrt::launch_shadow(tsh, shadowCnt + b, fb->sO, fb->sD, fb->sL, fb->radiance, qCap, st);
         }
     }
@@ -2066,6 +2093,19 @@ MCRT_API mcrt_status mcrt_framebuffer_retrace_counts(mcrt_framebuffer fb, int32_
         const bool live = b + 1 < fb->lastMaxDepth && fb->lastIntegrator == MCRT_INTEGRATOR_PT;
         if (retraces) retraces[b] = live ? c[96 + b] : 0;
     }
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_framebuffer_wave_clock(mcrt_framebuffer fb, int which, uint32_t* host_out, int64_t max_blocks,
+                                                 int64_t* blocks) {
+    if (!fb || which < 0 || which > 2 || !blocks) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "bad args");
+    mcrt_ctx ctx = fb->ctx;
+    *blocks = (int64_t)fb->waveClkBlocks[which];
+    if (!host_out || !fb->waveClk[which]) return MCRT_OK;
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, fb_sync(fb));
+    const size_t n = std::min((size_t)std::max<int64_t>(max_blocks, 0), fb->waveClkBlocks[which]);
+    HIPCHK(ctx, hipMemcpy(host_out, fb->waveClk[which], 8 * n, hipMemcpyDeviceToHost));
     return MCRT_OK;
 }
 

@@ -110,7 +110,9 @@ struct TraceCtx {
     const float4* qnodes;
     uint32_t qroot;
     int* retraces;          // closest-hit walks repeated on the exact records (near ties; NULL: not counted)
+    uint32_t* waveClock;    // diagnostics (MCRT_WAVE_CLOCK=1): per workgroup (start, end) of the 100-MHz clock
 };
+
 #define MCRT_HINT_PIXEL 1
 #define MCRT_HINT_CELL 2
 #define MCRT_HINT_CELL_BITS 25

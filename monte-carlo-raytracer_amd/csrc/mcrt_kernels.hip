@@ -172,8 +172,10 @@ __global__ __launch_bounds__(64) void k_primary_pk(TraceCtx c, FrameArgs f, cons
     r.tmax = 1000.0f;
     r.mask = -1;
     float t;
+    const uint32_t clk0 = c.waveClock ? waveClockNow() : 0u;
     const int tri = traversePacket<false>(c.nodes, r, valid, t);
     if (valid) hitOut[(size_t)k * f.W * f.H + (size_t)y * f.W + x] = closestRecord(c.nodes, r, tri, t);
+    waveClockStore(c.waveClock, clk0);
 }
 
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
@@ -222,12 +224,14 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     r.tmax = o.w;
     r.mask = -1;
     const int pix = __float_as_int(d.w);
+    const uint32_t clk0 = c.waveClock ? waveClockNow() : 0u;
     const float V = shadowOccluded<LAY>(c, r, pix, lds + lane, raySpill(c, blk, lane)) ? 0.0f : 1.0f;
     float4 acc = radiance[pix];
     acc.x += L.x * V;
     acc.y += L.y * V;
     acc.z += L.z * V;
     radiance[pix] = acc;
+    waveClockStore(c.waveClock, clk0);
 }
 
 // Shadow rays of bounce b and extension rays of bounce b+1 in ONE launch: both only depend on
@@ -254,7 +258,9 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.tmax = RT_MAX_TRACE_F;
         r.mask = -1;
         float t;
+        const uint32_t clk0 = c.waveClock ? waveClockNow() : 0u;
         hitOut[i] = traceClosest<LAY>(c, r, lds + lane, raySpill(c, blk, lane), t);
+        waveClockStore(c.waveClock, clk0);
     } else {
         const int ns = *shadowCount;
         const int sb = (ns + 63) >> 6;

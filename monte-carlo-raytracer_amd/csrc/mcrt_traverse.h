@@ -24,6 +24,17 @@ inline K pickLayout(const TraceCtx& c, K twoLevel, K quant, K plain) {
     return c.twoLevel ? twoLevel : c.qnodes ? quant : plain;
 }
 
+// Diagnostics (TraceCtx::waveClock): the wave's (start, end) of the constant 100-MHz clock into
+// clk[2 * block], one store per wave; the end is taken where the wave has left its traversal loop,
+// so it is the wave's, not lane 0's
+MCRT_DEV uint32_t waveClockNow() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+MCRT_DEV void waveClockStore(uint32_t* clk, uint32_t t0) {
+    if (clk && (threadIdx.x & 63) == 0) {
+        clk[2 * blockIdx.x] = t0;
+        clk[2 * blockIdx.x + 1] = waveClockNow();
+    }
+}
+
 struct TraceRay {
     f3 o, d;
     float tmax;

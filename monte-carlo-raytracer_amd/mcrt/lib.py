@@ -83,6 +83,7 @@ SIGNATURES = {
     "mcrt_framebuffer_queue_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.POINTER(_c.c_int32), _c.c_int]),
     "mcrt_framebuffer_hint_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.c_int]),
     "mcrt_framebuffer_retrace_counts": (_c.c_int, [_vp, _c.POINTER(_c.c_int32), _c.c_int]),
+    "mcrt_framebuffer_wave_clock": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_int64, _c.POINTER(_c.c_int64)]),
     "mcrt_postprocess": (_c.c_int, [_vp, _c.POINTER(T.PostprocessParams)]),
     "mcrt_render_aov": (_c.c_int, [_vp, _vp, _vp, _vp, _c.c_int, _vp]),
     "mcrt_framebuffer_read_bdpt": (_c.c_int, [_vp, _c.c_int, _vp, _c.c_uint64, _c.POINTER(_c.c_uint64)]),
@@ -459,6 +460,16 @@ class FrameBuffer:
         h = (_c.c_int32 * max_bounces)()
         _check(lib().mcrt_framebuffer_retrace_counts(self.h, h, max_bounces), self.ctx.h)
         return list(h)
+
+    def wave_clock(self, which):
+        """(blocks, 2) uint32 (start, end) 100-MHz clocks of the last PT call's launch `which` (0 camera,
+        1 shadow + extension, 2 last shadow); needs MCRT_WAVE_CLOCK=1 (diagnostics)."""
+        n = _c.c_int64()
+        _check(lib().mcrt_framebuffer_wave_clock(self.h, which, None, 0, _c.byref(n)), self.ctx.h)
+        out = np.zeros((n.value, 2), np.uint32)
+        if n.value:
+            _check(lib().mcrt_framebuffer_wave_clock(self.h, which, _p(out), n.value, _c.byref(n)), self.ctx.h)
+        return out
 
     def read_queue(self, which):
         """(a, b, c) float4 arrays of the last bounce's shadow (0) / extension (1) queue."""
