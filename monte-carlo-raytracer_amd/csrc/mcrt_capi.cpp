@@ -144,6 +144,12 @@ struct FrameSlot {
     int lastBatch = 1;           // frames of the slot's last render (mcrt_render_frames)
     int frames = 1;              // radiance / primary-hit planes of W*H allocated (batch capacity)
     size_t queueCap = 0;         // entries of each ray-queue buffer
+    // longest-first tile order (FrameArgs::tileOrder): the camera-wave cost of each tile recorded by
+    // this slot's last call, and the order made from it; stream-ordered on the slot's stream
+    uint32_t* tileCost = nullptr;
+    uint32_t* tileOrder = nullptr;
+    int costTiles = 0;           // tiles of the recorded costs (0: none)
+    int tileCap = 0;
 };
 #define SLOT_COUNTER_BYTES (512 + 176 * MCRT_MAX_BATCH_FRAMES + 1536)
 
@@ -1198,7 +1204,7 @@ static void fb_free_bdpt(mcrt_framebuffer fb) {
 static void slot_free(FrameSlot& k) {
     if (k.stream) hipStreamSynchronize(k.stream);
     void* ptrs[] = {k.radiance, k.hitsP, k.hitsE, k.eO[0], k.eO[1], k.eD[0], k.eD[1], k.eT[0], k.eT[1],
-                    k.sO,       k.sD,    k.sL,    k.counters, k.spill};
+                    k.sO,       k.sD,    k.sL,    k.counters, k.spill, k.tileCost, k.tileOrder};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (k.done) hipEventDestroy(k.done);
@@ -1441,6 +1447,8 @@ static bool frame_args(mcrt_framebuffer fb, const mcrt_frame_params* p, FrameArg
     f.primaryPack = 1;
     f.shadePack = 1;
     f.batch = 1;
+    f.tileOrder = nullptr;   // set per call by render_frames (longest-first)
+    f.tileCost = nullptr;
     f.numBands = p->num_bands <= 0 ? 1 : p->num_bands;
     f.bandIndex = p->band_index;
     f.bandRows = f.numBands == 1 ? 8 : p->band_rows;
@@ -1477,6 +1485,13 @@ static uint32_t* wave_clock_buf(mcrt_framebuffer fb, int which, size_t blocks, h
     }
     hipMemsetAsync(fb->waveClk[which], 0, 8 * fb->waveClkBlocks[which], st);
     return fb->waveClk[which];
+}
+
+#define MCRT_LPT_SHADE_MAX_PATHS 16000000
+// MCRT_LONGEST_FIRST=0: camera / first-shading tiles in plain tile order (A/B)
+static bool longest_first() {
+    static const bool on = [] { const char* e = std::getenv("MCRT_LONGEST_FIRST"); return !(e && std::atoi(e) == 0); }();
+    return on;
 }
 
 static int frames_in_flight(mcrt_framebuffer fb, const FrameArgs& f) {
@@ -1768,6 +1783,27 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     TraceCtx tcs = trace_ctx(s);
     tcs.spill = slot.spill;
     const int qCap = bandPaths;
+    if (longest_first()) {
+        // the camera / first-shading tiles in descending cost of this slot's previous call (same
+        // tiles), and this call's costs recorded for the next one -- all on the slot's stream
+        if (slot.tileCap < f.numTiles) {
+            HIPCHK(ctx, hipStreamSynchronize(st));
+            if (slot.tileCost) hipFree(slot.tileCost);
+            if (slot.tileOrder) hipFree(slot.tileOrder);
+            slot.tileCost = slot.tileOrder = nullptr;
+            slot.tileCap = slot.costTiles = 0;
+            HIPCHK(ctx, hipMalloc(&slot.tileCost, 4 * (size_t)f.numTiles));
+            HIPCHK(ctx, hipMalloc(&slot.tileOrder, 4 * (size_t)f.numTiles));
+            slot.tileCap = f.numTiles;
+        }
+        if (slot.costTiles == f.numTiles) {
+            mcrt::launch_tile_order(slot.tileCost, f.numTiles, slot.tileOrder, st);
+            f.tileOrder = slot.tileOrder;
+        }
+        HIPCHK(ctx, hipMemsetAsync(slot.tileCost, 0, 4 * (size_t)f.numTiles, st));
+        f.tileCost = slot.tileCost;
+        slot.costTiles = f.numTiles;
+    }
     {
         Timed t(ctx, K_PRIMARY, nullptr, (int64_t)bandPaths, st);
         TraceCtx tcp = packet_ctx(s);   // coherent camera rays: wave packets
@@ -1783,7 +1819,13 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
         q.eOout = fb->eO[b & 1]; q.eDout = fb->eD[b & 1]; q.eTout = fb->eT[b & 1];
         if (b == 0) {
             Timed t(ctx, K_SHADE0, nullptr, (int64_t)bandPaths, st);
-            mcrt::launch_shade0(sa, f, dCam, fb->hitsP, fb->radiance, q, st);
+            // the longest-first order also for the first shading (its extension queue then starts with
+            // the expensive tiles' rays) only for small launches: at a rank's share of N >= 4 GPUs it
+            // trims the extension launch's tail, on a whole 1080p image it costs the shading's
+            // spatial locality (+2.8 % k_shade0, +1.2 % k_shadow_extend; profiles/r05/ab/longest_first)
+            FrameArgs fs = f;
+            if ((int64_t)bandPaths > MCRT_LPT_SHADE_MAX_PATHS) fs.tileOrder = nullptr;
+            mcrt::launch_shade0(sa, fs, dCam, fb->hitsP, fb->radiance, q, st);
         } else {
             Timed t(ctx, K_SHADEN, extCnt + b - 1, 0, st);
             mcrt::launch_shadeN(sa, f, b, extCnt + b - 1, fb->eO[(b - 1) & 1], fb->eD[(b - 1) & 1],

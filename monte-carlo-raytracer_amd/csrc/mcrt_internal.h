@@ -42,6 +42,11 @@ struct FrameArgs {
     int tileMajor;          // launch order of (tile, frame k): 1 = a tile's frames adjacent, 0 = frame-major
     int primaryPack;        // camera launch: 1 = a wave holds a few pixels x all batch frames
     int shadePack;          // first shading launch: the same packing (its ray queues inherit the order)
+    // Longest-first tile order of the camera and first-shading launches (NULL: tile order): slot j
+    // of the launch takes tile tileOrder[j]; tileCost (NULL: not recorded) accumulates each tile's
+    // camera-wave time for the next call's order (mcrt_kernels.hip k_tile_order)
+    const uint32_t* tileOrder;
+    uint32_t* tileCost;
 };
 #define MCRT_MAX_BATCH_FRAMES 32
 // the reconstruction filter of each frame of a batch (device layout, KRN/kernel_data.h:63-80);
@@ -161,6 +166,8 @@ void launch_tonemap(int n, float Lwhite, const float4* in, float4* out, hipStrea
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st);
 // parent index of each triangle leaf into its record's word 13 (flat trees, finish_accel)
 void launch_leaf_parents(float4* nodes, uint32_t n, hipStream_t st);
+// order[0..n) = tiles by descending cost[tile] (bucketed; one workgroup)
+void launch_tile_order(const uint32_t* cost, int n, uint32_t* order, hipStream_t st);
 // compact records of a flat DFS tree (after launch_leaf_parents): *qOut (16-B units, caller frees),
 // *units its size; hipErrorNotSupported when the tree is not in DFS order (left child = i + 1)
 hipError_t build_qnodes(const float4* nodes, uint32_t n, float4** qOut, size_t* units, hipStream_t st);

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
 __global__ __launch_bounds__(64) void k_primary_pk(TraceCtx c, FrameArgs f, const mcrt_camera* __restrict__ camp,
                                                    float4* __restrict__ hitOut) {
     const int lane = threadIdx.x;
-    const int tileAll = xcdRemap(blockIdx.x, gridDim.x);
+    const int tileAll = orderedTileAll(f, xcdRemap(blockIdx.x, gridDim.x));
     int k, tile, pi = lane;
     if (f.primaryPack && f.batch > 1) {
         packedPath(f, tileAll, lane, k, tile, pi);
@@ -172,10 +172,12 @@ __global__ __launch_bounds__(64) void k_primary_pk(TraceCtx c, FrameArgs f, cons
     r.tmax = 1000.0f;
     r.mask = -1;
     float t;
-    const uint32_t clk0 = c.waveClock ? waveClockNow() : 0u;
+    const uint32_t clk0 = (c.waveClock || f.tileCost) ? waveClockNow() : 0u;
     const int tri = traversePacket<false>(c.nodes, r, valid, t);
     if (valid) hitOut[(size_t)k * f.W * f.H + (size_t)y * f.W + x] = closestRecord(c.nodes, r, tri, t);
     waveClockStore(c.waveClock, clk0);
+    // the wave's time into its tile's cost (the next call's longest-first order): one atomic per wave
+    if (f.tileCost && lane == 0 && tile < f.numTiles) atomicAdd(&f.tileCost[tile], waveClockNow() - clk0);
 }
 
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
@@ -513,7 +515,7 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
     const int lane = threadIdx.x & 63;
     // XCD-aware block order: an XCD shades contiguous runs of tiles (their hits share surface
     // records, materials and textures in its L2): k_shade0 -4 %
-    const int tileAll = xcdRemap(blockIdx.x, gridDim.x) * (SHADE0_BLOCK / 64) + (int)(threadIdx.x >> 6);
+    const int tileAll = orderedTileAll(f, xcdRemap(blockIdx.x, gridDim.x) * (SHADE0_BLOCK / 64) + (int)(threadIdx.x >> 6));
     int k, tile, pi = lane;   // batch frame k
     if (f.shadePack && f.batch > 1) {
         // as k_primary's packed waves; the bounce-0 shadow rays of a wave (one light direction,
@@ -965,6 +967,31 @@ __global__ __launch_bounds__(256) void k_qnodes_convert(const float4* __restrict
     dst[2] = make_float4(n2.x, n2.y, n2.z, __uint_as_float(i | (slow ? 0x80000000u : 0u)));
 }
 
+// Longest-first order of the camera / first-shading tiles from the previous call's camera-wave
+// times (FrameArgs::tileCost): tiles bucketed by log2 cost in 1/8 steps, buckets in descending
+// order (one workgroup; a tile's place inside its bucket is arbitrary -- any order gives the same
+// image).  The long waves then start first and the launch ends on short ones: at N = 8 a rank's
+// camera launch spent its last 90 us (12 %) on the 1 % longest waves (tools/wave_tail.py).
+__global__ __launch_bounds__(1024) void k_tile_order(const uint32_t* __restrict__ cost, int n,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[256];
+    for (int b = threadIdx.x; b < 256; b += 1024) hist[b] = 0;
+    __syncthreads();
+    auto bucket = [](uint32_t c) { return c == 0 ? 0 : min(255, (int)(__log2f((float)c) * 8.0f)); };
+    for (int t = threadIdx.x; t < n; t += 1024) atomicAdd(&hist[bucket(cost[t])], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {   // exclusive offsets, heaviest bucket first
+        uint32_t acc = 0;
+        for (int b = 255; b >= 0; --b) {
+            const uint32_t h = hist[b];
+            hist[b] = acc;
+            acc += h;
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < n; t += 1024) order[atomicAdd(&hist[bucket(cost[t])], 1u)] = (uint32_t)t;
+}
+
 // Attainable-bandwidth probe (mcrt_ctx_stream_copy): a persistent grid (8 workgroups per CU)
 // strides over the array; each lane keeps 4 independent 16-B nontemporal loads in flight.
 __global__ __launch_bounds__(256) void k_stream_copy(const f4* __restrict__ src, f4* __restrict__ dst, size_t n) {
@@ -1138,6 +1165,10 @@ hipError_t build_qnodes(const float4* nodes, uint32_t n, float4** qOut, size_t* 
     *qOut = q;
     *unitsOut = total;
     return hipSuccess;
+}
+
+void launch_tile_order(const uint32_t* cost, int n, uint32_t* order, hipStream_t st) {
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, cost, n, order);
 }
 
 void launch_stream_copy(const float4* src, float4* dst, size_t n4, int numCUs, hipStream_t st) {

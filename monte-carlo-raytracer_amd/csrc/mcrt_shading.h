@@ -16,6 +16,14 @@ MCRT_DEV bool tilePixel(const FrameArgs& f, int tile, int lane, int& x, int& y) 
     return x < (int)f.W && y < (int)f.H;
 }
 
+// Longest-first order (FrameArgs::tileOrder): the launch's tile slot j runs tile tileOrder[j], the
+// batch frames of a tile staying adjacent.  Any order gives the same paths (keyed by pixel, frame).
+MCRT_DEV int orderedTileAll(const FrameArgs& f, int tileAll) {
+    if (!f.tileOrder) return tileAll;
+    const int slot = tileAll / f.batch, part = tileAll - slot * f.batch;
+    return slot < f.numTiles ? (int)f.tileOrder[slot] * f.batch + part : tileAll;
+}
+
 // Launch index of the batched camera / first-bounce launches -> (batch frame k, 8x8 tile).
 MCRT_DEV void splitTileFrame(const FrameArgs& f, int tileAll, int& k, int& tile) {
     if (f.tileMajor) {
