@@ -251,7 +251,7 @@ def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
 
 
 def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing, split="band",
-                 batch=8):
+                 batch=8, sparse=True):
     """Config 4's integrator on the same scene and GPU(s): BDPT (RTBDPTPass::update), 1 spp per
     step, split over the ranks by frames (rank r renders frames r, r + N, ...; light-tracing splats
     land anywhere in the image) or by 8-row bands (one splat reduce-scatter per frame,
@@ -266,7 +266,11 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     filt = T.make_filter(T.BOX)
     first = [True]
     band = split == "band" and world > 1
-    if band:   # rank-major splats (chunks of this rank count x 8-row blocks x batch frames) + own chunk
+    xstats = [0, 0, 0]   # sparse exchange: calls, records sent, records received (this rank)
+    if band and sparse:   # the few splats into other ranks' rows as records, one all-to-all per call
+        fb.set_splat_exchange(True)
+        sbufs = mdist.SparseSplatBuffers("cuda")
+    elif band:   # rank-major splats (chunks of this rank count x 8-row blocks x batch frames) + own chunk
         cr = mdist.splat_chunk_rows(H, 8, world)   # uninitialised: mcrt_bdpt_splats_copy zeroes on its stream
         splat_full = torch.empty(mdist.SPLAT_CHANNELS * W * cr * batch * world, dtype=torch.float32, device="cuda")
         splat_own = torch.empty(mdist.SPLAT_CHANNELS * W * cr * batch, dtype=torch.float32, device="cuda")
@@ -284,7 +288,12 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
             cams = [cam_of(f + j) for j in range(k)]
             bands = dict(band_rows=8, num_bands=world, band_index=rank) if band else {}
             fb.render_frames(ds, cams, frame=f, max_depth=D, sampler=sampler, integrator=T.INTEGRATOR_BDPT, **bands)
-            if band:
+            if band and sparse:
+                sent, got = mdist.exchange_splats_sparse(fb, sbufs)
+                xstats[0] += 1
+                xstats[1] += sent
+                xstats[2] += got
+            elif band:
                 mdist.exchange_splats(fb, splat_full, splat_own)
             fb.accumulate_frames([filt] * k, 0 if first[0] else f)
             first[0] = False
@@ -323,7 +332,8 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
            "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong" if split == "band" else "weak",
            "workload": f"same scene {W}x{H}, BDPT, maxDepth {D}, 1 spp per step (SURVEY config 4's integrator), "
                        f"{batch} frames per mcrt_render_frames call, "
-                       + (f"band split x {world} + 1 splat reduce-scatter per call + 1 RCCL reduce" if band else
+                       + (f"band split x {world} + 1 sparse splat all-to-all per call + 1 RCCL reduce" if band and sparse
+                          else f"band split x {world} + 1 splat reduce-scatter per call + 1 RCCL reduce" if band else
                           f"frame split x {world} + 1 RCCL reduce" if world > 1 else "1 GPU"),
            "rays_per_path": {"subpath": round(st["closest_rays"] / (W * H * last[0]), 4),
                              "connection": round(st["any_rays"] / (W * H * last[0]), 4)}}
@@ -342,6 +352,11 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
                               "ms_per_frame": round(v["ms"] / kb, 4)} for k, v in ks.items()}
         out["kernels_note"] = f"one frame slot, one call of {kb} frames (per-kernel HIP events)"
     out["frames_per_call"] = batch
+    if band and sparse and xstats[0]:
+        out["splat_exchange"] = {"kind": "sparse all-to-all of (target, rgb) records, 16 B each",
+                                 "records_sent_per_frame_rank0": round(xstats[1] / (xstats[0] * batch), 1),
+                                 "bytes_sent_per_frame_rank0": round(16 * xstats[1] / (xstats[0] * batch)),
+                                 "dense_bytes_per_frame_per_rank": 12 * W * H}
     out["_fb"] = fb
     return out
 
@@ -458,6 +473,9 @@ def main():
                     help="multi-GPU BDPT: 8-row bands per rank with one splat reduce-scatter per frame (default: "
                          "the 1-GPU image up to splat summation order; mcrt.dist.exchange_splats) or whole frames "
                          "per rank (no per-frame exchange; each rank's sampled-light history differs, BDPT.cl:585)")
+    ap.add_argument("--splat-exchange", default="sparse", choices=["sparse", "dense"],
+                    help="band-split BDPT: the splats landing in other ranks' rows as records with one all-to-all "
+                         "(sparse), or the rank-major full-frame buffers with one reduce-scatter (dense)")
     ap.add_argument("--save-image", default=None, help="rank 0 saves the final accumulated image (.npy)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the product path); gloo only rehearses N ranks on one GPU")
@@ -560,6 +578,10 @@ def main():
     filt = T.make_filter(T.BOX)
     bdpt = args.integrator == "bdpt"
     band_bdpt = bdpt and args.bdpt_split == "band" and world > 1
+    sparse_x = band_bdpt and args.splat_exchange == "sparse"
+    if sparse_x:
+        fb.set_splat_exchange(True)
+        sbufs = mdist.SparseSplatBuffers("cuda")
     if band_bdpt:   # band split: every rank renders every frame's rows of its bands
         band = dict(band_rows=8, num_bands=world, band_index=rank, integrator=T.INTEGRATOR_BDPT)
         cr = mdist.splat_chunk_rows(H, 8, world)   # uninitialised: mcrt_bdpt_splats_copy zeroes on its stream
@@ -588,7 +610,9 @@ def main():
             fb.render(ds, cam_of(frame), frame=frame, **kw)
         else:
             fb.render_frames(ds, [cam_of(frame + k) for k in range(n)], frame=frame, **kw)
-        if band_bdpt:   # one splat exchange per call (all its frames)
+        if sparse_x:   # one splat exchange per call (all its frames)
+            mdist.exchange_splats_sparse(fb, sbufs)
+        elif band_bdpt:
             mdist.exchange_splats(fb, splat_full, splat_own)
         fb.accumulate(filt, 0 if first[0] else frame)   # 0: the first accumulation overwrites
         first[0] = False
@@ -683,7 +707,7 @@ def main():
     bd = None
     if not bdpt and not args.no_bdpt and not two_level:   # config 4's integrator beside the PT headline
         bd = bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, args.bdpt_steps, args.warmup,
-                          not args.no_kernel_timing, args.bdpt_split, args.bdpt_batch)
+                          not args.no_kernel_timing, args.bdpt_split, args.bdpt_batch, args.splat_exchange == "sparse")
 
     paths = W * H * args.steps * (world if bdpt and not band_bdpt else 1)
     value = paths / elapsed / 1e6
@@ -702,7 +726,8 @@ def main():
                            "device LBVH" if args.device_build else
                            "RadeonRays-identical SAH, " + ("host build" if args.host_build else "device build")),
                    "bvh_build_ms": round(info["build_ms"], 1),
-                   "parallelism": (f"band split x {world}, 1 splat reduce-scatter per frame + 1 RCCL reduce" if band_bdpt
+                   "parallelism": (f"band split x {world}, 1 sparse splat all-to-all per call + 1 RCCL reduce" if sparse_x
+                                   else f"band split x {world}, 1 splat reduce-scatter per call + 1 RCCL reduce" if band_bdpt
                                    else f"frame split x {world} + 1 RCCL reduce" if bdpt else
                                    f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL "
                                    + ("band gather" if args.end_collective == "gather" else "reduce")),

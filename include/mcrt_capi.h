@@ -559,6 +559,26 @@ MCRT_API mcrt_status mcrt_bdpt_splat_layout(mcrt_framebuffer fb, uint64_t* chunk
 MCRT_API mcrt_status mcrt_framebuffer_stream(mcrt_framebuffer fb, void** stream);
 MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst);
 MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_own_chunk);
+/* Sparse splat exchange (the band split's alternative to the dense rank-major buffer above): only a
+ * few per cent of a rank's paths splat into another rank's rows (San-Miguel proxy: ~2.6 %), so the
+ * ranks exchange those splats as records -- 4 floats: the target path index (k * W*H + pixel, int
+ * bits), r, g, b -- with one all-to-all instead of reducing whole frames:
+ *   mcrt_framebuffer_set_splat_exchange  MCRT_SPLAT_EXCHANGE_SPARSE before rendering (DENSE: default);
+ *                            k_bdpt_vis then adds the rank's own-row splats in place and lists the rest;
+ *   mcrt_bdpt_splats_sparse  counts[r] = records for rank r (counts[band_index] = 0), SYNCHRONOUS up to
+ *                            the frame's visibility pass (the sizes are host data for the all-to-all);
+ *                            when d_dst holds capacity >= sum(counts) records of device memory it also
+ *                            groups the records by rank into it, enqueued on the frame's stream (else
+ *                            counts only: grow the buffer and call again);
+ *   mcrt_bdpt_gather_sparse  adds the `records` received records (targets in this rank's rows) and
+ *                            completes the rank's bands, on the frame's stream.
+ * The frame equals the dense exchange's (and one GPU's) up to the order of the splat sums. */
+#define MCRT_SPLAT_EXCHANGE_DENSE 0
+#define MCRT_SPLAT_EXCHANGE_SPARSE 1
+MCRT_API mcrt_status mcrt_framebuffer_set_splat_exchange(mcrt_framebuffer fb, int32_t mode);
+MCRT_API mcrt_status mcrt_bdpt_splats_sparse(mcrt_framebuffer fb, void* d_dst, int64_t capacity, int64_t* counts,
+                                             int32_t num_counts);
+MCRT_API mcrt_status mcrt_bdpt_gather_sparse(mcrt_framebuffer fb, const void* d_recv, int64_t records);
 MCRT_API mcrt_status mcrt_framebuffer_read_bdpt(mcrt_framebuffer fb, int which, void* host_dst, uint64_t bytes,
                                                 uint64_t* needed);
 

@@ -978,7 +978,16 @@ __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const i
             if (occluded) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         } else if (!occluded) {
             const float4 L = sL[i];
-            float* dst = reinterpret_cast<float*>(&b.splat[~code]);
+            const int target = ~code;
+            if (b.splatList) {   // band split, sparse exchange: another rank's row -> the list
+                const int y = (target % b.splatN0) / b.splatW;
+                if (((y >> 3) / b.splatBpb) % b.splatBands != b.splatBand) {
+                    const int slot = atomicAdd(b.splatListCount, 1);   // at most D per path: never full
+                    if (slot < b.splatListCap) b.splatList[slot] = make_float4(__int_as_float(target), L.x, L.y, L.z);
+                    continue;
+                }
+            }
+            float* dst = reinterpret_cast<float*>(&b.splat[target]);
             atomicAdd(dst + 0, L.x);
             atomicAdd(dst + 1, L.y);
             atomicAdd(dst + 2, L.z);
@@ -1041,6 +1050,36 @@ __global__ __launch_bounds__(256) void k_bdpt_splat_pack(int W, int H, int batch
     o[0] = v.x;
     o[1] = v.y;
     o[2] = v.z;
+}
+
+// Sparse splat exchange (band split): the list's records per owner rank, then grouped by owner
+// (any order inside a group: the owner adds them with float atomics, like the reference's splats)
+__global__ __launch_bounds__(256) void k_splat_hist(BdptArgs b, int* __restrict__ hist) {
+    const int n = min(*b.splatListCount, b.splatListCap);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int y = (__float_as_int(b.splatList[i].x) % b.splatN0) / b.splatW;
+        atomicAdd(&hist[((y >> 3) / b.splatBpb) % b.splatBands], 1);
+    }
+}
+__global__ __launch_bounds__(256) void k_splat_group(BdptArgs b, mcrt::SplatOffsets off, int* __restrict__ cursor,
+                                                     float4* __restrict__ dst) {
+    const int n = min(*b.splatListCount, b.splatListCap);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const float4 r = b.splatList[i];
+        const int y = (__float_as_int(r.x) % b.splatN0) / b.splatW;
+        const int o = ((y >> 3) / b.splatBpb) % b.splatBands;
+        dst[off.off[o] + atomicAdd(&cursor[o], 1)] = r;
+    }
+}
+// received records (targets in this rank's rows) into its splat plane
+__global__ __launch_bounds__(256) void k_splat_unpack(const float4* __restrict__ recv, int n, float4* __restrict__ splat) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float4 r = recv[i];
+    float* d = reinterpret_cast<float*>(&splat[__float_as_int(r.x)]);
+    atomicAdd(d + 0, r.y);
+    atomicAdd(d + 1, r.z);
+    atomicAdd(d + 2, r.w);
 }
 
 // Splats that land outside the rank's bands (multi-GPU band split): added by the rank that owns
@@ -1110,6 +1149,15 @@ void launch_bdpt_splat_pack(const FrameArgs& f, size_t chunkPixels, const float4
     const size_t n = (size_t)f.W * f.H * f.batch;
     hipLaunchKernelGGL(k_bdpt_splat_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (int)f.W, (int)f.H,
                        f.batch, f.bandRows >> 3, f.numBands, chunkPixels, splat, out);
+}
+void launch_splat_hist(const BdptArgs& b, int* hist, hipStream_t st) {
+    hipLaunchKernelGGL(k_splat_hist, dim3(1024), dim3(256), 0, st, b, hist);
+}
+void launch_splat_group(const BdptArgs& b, SplatOffsets off, int* cursor, float4* dst, hipStream_t st) {
+    hipLaunchKernelGGL(k_splat_group, dim3(1024), dim3(256), 0, st, b, off, cursor, dst);
+}
+void launch_splat_unpack(const float4* recv, int n, float4* splat, hipStream_t st) {
+    if (n > 0) hipLaunchKernelGGL(k_splat_unpack, dim3((n + 255) / 256), dim3(256), 0, st, recv, n, splat);
 }
 void launch_bdpt_clear_splat(int n, float4* splat, hipStream_t st) {
     hipLaunchKernelGGL(k_bdpt_clear_splat, dim3((n + 255) / 256), dim3(256), 0, st, n, splat);

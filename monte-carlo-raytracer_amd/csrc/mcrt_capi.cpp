@@ -173,6 +173,11 @@ struct BdptSet {
     // wrote for every path of the band
     size_t constStride = 0;
     int constBand[3] = {0, 0, -1};
+    // band split, sparse splat exchange: the splats landing in other ranks' rows (BdptArgs::splatList)
+    // and 128 ints of grouping scratch (per-owner counts, cursors)
+    float4* splatList = nullptr;
+    size_t splatListCap = 0;
+    int* splatAux = nullptr;
 };   // [0..127] ints: counters; cameras (176 B each, <= MCRT_MAX_BATCH_FRAMES) from byte 512
 
 struct mcrt_framebuffer_s {
@@ -220,11 +225,13 @@ struct mcrt_framebuffer_s {
     int bdptBatch = 1;           // frames of the last BDPT call (plane stride N x bdptBatch)
     bool bdptOneSet = false;     // a second BDPT set did not fit in HBM: BDPT frames use slot 0 only
     bool bdptPendingGather = false;   // band-split BDPT frame waiting for the ranks' summed splats
+    int splatExchange = MCRT_SPLAT_EXCHANGE_DENSE;   // mcrt_framebuffer_set_splat_exchange
+    int bdptSet = 0;             // the BDPT set of the last BDPT call
 };
 
 // BDPT queue counters (64 ints per frame set): [d] the subpath-ray queue of depth d (d <= 33;
 // at depth 0 the light rays only), then these
-enum { BDPT_CNT_CONN = 40, BDPT_CNT_CAM0 = 41 };
+enum { BDPT_CNT_CONN = 40, BDPT_CNT_CAM0 = 41, BDPT_CNT_SPLATS = 42 };
 static int bdpt_max_connections(int D) { const int t = D + 2; return t * (t + 1) / 2 - 2; }   // RTBDPTPass.cpp:404-408
 
 // ---------------------------------------------------------------------------
@@ -1184,7 +1191,8 @@ MCRT_API mcrt_status mcrt_event_destroy(mcrt_event ev) {
 static void bset_free(BdptSet& b) {
     void* ptrs[] = {b.camV,   b.lightV, b.slots,  b.splat,  b.camCount, b.lightCount, b.bdptCounters,
                     b.bqO[0], b.bqO[1], b.bqD[0], b.bqD[1], b.bqT[0], b.bqT[1], b.bHits, b.cO, b.cD, b.cL, b.spill,
-                    b.lkey, b.lkey2, b.lslot, b.lperm, b.ekey, b.ekey2, b.eslot, b.eperm, b.sortTmp};
+                    b.lkey, b.lkey2, b.lslot, b.lperm, b.ekey, b.ekey2, b.eslot, b.eperm, b.sortTmp,
+                    b.splatList, b.splatAux};
     for (void* p : ptrs)
         if (p) hipFree(p);
     b = BdptSet();
@@ -1332,6 +1340,7 @@ static hipError_t bset_alloc(BdptSet& b, size_t N, size_t NQ, int D, int frames,
 // The fb's BDPT views show set k (the last BDPT frame).
 static void fb_bind_bdpt(mcrt_framebuffer fb, int k) {
     const BdptSet& b = fb->bset[k];
+    fb->bdptSet = k;
     fb->camV = b.camV; fb->lightV = b.lightV; fb->slots = b.slots; fb->splat = b.splat;
     fb->camCount = b.camCount; fb->lightCount = b.lightCount; fb->bdptCounters = b.bdptCounters;
     for (int i = 0; i < 2; ++i) { fb->bqO[i] = b.bqO[i]; fb->bqD[i] = b.bqD[i]; fb->bqT[i] = b.bqT[i]; }
@@ -1541,7 +1550,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     TraceCtx tcs = trace_ctx(s);
     tcs.spill = bs.spill;
     const SceneArgs sa = scene_args(s);
-    BdptArgs b;
+    BdptArgs b{};
     b.camV = fb->camV;
     b.lightV = fb->lightV;
     b.camCount = fb->camCount;
@@ -1591,8 +1600,31 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         return q;
     };
     const bool bandSplit = f.numBands > 1;
-    if (bandSplit)   // splats of this rank's light paths land in any pixel: clear the whole buffer
+    const bool sparse = bandSplit && fb->splatExchange == MCRT_SPLAT_EXCHANGE_SPARSE;
+    if (sparse) {
+        // the splats landing in other ranks' rows go to a list (at most D per path: t = 1, s = 2..D+1);
+        // the rank's own rows are zeroed by k_bdpt_start, the other rows of its plane stay unused
+        const size_t cap = (size_t)D * (size_t)bandQ;
+        if (bs.splatListCap < cap || !bs.splatAux) {
+            HIPCHK(ctx, hipStreamSynchronize(st));
+            if (bs.splatList) hipFree(bs.splatList);
+            bs.splatList = nullptr;
+            bs.splatListCap = 0;
+            HIPCHK(ctx, hipMalloc(&bs.splatList, 16 * cap));
+            bs.splatListCap = cap;
+            if (!bs.splatAux) HIPCHK(ctx, hipMalloc(&bs.splatAux, 128 * sizeof(int)));
+        }
+        b.splatList = bs.splatList;
+        b.splatListCount = cnt + BDPT_CNT_SPLATS;
+        b.splatListCap = (int)std::min(cap, (size_t)INT32_MAX);
+        b.splatW = (int)f.W;
+        b.splatN0 = (int)(f.W * f.H);
+        b.splatBpb = f.bandRows / 8;
+        b.splatBands = f.numBands;
+        b.splatBand = f.bandIndex;
+    } else if (bandSplit) {   // splats of this rank's light paths land in any pixel: clear the whole buffer
         mcrt::launch_bdpt_clear_splat((int)N, fb->splat, st);
+    }
     // depth 0: camera rays (coherent, 8x8 tiles in order) in the first half of queue 0's buffers
     // with their own count, light rays in the second half with count [0]; ONE launch traces both,
     // the camera rays as wave packets like PT's camera rays (packet_ctx); both
@@ -2197,9 +2229,85 @@ MCRT_API mcrt_status mcrt_bdpt_splat_layout(mcrt_framebuffer fb, uint64_t* chunk
     return MCRT_OK;
 }
 
+MCRT_API mcrt_status mcrt_framebuffer_set_splat_exchange(mcrt_framebuffer fb, int32_t mode) {
+    if (!fb || (mode != MCRT_SPLAT_EXCHANGE_DENSE && mode != MCRT_SPLAT_EXCHANGE_SPARSE))
+        return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "unknown splat exchange mode");
+    if (fb->bdptPendingGather) return fail(fb->ctx, MCRT_ERROR_NOT_READY, "band-split BDPT frame not completed");
+    fb->splatExchange = mode;
+    return MCRT_OK;
+}
+
+MCRT_API mcrt_status mcrt_bdpt_splats_sparse(mcrt_framebuffer fb, void* d_dst, int64_t capacity, int64_t* counts,
+                                             int32_t num_counts) {
+    if (!fb || !counts) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    mcrt_ctx ctx = fb->ctx;
+    const int bands = fb->bands.numBands;
+    if (num_counts < bands) return fail(ctx, MCRT_ERROR_INVALID_ARG, "counts must hold num_bands entries");
+    for (int r = 0; r < num_counts; ++r) counts[r] = 0;
+    if (!fb->bdptPendingGather) return MCRT_OK;   // nothing pending (light-less scene): no splats
+    if (fb->splatExchange != MCRT_SPLAT_EXCHANGE_SPARSE)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame rendered with the dense splat exchange (mcrt_bdpt_splats_copy)");
+    if (bands > 64) return fail(ctx, MCRT_ERROR_INVALID_ARG, "sparse splat exchange: at most 64 bands");
+    hipSetDevice(ctx->device);
+    BdptSet& bs = fb->bset[fb->bdptSet];
+    hipStream_t st = fb->slot[fb->cur].stream;
+    BdptArgs b{};
+    b.splatList = bs.splatList;
+    b.splatListCount = fb->bdptCounters + BDPT_CNT_SPLATS;
+    b.splatListCap = (int)std::min(bs.splatListCap, (size_t)INT32_MAX);
+    b.splatW = (int)fb->bands.W;
+    b.splatN0 = (int)(fb->bands.W * fb->bands.H);
+    b.splatBpb = fb->bands.bandRows / 8;
+    b.splatBands = bands;
+    b.splatBand = fb->bands.bandIndex;
+    int h[64];
+    HIPCHK(ctx, hipMemsetAsync(bs.splatAux, 0, 128 * sizeof(int), st));
+    mcrt::launch_splat_hist(b, bs.splatAux, st);
+    HIPCHK(ctx, hipMemcpyAsync(h, bs.splatAux, sizeof(int) * bands, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));   // the sizes go to the host (an all-to-all's split sizes)
+    mcrt::SplatOffsets off{};
+    int64_t total = 0;
+    for (int r = 0; r < bands; ++r) {
+        off.off[r] = (int)total;
+        counts[r] = h[r];
+        total += h[r];
+    }
+    if (!d_dst || capacity < total) return MCRT_OK;   // sizes only (the caller grows its buffer and calls again)
+    mcrt::launch_splat_group(b, off, bs.splatAux + 64, (float4*)d_dst, st);
+    HIPCHK(ctx, hipGetLastError());
+    return MCRT_OK;   // grouping enqueued on the frame's stream
+}
+
+MCRT_API mcrt_status mcrt_bdpt_gather_sparse(mcrt_framebuffer fb, const void* d_recv, int64_t records) {
+    if (!fb || (records > 0 && !d_recv)) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
+    mcrt_ctx ctx = fb->ctx;
+    if (!fb->bdptPendingGather) return MCRT_OK;
+    if (fb->splatExchange != MCRT_SPLAT_EXCHANGE_SPARSE)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame rendered with the dense splat exchange (mcrt_bdpt_gather)");
+    if (records < 0 || records > INT32_MAX) return fail(ctx, MCRT_ERROR_INVALID_ARG, "bad record count");
+    hipSetDevice(ctx->device);
+    FrameSlot& slot = fb->slot[fb->cur];
+    hipStream_t st = slot.stream;
+    mcrt::launch_splat_unpack((const float4*)d_recv, (int)records, fb->splat, st);
+    BdptArgs b{};
+    b.slots = fb->slots;
+    b.splat = fb->splat;
+    b.ownSlots = bdpt_max_connections(fb->bdptDepth) - fb->bdptDepth;
+    {
+        Timed t(ctx, K_BDPT_GATHER, nullptr, (int64_t)fb->bands.numTiles * 64 * fb->bands.batch, st);
+        mcrt::launch_bdpt_gather(fb->bands, b, fb->radiance, nullptr, 0, st);   // the rank's own plane
+    }
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(slot.done, st));
+    fb->bdptPendingGather = false;
+    return MCRT_OK;
+}
+
 MCRT_API mcrt_status mcrt_bdpt_splats_copy(mcrt_framebuffer fb, void* d_dst) {
     if (!fb || !d_dst) return fail(fb ? fb->ctx : nullptr, MCRT_ERROR_INVALID_ARG, "NULL argument");
     mcrt_ctx ctx = fb->ctx;
+    if (fb->bdptPendingGather && fb->splatExchange == MCRT_SPLAT_EXCHANGE_SPARSE)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame rendered with the sparse splat exchange (mcrt_bdpt_splats_sparse)");
     if (!fb->haveBands) return fail(ctx, MCRT_ERROR_NOT_READY, "no frame rendered yet");
     hipSetDevice(ctx->device);
     const size_t chunk = splat_chunk_pixels(fb->bands);   // per frame; a rank's chunk holds batch of them
@@ -2227,6 +2335,8 @@ MCRT_API mcrt_status mcrt_bdpt_gather(mcrt_framebuffer fb, const void* d_own_chu
     if (!fb) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "fb is NULL");
     mcrt_ctx ctx = fb->ctx;
     if (!fb->bdptPendingGather) return MCRT_OK;   // nothing deferred (whole-image or light-less frame)
+    if (fb->splatExchange == MCRT_SPLAT_EXCHANGE_SPARSE)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame rendered with the sparse splat exchange (mcrt_bdpt_gather_sparse)");
     hipSetDevice(ctx->device);
     FrameSlot& slot = fb->slot[fb->cur];
     hipStream_t st = slot.stream;

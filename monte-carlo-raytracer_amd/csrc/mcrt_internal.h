@@ -79,6 +79,13 @@ struct BdptArgs {
     uint32_t* extKey;    // per slot of a bounce queue that will be traced: the ray's direction octant and
     uint32_t* extSlot;   //   origin cell (NULL: no sort), and its slot
     float keyLo[3], keyScale[3];   // origin cell = (o - keyLo) * keyScale, 32 x 8 x 32 cells
+    // Band split, sparse splat exchange (NULL list: the dense rank-major exchange): light-tracing
+    // splats landing in another rank's rows are appended here as (target path index bits, r, g, b);
+    // the rank's own land in `splat`.  Owner of pixel row y: ((y / 8) / bpb) % bands.
+    float4* splatList;
+    int* splatListCount;
+    int splatListCap;
+    int splatW, splatN0, splatBpb, splatBands, splatBand;
 };
 struct BdptQueue {
     int* count;
@@ -186,6 +193,12 @@ void launch_bdpt_gather(const FrameArgs& f, const BdptArgs& b, float4* radiance,
                         size_t chunkPixels, hipStream_t st);
 void launch_bdpt_splat_pack(const FrameArgs& f, size_t chunkPixels, const float4* splat, float* out, hipStream_t st);
 void launch_bdpt_clear_splat(int n, float4* splat, hipStream_t st);
+// sparse splat exchange: per-owner counts of the list (hist[bands], zeroed by the caller), the list
+// grouped by owner into dst at off[owner] (cursor[bands] zeroed), received records added to splat
+void launch_splat_hist(const BdptArgs& b, int* hist, hipStream_t st);
+struct SplatOffsets { int off[64]; };
+void launch_splat_group(const BdptArgs& b, SplatOffsets off, int* cursor, float4* dst, hipStream_t st);
+void launch_splat_unpack(const float4* recv, int n, float4* splat, hipStream_t st);
 }  // namespace mcrt
 
 // Device BVH builder (mcrt_gpubuild.hip): linear BVH in the mcrt_bvh.cpp record format

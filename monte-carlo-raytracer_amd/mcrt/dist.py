@@ -128,6 +128,67 @@ def exchange_splats(fb, full, chunk, group=None):
     fb.bdpt_gather(chunk.data_ptr())
 
 
+class SparseSplatBuffers:
+    """Growable device buffers of exchange_splats_sparse (send and receive records, 4 floats each)."""
+
+    def __init__(self, device="cuda"):
+        self.device = device
+        self.bufs = {}
+
+    def get(self, name, records):
+        import torch
+        b = self.bufs.get(name)
+        if b is None or b.numel() < 4 * records:
+            b = torch.empty(4 * max(records + records // 4, 1024), dtype=torch.float32, device=self.device)
+            self.bufs[name] = b
+        return b
+
+
+def exchange_splats_sparse(fb, bufs, group=None):
+    """Band-split BDPT with the sparse splat exchange (mcrt_framebuffer_set_splat_exchange): each rank
+    lists the few light-tracing splats that land in other ranks' rows (~2.6 % of its paths on the
+    San-Miguel proxy, against a dense exchange of every pixel), ONE all-to-all of the per-rank counts
+    and ONE all-to-all of the records (RCCL on the frame's stream) deliver them to the rows' owners,
+    and mcrt_bdpt_gather_sparse adds them and completes the rank's bands.  The same frame as the
+    dense exchange up to the order of the splat sums.  The counts are host data (the all-to-all's split
+    sizes), so this waits for the frame's visibility pass."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    send = bufs.get("send", 0)
+    counts = fb.bdpt_splats_sparse(send.data_ptr(), send.numel() // 4)
+    total = int(counts.sum())
+    if total > send.numel() // 4:   # grow and group again
+        send = bufs.get("send", total)
+        counts = fb.bdpt_splats_sparse(send.data_ptr(), send.numel() // 4)
+    if len(counts) != world:
+        raise ValueError("the frame's band count differs from the group's size")
+    nccl = send.is_cuda and dist.get_backend(group) != "gloo"
+    sc = torch.as_tensor(counts, dtype=torch.int64, device=send.device if nccl else "cpu")
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    rcounts = rc.cpu().tolist()
+    rtotal = int(sum(rcounts))
+    recv = bufs.get("recv", rtotal)
+    ins, outs = [4 * int(c) for c in counts], [4 * int(c) for c in rcounts]
+    if nccl:
+        s = torch.cuda.ExternalStream(fb.stream(), device=send.device)
+        with torch.cuda.stream(s):
+            dist.all_to_all_single(recv[:4 * rtotal], send[:4 * total], output_split_sizes=outs, input_split_sizes=ins,
+                                   group=group)
+    else:   # gloo (CPU tests, one-GPU rehearsal): through the host
+        if send.is_cuda:
+            torch.cuda.synchronize(send.device)
+        hs = send[:4 * total].cpu()
+        hr = torch.empty(4 * rtotal, dtype=torch.float32)
+        dist.all_to_all_single(hr, hs, output_split_sizes=outs, input_split_sizes=ins, group=group)
+        recv[:4 * rtotal].copy_(hr)
+        if recv.is_cuda:
+            torch.cuda.current_stream(recv.device).synchronize()
+    fb.bdpt_gather_sparse(recv.data_ptr(), rtotal)
+    return total, rtotal
+
+
 def frame_split(num_frames, world, rank):
     """Frame split (BDPT, whose light-tracing splats land anywhere in the image): rank r renders
     whole frames r, r + N, r + 2N, ... of the sequence 0 .. num_frames-1."""

@@ -48,6 +48,9 @@ SIGNATURES = {
     "mcrt_bdpt_splat_layout": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_int32)]),
     "mcrt_framebuffer_stream": (_c.c_int, [_vp, _c.POINTER(_vp)]),
     "mcrt_bdpt_gather": (_c.c_int, [_vp, _vp]),
+    "mcrt_framebuffer_set_splat_exchange": (_c.c_int, [_vp, _c.c_int32]),
+    "mcrt_bdpt_splats_sparse": (_c.c_int, [_vp, _vp, _c.c_int64, _c.POINTER(_c.c_int64), _c.c_int32]),
+    "mcrt_bdpt_gather_sparse": (_c.c_int, [_vp, _vp, _c.c_int64]),
     "mcrt_obj_load": (_c.c_int, [_c.c_char_p, _c.c_uint32, _vp]),
     "mcrt_obj_add_directional_light": (_c.c_int, [_vp, _vp, _vp]),
     "mcrt_obj_add_point_light": (_c.c_int, [_vp, _vp, _vp]),
@@ -418,6 +421,28 @@ class FrameBuffer:
         """Completes a band-split BDPT frame with this rank's chunk of the summed splats (None:
         the rank's own splats)."""
         _check(lib().mcrt_bdpt_gather(self.h, own_chunk_ptr), self.ctx.h)
+
+    def set_splat_exchange(self, sparse):
+        """Band-split BDPT: the sparse (record lists, one all-to-all) or the dense (rank-major
+        planes, one reduce-scatter) splat exchange for the frames rendered from now on."""
+        _check(lib().mcrt_framebuffer_set_splat_exchange(self.h, 1 if sparse else 0), self.ctx.h)
+
+    def bdpt_splats_sparse(self, dst_ptr=None, capacity=0):
+        """Sparse exchange: per-rank record counts of this rank's splats into other ranks' rows
+        (waits for the frame's visibility pass); with dst_ptr also groups the records (4 floats
+        each) by rank into device memory on the frame's stream.  Returns an int64 array."""
+        n = self.bands_count()
+        counts = (_c.c_int64 * n)()
+        _check(lib().mcrt_bdpt_splats_sparse(self.h, dst_ptr, capacity, counts, n), self.ctx.h)
+        return np.array(counts, np.int64)
+
+    def bdpt_gather_sparse(self, recv_ptr, records):
+        """Sparse exchange: adds the received records and completes the rank's bands."""
+        _check(lib().mcrt_bdpt_gather_sparse(self.h, recv_ptr, int(records)), self.ctx.h)
+
+    def bands_count(self):
+        """Bands (ranks) of the last frame's split."""
+        return int(self.band_layout()[1])
 
     def set_accumulation(self, wsum_ptr, wts_ptr):
         _check(lib().mcrt_framebuffer_set_accumulation(self.h, wsum_ptr, wts_ptr), self.ctx.h)

@@ -310,3 +310,75 @@ def test_rank_major_splat_layout(height, band_rows, world):
         assert (packed[r, len(rows):] == 0).all()
         seen[rows] += 1
     assert (seen == 1).all()
+
+
+class _FakeSparseFB:
+    """The splat-list side of a band-split BDPT frame (mcrt_bdpt_splats_sparse / gather_sparse) on
+    the CPU: random splat records of this rank, each owned by the rank whose 8-row bands hold its
+    target row; gather_sparse keeps what arrives."""
+
+    def __init__(self, height, width, world, rank, n, seed):
+        rng = np.random.default_rng(seed + rank)
+        self.H, self.W, self.world, self.rank = height, width, world, rank
+        owner = np.zeros(height, np.int64)
+        for r in range(world):
+            owner[mdist.band_rows_of(height, 8, world, r)] = r
+        tgt = rng.integers(0, height * width, n).astype(np.int32)
+        keep = owner[tgt // width] != rank   # the rank's own splats stay in place (not listed)
+        self.rec = np.zeros((int(keep.sum()), 4), np.float32)
+        self.rec[:, 0] = tgt[keep].view(np.float32)
+        self.rec[:, 1:] = rng.random((int(keep.sum()), 3), dtype=np.float32)
+        self.owner = owner
+        self.got = None
+
+    def bdpt_splats_sparse(self, dst_ptr=None, capacity=0):
+        dest = self.owner[self.rec[:, 0].view(np.int32) // self.W]
+        order = np.argsort(dest, kind="stable")
+        counts = np.bincount(dest, minlength=self.world).astype(np.int64)
+        if dst_ptr is not None and capacity >= counts.sum():
+            _BUFS[dst_ptr][:4 * len(order)] = torch.from_numpy(self.rec[order].ravel())
+        return counts
+
+    def stream(self):
+        return 0
+
+    def bdpt_gather_sparse(self, recv_ptr, records):
+        self.got = _BUFS[recv_ptr][:4 * records].numpy().reshape(-1, 4).copy()
+
+
+class _CpuSparseBuffers(mdist.SparseSplatBuffers):
+    def get(self, name, records):
+        b = super().get(name, records)
+        _BUFS[b.data_ptr()] = b
+        return b
+
+
+def _sparse_worker(rank, world, port, out_path, height, width, n):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fb = _FakeSparseFB(height, width, world, rank, n, seed=5)
+    sent, got = mdist.exchange_splats_sparse(fb, _CpuSparseBuffers("cpu"))
+    np.savez(out_path + f".{rank}.npz", got=fb.got, sent=sent, recvd=got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,height", [(2, 40), (3, 64), (4, 1080 // 8)])
+def test_sparse_splat_exchange_routes_records(tmp_path, world, height):
+    """mcrt.dist.exchange_splats_sparse (the band split's sparse splat exchange) over gloo: one
+    all-to-all of the counts, one of the records; every record arrives exactly once, at the rank
+    whose bands hold its target row."""
+    width, n = 24, 300
+    out = str(tmp_path / "sp")
+    mp.start_processes(_sparse_worker, args=(world, _free_port(), out, height, width, n), nprocs=world, join=True,
+                       start_method="spawn")
+    fbs = [_FakeSparseFB(height, width, world, r, n, seed=5) for r in range(world)]
+    got = [np.load(out + f".{r}.npz") for r in range(world)]
+    for q in range(world):
+        want = np.concatenate([fb.rec[fb.owner[fb.rec[:, 0].view(np.int32) // width] == q] for fb in fbs])
+        g = got[q]["got"]
+        assert int(got[q]["recvd"]) == len(want) == len(g)
+        key = lambda a: a[np.lexsort(a.view(np.int32).T[::-1])]   # noqa: E731
+        assert np.array_equal(key(g).view(np.uint32), key(want).view(np.uint32))
+    assert sum(int(z["sent"]) for z in got) == sum(len(fb.rec) for fb in fbs)

@@ -373,3 +373,66 @@ def test_bdpt_batched_band_split(hip_ctx):
     for fb in fbs:
         fb.close()
     ds.close()
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_bdpt_band_split_sparse_exchange(hip_ctx, ranks):
+    """The sparse splat exchange (mcrt_framebuffer_set_splat_exchange, mcrt.dist.exchange_splats_sparse)
+    emulated on one GPU: rank r lists the splats landing in other ranks' rows, the lists are routed
+    to the rows' owners as an all-to-all would (here in Python), and every rank adds what it receives
+    (mcrt_bdpt_gather_sparse).  Every frame's radiance within the splat tolerance of whole frames;
+    the records are few (the dense exchange moves every pixel), each lands in its receiver's rows."""
+    import torch
+    from mcrt import lib
+    from mcrt import dist as mdist
+    name, W, H, D, frames = "mixed", 96, 64, 2, 4
+    ds = lib.DeviceScene(hip_ctx, build_scene(name))
+    cam = scene_camera(name, W, H)
+    filt = T.make_filter(T.BOX)
+    full = lib.FrameBuffer(hip_ctx, W, H)
+    fbs = [lib.FrameBuffer(hip_ctx, W, H) for _ in range(ranks)]
+    for fb in fbs:
+        fb.set_splat_exchange(True)
+    rows = [mdist.band_rows_of(H, 8, ranks, r) for r in range(ranks)]
+    owner = np.zeros(H, np.int64)
+    for r in range(ranks):
+        owner[rows[r]] = r
+    sent_total = 0
+    for f in range(frames):
+        full.render(ds, cam, frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT)
+        full.accumulate(filt, f)
+        lists = []
+        for r, fb in enumerate(fbs):
+            fb.render(ds, cam, frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT, band_rows=8, num_bands=ranks,
+                      band_index=r)
+            with pytest.raises(lib.MCRTError):   # the dense calls refuse a sparse frame
+                fb.bdpt_gather(None)
+            counts = fb.bdpt_splats_sparse()   # sizes only
+            buf = torch.zeros(4 * max(int(counts.sum()), 1), dtype=torch.float32, device="cuda")
+            again = fb.bdpt_splats_sparse(buf.data_ptr(), buf.numel() // 4)
+            np.testing.assert_array_equal(again, counts)
+            assert counts[r] == 0
+            torch.cuda.synchronize()
+            hip_ctx.sync()
+            rec = buf.cpu().numpy()[:4 * int(counts.sum())].reshape(-1, 4)
+            seg = np.repeat(np.arange(ranks), counts)   # grouped by receiving rank, in rank order
+            tgt = rec[:, 0].view(np.int32)
+            assert (owner[tgt // W] == seg).all()
+            lists.append((rec, seg))
+            sent_total += int(counts.sum())
+        for q, fb in enumerate(fbs):
+            mine = np.concatenate([rec[seg == q] for rec, seg in lists])
+            recv = torch.from_numpy(np.ascontiguousarray(mine, np.float32).ravel() if len(mine) else
+                                    np.zeros(4, np.float32)).cuda()
+            torch.cuda.synchronize()
+            fb.bdpt_gather_sparse(recv.data_ptr(), len(mine))
+            fb.accumulate(filt, f)
+        ref = full.read(0)
+        for r, fb in enumerate(fbs):
+            a, b = fb.read(0)[rows[r], :, :3], ref[rows[r], :, :3]
+            close = np.abs(a - b) <= REL_TOL * (np.abs(a) + np.abs(b)) + 1e-30
+            assert close.all(), (ranks, f, r, int((~close).sum()))
+    assert 0 < sent_total < frames * W * H   # few records against a dense exchange of every pixel
+    for fb in fbs + [full]:
+        fb.close()
+    ds.close()

@@ -75,6 +75,21 @@ def test_rccl_band_gather_and_splat_exchange(hip_ctx, nccl_one_rank):
             np.testing.assert_allclose(fb.read(1), plain.read(1), rtol=4e-6, atol=1e-30)
         plain.close()
         fb.close()
+    # the sparse splat exchange's two all-to-alls over RCCL (counts, then records on the frame's stream)
+    plain = lib.FrameBuffer(hip_ctx, W, H)
+    fb = lib.FrameBuffer(hip_ctx, W, H)
+    fb.set_splat_exchange(True)
+    sbufs = mdist.SparseSplatBuffers("cuda")
+    for f in range(frames):
+        plain.render(ds, cam, frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT)
+        plain.accumulate(filt, f)
+        fb.render(ds, cam, frame=f, max_depth=D, integrator=T.INTEGRATOR_BDPT, band_rows=8, num_bands=1, band_index=0)
+        mdist.exchange_splats_sparse(fb, sbufs)
+        fb.accumulate(filt, f)
+    hip_ctx.sync()
+    np.testing.assert_allclose(fb.read(2), plain.read(2), rtol=4e-6, atol=1e-30)
+    plain.close()
+    fb.close()
     # one more collective on the same group: the timing reduction bench.py ends with
     t = torch.tensor([1.5], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -103,6 +118,18 @@ def test_bench_gpus_flag_launches_ranks(tmp_path):
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2, (one, two)
     assert "x 2" in two["config"]["parallelism"]
     np.testing.assert_array_equal(img2.view(np.uint32), img1.view(np.uint32))
+
+
+@pytest.mark.timeout(600)
+def test_bench_bdpt_sparse_exchange_two_ranks(tmp_path):
+    """`bench.py --integrator bdpt --gpus 2 --dist-backend gloo`: the band split with the sparse splat
+    exchange (mcrt.dist.exchange_splats_sparse through gloo all-to-alls) against one rank: the same
+    accumulated image up to the order of the splat sums."""
+    extra = ("--integrator", "bdpt", "--bdpt-batch", "4")
+    one, img1 = _bench(tmp_path, 1, "b1", extra)
+    two, img2 = _bench(tmp_path, 2, "b2", extra + ("--dist-backend", "gloo"))
+    assert two["n_gpus"] == 2 and "sparse" in two["config"]["parallelism"], two["config"]
+    np.testing.assert_allclose(img2, img1, rtol=2e-5, atol=1e-30)
 
 
 def test_bench_nccl_needs_one_gpu_per_rank(tmp_path):

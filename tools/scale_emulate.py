@@ -53,6 +53,17 @@ def bdpt_exchange_ms(n, W, H, band_rows, batch):
     return ((n - 1) / n * full / (links * LINK_GBS * 1e9) * 1e3 + 2 * (n - 1) * STEP_US * 1e-3), full
 
 
+def sparse_exchange_ms(n, rec, batch):
+    """Modelled sparse splat exchange of one call (ms): an all-to-all of the counts, then one of the
+    16-B records; each rank sends to N - 1 receivers over N - 1 links at once, so the largest
+    per-receiver share bounds it.  The measured rank time already holds the host wait for the counts."""
+    if n == 1 or rec["calls"] == 0:
+        return 0.0, 0
+    per_call = rec["records"] / rec["calls"] * 16
+    biggest = rec["to_rank_max"] * 16
+    return (biggest / (LINK_GBS * 1e9) * 1e3 + 2 * STEP_US * 1e-3), int(per_call / batch)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ns", default="1,2,4,8")
@@ -66,6 +77,8 @@ def main():
     ap.add_argument("--kernels", action="store_true",
                     help="also report rank 0's per-kernel HIP-event ms per frame (a separate profiled pass)")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
+    ap.add_argument("--splat-exchange", default="sparse", choices=["sparse", "dense"],
+                    help="band-split BDPT: record lists + all-to-all (sparse) or rank-major planes + reduce-scatter")
     ap.add_argument("--ranks", default="", help="only these ranks (comma list; profiling one rank's call)")
     ap.add_argument("--base-ms", type=float, default=None,
                     help="1-GPU ms/frame (the efficiency base) when --ns does not include 1")
@@ -155,22 +168,39 @@ def bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out):
     from mcrt import dist as mdist
     from mcrt import types as T
     B = max(args.batch, 1)   # BDPT frames per mcrt_render_frames call
+    sparse = args.splat_exchange == "sparse"
+    fb.set_splat_exchange(sparse)
     for n in [int(x) for x in args.ns.split(",")]:
         per_rank = []
         cr = mdist.splat_chunk_rows(H, args.band_rows, n)
         C = mdist.SPLAT_CHANNELS
-        full = torch.zeros(C * W * cr * n * B, dtype=torch.float32, device="cuda")
+        full = None if sparse else torch.zeros(C * W * cr * n * B, dtype=torch.float32, device="cuda")
+        sbufs = mdist.SparseSplatBuffers("cuda")
+        rec = {"records": 0, "to_rank_max": 0, "calls": 0}   # sparse: records each rank sends per call
         for r in ranks_of(args, n):
             band = dict(band_rows=args.band_rows, num_bands=n, band_index=r, integrator=T.INTEGRATOR_BDPT)
-            own = full[r * C * W * cr * B:(r + 1) * C * W * cr * B]
+            own = None if sparse else full[r * C * W * cr * B:(r + 1) * C * W * cr * B]
 
-            def run(f0, count):
+            def run(f0, count, timed=False):
                 i = 0
                 while i < count:
                     k = min(B, count - i)
                     fb.render_frames(ds, [cams[(f0 + i + j) % 64] for j in range(k)], frame=f0 + i, max_depth=2,
                                      **band)
-                    if n > 1:
+                    if n > 1 and sparse:
+                        # the rank's records grouped by receiver (their host counts: the all-to-all's
+                        # split sizes); the receive side is the model's: its own splats are in place
+                        send = sbufs.get("send", 0)
+                        cnt = fb.bdpt_splats_sparse(send.data_ptr(), send.numel() // 4)
+                        if cnt.sum() > send.numel() // 4:
+                            send = sbufs.get("send", int(cnt.sum()))
+                            cnt = fb.bdpt_splats_sparse(send.data_ptr(), send.numel() // 4)
+                        fb.bdpt_gather_sparse(0, 0)
+                        if timed:
+                            rec["records"] += int(cnt.sum())
+                            rec["to_rank_max"] = max(rec["to_rank_max"], int(cnt.max()))
+                            rec["calls"] += 1
+                    elif n > 1:
                         fb.bdpt_splats_copy(full.data_ptr())
                         fb.bdpt_gather(own.data_ptr())
                     fb.accumulate_frames([filt] * k, f0 + i)
@@ -178,15 +208,19 @@ def bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out):
             run(0, 3 * B)
             ctx.sync()
             t0 = time.perf_counter()
-            run(16 * B, args.steps)
+            run(16 * B, args.steps, timed=True)
             ctx.sync()
             per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
-        call_ms, call_bytes = bdpt_exchange_ms(n, W, H, args.band_rows, B)
+        if sparse:
+            call_ms, call_bytes = sparse_exchange_ms(n, rec, B)
+        else:
+            call_ms, call_bytes = bdpt_exchange_ms(n, W, H, args.band_rows, B)
         calls = -(-args.steps // B)
         out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
                            "min_ms": round(min(per_rank), 4),
-                           "splat_exchange": {"reduce_scatter_in_bytes_per_rank_per_frame": call_bytes // B,
-                                              "reduce_scatter_ms_per_call_modelled": round(call_ms, 4),
+                           "splat_exchange": {"kind": "sparse all-to-all" if sparse else "dense reduce-scatter",
+                                              "bytes_per_rank_per_frame": call_bytes if sparse else call_bytes // B,
+                                              "ms_per_call_modelled": round(call_ms, 4),
                                               "calls": calls,
                                               "exposed_ms_per_frame_overlapped": round(call_ms / args.steps, 5),
                                               "exposed_ms_per_frame_serial": round(call_ms * calls / args.steps, 5)}}
@@ -196,8 +230,11 @@ def bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out):
     for n, v in out["per_n"].items():
         v["compute_eff"] = round(base / (n * v["max_ms"]), 4) if base else None
         x = v["splat_exchange"]
-        v["eff_with_collective"] = round(base / (n * (v["max_ms"] + x["exposed_ms_per_frame_overlapped"])), 4) \
-            if base else None
+        # sparse: the host waits for each call's counts, so every call's exchange is exposed (its host
+        # wait is already in max_ms, the RCCL part is modelled); dense: all but the last call's overlap
+        # the next call's render on the other frame slot
+        exposed = x["exposed_ms_per_frame_serial"] if sparse else x["exposed_ms_per_frame_overlapped"]
+        v["eff_with_collective"] = round(base / (n * (v["max_ms"] + exposed)), 4) if base else None
         v["eff_with_collective_serial"] = round(base / (n * (v["max_ms"] + x["exposed_ms_per_frame_serial"])), 4) \
             if base else None
     print(json.dumps(out), flush=True)
