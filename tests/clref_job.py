@@ -199,6 +199,13 @@ SCALE_CASES = {
     ],
 }
 BDPT_VERTEX_STRIDE = 17   # vertex records kept for every 17th pixel (the full arrays are ~0.5 GB at 960x540)
+# cases whose FULL vertex arrays are also written (raw .npy beside the job's npz, ~3.5 GB at 1080p), so
+# every pixel's vertices are compared: config 4's integrator at the bench's size
+FULL_VERTEX_CASES = ("sm_bdpt_1080p",)
+
+
+def full_vertex_path(out_path, key, which):
+    return f"{out_path}.{key}_{which}.npy"
 
 
 def bdpt_vertex_sel(W, H):
@@ -242,8 +249,12 @@ def scale_job(out_path, variant):
             N = W * H
             sel = bdpt_vertex_sel(W, H)
             for which, depths in (("camera_vertices", D + 2), ("light_vertices", D + 1)):
-                v = cs.read_bdpt(which).view(po.REF_VERTEX_DTYPE).reshape(N, depths)
+                raw = cs.read_bdpt(which)
+                v = raw.view(po.REF_VERTEX_DTYPE).reshape(N, depths)
                 res[f"{key}_{which}"] = np.ascontiguousarray(v[sel])
+                if key in FULL_VERTEX_CASES:
+                    np.save(full_vertex_path(out_path, key, which), raw)
+                del raw, v
             for which in ("camera_counts", "light_counts"):
                 res[f"{key}_{which}"] = cs.read_bdpt(which).view(np.int32)
         print(f"{key}: {len(frames)} frames in {time.time() - t0:.1f}s", flush=True)
