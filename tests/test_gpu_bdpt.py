@@ -357,11 +357,11 @@ def test_bdpt_batched_band_split(hip_ctx):
         fb.render_frames(ds, cams, frame=0, max_depth=D, integrator=T.INTEGRATOR_BDPT, band_rows=8,
                          num_bands=ranks, band_index=r)
         assert fb.bdpt_splat_layout() == (cr * W * B, ranks)
-        bufs.append(torch.zeros(4 * W * cr * B * ranks, dtype=torch.float32, device="cuda"))
+        bufs.append(torch.zeros(mdist.SPLAT_CHANNELS * W * cr * B * ranks, dtype=torch.float32, device="cuda"))
         fb.bdpt_splats_copy(bufs[r].data_ptr())
     torch.cuda.synchronize()
     total = bufs[0] + bufs[1]
-    per = 4 * W * cr * B
+    per = mdist.SPLAT_CHANNELS * W * cr * B
     for r, fb in enumerate(fbs):
         chunk = total[r * per:(r + 1) * per].clone()
         torch.cuda.synchronize()
