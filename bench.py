@@ -251,7 +251,7 @@ def pmc_traffic(kernel, summary="pmc_latest.json", last_launches=0):
 
 
 def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, kernel_timing, split="band",
-                 batch=8, sparse=True):
+                 batch=8, sparse=False):
     """Config 4's integrator on the same scene and GPU(s): BDPT (RTBDPTPass::update), 1 spp per
     step, split over the ranks by frames (rank r renders frames r, r + N, ...; light-tracing splats
     land anywhere in the image) or by 8-row bands (one splat reduce-scatter per frame,
@@ -473,9 +473,11 @@ def main():
                     help="multi-GPU BDPT: 8-row bands per rank with one splat reduce-scatter per frame (default: "
                          "the 1-GPU image up to splat summation order; mcrt.dist.exchange_splats) or whole frames "
                          "per rank (no per-frame exchange; each rank's sampled-light history differs, BDPT.cl:585)")
-    ap.add_argument("--splat-exchange", default="sparse", choices=["sparse", "dense"],
-                    help="band-split BDPT: the splats landing in other ranks' rows as records with one all-to-all "
-                         "(sparse), or the rank-major full-frame buffers with one reduce-scatter (dense)")
+    ap.add_argument("--splat-exchange", default="dense", choices=["sparse", "dense"],
+                    help="band-split BDPT: the rank-major full-frame buffers with one stream-ordered reduce-scatter "
+                         "(dense, default: the exchange overlaps the next call), or the splats landing in other "
+                         "ranks' rows as records with one all-to-all (sparse: 100x fewer bytes, but its host-side "
+                         "split sizes stop the calls overlapping -- 13 %% slower per rank, profiles/r05/ab/splat_exchange)")
     ap.add_argument("--save-image", default=None, help="rank 0 saves the final accumulated image (.npy)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the product path); gloo only rehearses N ranks on one GPU")

@@ -974,6 +974,8 @@ __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const i
         // light-tracing rays toward the camera leave one cell nearly parallel
         const bool occluded = shadowOccluded<LAY>(c, r, 0, lds + lane, raySpill(c, blockIdx.x, lane));
         const int code = __float_as_int(d.w);
+        bool listIt = false;
+        float4 rec = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (code >= 0) {
             if (occluded) b.slots[code] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         } else if (!occluded) {
@@ -981,16 +983,24 @@ __global__ __launch_bounds__(64) void k_bdpt_vis(TraceCtx c, BdptArgs b, const i
             const int target = ~code;
             if (b.splatList) {   // band split, sparse exchange: another rank's row -> the list
                 const int y = (target % b.splatN0) / b.splatW;
-                if (((y >> 3) / b.splatBpb) % b.splatBands != b.splatBand) {
-                    const int slot = atomicAdd(b.splatListCount, 1);   // at most D per path: never full
-                    if (slot < b.splatListCap) b.splatList[slot] = make_float4(__int_as_float(target), L.x, L.y, L.z);
-                    continue;
-                }
+                listIt = ((y >> 3) / b.splatBpb) % b.splatBands != b.splatBand;
+                rec = make_float4(__int_as_float(target), L.x, L.y, L.z);
             }
-            float* dst = reinterpret_cast<float*>(&b.splat[target]);
-            atomicAdd(dst + 0, L.x);
-            atomicAdd(dst + 1, L.y);
-            atomicAdd(dst + 2, L.z);
+            if (!listIt) {
+                float* dst = reinterpret_cast<float*>(&b.splat[target]);
+                atomicAdd(dst + 0, L.x);
+                atomicAdd(dst + 1, L.y);
+                atomicAdd(dst + 2, L.z);
+            }
+        }
+        // the list's entries: ONE atomic per wave (a per-lane append on one counter serialises in L2)
+        const uint64_t m = __ballot(listIt);
+        if (m) {
+            const int leader = __builtin_ctzll(m);
+            int at = 0;
+            if (lane == leader) at = atomicAdd(b.splatListCount, __popcll(m));
+            at = __shfl(at, leader) + __popcll(m & ((1ull << lane) - 1));
+            if (listIt && at < b.splatListCap) b.splatList[at] = rec;   // at most D per path: never full
         }
     }
 }

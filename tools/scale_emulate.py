@@ -77,7 +77,7 @@ def main():
     ap.add_argument("--kernels", action="store_true",
                     help="also report rank 0's per-kernel HIP-event ms per frame (a separate profiled pass)")
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
-    ap.add_argument("--splat-exchange", default="sparse", choices=["sparse", "dense"],
+    ap.add_argument("--splat-exchange", default="dense", choices=["sparse", "dense"],
                     help="band-split BDPT: record lists + all-to-all (sparse) or rank-major planes + reduce-scatter")
     ap.add_argument("--ranks", default="", help="only these ranks (comma list; profiling one rank's call)")
     ap.add_argument("--base-ms", type=float, default=None,
