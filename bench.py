@@ -1,16 +1,22 @@
 """Benchmark: Mpaths/s of the MI355X path tracer on the San-Miguel proxy at 1920x1080
 (BASELINE.json metric), PT with maxDepth 2 (the reference default), random sampler.
 `--integrator bdpt` measures the BDPT integrator instead: one path =
-one camera + one light subpath with all their connections; N GPUs split each frame into 8-row
-bands (light-tracing splats land anywhere: one rank-major reduce-scatter of the splats per frame,
-"scaling": "strong"; --bdpt-split frame: whole frames per rank, "weak").
+one camera + one light subpath with all their connections.
 
-One step = one 1-spp frame of the whole image (mcrt_render_frame + mcrt_accumulate).
-N GPUs: one process per GPU (torch.distributed.run), the image is tile-split into 8-row bands
-dealt round-robin to the ranks (north star), each rank accumulates its bands, and one RCCL
+One step = one 1-spp frame of the whole image per GPU (mcrt_render_frames + mcrt_accumulate_frames).
+N GPUs: one process per GPU (torch.distributed.run).  The image is tile-split into 8-row bands
+dealt round-robin to the ranks (north star); each rank accumulates its bands, and one RCCL
 collective ends the job (inside the timed region): a gather of every rank's own band rows to
 rank 0 (--end-collective reduce: the full-frame sum-reduce instead; the same bits).
-Total work per step is fixed -> "scaling": "strong".
+  --scaling weak (default): a step is N frames (global batch N, 1 frame per GPU), each frame
+      tile-split over the ranks, so a rank's launches hold as many paths as one GPU's (20 steps
+      at N = 8: 160 band-frames in one call) -- the shape of the BASELINE configs' 1024-8192 spp
+      jobs; the image equals one GPU rendering the N x steps frames, bit for bit.  BDPT: whole
+      frames per rank (its per-frame arrays are whole-frame sized, so its band-split calls cannot
+      widen), one reduce of the accumulators at the end.
+  --scaling strong: a step is one frame split over the ranks (a rank's launches hold 1/N of the
+      paths; their tails weigh N times more); BDPT band split with one splat
+      reduce-scatter per call.
 
 Also reported (one JSON line on rank 0):
   roofline      dominant kernel (k_shadow_extend): compulsory bytes per launch (ray I/O + 64 B per
@@ -469,10 +475,14 @@ def main():
     ap.add_argument("--integrator", default="pt", choices=["pt", "bdpt"])
     ap.add_argument("--no-bdpt", action="store_true", help="skip the BDPT object (config 4) of the PT run")
     ap.add_argument("--bdpt-steps", type=int, default=32, help="timed BDPT frames of the BDPT object")
-    ap.add_argument("--bdpt-split", default="band", choices=["frame", "band"],
-                    help="multi-GPU BDPT: 8-row bands per rank with one splat reduce-scatter per frame (default: "
-                         "the 1-GPU image up to splat summation order; mcrt.dist.exchange_splats) or whole frames "
-                         "per rank (no per-frame exchange; each rank's sampled-light history differs, BDPT.cl:585)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1: weak = N frames per step (1 per GPU), each tile-split over the ranks (PT) or whole "
+                         "frames per rank (BDPT); strong = one frame per step split over the ranks")
+    ap.add_argument("--bdpt-split", default=None, choices=["frame", "band"],
+                    help="multi-GPU BDPT (default: frame for --scaling weak, band for strong): 8-row bands per rank "
+                         "with one splat reduce-scatter per call (the 1-GPU image up to splat summation order; "
+                         "mcrt.dist.exchange_splats) or whole frames per rank (no per-call exchange; each rank's "
+                         "sampled-light history differs, BDPT.cl:585)")
     ap.add_argument("--splat-exchange", default="dense", choices=["sparse", "dense"],
                     help="band-split BDPT: the rank-major full-frame buffers with one stream-ordered reduce-scatter "
                          "(dense, default: the exchange overlaps the next call), or the splats landing in other "
@@ -517,6 +527,9 @@ def main():
         sys.exit(launch_ranks(args.gpus))
     if env_world is not None and int(env_world) != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={env_world} from the launcher but --gpus {args.gpus}; they must agree")
+
+    if args.bdpt_split is None:
+        args.bdpt_split = "frame" if args.scaling == "weak" else "band"
 
     import torch
     import torch.distributed as dist
@@ -599,9 +612,14 @@ def main():
     # sweep tools/r2_gpu27.sh measured 1297 / 1315 Mpaths/s at 16 / 32 frames per launch, and a
     # 1/N band share x 32 frames keeps every multi-GPU launch at >= 4 whole images of paths
     batch = args.bdpt_batch if bdpt else (args.batch if args.batch > 0 else (32 if W * H <= 2_100_000 else 16))
+    # PT, weak scaling: a step is `world` frames, each tile-split over the ranks; a rank's calls take
+    # world x as many frames (its 1/world band share of each), so they hold as many paths as one
+    # GPU's calls (MCRT_MAX_BATCH_FRAMES = 256)
+    fps = world if (args.scaling == "weak" and not bdpt) else 1   # frames per step
+    batch = min(256, batch * fps)
     # the untimed per-kernel pass and the roofline price the TIMED launch shape: calls of
-    # min(batch, steps) frames (the driver's 20 steps are one 20-frame call)
-    stats_batch = min(batch, args.steps)
+    # min(batch, frames) frames (the driver's 20 steps are one 20-frame call, 160 band-frames at N = 8)
+    stats_batch = min(batch, args.steps * fps)
 
     def step(i, n=1):
         """frames i .. i+n-1 (one mcrt_render_frames call when n > 1)"""
@@ -664,7 +682,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    run(frame0, args.steps)
+    run(frame0, args.steps * fps)
     if world > 1:   # one collective: each rank's own band rows gathered to rank 0 (north star)
         # no try/except here: a fallback taken by one rank while the others sit in the gather would
         # hang the job; an error exits this rank and torch.distributed.run stops the others
@@ -696,11 +714,11 @@ def main():
         # share the GPU with another frame's launches, so each duration is the kernel's own), calls
         # of the timed region's shape (stats_batch frames each)
         fb.set_frames_in_flight(1)
-        run(frame0 + args.steps, stats_batch, stats_batch)   # the slot re-binds outside the profiled launches
+        run(frame0 + args.steps * fps, stats_batch, stats_batch)   # the slot re-binds outside the profiled launches
         ctx.sync()
         ctx.set_profiling(True)
         ctx.reset_stats()
-        run(frame0 + args.steps + stats_batch, args.stats_launches * stats_batch, stats_batch)
+        run(frame0 + args.steps * fps + stats_batch, args.stats_launches * stats_batch, stats_batch)
         ctx.sync()
         kstats = ctx.kernel_stats()
         ctx.set_profiling(False)
@@ -711,19 +729,22 @@ def main():
         bd = bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, args.bdpt_steps, args.warmup,
                           not args.no_kernel_timing, args.bdpt_split, args.bdpt_batch, args.splat_exchange == "sparse")
 
-    paths = W * H * args.steps * (world if bdpt and not band_bdpt else 1)
+    gb = world if bdpt and not band_bdpt else fps   # frames per step (global batch)
+    paths = W * H * args.steps * gb
     value = paths / elapsed / 1e6
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "warmup_frames_run": warm_frames,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak" if bdpt and not band_bdpt else "strong", "vs_baseline": None, "dtype": "f32",
+        "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic: deterministic {args.scene} ({scene.num_triangles} tris, seeded generator mcrt/scenes.py)",
         "config": {"workload": f"{args.scene} {W}x{H}, {'BDPT' if bdpt else 'unidirectional PT'}, maxDepth {D}, "
-                               f"{args.sampler} sampler, 1 spp per step, box-filter accumulate"
+                               f"{args.sampler} sampler, "
+                               + (f"{gb} spp per step (1 per GPU)" if gb > 1 else "1 spp per step")
+                               + ", box-filter accumulate"
                                + (f", Russian roulette from bounce {args.rr_start} (perf mode)"
                                   if args.russian_roulette and not bdpt else ""), "width": W, "height": H,
-                   "triangles": scene.num_triangles, "max_depth": D, "spp_per_step": 1,
+                   "triangles": scene.num_triangles, "max_depth": D, "spp_per_step": gb, "global_batch": gb,
                    "bvh": ("two-level (instanced), RadeonRays-identical Bvh trees" if two_level else
                            "device LBVH" if args.device_build else
                            "RadeonRays-identical SAH, " + ("host build" if args.host_build else "device build")),
@@ -731,7 +752,8 @@ def main():
                    "parallelism": (f"band split x {world}, 1 sparse splat all-to-all per call + 1 RCCL reduce" if sparse_x
                                    else f"band split x {world}, 1 splat reduce-scatter per call + 1 RCCL reduce" if band_bdpt
                                    else f"frame split x {world} + 1 RCCL reduce" if bdpt else
-                                   f"tile-split {args.band_rows}-row bands x {world} + 1 RCCL "
+                                   f"tile-split {args.band_rows}-row bands x {world}"
+                                   + (f", {fps} frames per step" if fps > 1 else "") + " + 1 RCCL "
                                    + ("band gather" if args.end_collective == "gather" else "reduce")),
                    "frames_per_launch": stats_batch, "max_frames_per_call": batch},
     }

@@ -409,11 +409,13 @@ MCRT_API mcrt_status mcrt_render_frame(mcrt_scene scene, mcrt_framebuffer fb, co
  * After mcrt_render_frames it accumulates every frame of that batch in frame order
  * (frame_index = the batch's first frame), all with this filter. */
 MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* filter, int32_t frame_index);
-/* Batched frames (PT and BDPT): renders the `count` (1..32) consecutive 1-spp frames
+/* Batched frames (PT and BDPT): renders the `count` (PT 1..256, BDPT 1..32: its per-frame arrays
+ * are whole-frame sized) consecutive 1-spp frames
  * params->frame_index + k, k < count, with cameras[k] (per-frame TAA jitter), in ONE pass --
  * every launch (camera rays, shading, shadow + extension rays) covers all count frames' paths,
  * so a small per-rank band share (tile split over N GPUs) still fills the 256 CUs and the
- * divergent tail of each launch is paid once per batch.  Per frame the arithmetic, the RNG
+ * divergent tail of each launch is paid once per batch (1/8 of the bands x 160 frames = the
+ * paths of one GPU's 20-frame call).  Per frame the arithmetic, the RNG
  * streams (keyed by pixel, frame_index + k, bounce) and the radiance are exactly those of
  * mcrt_render_frame; mcrt_accumulate_frames (or mcrt_accumulate) then sums them in frame order,
  * so the image equals count x (mcrt_render_frame + mcrt_accumulate) bit for bit.  Radiance read

@@ -151,7 +151,8 @@ struct FrameSlot {
     int costTiles = 0;           // tiles of the recorded costs (0: none)
     int tileCap = 0;
 };
-#define SLOT_COUNTER_BYTES (512 + 176 * MCRT_MAX_BATCH_FRAMES + 1536)
+#define SLOT_FILTER_OFFSET (512 + 176 * MCRT_MAX_BATCH_FRAMES)   // the batch's filters (mcrt_accumulate_frames)
+#define SLOT_COUNTER_BYTES (SLOT_FILTER_OFFSET + (int)sizeof(mcrt_filter) * MCRT_MAX_BATCH_FRAMES + 1536)
 
 // Per-frame BDPT arrays (RTBDPTPass::createBuffers, RTBDPTPass.cpp:442-479), one set per frame
 // slot so BDPT frames overlap like PT frames; layouts in mcrt_bdpt.hip.
@@ -178,7 +179,7 @@ struct BdptSet {
     float4* splatList = nullptr;
     size_t splatListCap = 0;
     int* splatAux = nullptr;
-};   // [0..127] ints: counters; cameras (176 B each, <= MCRT_MAX_BATCH_FRAMES) from byte 512
+};   // [0..127] ints: counters; cameras (176 B each, <= MCRT_MAX_BATCH_FRAMES) from byte 512, then filters
 
 struct mcrt_framebuffer_s {
     mcrt_ctx ctx = nullptr;
@@ -1705,7 +1706,9 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     if (fb->ctx != ctx) return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame buffer belongs to another context");
     if (!s->dNodes) return fail(ctx, MCRT_ERROR_NOT_READY, "mcrt_accel_build has not been called");
     if (count < 1 || count > MCRT_MAX_BATCH_FRAMES)
-        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame count must be 1 .. MCRT_MAX_BATCH_FRAMES (32)");
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "frame count must be 1 .. MCRT_MAX_BATCH_FRAMES (256)");
+    if (p->integrator == MCRT_INTEGRATOR_BDPT && count > MCRT_MAX_BDPT_BATCH_FRAMES)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "BDPT frame count must be 1 .. MCRT_MAX_BDPT_BATCH_FRAMES (32)");
     for (int k = 0; k < count; ++k)
         if (cam[k].width != fb->W || cam[k].height != fb->H)
             return fail(ctx, MCRT_ERROR_INVALID_ARG, "camera size differs from the frame buffer");
@@ -1953,14 +1956,17 @@ static mcrt_status accumulate(mcrt_framebuffer fb, const mcrt_filter* filters, i
     const int batch = slot.lastBatch;
     if (nfilters != 1 && nfilters != batch)
         return fail(ctx, MCRT_ERROR_INVALID_ARG, "one filter, or one per frame of the last mcrt_render_frames");
-    BatchFilters w{};   // weights are evaluated on the device (k_accumulate, filters.cl)
-    for (int k = 0; k < batch; ++k) w.f[k] = filters[nfilters == 1 ? 0 : k];
     FrameArgs f = fb->bands;
     f.batch = batch;
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, slot.done, 0));   // the frame's render (its slot stream)
+    // weights are evaluated on the device (k_accumulate, filters.cl); the filters go to the slot's
+    // counter block, which its next render (after slot.free below) does not touch before this launch
+    mcrt_filter* dFilt = reinterpret_cast<mcrt_filter*>(reinterpret_cast<char*>(slot.counters) + SLOT_FILTER_OFFSET);
+    HIPCHK(ctx, hipMemcpyAsync(dFilt, filters, sizeof(mcrt_filter) * nfilters, hipMemcpyHostToDevice, ctx->stream));
     {
         Timed t(ctx, K_ACCUM, nullptr, (int64_t)f.numTiles * 64 * batch);
-        mcrt::launch_accumulate(f, frame_index, w, fb->radiance, fb->wsum, fb->wts, fb->image, ctx->stream);
+        mcrt::launch_accumulate(f, frame_index, dFilt, nfilters == 1 ? 0 : 1, fb->radiance, fb->wsum, fb->wts, fb->image,
+                                ctx->stream);
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(slot.free, ctx->stream));   // the slot may take its next frame

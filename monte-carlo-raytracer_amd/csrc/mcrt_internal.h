@@ -48,10 +48,12 @@ struct FrameArgs {
     const uint32_t* tileOrder;
     uint32_t* tileCost;
 };
-#define MCRT_MAX_BATCH_FRAMES 32
-// the reconstruction filter of each frame of a batch (device layout, KRN/kernel_data.h:63-80);
-// k_accumulate evaluates its weight on the device like ReconstructionPass (reconstruction.cl:21-42)
-struct BatchFilters { mcrt_filter f[MCRT_MAX_BATCH_FRAMES]; };
+// Frames per mcrt_render_frames call.  PT: a rank's share of a multi-GPU step (1/N of each frame's
+// bands) x N frames per step keeps its launches as large as one GPU's (N = 8: 20 steps = 160
+// band-frames in one call).  BDPT's per-frame arrays are whole-frame sized (~3.2 KB per pixel), so
+// its calls stay at 32 frames.
+#define MCRT_MAX_BATCH_FRAMES 256
+#define MCRT_MAX_BDPT_BATCH_FRAMES 32
 
 struct QueueArgs {
     int* shadowCount;
@@ -162,7 +164,9 @@ void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int
                    int maxCount, hipStream_t st);
 void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits, int which,
                 float4* out, hipStream_t st);
-void launch_accumulate(const FrameArgs& f, int frame, const BatchFilters& w, const float4* radiance, float4* wsum, float* wts,
+// filters: the reconstruction filter of each batch frame in device memory (KRN/kernel_data.h:63-80), k_accumulate
+// evaluates its weight like ReconstructionPass (reconstruction.cl:21-42); filterStride 0 = one filter for all frames
+void launch_accumulate(const FrameArgs& f, int frame, const mcrt_filter* filters, int filterStride, const float4* radiance, float4* wsum, float* wts,
                        float4* image, hipStream_t st);
 void launch_resolve(uint32_t W, uint32_t H, const float4* wsum, const float* wts, float4* image, hipStream_t st);
 void launch_band_pack(const FrameArgs& f, const float4* wsum, const float* wts, float* out, hipStream_t st);

@@ -682,8 +682,8 @@ MCRT_DEV float filterWeight(const mcrt_filter& fp) {
 }
 
 // A batch of f.batch frames (mcrt_render_frames) is accumulated in frame order, frame + k with
-// filter bf.f[k]: per pixel the same operations as f.batch single-frame launches.
-__global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, BatchFilters bf,
+// filter filters[k * fstride]: per pixel the same operations as f.batch single-frame launches.
+__global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, const mcrt_filter* __restrict__ filters, int fstride,
                                                     const float4* __restrict__ radiance, float4* __restrict__ wsum,
                                                     float* __restrict__ wts, float4* __restrict__ image) {
     const int lane = threadIdx.x & 63;
@@ -702,7 +702,7 @@ __global__ __launch_bounds__(256) void k_accumulate(FrameArgs f, int frame, Batc
         const float4 r4 = radiance[(size_t)k * f.W * f.H + pix];
         const f4 radiance4 = f4{cl_clamp(r4.x, 0.0f, 1000.0f), cl_clamp(r4.y, 0.0f, 1000.0f),
                                 cl_clamp(r4.z, 0.0f, 1000.0f), cl_clamp(r4.w, 0.0f, 1000.0f)};
-        const float w = filterWeight(bf.f[k]);
+        const float w = filterWeight(filters[k * fstride]);
         if (frame + k == 0) {
             s = radiance4 * w;
             ws = w;
@@ -1095,10 +1095,11 @@ void launch_aov(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, 
     const int blocks = (f.numTiles * 64 + 255) / 256;
     hipLaunchKernelGGL(k_aov, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, s, f, cam, hits, which, out);
 }
-void launch_accumulate(const FrameArgs& f, int frame, const BatchFilters& w, const float4* radiance, float4* wsum,
-                       float* wts, float4* image, hipStream_t st) {
+void launch_accumulate(const FrameArgs& f, int frame, const mcrt_filter* filters, int filterStride, const float4* radiance,
+                       float4* wsum, float* wts, float4* image, hipStream_t st) {
     const int blocks = (f.numTiles * 64 + 255) / 256;
-    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(256), 0, st, f, frame, w, radiance, wsum, wts, image);
+    hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(256), 0, st, f, frame, filters, filterStride, radiance, wsum,
+                       wts, image);
 }
 
 void launch_denoise(int W, int H, int r, float ss, float sr, const float4* in, float4* out, hipStream_t st) {

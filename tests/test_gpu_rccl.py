@@ -113,11 +113,27 @@ def _bench(tmp_path, gpus, tag, extra=()):
 
 @pytest.mark.timeout(600)
 def test_bench_gpus_flag_launches_ranks(tmp_path):
-    one, img1 = _bench(tmp_path, 1, "n1")
-    two, img2 = _bench(tmp_path, 2, "n2", ("--dist-backend", "gloo"))
+    """Strong scaling: the 2-rank job (one frame per step split over the ranks) saves the 1-rank image."""
+    one, img1 = _bench(tmp_path, 1, "n1", ("--scaling", "strong"))
+    two, img2 = _bench(tmp_path, 2, "n2", ("--dist-backend", "gloo", "--scaling", "strong"))
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2, (one, two)
-    assert "x 2" in two["config"]["parallelism"]
+    assert "x 2" in two["config"]["parallelism"] and two["scaling"] == "strong"
     np.testing.assert_array_equal(img2.view(np.uint32), img1.view(np.uint32))
+
+
+@pytest.mark.timeout(600)
+def test_bench_weak_scaling_two_ranks(tmp_path):
+    """Weak scaling (the default): 2 ranks x 6 steps = 12 frames, each tile-split over the ranks in
+    calls of 2 x 4 band-frames, save the image of ONE rank rendering 12 frames in calls of 8 (the
+    same frame sequence, warmup included), bit for bit; value counts 2 frames per step."""
+    one, img1 = _bench(tmp_path, 1, "w1", ("--steps", "12", "--batch", "8"))
+    two, img2 = _bench(tmp_path, 2, "w2", ("--dist-backend", "gloo"))
+    assert one["scaling"] == two["scaling"] == "weak"
+    assert two["config"]["global_batch"] == 2 and two["config"]["max_frames_per_call"] == 8, two["config"]
+    assert two["config"]["frames_per_launch"] == 8 and "2 frames per step" in two["config"]["parallelism"]
+    np.testing.assert_array_equal(img2.view(np.uint32), img1.view(np.uint32))
+    # value = whole-job paths / time: 256 x 200 x 6 steps x 2 frames per step
+    assert abs(two["value"] - 256 * 200 * 12 / (two["ms_per_step"] * 6 * 1e-3) / 1e6) < 1e-2 * two["value"]
 
 
 @pytest.mark.timeout(600)
@@ -125,7 +141,7 @@ def test_bench_bdpt_sparse_exchange_two_ranks(tmp_path):
     """`bench.py --integrator bdpt --gpus 2 --dist-backend gloo`: the band split with the sparse splat
     exchange (mcrt.dist.exchange_splats_sparse through gloo all-to-alls) against one rank: the same
     accumulated image up to the order of the splat sums."""
-    extra = ("--integrator", "bdpt", "--bdpt-batch", "4")
+    extra = ("--integrator", "bdpt", "--bdpt-batch", "4", "--scaling", "strong", "--splat-exchange", "sparse")
     one, img1 = _bench(tmp_path, 1, "b1", extra)
     two, img2 = _bench(tmp_path, 2, "b2", extra + ("--dist-backend", "gloo"))
     assert two["n_gpus"] == 2 and "sparse" in two["config"]["parallelism"], two["config"]

@@ -217,11 +217,13 @@ def test_russian_roulette_unbiased(hip_ctx, mixed):
     ds.close()
 
 
-@pytest.mark.parametrize("num_bands,band_index,count", [(1, 0, 2), (1, 0, 4), (1, 0, 5), (4, 3, 8), (2, 1, 16), (1, 0, 32)])
+@pytest.mark.parametrize("num_bands,band_index,count", [(1, 0, 2), (1, 0, 4), (1, 0, 5), (4, 3, 8), (2, 1, 16), (1, 0, 32),
+                                                       (1, 0, 64), (8, 5, 160)])
 def test_batched_frames_bit_exact(hip_ctx, mixed, num_bands, band_index, count):
     """mcrt_render_frames + mcrt_accumulate_frames over `count` frames (per-frame jittered
     cameras, per-frame filter weights) give the accumulators of `count` single-frame renders
-    and accumulations bit for bit, and the batch's first-frame radiance."""
+    and accumulations bit for bit, and the batch's first-frame radiance.  160 frames of one band
+    of 8: a rank's call in bench.py's weak scaling at N = 8 (20 steps x 8 frames)."""
     from mcrt import lib
     sc, _ = mixed
     W, H, D = 96, 72, 3
@@ -249,8 +251,10 @@ def test_batched_frames_bit_exact(hip_ctx, mixed, num_bands, band_index, count):
     assert st["closest_rays"] > 0
     with pytest.raises(lib.MCRTError):
         fb.accumulate_frames(filts[:2] if count != 2 else filts[:3], 0)   # neither 1 nor count filters
-    with pytest.raises(lib.MCRTError):
-        fb.render_frames(ds, [cams[0]] * 33, frame=0, max_depth=D)
+    with pytest.raises(lib.MCRTError):   # MCRT_MAX_BATCH_FRAMES
+        fb.render_frames(ds, [cams[0]] * 257, frame=0, max_depth=D)
+    with pytest.raises(lib.MCRTError):   # BDPT: MCRT_MAX_BDPT_BATCH_FRAMES (whole-frame arrays per frame)
+        fb.render_frames(ds, [cams[0]] * 33, frame=0, max_depth=D, integrator=T.INTEGRATOR_BDPT)
     fb.close()
     ref.close()
     ds.close()

@@ -1,9 +1,11 @@
 """Per-rank work of the N-GPU tile split, emulated on ONE GPU, plus the modelled collectives.
 
-For N in --ns, renders K frames of each rank's bands (band_index = r of num_bands = N) one rank
-at a time on cuda:0 and reports the slowest rank's ms/frame next to the 1-GPU ms/frame.  The
-ratio is the compute part of the strong-scaling efficiency (the final RCCL reduce and the
-launch gaps of concurrent processes are not in it).  --integrator bdpt: the band-split BDPT frame
+For N in --ns, renders each rank's bands (band_index = r of num_bands = N) one rank at a time on
+cuda:0 and reports the slowest rank's ms per band-frame next to the 1-GPU ms/frame; efficiency =
+base / (N x that), the compute part of the scaling efficiency (the launch gaps of concurrent
+processes are not in it).  --scaling strong: K frames per rank (a step = one frame split over the
+ranks); weak (bench.py's default): K x N frames per rank, calls of N x the --chunks frames (capped
+at 256), as a step = N frames.  --integrator bdpt: the band-split BDPT frame
 of each rank (render, rank-major splat pack, gather of its own chunk) and the bytes of the one
 splat reduce-scatter per frame, against the full-frame all-reduce it replaced.  Prints one JSON
 line.
@@ -35,7 +37,7 @@ STEP_US = 10.0    # latency per collective step
 
 
 def pt_gather_ms(n, W, H, band_rows, steps):
-    """Modelled end-of-job band gather, ms per frame of the job."""
+    """Modelled end-of-job band gather, ms per (band-)frame of the job (steps = its frames)."""
     if n == 1:
         return 0.0
     from mcrt import dist as mdist
@@ -67,6 +69,7 @@ def sparse_exchange_ms(n, rec, batch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--scene", default="san_miguel_proxy")
@@ -97,6 +100,7 @@ def main():
     filt = T.make_filter(T.BOX)
     fb.set_frames_in_flight(args.fif)
     out = {"fif": args.fif, "batch": args.batch, "chunks": args.chunks, "scene": args.scene, "steps": args.steps,
+           "scaling": args.scaling if args.integrator == "pt" else "strong",
            "band_rows": args.band_rows, "integrator": args.integrator, "per_n": {}}
     if args.integrator == "bdpt":
         bdpt_sweep(args, ctx, ds, fb, cams, filt, W, H, out)
@@ -106,8 +110,9 @@ def main():
         for r in ranks_of(args, n):
             band = dict(band_rows=args.band_rows, num_bands=n, band_index=r)
             B = args.batch if args.batch > 0 else n
-
-            plan = [int(c) for c in args.chunks.split(",")] if args.chunks else [B]
+            mult = n if args.scaling == "weak" else 1   # frames per step
+            plan = [min(256, int(c) * mult) for c in args.chunks.split(",")] if args.chunks else [min(256, B * mult)]
+            frames = args.steps * mult
 
             def run(f0, count):
                 i = calls = 0
@@ -126,19 +131,20 @@ def main():
             run(0, max(3, 4 * max(plan)))   # every frame slot allocated before timing
             ctx.sync()
             t0 = time.perf_counter()
-            run(16, args.steps)
+            run(16, frames)
             ctx.sync()
-            per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
+            per_rank.append((time.perf_counter() - t0) / frames * 1e3)
             if args.kernels and len(per_rank) == 1:
                 ctx.set_profiling(True)
                 ctx.reset_stats()
-                run(16 + args.steps, args.steps)
+                run(16 + frames, frames)
                 ctx.sync()
                 ks = ctx.kernel_stats()
                 ctx.set_profiling(False)
-                kern = {k: round(v["ms"] / args.steps, 4) for k, v in ks.items()}
-        out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / n, 4),
-                           "min_ms": round(min(per_rank), 4), "rank_ms": [round(x, 4) for x in per_rank]}
+                kern = {k: round(v["ms"] / frames, 4) for k, v in ks.items()}
+        out["per_n"][n] = {"max_ms": round(max(per_rank), 4), "mean_ms": round(sum(per_rank) / len(per_rank), 4),
+                           "min_ms": round(min(per_rank), 4), "rank_ms": [round(x, 4) for x in per_rank],
+                           "frames_per_rank": frames, "frames_per_call": plan}
         if args.kernels:
             out["per_n"][n]["rank0_kernel_ms_per_frame"] = kern
     # efficiency is relative to ONE GPU rendering the whole image: the N = 1 run of this sweep, or
@@ -148,7 +154,7 @@ def main():
     out["model"] = {"link_gbs_per_direction": LINK_GBS, "step_us": STEP_US}
     for n, v in out["per_n"].items():
         v["compute_eff"] = round(base / (n * v["max_ms"]), 4) if base else None
-        g = pt_gather_ms(n, W, H, args.band_rows, args.steps)
+        g = pt_gather_ms(n, W, H, args.band_rows, v["frames_per_rank"])
         v["gather_ms_per_frame_modelled"] = round(g, 5)
         v["eff_with_collective"] = round(base / (n * (v["max_ms"] + g)), 4) if base else None
     print(json.dumps(out), flush=True)
