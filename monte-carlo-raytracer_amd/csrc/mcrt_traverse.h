@@ -180,17 +180,21 @@ MCRT_DEV int traverseOct(const float4* __restrict__ nodes, const TraceRay& r, f3
 // work) and every step runs one path (internal or leaf) instead of both.  At an internal node each
 // lane in the mask tests both child boxes with its own ray and its own closest t, exactly as
 // traverseOct does; the wave descends into a child if any lane hits it, carrying the mask of the
-// lanes that do, and defers the other child (with its mask) on a per-wave LDS stack.  When lanes
+// lanes that do, and defers the other child (with its mask) on a per-wave stack.  When lanes
 // hit both children the wave goes first where most of them would (nearer child first per ray).
 // So every lane tests exactly the nodes whose box it hit at the parent -- the per-ray traversal's
 // rule -- and the closest hit is the same; only the ORDER of a lane's leaves can differ from
 // nearer-first, which matters for exactly-equal t (a tie) alone, as for any other visit order.
 // ---------------------------------------------------------------------------
-// The wave's stack lives in three VGPRs, entry k in lane k (node word, mask low and high halves):
-// a push is a lane compare + selects, a pop three v_readlane with the wave-uniform stack pointer,
-// so neither costs an LDS access, a wait or an exec-mask change for a leader lane.  A level pushes at most 2 entries,
-// so a tree of depth D (leaves at level D) needs 2 D entries and writes at most entry 2 D - 1: the
-// host takes this path for 2 D <= MCRT_PK_STACK = 64 (mcrt_capi.cpp finish_accel).
+// The lane state lives in VGPRs: the current mask is a per-lane flag, stack entry k's node is lane
+// k of one VGPR (a pop is one v_readlane with the wave-uniform stack pointer) and its mask bit k of
+// a per-lane 64-bit field, so the mask arithmetic runs on the vector units; the scalar unit (ONE
+// per CU, shared by its four SIMDs: MI355X_MICROARCH "CU") keeps the node, the stack pointer and
+// the wave-level decisions only.  (With 64-bit SGPR masks the camera launch was scalar-bound: SALU
+// busy 0.85, profiles/pmc_latest.json round 5; this layout halves the scalar instructions of an
+// internal step, profiles/r05/ab/README.txt item 12.)  A level pushes at most 2 entries, so a tree
+// of depth D (leaves at level D) needs 2 D entries: the host takes this path for 2 D <= MCRT_PK_STACK
+// = 64 (mcrt_capi.cpp finish_accel).
 typedef float __attribute__((ext_vector_type(4))) PkV4;
 typedef const __attribute__((address_space(4))) PkV4* PkNodes;   // uniform loads -> s_load
 static_assert(MCRT_PK_STACK == 64, "the packet stack is one VGPR lane per entry");
@@ -199,9 +203,13 @@ MCRT_DEV float4 pkLoad(PkNodes p, int i) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// triHit (RR common.cl:177-218) without branches: the same arithmetic, the early outs become one
-// final select, so a packet's leaf step costs no exec-mask bookkeeping (scalar instructions are
-// what a packet step is short of, not vector ones).
+// triHit (RR common.cl:177-218) without branches: the same arithmetic, the early outs one final
+// select, so a packet's leaf step costs no exec-mask bookkeeping.  SEL (the any-hit packets of the
+// bounce-0 shadow rays): each early out a select of tmax kept in a VGPR (the asm barrier stops the
+// selects from merging into one OR of lane masks), so no scalar mask arithmetic either
+// (k_shadow_extend -4.6 %; the closest-hit camera packets are 2 % faster with the OR-ed lane
+// masks: profiles/r05/ab/README.txt item 12).
+template <bool SEL = true>
 MCRT_DEV float triHitSel(const TraceRay& r, float4 A, float4 E1, float4 E2, float tmax) {
     const f3 e1 = ld3(E1), e2 = ld3(E2);
     const f3 s1 = cl_cross(r.d, e2);
@@ -213,28 +221,42 @@ MCRT_DEV float triHitSel(const TraceRay& r, float4 A, float4 E1, float4 E2, floa
     const float b2 = cl_dot(r.d, s2) * invd;
     float temp = cl_dot(e2, s2) * invd;
     __asm__ volatile("" : "+v"(temp));   // computed by every lane: no exec-mask branch around it
-    const bool miss = denom == 0.f || b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || temp < 0.f || temp > tmax;
-    return miss ? tmax : temp;
+    if constexpr (!SEL) {
+        const bool miss = denom == 0.f || b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || temp < 0.f || temp > tmax;
+        return miss ? tmax : temp;
+    }
+    float res = temp;
+    auto out = [&](bool miss) {
+        res = miss ? tmax : res;
+        __asm__ volatile("" : "+v"(res));
+    };
+    out(denom == 0.f);
+    out(b1 < 0.f);
+    out(b1 > 1.f);
+    out(b2 < 0.f);
+    out(b1 + b2 > 1.f);
+    out(temp < 0.f);
+    out(temp > tmax);
+    return res;
 }
 
 template <bool ANY, int OCT>
 MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay& r, f3 inv, bool valid,
-                               float& tHit) {
+                                float& tHit) {
     const PkNodes cn = (PkNodes)(const void*)nodes;
     const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
     const int lane = (int)__lane_id();
-    const uint64_t laneBit = 1ull << lane;
-    int stN = 0, stLo = 0, stHi = 0;   // the stack: entry k in lane k
+    uint32_t bitsLo = 0, bitsHi = 0;   // stack entry k's mask: bit k
+    int stN = 0;                       // stack entry k's node: lane k
     float t = r.tmax;
     int hit = -1;
-    uint64_t mask = __ballot(valid);
-    uint64_t alive = mask;   // any hit: lanes still without a hit
+    uint32_t act = valid ? 1u : 0u;
+    uint32_t alive = act;   // any hit: lanes still without a hit
     uint32_t node = 0;
     int sp = 0;
     while (true) {
-        if (ANY) mask &= alive;
-        if (mask != 0) {
-            // 32-bit byte offset (s_load's SGPR offset, no 64-bit add): < 2^26 nodes (finish_accel)
+        if (ANY) act &= alive;
+        if (__ballot(act != 0u) != 0) {
             const PkNodes q = (PkNodes)((const char __attribute__((address_space(4)))*)cn + (uint32_t)(node << 6));
             const float4 n0 = pkLoad(q, 0), n1 = pkLoad(q, 1), n2 = pkLoad(q, 2), n3f = pkLoad(q, 3);
             const int c0 = __builtin_amdgcn_readfirstlane(__float_as_int(n3f.x));
@@ -265,8 +287,6 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                     b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
                     b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), t);
                 }
-                // lane masks straight from the compares (the lanes outside `mask` drop out here)
-                const uint64_t mL = __ballot(a0 <= a1) & mask, mR = __ballot(b0 <= b1) & mask;
                 // lanes hitting both children go to the nearer one first: the right one where
                 // a0 > b0 (intersect_bvh2_lds.cl:128-141).  The wave takes the majority's first
                 // child F with every lane that hits F and prefers it (or hits F only), then the
@@ -275,44 +295,44 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                 // every lane's sequence of tests -- hence its t at every culling test and the
                 // first of equal-t hits it keeps -- is exactly traverseOct's.  (Any hit: the
                 // answer does not depend on the order, so no third pass.)
-                const uint64_t both = mL & mR;
-                const uint64_t pr = __ballot(a0 > b0) & both;   // lanes preferring the right child
-                const bool goR = (mL == 0) | (2 * __popcll(pr) > __popcll(both));   // no branch
-                const uint64_t late = ANY ? 0ull : (goR ? both & ~pr : pr);   // first child, visited later
-                const uint64_t mF = goR ? mR : mL, mS = goR ? mL : mR;
+                const uint32_t hL = a0 <= a1 ? act : 0u, hR = b0 <= b1 ? act : 0u;
+                const uint32_t hB = hL & hR;
+                const uint32_t hP = a0 > b0 ? hB : 0u;   // prefers the right child
+                const uint64_t mL = __ballot(hL != 0u), mB = __ballot(hB != 0u), mP = __ballot(hP != 0u);
+                const bool goR = (mL == 0) | (2 * __popcll(mP) > __popcll(mB));
+                const uint32_t inF = goR ? hR : hL, inS = goR ? hL : hR;
+                const uint32_t late = ANY ? 0u : (goR ? hB & ~hP : hP);
                 const uint32_t cF = (uint32_t)(goR ? c1 : c0), cS = (uint32_t)(goR ? c0 : c1);
-                // deferred entries, bottom to top: F for the late lanes, then S.  Each slot is
-                // written whether or not it is pushed (the pointer only advances for a push), which
-                // stays below entry 2 D (see above)
-                const bool at0 = lane == sp;
-                stN = at0 ? (int)cF : stN;
-                stLo = at0 ? (int)(uint32_t)late : stLo;
-                stHi = at0 ? (int)(uint32_t)(late >> 32) : stHi;
-                sp += late != 0 ? 1 : 0;
-                const bool at1 = lane == sp;
-                stN = at1 ? (int)cS : stN;
-                stLo = at1 ? (int)(uint32_t)mS : stLo;
-                stHi = at1 ? (int)(uint32_t)(mS >> 32) : stHi;
-                sp += mS != 0 ? 1 : 0;
+                auto push = [&](uint32_t nodeK, uint32_t in) {
+                    const uint32_t m = 1u << (sp & 31), v = in != 0u ? m : 0u;
+                    if (sp < 32) bitsLo = (bitsLo & ~m) | v; else bitsHi = (bitsHi & ~m) | v;
+                    stN = lane == sp ? (int)nodeK : stN;
+                    ++sp;
+                };
+                if (!ANY && __ballot(late != 0u) != 0) push(cF, late);
+                if (__ballot(inS != 0u) != 0) push(cS, inS);
                 node = cF;
-                mask = mF & ~late;
+                act = inF & ~late;
             } else {
-                // every lane computes, the lanes of the mask that pass RR_RAY_MASK take the hit
-                const float th = triHitSel(r, n0, n1, n2, t);
-                const bool take = (mask & laneBit) != 0 && r.mask != __float_as_int(n0.w) && th < t;
+                // every lane computes, the active lanes that pass RR_RAY_MASK take the hit
+                // t for the lanes outside the mask or whose RR_RAY_MASK matches the leaf's shape
+                float th = triHitSel<ANY>(r, n0, n1, n2, t);
+                th = act != 0u ? th : t;
+                __asm__ volatile("" : "+v"(th));
+                th = r.mask != __float_as_int(n0.w) ? th : t;
+                const bool take = th < t;
                 hit = take ? (int)node : hit;
                 t = take ? th : t;
-                if (ANY) alive &= ~__ballot(take);   // a lane with a hit is done (next = DONE)
-                mask = 0;
+                if (ANY) alive = take ? 0u : alive;   // a lane with a hit is done (next = DONE)
+                act = 0u;
             }
         }
-        if (ANY && alive == 0) break;
-        if (mask == 0) {
+        if (ANY && __ballot(alive != 0u) == 0) break;
+        if (__ballot(act != 0u) == 0) {
             if (sp == 0) break;
             --sp;
             node = (uint32_t)__builtin_amdgcn_readlane(stN, sp);
-            mask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(stHi, sp) << 32) |
-                   (uint32_t)__builtin_amdgcn_readlane(stLo, sp);
+            act = ((sp < 32 ? bitsLo : bitsHi) >> (sp & 31)) & 1u;
         }
     }
     tHit = t;
