@@ -127,7 +127,7 @@ struct mcrt_scene_s {
 // for bit.  Small per-rank frames (tile split over many GPUs) do not fill 256 CUs alone.
 struct FrameSlot {
     float4* radiance = nullptr;
-    float4* hitsP = nullptr;     // primary hits by pixel
+    float4* hitsP = nullptr;     // primary hits (mcrt_kernels.hip hitSlot)
     float4* hitsE = nullptr;     // extension hits by queue slot
     float4* eO[2] = {};
     float4* eD[2] = {};
@@ -196,7 +196,7 @@ struct mcrt_framebuffer_s {
     float4* denoised = nullptr;  // RTDenoisePass output (persistent: the reference keeps its image)
     float4* display = nullptr;   // post-processed image (mcrt_postprocess)
     uint32_t* hintPix = nullptr; // occluder hint of each pixel's bounce-0 shadow ray (TraceCtx::hint)
-    float4* hitsP = nullptr;     // primary hits by pixel
+    float4* hitsP = nullptr;     // primary hits (mcrt_kernels.hip hitSlot)
     float4* hitsE = nullptr;     // extension hits by queue slot
     float4* eO[2] = {};
     float4* eD[2] = {};
@@ -1235,14 +1235,15 @@ static void fb_free(mcrt_framebuffer fb) {
 }
 
 // Per-frame planes (radiance, primary hits) for `frames` frames of N pixels; ray queues of Q entries.
-static hipError_t slot_alloc(FrameSlot& k, size_t N, int frames = 1, size_t Q = 0) {
+// N: pixels; T: the frame's 8x8 tiles x 64 (the packed hit slots, mcrt_kernels.hip hitSlot)
+static hipError_t slot_alloc(FrameSlot& k, size_t N, size_t T, int frames = 1, size_t Q = 0) {
     hipError_t e = hipSuccess;
     if (Q < N) Q = N;
     auto A = [&](auto** p, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc((void**)p, bytes);
     };
     A(&k.radiance, 16 * N * frames);
-    A(&k.hitsP, 16 * N * frames);
+    A(&k.hitsP, 16 * std::max(N, T) * frames);
     A(&k.hitsE, 16 * Q);
     for (int i = 0; i < 2; ++i) { A(&k.eO[i], 16 * Q); A(&k.eD[i], 16 * Q); A(&k.eT[i], 16 * Q); }
     A(&k.sO, 16 * Q);
@@ -1351,6 +1352,7 @@ static void fb_bind_bdpt(mcrt_framebuffer fb, int k) {
 // RTBDPTPass::createBuffers (RTBDPTPass.cpp:442-479), sized for max depth D: set k of the
 // per-frame arrays, plus the persistent sampled-light-vertex planes, which start zeroed (the
 // reference's buffer starts with whatever the allocation holds; its clref runner zero-fills it too).
+// (also the packed camera-hit slots per frame: every 8x8 tile of the frame x 64)
 static size_t bdpt_queue_cap(mcrt_framebuffer fb) {
     return (size_t)((fb->W + 7) / 8) * ((fb->H + 7) / 8) * 64;
 }
@@ -1403,7 +1405,7 @@ MCRT_API mcrt_status mcrt_framebuffer_create(mcrt_ctx ctx, uint32_t width, uint3
     A(&fb->display, 16 * N);
     A(&fb->hintPix, 4 * N);
     fb->slot.resize(MCRT_MAX_FRAMES_IN_FLIGHT);
-    if (e == hipSuccess) e = slot_alloc(fb->slot[0], N);
+    if (e == hipSuccess) e = slot_alloc(fb->slot[0], N, N);   // one frame: hits by pixel
     if (e == hipSuccess) fb_bind(fb, 0);
     // zero-fills on slot 0's (private) stream, finished before the frame buffer is handed out:
     // only this buffer's work is waited for, not the device (other contexts, a captured caller stream)
@@ -1756,12 +1758,12 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     FrameSlot& slot = fb->slot[ks];
     if (bdpt) {   // BDPT frames overlap the same way (set ks)
         if (!slot.stream) {
-            HIPCHK(ctx, slot_alloc(slot, fb->N, count));
+            HIPCHK(ctx, slot_alloc(slot, fb->N, bdpt_queue_cap(fb), count));
         } else if (slot.frames < count) {   // radiance planes for a larger batch
             HIPCHK(ctx, hipEventSynchronize(slot.free));
             HIPCHK(ctx, hipStreamSynchronize(slot.stream));
             slot_free(slot);
-            HIPCHK(ctx, slot_alloc(slot, fb->N, count));
+            HIPCHK(ctx, slot_alloc(slot, fb->N, bdpt_queue_cap(fb), count));
         }
         HIPCHK(ctx, hipStreamWaitEvent(slot.stream, slot.free, 0));
         fb_bind(fb, ks);
@@ -1777,11 +1779,11 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     const int bandPaths = f.numTiles * 64 * count;
     const size_t qNeed = std::max(fb->N, (size_t)bandPaths);
     if (!slot.stream) {
-        HIPCHK(ctx, slot_alloc(slot, fb->N, count, qNeed));
+        HIPCHK(ctx, slot_alloc(slot, fb->N, bdpt_queue_cap(fb), count, qNeed));
     } else if (slot.frames < count || slot.queueCap < qNeed) {   // grow for a larger batch
         HIPCHK(ctx, hipEventSynchronize(slot.free));
         slot_free(slot);
-        HIPCHK(ctx, slot_alloc(slot, fb->N, count, qNeed));
+        HIPCHK(ctx, slot_alloc(slot, fb->N, bdpt_queue_cap(fb), count, qNeed));
     }
     const int cap = s->spillCap;
     const size_t spillRays = (std::max((size_t)bandPaths, 2 * qNeed + 64) + 63) / 64 * 64;

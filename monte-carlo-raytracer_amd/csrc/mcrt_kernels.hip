@@ -118,6 +118,15 @@ MCRT_DEV void packedPath(const FrameArgs& f, int tileAll, int lane, int& k, int&
     k = q - pi * f.batch;
 }
 
+// Slot of a camera-ray hit record (k_primary* write it, k_shade0 / k_aov read it).  Packed waves:
+// (tile, pixel-in-tile, frame) with the frames fastest, the packed launches' own order, so a wave's
+// 64 records are one contiguous 1-KB run for its writes and reads (frame-plane order,
+// k * W*H + pixel, put each lane of a packed wave in another plane).  Else the frame plane's pixel.
+MCRT_DEV size_t hitSlot(const FrameArgs& f, int tile, int pi, int k, int x, int y) {
+    if (f.primaryPack && f.batch > 1) return ((size_t)tile * 64 + (size_t)pi) * (size_t)f.batch + (size_t)k;
+    return (size_t)k * f.W * f.H + (size_t)y * f.W + x;
+}
+
 // Camera ray generation fused with the first closest-hit query (RTPrimaryRaysPass):
 // one workgroup = one wave = one 8x8 pixel tile of the rank's bands.
 template <int LAY>
@@ -143,8 +152,7 @@ __global__ __launch_bounds__(64) void k_primary(TraceCtx c, FrameArgs f, const m
     r.tmax = 1000.0f;
     r.mask = -1;
     float t;
-    hitOut[(size_t)k * f.W * f.H + (size_t)y * f.W + x] =
-        traceClosest<LAY>(c, r, lds + lane, raySpill(c, tileAll, lane), t);
+    hitOut[hitSlot(f, tile, pi, k, x, y)] = traceClosest<LAY>(c, r, lds + lane, raySpill(c, tileAll, lane), t);
 }
 
 // The camera-ray launch with wave-packet traversal (traversePacket, plain records): the same rays
@@ -174,7 +182,7 @@ __global__ __launch_bounds__(64) void k_primary_pk(TraceCtx c, FrameArgs f, cons
     float t;
     const uint32_t clk0 = (c.waveClock || f.tileCost) ? waveClockNow() : 0u;
     const int tri = traversePacket<false>(c.nodes, r, valid, t);
-    if (valid) hitOut[(size_t)k * f.W * f.H + (size_t)y * f.W + x] = closestRecord(c.nodes, r, tri, t);
+    if (valid) hitOut[hitSlot(f, tile, pi, k, x, y)] = closestRecord(c.nodes, r, tri, t);
     waveClockStore(c.waveClock, clk0);
     // the wave's time into its tile's cost (the next call's longest-first order): one atomic per wave
     if (f.tileCost && lane == 0 && tile < f.numTiles) atomicAdd(&f.tileCost[tile], waveClockNow() - clk0);
@@ -537,7 +545,8 @@ __global__ __launch_bounds__(SHADE0_BLOCK) void k_shade0(SceneArgs s, FrameArgs 
         const f3 dir = cameraDir(cam, x, y);
         f3 dx = splat3(0.0f), dy = splat3(0.0f);
         if (LOD) cameraDiffDirs(cam, x, y, dx, dy);
-        const f3 add = shadePath<LOD, true, RR>(s, f, 0, pix, hits[pix], dir, splat3(1.0f), 0, o, ld3(cam.pos), dx, dy);
+        const f3 add = shadePath<LOD, true, RR>(s, f, 0, pix, hits[hitSlot(f, tile, pi, k, x, y)], dir, splat3(1.0f), 0,
+                                                o, ld3(cam.pos), dx, dy);
         radiance[pix] = make_float4(add.x, add.y, add.z, 0.0f);
     }
     const int ss = blockAppend<SHADE0_BLOCK / 64>(q.shadowCount, o.pushS, ldsWave);
@@ -603,7 +612,7 @@ __global__ __launch_bounds__(256) void k_aov(SceneArgs s, FrameArgs f, const mcr
     const int stride = which == MCRT_AOV_TEXTURE_LOD ? 3 : 1;
     float4* o = out + (size_t)pix * stride;
     for (int k = 0; k < stride; ++k) o[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const float4 hit = hits[pix];
+    const float4 hit = hits[hitSlot(f, tile, lane, 0, x, y)];
     const int shapeIdx = __float_as_int(hit.z), primIdx = __float_as_int(hit.w);
     if (shapeIdx < 0) return;
     const mcrt_camera& cam = *camp;
