@@ -14,7 +14,8 @@
 #   tools/gpu_task.sh bdpt-prof [DIR]                     the same for the BDPT object (-> pmc_bdpt.json)
 #   tools/gpu_task.sh configs   [DIR]                     every BASELINE config, 1 spp per step
 #   tools/gpu_task.sh rehearse  [DIR] [N]                 bench.py --gpus N (no launcher; gloo, all ranks on
-#                                                         cuda:0) vs 1 rank: images bit-identical
+#                                                         cuda:0) vs 1 rank, weak and strong scaling:
+#                                                         images bit-identical
 # Output under gpurun_out/DIR (default: the task name).
 export TMPDIR=/tmp
 task=$1
@@ -115,15 +116,20 @@ configs)
   run sm_1080p_96 --steps 96
   ;;
 rehearse)
+  # weak scaling (the default): N ranks x 20 steps = one rank's 20 N frames in calls of 32 N (the
+  # same warmup and call sequence, so the images must match bit for bit); then strong scaling
   P=gpurun_out/${1:-rehearse}; N=${2:-2}; mkdir -p $P
-  C="bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline-model --no-kernel-timing --no-bdpt"
-  timeout -k 10 400 python3 $C --save-image $P/img1.npy > $P/n1.json 2> $P/n1.err || fail n1 $P/n1.err
-  timeout -k 10 600 python3 $C --gpus $N --dist-backend gloo --save-image $P/imgN.npy > $P/nN.json 2> $P/nN.err || fail nN $P/nN.err 4
+  C="bench.py --warmup 5 --no-cpu-baseline --no-roofline-model --no-kernel-timing --no-bdpt"
+  timeout -k 10 400 python3 $C --steps $((20 * N)) --batch $((32 * N)) --save-image $P/img1.npy > $P/n1.json 2> $P/n1.err || fail n1 $P/n1.err
+  timeout -k 10 600 python3 $C --steps 20 --gpus $N --dist-backend gloo --save-image $P/imgN.npy > $P/nN.json 2> $P/nN.err || fail nN $P/nN.err 4
+  timeout -k 10 400 python3 $C --steps 20 --scaling strong --save-image $P/img1s.npy > $P/n1s.json 2> $P/n1s.err || fail n1s $P/n1s.err
+  timeout -k 10 600 python3 $C --steps 20 --scaling strong --gpus $N --dist-backend gloo --save-image $P/imgNs.npy > $P/nNs.json 2> $P/nNs.err || fail nNs $P/nNs.err 4
   python3 -c "
 import numpy as np
-a = np.load('$P/img1.npy'); b = np.load('$P/imgN.npy')
-print('images bit-identical:', a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32)), a.shape)"
-  summary $P/n1.json $P/nN.json
+for a, b in (('img1', 'imgN'), ('img1s', 'imgNs')):
+    x = np.load('$P/' + a + '.npy'); y = np.load('$P/' + b + '.npy')
+    print(a, b, 'images bit-identical:', x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32)), x.shape)"
+  summary $P/n1.json $P/nN.json $P/n1s.json $P/nNs.json
   ;;
 *)
   echo "unknown task '$task' (suite | bench | ab | sweep | evidence | bdpt-prof | configs | rehearse)"; exit 2
