@@ -128,7 +128,8 @@ rehearse)
 import numpy as np
 for a, b in (('img1', 'imgN'), ('img1s', 'imgNs')):
     x = np.load('$P/' + a + '.npy'); y = np.load('$P/' + b + '.npy')
-    print(a, b, 'images bit-identical:', x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32)), x.shape)"
+    print(a, b, 'images bit-identical:', x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32)), x.shape)" | tee $P/compare.txt
+  rm -f $P/*.npy   # 33 MB each: keep the box's output under gpurun's copy-back limit
   summary $P/n1.json $P/nN.json $P/n1s.json $P/nNs.json
   ;;
 *)
