@@ -902,17 +902,21 @@ __global__ __launch_bounds__(256) void k_qnodes_sizes(const float4* __restrict__
     if (w.x >= 0 && w.x != (int)i + 1) atomicOr(notDfs, 1);
 }
 
-// One axis of an internal record: the two children's (lo, hi) as bytes q with fmaf(q, s, o) <= lo
-// and >= hi exactly as the traversal decodes them (s = 2^(e - 127), o = the smaller lo).  Returns
-// false when no byte reaches a bound (non-finite boxes).
-MCRT_DEV bool quantAxis(float lo0, float hi0, float lo1, float hi1, float& o, uint32_t& bytes, uint32_t& e) {
+// One axis of an internal record: its origin (the smaller lo) and the exponent byte e of its step,
+// 2^(e - 127) >= extent / 250.  False for non-finite boxes.
+MCRT_DEV bool quantExp(float lo0, float hi0, float lo1, float hi1, float& o, uint32_t& e) {
     o = fminf(lo0, lo1);
     const float ext = fmaxf(hi0, hi1) - o;
     if (!(ext >= 0.0f) || ext == __builtin_inff()) return false;
     int k = -126;
     if (ext > 0.0f) frexpf(ext * (1.0f / 250.0f), &k);   // ext / 250 <= 2^k
     e = (uint32_t)min(max(k + 127, 1), 254);
-    const float sc = __uint_as_float(e << 23);
+    return true;
+}
+// The two children's (lo, hi) on that axis as bytes q with fmaf(q, s, o) <= lo and >= hi exactly as
+// the traversal decodes them; s = the walk's step (qScales: 2^(e - 127) times a mantissa the meta
+// word's lower fields supply, in [1, 1.04)), so 255 s covers the extent.  False if no byte reaches.
+MCRT_DEV bool quantBytes(float lo0, float hi0, float lo1, float hi1, float o, float sc, uint32_t& bytes) {
     const float b[4] = {lo0, hi0, lo1, hi1};
     bytes = 0;
     for (int j = 0; j < 4; ++j) {
@@ -941,21 +945,24 @@ __global__ __launch_bounds__(256) void k_qnodes_convert(const float4* __restrict
     float4* dst = q + off[i];
     if (w.x >= 0) {   // child 0 box (n0.x, n0.z, n2.x)-(n0.y, n0.w, n2.y), child 1 (n1.x, n1.z, n2.z)-(n1.y, n1.w, n2.w)
         float ox, oy, oz;
-        uint32_t bx, by, bz, ex, ey, ez;
-        const bool ok = quantAxis(n0.x, n0.y, n1.x, n1.y, ox, bx, ex) && quantAxis(n0.z, n0.w, n1.z, n1.w, oy, by, ey) &&
-                        quantAxis(n2.x, n2.y, n2.z, n2.w, oz, bz, ez);
-        if (!ok || (uint32_t)w.y >= n) {
+        uint32_t bx = 0, by = 0, bz = 0, ex = 0, ey = 0, ez = 0;
+        bool ok = quantExp(n0.x, n0.y, n1.x, n1.y, ox, ex) && quantExp(n0.z, n0.w, n1.z, n1.w, oy, ey) &&
+                  quantExp(n2.x, n2.y, n2.z, n2.w, oz, ez) && (uint32_t)w.y < n;
+        const uint32_t leaf0 = ok && reinterpret_cast<const int4*>(&nodes[4 * (size_t)w.x + 3])->x < 0 ? 1u : 0u;
+        const uint32_t leaf1 = ok && reinterpret_cast<const int4*>(&nodes[4 * (size_t)w.y + 3])->x < 0 ? 1u : 0u;
+        const uint32_t meta = ex | (ey << 9) | (ez << 18) | (leaf0 << 27);
+        const QScales sc = qScales(meta);
+        ok = ok && quantBytes(n0.x, n0.y, n1.x, n1.y, ox, sc.x, bx) && quantBytes(n0.z, n0.w, n1.z, n1.w, oy, sc.y, by) &&
+             quantBytes(n2.x, n2.y, n2.z, n2.w, oz, sc.z, bz);
+        if (!ok) {
             atomicOr(fail, 1);
             return;
         }
-        const uint32_t leaf0 = reinterpret_cast<const int4*>(&nodes[4 * (size_t)w.x + 3])->x < 0 ? 1u : 0u;
-        const uint32_t leaf1 = reinterpret_cast<const int4*>(&nodes[4 * (size_t)w.y + 3])->x < 0 ? 1u : 0u;
-        dst[0] = make_float4(ox, oy, oz, __uint_as_float(off[w.y]));
-        dst[1] = make_float4(__uint_as_float(bx), __uint_as_float(by), __uint_as_float(bz),
-                             __uint_as_float(ex | (ey << 8) | (ez << 16) | (leaf0 << 24) | (leaf1 << 25)));
+        dst[0] = make_float4(ox, oy, oz, __uint_as_float((off[w.y] << 1) | leaf1));
+        dst[1] = make_float4(__uint_as_float(bx), __uint_as_float(by), __uint_as_float(bz), __uint_as_float(meta));
         return;
     }
-    // leaf: its exact box (as the parent's record stores it) must be min / max of v0, v0 + e1, v0 + e2
+// leaf: its exact box (as the parent's record stores it) must be min / max of v0, v0 + e1, v0 + e2
     // for the compact walk to test it from the triangle; else bit 31 sends the walk to the parent
     bool slow = true;
     const int par = w.y;   // k_leaf_parents

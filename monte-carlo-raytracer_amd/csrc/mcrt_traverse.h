@@ -396,8 +396,9 @@ MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint3
 // memory pipeline (TA busy 0.94, one cache access per 16-B lane load), not by arithmetic.
 //   internal (32 B): (origin.xyz, right child ref) | (x bytes, y bytes, z bytes, meta): for axis a
 //     the bytes are (child 0 lo, child 0 hi, child 1 lo, child 1 hi) and a bound decodes as
-//     fmaf(q, 2^(e_a - 127), origin_a); meta = e_x | e_y << 8 | e_z << 16 | leaf(child 0) << 24 |
-//     leaf(child 1) << 25.  The left child is the next record (depth-first order).
+//     fmaf(q, s_a, origin_a), s_a = qScales(meta) (2^(e_a - 127) up to a mantissa < 1.04); meta =
+//     e_x | e_y << 9 | e_z << 18 | leaf(child 0) << 27.  The left child is the next record
+//     (depth-first order, ref + 4); the right child's ref (16-B offset << 1 | leaf bit) is stored.
 //   leaf (48 B): (v0 | shape id), (v1 - v0 | prim id), (v2 - v0 | 64-B record index, bit 31 set when
 //     the leaf's exact box must come from its parent's 64-B record).
 // Why the answers are the 64-B walk's (RR intersect_bvh2_lds.cl:107-178):
@@ -419,7 +420,14 @@ MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint3
 #define QTIE_HI (1.0f + 0x1.0p-18f)
 #define QTIE_LO (1.0f - 0x1.0p-18f)
 
-MCRT_DEV float qScale(uint32_t meta, int axis) { return __uint_as_float(((meta >> (8 * axis)) & 0xffu) << 23); }
+// The three steps of an internal record from its meta word in one shift each: exponent byte e_k
+// at bits 9k..9k+7 with a zero bit above it, so meta << (23 - 9k) puts e_k in the float's exponent
+// and a clear sign bit; the fields below land in the mantissa (x: none; y, z: a factor < 1.04),
+// which the converter (k_qnodes_convert) quantises with, so the decoded bounds stay outward.
+struct QScales { float x, y, z; };
+MCRT_DEV QScales qScales(uint32_t meta) {
+    return QScales{__uint_as_float(meta << 23), __uint_as_float(meta << 14), __uint_as_float(meta << 5)};
+}
 MCRT_DEV float qByte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xffu); }
 
 // RR common.cl:177-218 without the tmax test: the hit distance or +inf (the caller compares)
@@ -468,6 +476,16 @@ MCRT_DEV bool parentBoxHit(const TraceCtx& c, uint32_t leaf, f3 inv, f3 oxi, flo
     return slabHit<-1>(lo, hi, inv, oxi, t);
 }
 
+// min(x, y, z, tc) as v_min_f32 + v_min3_f32: the same value as the fminf chain (the hardware min
+// returns the other operand for a quiet NaN, and no operand here is a signalling NaN), without the
+// v_max canonicalisation of the loop-carried tc the compiler adds to every node step for fminf.
+MCRT_DEV float minFar(float x, float y, float z, float tc) {
+    float m, r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(m) : "v"(z), "v"(tc));
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(m));
+    return r;
+}
+
 // Returns the hit leaf's 64-B record index or -1; tie: a near tie at the final distance (closest hit).
 template <bool ANY, int OCT>
 MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t* stk, uint32_t* spill,
@@ -487,12 +505,14 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
         // a leaf's third piece in the same round trip (the leaf bit is in the reference, known
         // before the fetch): without this the compiler issues it after the branch, a second
         // dependent fetch on every leaf visit
-        float4 e2 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float4 e2;   // only a leaf reads it: no zeroing for the internal nodes
+        asm("" : "=v"(e2.x), "=v"(e2.y), "=v"(e2.z), "=v"(e2.w));
         if (ref & 1u) e2 = p[2];
         asm volatile("" ::"v"(e2.w), "v"(b.w));
         uint32_t next;
         if (!(ref & 1u)) {
-            const float sx = qScale(b.w, 0), sy = qScale(b.w, 1), sz = qScale(b.w, 2);
+            const QScales qs = qScales(b.w);
+            const float sx = qs.x, sy = qs.y, sz = qs.z;
             const f3 lo0 = f3{fmaf(qByte(b.x, 0), sx, a.x), fmaf(qByte(b.y, 0), sy, a.y), fmaf(qByte(b.z, 0), sz, a.z)};
             const f3 hi0 = f3{fmaf(qByte(b.x, 1), sx, a.x), fmaf(qByte(b.y, 1), sy, a.y), fmaf(qByte(b.z, 1), sz, a.z)};
             const f3 lo1 = f3{fmaf(qByte(b.x, 2), sx, a.x), fmaf(qByte(b.y, 2), sy, a.y), fmaf(qByte(b.z, 2), sz, a.z)};
@@ -507,9 +527,9 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
                 const float byn = fmaf(SY ? hi1.y : lo1.y, inv.y, oxi.y), byf = fmaf(SY ? lo1.y : hi1.y, inv.y, oxi.y);
                 const float bzn = fmaf(SZ ? hi1.z : lo1.z, inv.z, oxi.z), bzf = fmaf(SZ ? lo1.z : hi1.z, inv.z, oxi.z);
                 a0 = fmaxf(fmaxf(axn, ayn), fmaxf(azn, 0.0f));
-                a1 = fminf(fminf(axf, ayf), fminf(azf, tc));
+                a1 = minFar(axf, ayf, azf, tc);
                 b0 = fmaxf(fmaxf(bxn, byn), fmaxf(bzn, 0.0f));
-                b1 = fminf(fminf(bxf, byf), fminf(bzf, tc));
+                b1 = minFar(bxf, byf, bzf, tc);
             } else {
                 const float ax0 = fmaf(lo0.x, inv.x, oxi.x), ax1 = fmaf(hi0.x, inv.x, oxi.x);
                 const float ay0 = fmaf(lo0.y, inv.y, oxi.y), ay1 = fmaf(hi0.y, inv.y, oxi.y);
@@ -518,12 +538,12 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
                 const float by0 = fmaf(lo1.y, inv.y, oxi.y), by1 = fmaf(hi1.y, inv.y, oxi.y);
                 const float bz0 = fmaf(lo1.z, inv.z, oxi.z), bz1 = fmaf(hi1.z, inv.z, oxi.z);
                 a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
-                a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), tc);
+                a1 = minFar(fmaxf(ax0, ax1), fmaxf(ay0, ay1), fmaxf(az0, az1), tc);
                 b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
-                b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), tc);
+                b1 = minFar(fmaxf(bx0, bx1), fmaxf(by0, by1), fmaxf(bz0, bz1), tc);
             }
-            const uint32_t cl = (((ref >> 1) + 2u) << 1) | ((b.w >> 24) & 1u);
-            const uint32_t cr = (__float_as_uint(a.w) << 1) | ((b.w >> 25) & 1u);
+            const uint32_t cl = ref + 4u + ((b.w >> 27) & 1u);   // the next record (+32 B), its leaf bit
+            const uint32_t cr = __float_as_uint(a.w);            // the right child's reference
             const bool h0 = a0 <= a1, h1 = b0 <= b1;
             const bool c1first = h1 && (a0 > b0);   // intersect_bvh2_lds.cl:128-141
             if (h0 && h1) {   // defer the far child
