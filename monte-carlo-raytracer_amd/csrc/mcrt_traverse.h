@@ -492,6 +492,14 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
                           float& tHit, bool& tie) {
     const char* __restrict__ base = reinterpret_cast<const char*>(c.qnodes);
     const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
+    // OCT -2 (lanes of any octants): per axis a byte permutation that puts each child's NEAR bound
+    // byte first -- (lo0, hi0, lo1, hi1) as is for a positive inverse direction, (hi0, lo0, hi1, lo1)
+    // for a negative one -- so every lane runs the octant-specialised slab test of octant 0 on its
+    // own bytes: the same operations, hence the same values, as traverseQOct<OCT> for its octant
+    // (one v_perm per axis instead of the generic test's min / max pairs)
+    const uint32_t selX = (__float_as_uint(inv.x) >> 31) ? 0x02030001u : 0x03020100u;
+    const uint32_t selY = (__float_as_uint(inv.y) >> 31) ? 0x02030001u : 0x03020100u;
+    const uint32_t selZ = (__float_as_uint(inv.z) >> 31) ? 0x02030001u : 0x03020100u;
     float t = r.tmax, tc = r.tmax, tieT = -1.0f;
     int hit = -1;
     uint32_t ref = c.qroot;
@@ -513,13 +521,20 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
         if (!(ref & 1u)) {
             const QScales qs = qScales(b.w);
             const float sx = qs.x, sy = qs.y, sz = qs.z;
-            const f3 lo0 = f3{fmaf(qByte(b.x, 0), sx, a.x), fmaf(qByte(b.y, 0), sy, a.y), fmaf(qByte(b.z, 0), sz, a.z)};
-            const f3 hi0 = f3{fmaf(qByte(b.x, 1), sx, a.x), fmaf(qByte(b.y, 1), sy, a.y), fmaf(qByte(b.z, 1), sz, a.z)};
-            const f3 lo1 = f3{fmaf(qByte(b.x, 2), sx, a.x), fmaf(qByte(b.y, 2), sy, a.y), fmaf(qByte(b.z, 2), sz, a.z)};
-            const f3 hi1 = f3{fmaf(qByte(b.x, 3), sx, a.x), fmaf(qByte(b.y, 3), sy, a.y), fmaf(qByte(b.z, 3), sz, a.z)};
+            uint4 bq = b;
+            if constexpr (OCT == -2) {
+                bq.x = __builtin_amdgcn_perm(b.x, b.x, selX);
+                bq.y = __builtin_amdgcn_perm(b.y, b.y, selY);
+                bq.z = __builtin_amdgcn_perm(b.z, b.z, selZ);
+            }
+            const f3 lo0 = f3{fmaf(qByte(bq.x, 0), sx, a.x), fmaf(qByte(bq.y, 0), sy, a.y), fmaf(qByte(bq.z, 0), sz, a.z)};
+            const f3 hi0 = f3{fmaf(qByte(bq.x, 1), sx, a.x), fmaf(qByte(bq.y, 1), sy, a.y), fmaf(qByte(bq.z, 1), sz, a.z)};
+            const f3 lo1 = f3{fmaf(qByte(bq.x, 2), sx, a.x), fmaf(qByte(bq.y, 2), sy, a.y), fmaf(qByte(bq.z, 2), sz, a.z)};
+            const f3 hi1 = f3{fmaf(qByte(bq.x, 3), sx, a.x), fmaf(qByte(bq.y, 3), sy, a.y), fmaf(qByte(bq.z, 3), sz, a.z)};
             float a0, a1, b0, b1;
-            if constexpr (OCT >= 0) {
-                constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
+            if constexpr (OCT >= 0 || OCT == -2) {   // -2: lo* / hi* are each lane's near / far bounds
+                constexpr int O = OCT >= 0 ? OCT : 0;
+                constexpr bool SX = (O & 1) != 0, SY = (O & 2) != 0, SZ = (O & 4) != 0;
                 const float axn = fmaf(SX ? hi0.x : lo0.x, inv.x, oxi.x), axf = fmaf(SX ? lo0.x : hi0.x, inv.x, oxi.x);
                 const float ayn = fmaf(SY ? hi0.y : lo0.y, inv.y, oxi.y), ayf = fmaf(SY ? lo0.y : hi0.y, inv.y, oxi.y);
                 const float azn = fmaf(SZ ? hi0.z : lo0.z, inv.z, oxi.z), azf = fmaf(SZ ? lo0.z : hi0.z, inv.z, oxi.z);
@@ -609,29 +624,14 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
     return hit;
 }
 
+// The compact walk of one ray: every lane in the byte-permutation form (OCT -2), whatever the octants
+// of its wave's rays.  Dispatching octant-uniform waves (41 % of the headline's extension waves) to
+// the specialised instantiations and the rest to the generic min / max test cost 2 % more
+// (profiles/r05/ab/README.txt item 17).
 template <bool ANY>
 MCRT_DEV int traverseQ(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, float& tHit,
                        bool& tie) {
-    const f3 inv = safeInvDir(r.d);
-#define MCRT_TRAVQ_CALL(OCT) return traverseQOct<ANY, OCT>(c, r, inv, stk, spill, tHit, tie)
-    const int oct = (int)(__float_as_uint(inv.x) >> 31) | (int)((__float_as_uint(inv.y) >> 31) << 1) |
-                    (int)((__float_as_uint(inv.z) >> 31) << 2);
-    const int oct0 = __builtin_amdgcn_readfirstlane(oct);
-    if (__all(oct == oct0)) {
-        switch (oct0) {
-            case 0: MCRT_TRAVQ_CALL(0);
-            case 1: MCRT_TRAVQ_CALL(1);
-            case 2: MCRT_TRAVQ_CALL(2);
-            case 3: MCRT_TRAVQ_CALL(3);
-            case 4: MCRT_TRAVQ_CALL(4);
-            case 5: MCRT_TRAVQ_CALL(5);
-            case 6: MCRT_TRAVQ_CALL(6);
-            case 7: MCRT_TRAVQ_CALL(7);
-            default: break;
-        }
-    }
-    MCRT_TRAVQ_CALL(-1);
-#undef MCRT_TRAVQ_CALL
+    return traverseQOct<ANY, -2>(c, r, safeInvDir(r.d), stk, spill, tHit, tie);
 }
 
 // RR common.cl:249-277 (triangle_calculate_barycentrics)
