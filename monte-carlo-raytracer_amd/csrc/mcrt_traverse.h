@@ -240,6 +240,16 @@ MCRT_DEV float triHitSel(const TraceRay& r, float4 A, float4 E1, float4 E2, floa
     return res;
 }
 
+// min(x, y, z, tc) as v_min_f32 + v_min3_f32: the same value as the fminf chain (the hardware min
+// returns the other operand for a quiet NaN, and no operand here is a signalling NaN), without the
+// v_max canonicalisation of the loop-carried tc the compiler adds to every node step for fminf.
+MCRT_DEV float minFar(float x, float y, float z, float tc) {
+    float m, r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(m) : "v"(z), "v"(tc));
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(m));
+    return r;
+}
+
 template <bool ANY, int OCT>
 MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay& r, f3 inv, bool valid,
                                 float& tHit) {
@@ -272,9 +282,9 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                     const float byn = fmaf(SY ? n1.w : n1.z, inv.y, oxi.y), byf = fmaf(SY ? n1.z : n1.w, inv.y, oxi.y);
                     const float bzn = fmaf(SZ ? n2.w : n2.z, inv.z, oxi.z), bzf = fmaf(SZ ? n2.z : n2.w, inv.z, oxi.z);
                     a0 = fmaxf(fmaxf(axn, ayn), fmaxf(azn, 0.0f));
-                    a1 = fminf(fminf(axf, ayf), fminf(azf, t));
+                    a1 = minFar(axf, ayf, azf, t);
                     b0 = fmaxf(fmaxf(bxn, byn), fmaxf(bzn, 0.0f));
-                    b1 = fminf(fminf(bxf, byf), fminf(bzf, t));
+                    b1 = minFar(bxf, byf, bzf, t);
                 } else {   // RR intersect_bvh2_lds.cl:54-63 (fast_intersect_bbox2)
                     const float ax0 = fmaf(n0.x, inv.x, oxi.x), ax1 = fmaf(n0.y, inv.x, oxi.x);
                     const float ay0 = fmaf(n0.z, inv.y, oxi.y), ay1 = fmaf(n0.w, inv.y, oxi.y);
@@ -283,9 +293,9 @@ MCRT_DEV int traversePacketOct(const float4* __restrict__ nodes, const TraceRay&
                     const float by0 = fmaf(n1.z, inv.y, oxi.y), by1 = fmaf(n1.w, inv.y, oxi.y);
                     const float bz0 = fmaf(n2.z, inv.z, oxi.z), bz1 = fmaf(n2.w, inv.z, oxi.z);
                     a0 = fmaxf(fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1)), 0.0f);
-                    a1 = fminf(fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1)), t);
+                    a1 = minFar(fmaxf(ax0, ax1), fmaxf(ay0, ay1), fmaxf(az0, az1), t);
                     b0 = fmaxf(fmaxf(fmaxf(fminf(bx0, bx1), fminf(by0, by1)), fminf(bz0, bz1)), 0.0f);
-                    b1 = fminf(fminf(fminf(fmaxf(bx0, bx1), fmaxf(by0, by1)), fmaxf(bz0, bz1)), t);
+                    b1 = minFar(fmaxf(bx0, bx1), fmaxf(by0, by1), fmaxf(bz0, bz1), t);
                 }
                 // lanes hitting both children go to the nearer one first: the right one where
                 // a0 > b0 (intersect_bvh2_lds.cl:128-141).  The wave takes the majority's first
@@ -474,16 +484,6 @@ MCRT_DEV bool parentBoxHit(const TraceCtx& c, uint32_t leaf, f3 inv, f3 oxi, flo
     const f3 lo = right ? f3{p1.x, p1.z, p2.z} : f3{p0.x, p0.z, p2.x};
     const f3 hi = right ? f3{p1.y, p1.w, p2.w} : f3{p0.y, p0.w, p2.y};
     return slabHit<-1>(lo, hi, inv, oxi, t);
-}
-
-// min(x, y, z, tc) as v_min_f32 + v_min3_f32: the same value as the fminf chain (the hardware min
-// returns the other operand for a quiet NaN, and no operand here is a signalling NaN), without the
-// v_max canonicalisation of the loop-carried tc the compiler adds to every node step for fminf.
-MCRT_DEV float minFar(float x, float y, float z, float tc) {
-    float m, r;
-    asm("v_min_f32 %0, %1, %2" : "=v"(m) : "v"(z), "v"(tc));
-    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(m));
-    return r;
 }
 
 // Returns the hit leaf's 64-B record index or -1; tie: a near tie at the final distance (closest hit).
