@@ -13,9 +13,11 @@
 #                                                         SCALE=1 adds the per-rank scaling emulation
 #   tools/gpu_task.sh bdpt-prof [DIR]                     the same for the BDPT object (-> pmc_bdpt.json)
 #   tools/gpu_task.sh configs   [DIR]                     every BASELINE config, 1 spp per step
-#   tools/gpu_task.sh rehearse  [DIR] [N]                 bench.py --gpus N (no launcher; gloo, all ranks on
+#   tools/gpu_task.sh rehearse  [DIR] [N] [W H]           bench.py --gpus N (no launcher; gloo, all ranks on
 #                                                         cuda:0) vs 1 rank, weak and strong scaling:
-#                                                         images bit-identical
+#                                                         images bit-identical (W x H: all N ranks' slot
+#                                                         buffers share one GPU here, so N = 8 needs a
+#                                                         smaller frame than 1080p)
 # Output under gpurun_out/DIR (default: the task name).
 export TMPDIR=/tmp
 task=$1
@@ -118,9 +120,12 @@ configs)
 rehearse)
   # weak scaling (the default): N ranks x 20 steps = one rank's 20 N frames in calls of 32 N (the
   # same warmup and call sequence, so the images must match bit for bit); then strong scaling
+  # (the 1-rank run takes the same frames in 32-frame calls: a full-frame call of 32 N frames would
+  # need 32 N frames of queues; the warm-up frame count, 4 calls of the ranks' batch, is matched)
   P=gpurun_out/${1:-rehearse}; N=${2:-2}; mkdir -p $P
-  C="bench.py --warmup 5 --no-cpu-baseline --no-roofline-model --no-kernel-timing --no-bdpt"
-  timeout -k 10 400 python3 $C --steps $((20 * N)) --batch $((32 * N)) --save-image $P/img1.npy > $P/n1.json 2> $P/n1.err || fail n1 $P/n1.err
+  B=$((32 * N)); [ $B -gt 256 ] && B=256
+  C="bench.py --warmup 5 --no-cpu-baseline --no-roofline-model --no-kernel-timing --no-bdpt --width ${3:-1920} --height ${4:-1080}"
+  timeout -k 10 400 python3 $C --steps $((20 * N)) --batch 32 --warmup $((4 * B)) --save-image $P/img1.npy > $P/n1.json 2> $P/n1.err || fail n1 $P/n1.err
   timeout -k 10 600 python3 $C --steps 20 --gpus $N --dist-backend gloo --save-image $P/imgN.npy > $P/nN.json 2> $P/nN.err || fail nN $P/nN.err 4
   timeout -k 10 400 python3 $C --steps 20 --scaling strong --save-image $P/img1s.npy > $P/n1s.json 2> $P/n1s.err || fail n1s $P/n1s.err
   timeout -k 10 600 python3 $C --steps 20 --scaling strong --gpus $N --dist-backend gloo --save-image $P/imgNs.npy > $P/nNs.json 2> $P/nNs.err || fail nNs $P/nNs.err 4
