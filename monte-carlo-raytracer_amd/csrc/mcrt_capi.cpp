@@ -150,6 +150,11 @@ struct FrameSlot {
     uint32_t* tileOrder = nullptr;
     int costTiles = 0;           // tiles of the recorded costs (0: none)
     int tileCap = 0;
+    // suspended extension walks (TraceCtx::walkCap): MCRT_SUSPEND_F4 float4 per queue entry, and
+    // one count per bounce (zeroed per call)
+    float4* suspend = nullptr;
+    size_t suspendCap = 0;
+    int* suspendCnt = nullptr;
 };
 #define SLOT_FILTER_OFFSET (512 + 176 * MCRT_MAX_BATCH_FRAMES)   // the batch's filters (mcrt_accumulate_frames)
 #define SLOT_COUNTER_BYTES (SLOT_FILTER_OFFSET + (int)sizeof(mcrt_filter) * MCRT_MAX_BATCH_FRAMES + 1536)
@@ -411,6 +416,19 @@ static void with_hints(TraceCtx& c, mcrt_scene s, uint32_t* pix, uint32_t n) {
     c.hint = pix ? pix : s->dHintCell;
     c.hintMode = pix ? MCRT_HINT_PIXEL : MCRT_HINT_CELL;
     c.hintPixels = n;
+}
+
+// Stop rule of the extension rays' compact walks (TraceCtx::walkCap / walkLanes): a wave stops
+// once it has taken MCRT_WALK_CAP steps (0 = never) and MCRT_WALK_LANES of its lanes or fewer are
+// still walking (64: a fixed step limit).  Default 60 / 8: k_shadow_extend 0.643 -> 0.603 ms per
+// frame on the headline (a fixed 130-step limit 0.609; profiles/r05/ab/README.txt item 20)
+static int walk_cap() {
+    const char* e = std::getenv("MCRT_WALK_CAP");
+    return e ? std::max(0, std::atoi(e)) : 60;
+}
+static int walk_lanes() {
+    const char* e = std::getenv("MCRT_WALK_LANES");
+    return e ? std::min(64, std::max(0, std::atoi(e))) : 8;
 }
 
 // the coherent launches' view (camera rays, bounce-0 shadow rays): wave packets when the tree allows
@@ -1213,7 +1231,8 @@ static void fb_free_bdpt(mcrt_framebuffer fb) {
 static void slot_free(FrameSlot& k) {
     if (k.stream) hipStreamSynchronize(k.stream);
     void* ptrs[] = {k.radiance, k.hitsP, k.hitsE, k.eO[0], k.eO[1], k.eD[0], k.eD[1], k.eT[0], k.eT[1],
-                    k.sO,       k.sD,    k.sL,    k.counters, k.spill, k.tileCost, k.tileOrder};
+                    k.sO,       k.sD,    k.sL,    k.counters, k.spill, k.tileCost, k.tileOrder,
+                    k.suspend,  k.suspendCnt};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (k.done) hipEventDestroy(k.done);
@@ -1820,6 +1839,19 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     TraceCtx tcs = trace_ctx(s);
     tcs.spill = slot.spill;
     const int qCap = bandPaths;
+    const int wcap = tcs.qnodes && !tcs.twoLevel && p->max_depth > 1 ? walk_cap() : 0;
+    if (wcap > 0) {
+        if (slot.suspendCap < (size_t)qCap) {
+            HIPCHK(ctx, hipStreamSynchronize(st));
+            if (slot.suspend) hipFree(slot.suspend);
+            slot.suspend = nullptr;
+            slot.suspendCap = 0;
+            HIPCHK(ctx, hipMalloc(&slot.suspend, sizeof(float4) * MCRT_SUSPEND_F4 * (size_t)qCap));
+            slot.suspendCap = qCap;
+        }
+        if (!slot.suspendCnt) HIPCHK(ctx, hipMalloc(&slot.suspendCnt, 32 * sizeof(int)));
+        HIPCHK(ctx, hipMemsetAsync(slot.suspendCnt, 0, 32 * sizeof(int), st));
+    }
     if (longest_first()) {
         // the camera / first-shading tiles in descending cost of this slot's previous call (same
         // tiles), and this call's costs recorded for the next one -- all on the slot's stream
@@ -1879,8 +1911,15 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
             if (tse.hint && ctx->countHints) tse.hintHits = fb->counters + 64 + b;
             if (tse.qnodes && ctx->countHints) tse.retraces = fb->counters + 96 + b;
             if (b == 0) tse.waveClock = wave_clock_buf(fb, 1, 2 * (((size_t)qCap + 63) / 64), st);
+            if (wcap > 0) {
+                tse.walkCap = wcap;
+                tse.walkLanes = walk_lanes();
+                tse.suspend = slot.suspend;
+                tse.suspendCount = slot.suspendCnt + b;
+            }
             mcrt::launch_shadow_extend(tse, extCnt + b, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, shadowCnt + b,
                                        fb->sO, fb->sD, fb->sL, fb->radiance, qCap, qCap, st);
+            if (wcap > 0) mcrt::launch_walk_resume(tse, fb->eO[b & 1], fb->eD[b & 1], fb->hitsE, qCap, st);
         } else {
             Timed t(ctx, K_SHADOW, shadowCnt + b, 0, st);
             TraceCtx tsh = tcs;

@@ -125,7 +125,15 @@ struct TraceCtx {
     uint32_t qroot;
     int* retraces;          // closest-hit walks repeated on the exact records (near ties; NULL: not counted)
     uint32_t* waveClock;    // diagnostics (MCRT_WAVE_CLOCK=1): per workgroup (start, end) of the 100-MHz clock
+    // Stop rule of the extension rays' compact walks in k_shadow_extend (walkCap 0: none).  A wave
+    // stops once it has taken walkCap steps and at most walkLanes of its lanes are still walking;
+    // the unfinished walks are appended to `suspend` (MCRT_SUSPEND_F4 float4 each, *suspendCount of
+    // them) and k_walk_resume finishes them in dense waves.
+    int walkCap, walkLanes;
+    float4* suspend;
+    int* suspendCount;
 };
+#define MCRT_SUSPEND_F4 6
 
 #define MCRT_HINT_PIXEL 1
 #define MCRT_HINT_CELL 2
@@ -157,6 +165,9 @@ void launch_shadow(const TraceCtx& c, const int* count, const float4* sO, const 
 void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* qO, const float4* qD, float4* hits,
                           const int* shadowCount, const float4* sO, const float4* sD, const float4* sL,
                           float4* radiance, int maxExt, int maxShadow, hipStream_t st);
+// the walks k_shadow_extend suspended (c.walkCap > 0): at most maxExt of them
+void launch_walk_resume(const TraceCtx& c, const float4* qO, const float4* qD, float4* hits, int maxExt,
+                        hipStream_t st);
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st);
 void launch_shadeN(const SceneArgs& s, const FrameArgs& f, int bounce, const int* countIn, const float4* qO,

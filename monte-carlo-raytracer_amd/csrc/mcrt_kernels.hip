@@ -244,6 +244,20 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     waveClockStore(c.waveClock, clk0);
 }
 
+// A stopped extension walk (TraceCtx::walkCap) of queue slot i, whose lane owns spill column `col`
+// (wave col / 64, lane col % 64), appended to the suspend list for k_walk_resume: MCRT_SUSPEND_F4
+// float4 = (slot, next record, t, culling t), (tie t, hit, sp, spillTop), the 16 LDS stack entries
+// with entry 0 (the QREF_DONE sentinel) replaced by the column.  Divergent call: suspended lanes only.
+MCRT_DEV void suspendWalk(const TraceCtx& c, int i, int col, const QWalk& w, const uint32_t* stk) {
+    const int slot = waveAppend(c.suspendCount, true);
+    float4* sv = c.suspend + (size_t)slot * MCRT_SUSPEND_F4;
+    sv[0] = make_float4(__int_as_float(i), __uint_as_float(w.ref), w.t, w.tc);
+    sv[1] = make_float4(w.tieT, __int_as_float(w.hit), __int_as_float(w.sp), __int_as_float(w.spillTop));
+    for (int k = 0; k < STACK_LDS / 4; ++k)
+        sv[2 + k] = make_float4(__uint_as_float(k == 0 ? (uint32_t)col : stk[(4 * k) * 64]), __uint_as_float(stk[(4 * k + 1) * 64]),
+                                __uint_as_float(stk[(4 * k + 2) * 64]), __uint_as_float(stk[(4 * k + 3) * 64]));
+}
+
 // Shadow rays of bounce b and extension rays of bounce b+1 in ONE launch: both only depend on
 // the shading of bounce b.  Extension workgroups come first (their rays are the longer ones),
 // shadow workgroups fill the extension launch's divergent tail instead of waiting for it.
@@ -267,8 +281,26 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.d = ld3(d);
         r.tmax = RT_MAX_TRACE_F;
         r.mask = -1;
-        float t;
         const uint32_t clk0 = c.waveClock ? waveClockNow() : 0u;
+        if constexpr (LAY == LAY_QUANT) {
+            if (c.walkCap > 0) {
+                // the wave stops once it has taken walkCap steps and at most walkLanes lanes are
+                // still walking: those are appended to the suspend list and finished by
+                // k_walk_resume in dense waves, so a few long walks no longer hold a mostly idle wave
+                uint32_t* stk = lds + lane;
+                uint32_t* spill = raySpill(c, blk, lane);
+                QWalk w = qwalkStart(c, r, stk);
+                qwalk<false, -2, true>(c, r, safeInvDir(r.d), stk, spill, w, c.walkCap, c.walkLanes);
+                if (w.ref != QREF_DONE) {
+                    suspendWalk(c, i, i, w, stk);
+                } else {
+                    hitOut[i] = qwalkClosest(c, r, stk, spill, w);
+                }
+                waveClockStore(c.waveClock, clk0);
+                return;
+            }
+        }
+        float t;
         hitOut[i] = traceClosest<LAY>(c, r, lds + lane, raySpill(c, blk, lane), t);
         waveClockStore(c.waveClock, clk0);
     } else {
@@ -341,6 +373,43 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         acc.z += L.z * V;
         radiance[pix] = acc;
     }
+}
+
+// The extension walks k_shadow_extend suspended (TraceCtx::walkCap): each lane restores one walk's
+// state -- next record, hit so far, LDS stack; its spill entries stay in the spill column the
+// suspending lane owned -- and finishes it, then writes its queue slot's hit record.  The same
+// steps as one uncut walk, so the same record bit for bit.
+__global__ __launch_bounds__(64) void k_walk_resume(TraceCtx c, const float4* __restrict__ qO,
+                                                    const float4* __restrict__ qD, float4* __restrict__ hitOut) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[STACK_LDS * 64];
+    const int n = *c.suspendCount;
+    if ((int)blockIdx.x * 64 >= n) return;
+    const int lane = threadIdx.x;
+    const int j = blockIdx.x * 64 + lane;
+    if (j >= n) return;
+    const float4* sv = c.suspend + (size_t)j * MCRT_SUSPEND_F4;
+    const float4 s0 = sv[0], s1 = sv[1];
+    const int i = __float_as_int(s0.x);
+    uint32_t* stk = lds + lane;
+    uint32_t col = 0;
+    for (int k = 0; k < STACK_LDS / 4; ++k) {
+        const float4 e = sv[2 + k];
+        if (k == 0) col = __float_as_uint(e.x);   // entry 0 is the QREF_DONE sentinel: saved as the column
+        stk[(4 * k) * 64] = k == 0 ? QREF_DONE : __float_as_uint(e.x);
+        stk[(4 * k + 1) * 64] = __float_as_uint(e.y);
+        stk[(4 * k + 2) * 64] = __float_as_uint(e.z);
+        stk[(4 * k + 3) * 64] = __float_as_uint(e.w);
+    }
+    QWalk w{__float_as_uint(s0.y), s0.z, s0.w, s1.x, __float_as_int(s1.y), __float_as_int(s1.z), __float_as_int(s1.w)};
+    const float4 o = qO[i], d = qD[i];
+    TraceRay r;
+    r.o = ld3(o);
+    r.d = ld3(d);
+    r.tmax = RT_MAX_TRACE_F;
+    r.mask = -1;
+    uint32_t* spill = raySpill(c, (int)(col >> 6), (int)(col & 63));
+    qwalk<false, -2>(c, r, safeInvDir(r.d), stk, spill, w);
+    hitOut[i] = qwalkClosest(c, r, stk, spill, w);
 }
 
 // Closest hit over two queues in ONE launch: BDPT's first camera rays (coherent: wave packets when
@@ -1088,6 +1157,10 @@ void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* 
     hipLaunchKernelGGL(pickLayout(c, k_shadow_extend<LAY_TWO_LEVEL>, k_shadow_extend<LAY_QUANT>, k_shadow_extend<LAY_PLAIN>),
                        dim3(blocks > 0 ? blocks : 1), dim3(64), 0, st, c, extCount, qO, qD, hits, shadowCount, sO, sD,
                        sL, radiance);
+}
+void launch_walk_resume(const TraceCtx& c, const float4* qO, const float4* qD, float4* hits, int maxExt,
+                        hipStream_t st) {
+    hipLaunchKernelGGL(k_walk_resume, dim3(maxExt > 0 ? (maxExt + 63) / 64 : 1), dim3(64), 0, st, c, qO, qD, hits);
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {

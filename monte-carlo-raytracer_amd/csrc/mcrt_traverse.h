@@ -486,10 +486,24 @@ MCRT_DEV bool parentBoxHit(const TraceCtx& c, uint32_t leaf, f3 inv, f3 oxi, flo
     return slabHit<-1>(lo, hi, inv, oxi, t);
 }
 
-// Returns the hit leaf's 64-B record index or -1; tie: a near tie at the final distance (closest hit).
-template <bool ANY, int OCT>
-MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t* stk, uint32_t* spill,
-                          float& tHit, bool& tie) {
+// The loop state of a compact walk: the next record, the hit so far and the stack (LDS entries
+// stk[0..sp), spill entries [0, spillTop) in the ray's spill column).  A walk with a stop rule
+// (CAP) leaves the loop with ref != QREF_DONE once its wave has taken at least `cap` steps and at
+// most `capLanes` of its lanes are still walking; the state then resumes it exactly
+// (mcrt_kernels.hip k_walk_resume), so the visits, hence the answer, are those of one uncut walk.
+struct QWalk {
+    uint32_t ref;
+    float t, tc, tieT;
+    int hit, sp, spillTop;
+};
+MCRT_DEV QWalk qwalkStart(const TraceCtx& c, const TraceRay& r, uint32_t* stk) {
+    stk[0] = QREF_DONE;
+    return QWalk{c.qroot, r.tmax, r.tmax, -1.0f, -1, 1, 0};
+}
+
+template <bool ANY, int OCT, bool CAP = false>
+MCRT_DEV void qwalk(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t* stk, uint32_t* spill, QWalk& w,
+                    int cap = 0, int capLanes = 64) {
     const char* __restrict__ base = reinterpret_cast<const char*>(c.qnodes);
     const f3 oxi = -r.o * inv;   // intersect_bvh2_lds.cl:91
     // OCT -2 (lanes of any octants): per axis a byte permutation that puts each child's NEAR bound
@@ -500,13 +514,17 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
     const uint32_t selX = (__float_as_uint(inv.x) >> 31) ? 0x02030001u : 0x03020100u;
     const uint32_t selY = (__float_as_uint(inv.y) >> 31) ? 0x02030001u : 0x03020100u;
     const uint32_t selZ = (__float_as_uint(inv.z) >> 31) ? 0x02030001u : 0x03020100u;
-    float t = r.tmax, tc = r.tmax, tieT = -1.0f;
-    int hit = -1;
-    uint32_t ref = c.qroot;
-    stk[0] = QREF_DONE;
-    int sp = 1, spillTop = 0;
+    float t = w.t, tc = w.tc, tieT = w.tieT;
+    int hit = w.hit;
+    uint32_t ref = w.ref;
+    int sp = w.sp, spillTop = w.spillTop;
     constexpr uint32_t POP = QREF_DONE - 1;
+    int steps = 0;   // the wave's steps: every active lane takes each one, so the count is uniform
     while (ref != QREF_DONE) {
+        if constexpr (CAP) {   // wave-uniform: the step count and the active-lane count
+            if (steps >= cap && (int)__popcll(__ballot(1)) <= capLanes) break;
+            ++steps;
+        }
         const float4* p = reinterpret_cast<const float4*>(base + (size_t)(ref >> 1) * 16);
         const float4 a = p[0];
         const uint4 b = *reinterpret_cast<const uint4*>(p + 1);
@@ -619,9 +637,18 @@ MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t
         }
         ref = next;
     }
-    tHit = t;
-    tie = !ANY && hit >= 0 && tieT == t;
-    return hit;
+    w = QWalk{ref, t, tc, tieT, hit, sp, spillTop};
+}
+
+// Returns the hit leaf's 64-B record index or -1; tie: a near tie at the final distance (closest hit).
+template <bool ANY, int OCT>
+MCRT_DEV int traverseQOct(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t* stk, uint32_t* spill,
+                          float& tHit, bool& tie) {
+    QWalk w = qwalkStart(c, r, stk);
+    qwalk<ANY, OCT>(c, r, inv, stk, spill, w);
+    tHit = w.t;
+    tie = !ANY && w.hit >= 0 && w.tieT == w.t;
+    return w.hit;
 }
 
 // The compact walk of one ray: every lane in the byte-permutation form (OCT -2), whatever the octants
@@ -875,6 +902,16 @@ MCRT_DEV float4 traceClosest(const TraceCtx& c, const TraceRay& r, uint32_t* stk
         const int tri = traverse<false, LAY>(c, r, stk, spill, t);
         return closestRecord(c.nodes, r, tri, t);
     }
+}
+// The end of a closest-hit compact walk run as QWalk steps (traceClosest<LAY_QUANT>'s tail)
+MCRT_DEV float4 qwalkClosest(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill, const QWalk& w) {
+    float t = w.t;
+    int tri = w.hit;
+    if (w.hit >= 0 && w.tieT == w.t) {
+        if (c.retraces) atomicAdd(c.retraces, 1);
+        tri = traverse<false, LAY_PLAIN>(c, r, stk, spill, t);
+    }
+    return closestRecord(c.nodes, r, tri, t);
 }
 template <int LAY>
 MCRT_DEV bool traceAny(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint32_t* spill) {

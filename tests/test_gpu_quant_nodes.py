@@ -75,6 +75,23 @@ def test_pt_frames_identical_to_64b_records(hip_ctx, sm_small, name, W, H, D):
     assert rays > 0 and retr <= max(8, rays // 100), (retr, rays)
 
 
+@pytest.mark.parametrize("cap,lanes", [("1", "64"), ("17", "64"), ("60", "8"), ("8", "48")])
+@pytest.mark.parametrize("name,W,H,D", [CASES[1], CASES[3]])
+def test_capped_walks_identical(hip_ctx, sm_small, name, W, H, D, cap, lanes):
+    """MCRT_WALK_CAP / MCRT_WALK_LANES: k_shadow_extend stops a wave's extension walks once it has
+    taken `cap` steps and at most `lanes` lanes still walk; k_walk_resume finishes the unfinished
+    ones from their saved state (next record, hit so far, stack).  The visits are those of one
+    uncut walk, so the frames are bit-identical to walks that never stop; cap 1 with 64 lanes
+    suspends nearly every walk.  (60, 8) is the default."""
+    sc, cam = (scenes.test_scene(), "mixed") if name == "mixed" else (sm_small, "san_miguel_proxy")
+    a, _, _, _ = _with_env({"MCRT_WALK_CAP": cap, "MCRT_WALK_LANES": lanes},
+                           lambda: _frames(hip_ctx, sc, cam, W, H, D))
+    b, _, _, _ = _with_env({"MCRT_WALK_CAP": "0"}, lambda: _frames(hip_ctx, sc, cam, W, H, D))
+    assert np.isfinite(a).all() and a[..., :3].max() > 0
+    diff = a.view(np.uint32) != b.view(np.uint32)
+    assert not diff.any(), f"{int(diff.any(-1).sum())} pixels differ"
+
+
 def test_bdpt_frames_match_64b_records(hip_ctx, sm_small):
     """BDPT: the subpath and connection rays over the compact records; equal up to the order of the
     light-tracing splats' float atomics (tests/test_gpu_bdpt.py's 4e-6)."""
