@@ -184,6 +184,11 @@ struct BdptSet {
     float4* splatList = nullptr;
     size_t splatListCap = 0;
     int* splatAux = nullptr;
+    // suspended closest-hit walks (TraceCtx::walkCap): MCRT_SUSPEND_F4 float4 per queue entry, one
+    // count per traced queue (zeroed per call)
+    float4* suspend = nullptr;
+    size_t suspendCap = 0;
+    int* suspendCnt = nullptr;
 };   // [0..127] ints: counters; cameras (176 B each, <= MCRT_MAX_BATCH_FRAMES) from byte 512, then filters
 
 struct mcrt_framebuffer_s {
@@ -1211,7 +1216,7 @@ static void bset_free(BdptSet& b) {
     void* ptrs[] = {b.camV,   b.lightV, b.slots,  b.splat,  b.camCount, b.lightCount, b.bdptCounters,
                     b.bqO[0], b.bqO[1], b.bqD[0], b.bqD[1], b.bqT[0], b.bqT[1], b.bHits, b.cO, b.cD, b.cL, b.spill,
                     b.lkey, b.lkey2, b.lslot, b.lperm, b.ekey, b.ekey2, b.eslot, b.eperm, b.sortTmp,
-                    b.splatList, b.splatAux};
+                    b.splatList, b.splatAux, b.suspend, b.suspendCnt};
     for (void* p : ptrs)
         if (p) hipFree(p);
     b = BdptSet();
@@ -1572,6 +1577,26 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     TraceCtx tcs = trace_ctx(s);
     tcs.spill = bs.spill;
     const SceneArgs sa = scene_args(s);
+    // the closest-hit launches' stop rule (TraceCtx::walkCap): a traced queue holds at most
+    // max(bandQ, nSort) = nSort rays (below)
+    const int wcap = tcs.qnodes && !tcs.twoLevel ? walk_cap() : 0;
+    TraceCtx tce = tcs;
+    if (wcap > 0) {
+        const size_t need = (size_t)std::min((size_t)2 * N, (size_t)2 * (size_t)f.numTiles * 64 * B);
+        if (bs.suspendCap < need) {
+            HIPCHK(ctx, hipStreamSynchronize(st));
+            if (bs.suspend) hipFree(bs.suspend);
+            bs.suspend = nullptr;
+            bs.suspendCap = 0;
+            HIPCHK(ctx, hipMalloc(&bs.suspend, sizeof(float4) * MCRT_SUSPEND_F4 * need));
+            bs.suspendCap = need;
+        }
+        if (!bs.suspendCnt) HIPCHK(ctx, hipMalloc(&bs.suspendCnt, 64 * sizeof(int)));
+        HIPCHK(ctx, hipMemsetAsync(bs.suspendCnt, 0, 64 * sizeof(int), st));
+        tce.walkCap = wcap;
+        tce.walkLanes = walk_lanes();
+        tce.suspend = bs.suspend;
+    }
     BdptArgs b{};
     b.camV = fb->camV;
     b.lightV = fb->lightV;
@@ -1667,8 +1692,11 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         // exactly the slots k_bdpt_start wrote (the light queue's count, f.numTiles x 64 x B <= NQ)
         HIPCHK(ctx, mcrt::bdpt_light_sort(bs.lkey, bs.lkey2, bs.lslot, bs.lperm, f.numTiles * 64 * B, bs.sortTmp,
                                           bs.sortTmpBytes, st));
-        mcrt::launch_extend_pair(tcc, tcs, camQ.count, camQ.o, camQ.d, fb->bHits, lightQ.count, lightQ.o, lightQ.d,
+        TraceCtx tl = tce;
+        tl.suspendCount = wcap > 0 ? bs.suspendCnt : nullptr;
+        mcrt::launch_extend_pair(tcc, tl, camQ.count, camQ.o, camQ.d, fb->bHits, lightQ.count, lightQ.o, lightQ.d,
                                  fb->bHits + NQ, bandQ, bandQ, st, bs.lperm);   // grids sized to the band
+        if (wcap > 0) mcrt::launch_walk_resume(tl, lightQ.o, lightQ.d, fb->bHits + NQ, bandQ, st);
     }
     HIPCHK(ctx, clearKeys());   // queue 1 is traced (D >= 1)
     {
@@ -1685,7 +1713,10 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
             Timed t(ctx, K_EXTEND, qIn.count, 0, st);
             HIPCHK(ctx, mcrt::bdpt_light_sort(bs.ekey, bs.ekey2, bs.eslot, bs.eperm, nSort, bs.sortTmp,
                                               bs.sortTmpBytes, st, 16));
-            mcrt::launch_extend(tcs, qIn.count, qIn.o, qIn.d, fb->bHits, nSort, st, bs.eperm);
+            TraceCtx te = tce;
+            te.suspendCount = wcap > 0 ? bs.suspendCnt + d : nullptr;
+            mcrt::launch_extend(te, qIn.count, qIn.o, qIn.d, fb->bHits, nSort, st, bs.eperm);
+            if (wcap > 0) mcrt::launch_walk_resume(te, qIn.o, qIn.d, fb->bHits, nSort, st);
         }
         const bool traced = d <= D;   // queue d is traced by the next round
         if (traced) HIPCHK(ctx, clearKeys());

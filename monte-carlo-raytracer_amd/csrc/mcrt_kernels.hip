@@ -188,6 +188,42 @@ __global__ __launch_bounds__(64) void k_primary_pk(TraceCtx c, FrameArgs f, cons
     if (f.tileCost && lane == 0 && tile < f.numTiles) atomicAdd(&f.tileCost[tile], waveClockNow() - clk0);
 }
 
+// A stopped extension walk (TraceCtx::walkCap) of queue slot i, whose lane owns spill column `col`
+// (wave col / 64, lane col % 64), appended to the suspend list for k_walk_resume: MCRT_SUSPEND_F4
+// float4 = (slot, next record, t, culling t), (tie t, hit, sp, spillTop), the 16 LDS stack entries
+// with entry 0 (the QREF_DONE sentinel) replaced by the column.  Divergent call: suspended lanes only.
+MCRT_DEV void suspendWalk(const TraceCtx& c, int i, int col, const QWalk& w, const uint32_t* stk) {
+    const int slot = waveAppend(c.suspendCount, true);
+    float4* sv = c.suspend + (size_t)slot * MCRT_SUSPEND_F4;
+    sv[0] = make_float4(__int_as_float(i), __uint_as_float(w.ref), w.t, w.tc);
+    sv[1] = make_float4(w.tieT, __int_as_float(w.hit), __int_as_float(w.sp), __int_as_float(w.spillTop));
+    for (int k = 0; k < STACK_LDS / 4; ++k)
+        sv[2 + k] = make_float4(__uint_as_float(k == 0 ? (uint32_t)col : stk[(4 * k) * 64]), __uint_as_float(stk[(4 * k + 1) * 64]),
+                                __uint_as_float(stk[(4 * k + 2) * 64]), __uint_as_float(stk[(4 * k + 3) * 64]));
+}
+
+// Closest hit of queue slot i by a lane owning spill column `col`; over the compact records with a
+// stop rule (TraceCtx::walkCap) a walk still running when its wave stops is suspended instead
+// (k_walk_resume writes hitOut[i] then).
+template <int LAY>
+MCRT_DEV void closestOrSuspend(const TraceCtx& c, const TraceRay& r, uint32_t* stk, int col, int i,
+                               float4* __restrict__ hitOut) {
+    uint32_t* spill = raySpill(c, col >> 6, col & 63);
+    if constexpr (LAY == LAY_QUANT) {
+        if (c.walkCap > 0) {
+            QWalk w = qwalkStart(c, r, stk);
+            qwalk<false, -2, true>(c, r, safeInvDir(r.d), stk, spill, w, c.walkCap, c.walkLanes);
+            if (w.ref != QREF_DONE)
+                suspendWalk(c, i, col, w, stk);
+            else
+                hitOut[i] = qwalkClosest(c, r, stk, spill, w);
+            return;
+        }
+    }
+    float t;
+    hitOut[i] = traceClosest<LAY>(c, r, stk, spill, t);
+}
+
 // Closest hit over the extension queue: qO = (o.xyz, pix), qD = (d.xyz, flags); tmax = 1000.
 // The grid covers the queue's capacity; workgroups past the device-side count exit at once.
 template <int LAY>
@@ -210,8 +246,7 @@ __global__ __launch_bounds__(64) void k_extend(TraceCtx c, const int* __restrict
     r.d = ld3(d);
     r.tmax = RT_MAX_TRACE_F;
     r.mask = -1;
-    float t;
-    hitOut[i] = traceClosest<LAY>(c, r, lds + lane, raySpill(c, blk, lane), t);
+    closestOrSuspend<LAY>(c, r, lds + lane, j, i, hitOut);
 }
 
 // Any hit over the shadow queue + ShadowPass (PathTracing.cl:186-217):
@@ -244,20 +279,6 @@ __global__ __launch_bounds__(64) void k_shadow(TraceCtx c, const int* __restrict
     waveClockStore(c.waveClock, clk0);
 }
 
-// A stopped extension walk (TraceCtx::walkCap) of queue slot i, whose lane owns spill column `col`
-// (wave col / 64, lane col % 64), appended to the suspend list for k_walk_resume: MCRT_SUSPEND_F4
-// float4 = (slot, next record, t, culling t), (tie t, hit, sp, spillTop), the 16 LDS stack entries
-// with entry 0 (the QREF_DONE sentinel) replaced by the column.  Divergent call: suspended lanes only.
-MCRT_DEV void suspendWalk(const TraceCtx& c, int i, int col, const QWalk& w, const uint32_t* stk) {
-    const int slot = waveAppend(c.suspendCount, true);
-    float4* sv = c.suspend + (size_t)slot * MCRT_SUSPEND_F4;
-    sv[0] = make_float4(__int_as_float(i), __uint_as_float(w.ref), w.t, w.tc);
-    sv[1] = make_float4(w.tieT, __int_as_float(w.hit), __int_as_float(w.sp), __int_as_float(w.spillTop));
-    for (int k = 0; k < STACK_LDS / 4; ++k)
-        sv[2 + k] = make_float4(__uint_as_float(k == 0 ? (uint32_t)col : stk[(4 * k) * 64]), __uint_as_float(stk[(4 * k + 1) * 64]),
-                                __uint_as_float(stk[(4 * k + 2) * 64]), __uint_as_float(stk[(4 * k + 3) * 64]));
-}
-
 // Shadow rays of bounce b and extension rays of bounce b+1 in ONE launch: both only depend on
 // the shading of bounce b.  Extension workgroups come first (their rays are the longer ones),
 // shadow workgroups fill the extension launch's divergent tail instead of waiting for it.
@@ -282,26 +303,10 @@ __global__ __launch_bounds__(64) void k_shadow_extend(TraceCtx c, const int* __r
         r.tmax = RT_MAX_TRACE_F;
         r.mask = -1;
         const uint32_t clk0 = c.waveClock ? waveClockNow() : 0u;
-        if constexpr (LAY == LAY_QUANT) {
-            if (c.walkCap > 0) {
-                // the wave stops once it has taken walkCap steps and at most walkLanes lanes are
-                // still walking: those are appended to the suspend list and finished by
-                // k_walk_resume in dense waves, so a few long walks no longer hold a mostly idle wave
-                uint32_t* stk = lds + lane;
-                uint32_t* spill = raySpill(c, blk, lane);
-                QWalk w = qwalkStart(c, r, stk);
-                qwalk<false, -2, true>(c, r, safeInvDir(r.d), stk, spill, w, c.walkCap, c.walkLanes);
-                if (w.ref != QREF_DONE) {
-                    suspendWalk(c, i, i, w, stk);
-                } else {
-                    hitOut[i] = qwalkClosest(c, r, stk, spill, w);
-                }
-                waveClockStore(c.waveClock, clk0);
-                return;
-            }
-        }
-        float t;
-        hitOut[i] = traceClosest<LAY>(c, r, lds + lane, raySpill(c, blk, lane), t);
+        // with a stop rule the wave stops once it has taken walkCap steps and at most walkLanes
+        // lanes are still walking: those are suspended and finished by k_walk_resume in dense
+        // waves, so a few long walks no longer hold a mostly idle wave
+        closestOrSuspend<LAY>(c, r, lds + lane, i, i, hitOut);
         waveClockStore(c.waveClock, clk0);
     } else {
         const int ns = *shadowCount;
@@ -457,14 +462,14 @@ __global__ __launch_bounds__(64) void k_extend_pair(TraceCtx cc, TraceCtx c, con
             if (j >= n1) return;
             r.o = ld3(qO1[j]);
             r.d = ld3(qD1[j]);
-            hit1[j] = traceClosest<LAY1>(c, r, lds + lane, raySpill(c, blockIdx.x, lane), t);
+            closestOrSuspend<LAY1>(c, r, lds + lane, (int)blockIdx.x * 64 + lane, j, hit1);
             return;
         }
         if (j >= n1) return;
         const int i = (int)perm1[j];
         r.o = ld3(qO1[i]);
         r.d = ld3(qD1[i]);
-        hit1[i] = traceClosest<LAY1>(c, r, lds + lane, raySpill(c, blockIdx.x, lane), t);
+        closestOrSuspend<LAY1>(c, r, lds + lane, (int)blockIdx.x * 64 + lane, i, hit1);
     }
 }
 
