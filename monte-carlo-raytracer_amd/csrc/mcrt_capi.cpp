@@ -435,6 +435,14 @@ static int walk_cap() {
 // full-size one).  At depth 5 the later, smaller launches -- whose any-hit shadow blocks otherwise
 // overlap the long walks' tail -- lost what the first gained: k_shadow_extend 2.951 ms per frame
 // without the rule, 2.943 with it on every launch, 2.915 on the first only (item 20)
+// ... and only for calls of at least MCRT_WALK_MIN_PATHS paths (default 16 M): a rank's share of a
+// strong-scaled frame (N = 8: 5 M paths per call) finishes the resumed walks in a launch too small
+// to hide their tail (emulated N = 8 rank 0.175 -> 0.179 ms per frame with the rule; BDPT 0.649 ->
+// 0.659).  The tests set it to 0 to run the rule on small frames.
+static int64_t walk_min_paths() {
+    const char* e = std::getenv("MCRT_WALK_MIN_PATHS");
+    return e ? std::atoll(e) : 16000000;
+}
 static int walk_max_bounce() {
     const char* e = std::getenv("MCRT_WALK_MAXB");
     return e ? std::atoi(e) : 0;
@@ -1587,7 +1595,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     const SceneArgs sa = scene_args(s);
     // the closest-hit launches' stop rule (TraceCtx::walkCap): a traced queue holds at most
     // max(bandQ, nSort) = nSort rays (below)
-    const int wcap = tcs.qnodes && !tcs.twoLevel ? walk_cap() : 0;
+    const int wcap = tcs.qnodes && !tcs.twoLevel && (int64_t)f.numTiles * 64 * B >= walk_min_paths() ? walk_cap() : 0;
     TraceCtx tce = tcs;
     if (wcap > 0) {
         const size_t need = (size_t)std::min((size_t)2 * N, (size_t)2 * (size_t)f.numTiles * 64 * B);
@@ -1878,7 +1886,7 @@ static mcrt_status render_frames(mcrt_scene s, mcrt_framebuffer fb, const mcrt_c
     TraceCtx tcs = trace_ctx(s);
     tcs.spill = slot.spill;
     const int qCap = bandPaths;
-    const int wcap = tcs.qnodes && !tcs.twoLevel && p->max_depth > 1 ? walk_cap() : 0;
+    const int wcap = tcs.qnodes && !tcs.twoLevel && p->max_depth > 1 && bandPaths >= walk_min_paths() ? walk_cap() : 0;
     if (wcap > 0) {
         if (slot.suspendCap < (size_t)qCap) {
             HIPCHK(ctx, hipStreamSynchronize(st));

@@ -82,10 +82,11 @@ def test_capped_walks_identical(hip_ctx, sm_small, name, W, H, D, cap, lanes):
     taken `cap` steps and at most `lanes` lanes still walk; k_walk_resume finishes the unfinished
     ones from their saved state (next record, hit so far, stack).  The visits are those of one
     uncut walk, so the frames are bit-identical to walks that never stop; cap 1 with 64 lanes
-    suspends nearly every walk.  (60, 8) is the default."""
+    suspends nearly every walk.  (60, 8) is the default; here on every extension launch and at any
+    call size (the defaults: the first launch of calls of >= 16 M paths)."""
     sc, cam = (scenes.test_scene(), "mixed") if name == "mixed" else (sm_small, "san_miguel_proxy")
-    a, _, _, _ = _with_env({"MCRT_WALK_CAP": cap, "MCRT_WALK_LANES": lanes},
-                           lambda: _frames(hip_ctx, sc, cam, W, H, D))
+    a, _, _, _ = _with_env({"MCRT_WALK_CAP": cap, "MCRT_WALK_LANES": lanes, "MCRT_WALK_MIN_PATHS": "0",
+                            "MCRT_WALK_MAXB": "8"}, lambda: _frames(hip_ctx, sc, cam, W, H, D))
     b, _, _, _ = _with_env({"MCRT_WALK_CAP": "0"}, lambda: _frames(hip_ctx, sc, cam, W, H, D))
     assert np.isfinite(a).all() and a[..., :3].max() > 0
     diff = a.view(np.uint32) != b.view(np.uint32)
@@ -100,6 +101,18 @@ def test_bdpt_frames_match_64b_records(hip_ctx, sm_small):
     p = _with_env({"MCRT_QUANT_NODES": "0"}, lambda: _frames(*args))[0]
     assert np.isfinite(q).all() and q[..., :3].max() > 0
     np.testing.assert_allclose(q[..., :3], p[..., :3], rtol=4e-6, atol=4e-6)
+
+
+@pytest.mark.parametrize("cap,lanes", [("1", "64"), ("60", "8")])
+def test_bdpt_capped_walks_match(hip_ctx, sm_small, cap, lanes):
+    """BDPT's closest-hit launches (k_extend, the light rays of k_extend_pair) with the stop rule on
+    (at any call size; cap 1 suspends nearly every walk): the same hits, so the frames equal those
+    without it up to the order of the light-tracing splats' float atomics."""
+    args = (hip_ctx, sm_small, "san_miguel_proxy", 256, 144, 2, T.INTEGRATOR_BDPT)
+    a = _with_env({"MCRT_WALK_CAP": cap, "MCRT_WALK_LANES": lanes, "MCRT_WALK_MIN_PATHS": "0"}, lambda: _frames(*args))[0]
+    b = _with_env({"MCRT_WALK_CAP": "0"}, lambda: _frames(*args))[0]
+    assert np.isfinite(a).all() and a[..., :3].max() > 0
+    np.testing.assert_allclose(a[..., :3], b[..., :3], rtol=4e-6, atol=4e-6)
 
 
 @pytest.mark.parametrize("name", ["mixed", "sm"])
