@@ -164,10 +164,15 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
     alg = batch * (n_ext * 48 + n_sh * 80) + node_bytes
     achieved = alg / (avg_ms * 1e-3) / 1e9
     tr = pmc_traffic("k_shadow_extend")
+    rs = pmc_traffic("k_walk_resume")   # the stopped walks' second launch (mcrt_kernels.hip k_walk_resume)
+    if tr is not None and rs is not None:
+        tr["fetch_raw"] += rs["fetch_raw"]
+        tr["write"] += rs["write"]
     traffic = None
     if tr is not None:   # streamed reads: ray (o, d) 32 B, shadow ray 48 B + radiance 16 B
         traffic = calibrated_traffic(tr["fetch_raw"], tr["write"], batch * (n_ext * 32 + n_sh * 64))
-    out = {"bound": "hbm", "kernel": "k_shadow_extend", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+    out = {"bound": "hbm", "kernel": "k_shadow_extend" + (" + k_walk_resume" if rs is not None else ""),
+           "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
            "traffic": None if traffic is None else round(traffic),
            "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(avg_ms, 4),
@@ -182,7 +187,8 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
     if tr is not None:
         out["traffic_source"] = tr["source"]
         out["traffic_rule"] = ("FETCH_SIZE x 1024 (exact for 64-B node gathers, calibrated) + half the launch's "
-                               "streamed ray-record reads (reported at half) + WRITE_SIZE x 1024")
+                               "streamed ray-record reads (reported at half) + WRITE_SIZE x 1024; with "
+                               "k_walk_resume's FETCH_SIZE / WRITE_SIZE added (the HIP-event time covers both)")
         out["traffic_rate_gbs"] = round(traffic / (avg_ms * 1e-3) / 1e9, 1)
         out["traffic_over_alg"] = round(traffic / alg, 2)
         if "limiter" in tr:
@@ -408,6 +414,11 @@ def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s, quant=F
                                     ("32 B per internal / 48 B per leaf compact record" if quant else "64 B per record"),
                            "node_bytes_per_frame": int(node_bytes)}
         pm = pmc_traffic("k_extend", "pmc_bdpt.json", last_launches=2 * (D + 1))
+        rs = pmc_traffic("k_walk_resume", "pmc_bdpt.json", last_launches=2 * (D + 1))
+        if pm and rs and "fetch_raw_last" in pm and "fetch_raw_last" in rs:   # the stopped walks' launches
+            pm["fetch_raw_last"] += rs["fetch_raw_last"]
+            pm["write_last"] += rs["write_last"]
+            out["roofline"]["kernel"] = "k_extend + k_walk_resume (BDPT, D+1 launches each per frame)"
         if pm and "fetch_raw_last" in pm:
             # the counter run's last two calls (2 x (D + 1) k_extend dispatches, interleaved by the
             # two frames in flight; res["frames_per_call"] frames each, the timed calls' shape)

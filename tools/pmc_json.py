@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import dispatches  # noqa: E402
 
 # longest names first: "k_shadow" is a prefix of "k_shadow_extend"
-KERNELS = ["k_shadow_extend", "k_primary", "k_extend", "k_shadow", "k_shade0", "k_shadeN", "k_accumulate",
+KERNELS = ["k_shadow_extend", "k_walk_resume", "k_primary", "k_extend", "k_shadow", "k_shade0", "k_shadeN", "k_accumulate",
            "k_bdpt_start", "k_bdpt_vertex", "k_bdpt_connect", "k_bdpt_vis", "k_bdpt_gather"]
 
 

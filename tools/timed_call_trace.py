@@ -10,7 +10,7 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import dispatches  # noqa: E402
 
-PT = ["k_primary", "k_shade0", "k_shadow_extend", "k_shadeN", "k_shadow", "k_accumulate"]
+PT = ["k_primary", "k_shade0", "k_shadow_extend", "k_walk_resume", "k_shadeN", "k_shadow", "k_accumulate"]
 
 
 def short(name):
@@ -39,6 +39,9 @@ def main(db):
         avg = statistics.mean(x["ms"] for x in per[k])
         print(f"{k:18s} {last['grid']:10d} {last['ms']:10.4f} {last['ms'] / f:9.4f}   {avg:20.4f} {len(per[k]):3d}")
     print(f"{'sum':18s} {'':10s} {tot:10.4f} {tot / (frames or 1):9.4f}   (frames in the timed call: {frames})")
+    if "k_shadow_extend" in per and "k_walk_resume" in per:   # the bench's K_SHADOW_EXTEND events span both
+        both = per["k_shadow_extend"][-1]["ms"] + per["k_walk_resume"][-1]["ms"]
+        print(f"k_shadow_extend + k_walk_resume (the bench's kernel): {both:.4f} ms, {both / (frames or 1):.4f} ms/frame")
 
 
 if __name__ == "__main__":
