@@ -426,9 +426,9 @@ MCRT_API mcrt_status mcrt_accumulate(mcrt_framebuffer fb, const mcrt_filter* fil
  * reads is the one the previous frame wrote (BDPT.cl:585-586), as in count single calls; vertices
  * and own strategies are those of count single calls bit for bit, splat sums up to atomic order.
  * With a band split, mcrt_bdpt_splat_layout's chunk then holds the batch's frames.
- * Memory (PT): each frame slot (2 in flight) holds about 0.7 KB per path of the call (ray queues,
- * hit records and the per-ray traversal stack spill) plus 32 B per pixel and frame: 1080p x 20
- * frames ~ 30 GB per slot.  A call that does not fit fails with the hipMalloc error (nothing is
+ * Memory (PT): each frame slot (2 in flight) holds about 0.8 KB per path of the call (ray queues,
+ * hit records, the per-ray traversal stack spill and, for calls of >= 16 M paths, the stopped
+ * walks' state) plus 32 B per pixel and frame: 1080p x 20 frames ~ 34 GB per slot.  A call that does not fit fails with the hipMalloc error (nothing is
  * rendered; smaller calls still work), e.g. 256 whole 1080p frames; 256 band-frames of a 1/8
  * band share fit. */
 MCRT_API mcrt_status mcrt_render_frames(mcrt_scene scene, mcrt_framebuffer fb, const mcrt_camera* cameras,
