@@ -989,7 +989,8 @@ MCRT_DEV bool quantExp(float lo0, float hi0, float lo1, float hi1, float& o, uin
 }
 // The two children's (lo, hi) on that axis as bytes q with fmaf(q, s, o) <= lo and >= hi exactly as
 // the traversal decodes them; s = the walk's step (qScales: 2^(e - 127) times a mantissa the meta
-// word's lower fields supply, in [1, 1.04)), so 255 s covers the extent.  False if no byte reaches.
+// word's lower fields supply: 1 for x, about 1.24 for y and z), so 255 s covers the extent.
+// False if no byte reaches.
 MCRT_DEV bool quantBytes(float lo0, float hi0, float lo1, float hi1, float o, float sc, uint32_t& bytes) {
     const float b[4] = {lo0, hi0, lo1, hi1};
     bytes = 0;
@@ -1024,7 +1025,13 @@ __global__ __launch_bounds__(256) void k_qnodes_convert(const float4* __restrict
                   quantExp(n2.x, n2.y, n2.z, n2.w, oz, ez) && (uint32_t)w.y < n;
         const uint32_t leaf0 = ok && reinterpret_cast<const int4*>(&nodes[4 * (size_t)w.x + 3])->x < 0 ? 1u : 0u;
         const uint32_t leaf1 = ok && reinterpret_cast<const int4*>(&nodes[4 * (size_t)w.y + 3])->x < 0 ? 1u : 0u;
-        const uint32_t meta = ex | (ey << 9) | (ez << 18) | (leaf0 << 27);
+        // the y and z steps carry a mantissa from the fields below their exponent (qScales: 1 + e_x / 512
+        // for y, 1 + e_y / 512 + e_x / 2^18 for z, about 1.24): one exponent less then often still covers
+        // the extent, which gives those axes the x axis's step sizes (1.44 x the ideal step on average
+        // instead of 1.79); quantBytes decides, y first (z's mantissa depends on e_y)
+        uint32_t meta = ex | (ey << 9) | (ez << 18) | (leaf0 << 27);
+        if (ok && ey > 1 && quantBytes(n0.z, n0.w, n1.z, n1.w, oy, qScales(meta - (1u << 9)).y, by)) meta -= 1u << 9;
+        if (ok && ez > 1 && quantBytes(n2.x, n2.y, n2.z, n2.w, oz, qScales(meta - (1u << 18)).z, bz)) meta -= 1u << 18;
         const QScales sc = qScales(meta);
         ok = ok && quantBytes(n0.x, n0.y, n1.x, n1.y, ox, sc.x, bx) && quantBytes(n0.z, n0.w, n1.z, n1.w, oy, sc.y, by) &&
              quantBytes(n2.x, n2.y, n2.z, n2.w, oz, sc.z, bz);

@@ -406,7 +406,7 @@ MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint3
 // memory pipeline (TA busy 0.94, one cache access per 16-B lane load), not by arithmetic.
 //   internal (32 B): (origin.xyz, right child ref) | (x bytes, y bytes, z bytes, meta): for axis a
 //     the bytes are (child 0 lo, child 0 hi, child 1 lo, child 1 hi) and a bound decodes as
-//     fmaf(q, s_a, origin_a), s_a = qScales(meta) (2^(e_a - 127) up to a mantissa < 1.04); meta =
+//     fmaf(q, s_a, origin_a), s_a = qScales(meta) (2^(e_a - 127) times a mantissa, qScales); meta =
 //     e_x | e_y << 9 | e_z << 18 | leaf(child 0) << 27.  The left child is the next record
 //     (depth-first order, ref + 4); the right child's ref (16-B offset << 1 | leaf bit) is stored.
 //   leaf (48 B): (v0 | shape id), (v1 - v0 | prim id), (v2 - v0 | 64-B record index, bit 31 set when
@@ -415,16 +415,31 @@ MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint3
 //   * every decoded bound is rounded outward (the converter checks each fmaf decode against the
 //     exact bound), and fma rounds monotonically, so a decoded box's slab interval contains the
 //     exact box's: every internal test the exact walk passes, this walk passes;
-//   * at a leaf the EXACT box test runs before the triangle test (the box is min/max of the
-//     vertices v0, v0 + e1, v0 + e2, which the converter checked against the box the parent's 64-B
-//     record stores, else bit 31 sends the lane to that record), so the triangles that can hit are
-//     exactly the exact walk's;
-//   * any hit: the answer (hit or not) is then the exact walk's;
-//   * closest hit: the nearest hit is the same, but equal distances resolve by visit order, which
-//     the outward boxes may change.  A hit within QTIE_EPS of the current closest (either side)
-//     marks a near tie; a walk whose final distance carries a near tie is repeated on the exact
-//     records (traceClosest<LAY_QUANT>), so the reference's order decides it.  The culling distance
-//     is widened by the same margin once a hit exists, so a near-tie candidate is always tested.
+//   * at a leaf, for a triangle that would count (its distance within the culling distance), the
+//     EXACT box test the 64-B walk runs at the parent (the box is min/max of v0, v0 + e1, v0 + e2,
+//     which the converter checked against the box the parent's 64-B record stores, else bit 31
+//     sends the lane to that record);
+//   * any hit: the culling distance is the ray's tmax throughout, so every box decision is the
+//     exact walk's whatever the order, and the answer (hit or not) is the exact walk's;
+//   * closest hit: the reference's answer is the nearest hit unless a triangle's box entry and its
+//     distance, computed differently, disagree: a triangle X hit at t_X whose leaf box enters at
+//     e_X > t_X is culled by the reference if it has already found a hit between t_X and e_X, so
+//     its answer depends on its visit order, which the outward boxes change.  A walk is repeated
+//     on the exact records (traceClosest<LAY_QUANT>, the reference's order) when its final
+//     distance carries a mark:
+//       - a near tie: a hit within 2^-18 of the current closest (either side); the culling
+//         distance is widened by the same margin once a hit exists, so such a candidate is tested;
+//       - an order-dependent pair: a triangle hit nearer than the current closest whose exact box
+//         test fails (the walk holds a hit between its t and e) is taken provisionally with the
+//         mark; an accepted triangle whose entry e exceeds its t by more than the margin widens the
+//         culling distance to e, so any other hit in (t, e] is met and marks a near tie.
+//     What stays open is an order-dependent triangle whose whole subtree the compact walk culls
+//     above the leaf (its ancestors' entries beyond the culling distance):
+//     tests/test_tie_premise_cpu.py enumerates every order-dependent pair of hits beyond the margin
+//     -- none on the headline scene at 1080p; on the same scene moved 1000 units from the origin, 1
+//     ray in 10^5 (a ray leaving a surface nearly parallel to it, whose slab values carry errors of
+//     |o / d| ulp) -- and the GPU tests compare both scenes' frames with the exact walk's bit for
+//     bit (test_gpu_quant_nodes.py).
 // ---------------------------------------------------------------------------
 #define QREF_DONE 0xffffffffu
 #define QTIE_HI (1.0f + 0x1.0p-18f)
@@ -432,8 +447,10 @@ MCRT_DEV int traverse(const TraceCtx& c, const TraceRay& r, uint32_t* stk, uint3
 
 // The three steps of an internal record from its meta word in one shift each: exponent byte e_k
 // at bits 9k..9k+7 with a zero bit above it, so meta << (23 - 9k) puts e_k in the float's exponent
-// and a clear sign bit; the fields below land in the mantissa (x: none; y, z: a factor < 1.04),
-// which the converter (k_qnodes_convert) quantises with, so the decoded bounds stay outward.
+// and a clear sign bit; the fields below land in the mantissa (x: none; y: 1 + e_x / 512, z: 1 +
+// e_y / 512 + e_x / 2^18, about 1.24 for exponents near 127), which the converter (k_qnodes_convert)
+// quantises with -- and takes one exponent less where that still covers the extent -- so the
+// decoded bounds stay outward.
 struct QScales { float x, y, z; };
 MCRT_DEV QScales qScales(uint32_t meta) {
     return QScales{__uint_as_float(meta << 23), __uint_as_float(meta << 14), __uint_as_float(meta << 5)};
@@ -456,34 +473,37 @@ MCRT_DEV float triRaw(const TraceRay& r, float4 A, float4 E1, float4 E2) {
     return temp;
 }
 
-// fast_intersect_bbox2 (intersect_bvh2_lds.cl:54-63) of one box, entry <= exit
+// fast_intersect_bbox2 (intersect_bvh2_lds.cl:54-63) of one box, entry <= exit; `entry` = the
+// clamped entry distance t0 (the compact walk's order-dependence check at a leaf)
 template <int OCT>
-MCRT_DEV bool slabHit(f3 lo, f3 hi, f3 inv, f3 oxi, float t) {
+MCRT_DEV bool slabHit(f3 lo, f3 hi, f3 inv, f3 oxi, float t, float& entry) {
     if constexpr (OCT >= 0) {
         constexpr bool SX = (OCT & 1) != 0, SY = (OCT & 2) != 0, SZ = (OCT & 4) != 0;
         const float xn = fmaf(SX ? hi.x : lo.x, inv.x, oxi.x), xf = fmaf(SX ? lo.x : hi.x, inv.x, oxi.x);
         const float yn = fmaf(SY ? hi.y : lo.y, inv.y, oxi.y), yf = fmaf(SY ? lo.y : hi.y, inv.y, oxi.y);
         const float zn = fmaf(SZ ? hi.z : lo.z, inv.z, oxi.z), zf = fmaf(SZ ? lo.z : hi.z, inv.z, oxi.z);
-        return fmaxf(fmaxf(xn, yn), fmaxf(zn, 0.0f)) <= fminf(fminf(xf, yf), fminf(zf, t));
+        entry = fmaxf(fmaxf(xn, yn), fmaxf(zn, 0.0f));
+        return entry <= fminf(fminf(xf, yf), fminf(zf, t));
     } else {
         const float x0 = fmaf(lo.x, inv.x, oxi.x), x1 = fmaf(hi.x, inv.x, oxi.x);
         const float y0 = fmaf(lo.y, inv.y, oxi.y), y1 = fmaf(hi.y, inv.y, oxi.y);
         const float z0 = fmaf(lo.z, inv.z, oxi.z), z1 = fmaf(hi.z, inv.z, oxi.z);
-        return fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), 0.0f) <=
-               fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), t);
+        entry = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), 0.0f);
+        return entry <= fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), t);
     }
 }
 
 // The exact box of 64-B leaf `leaf` as its parent's record stores it (the rare leaves whose box the
 // compact record cannot reproduce; the root leaf has no box test, as in the exact walk)
-MCRT_DEV bool parentBoxHit(const TraceCtx& c, uint32_t leaf, f3 inv, f3 oxi, float t) {
+MCRT_DEV bool parentBoxHit(const TraceCtx& c, uint32_t leaf, f3 inv, f3 oxi, float t, float& entry) {
     const int par = reinterpret_cast<const int4*>(&c.nodes[4 * leaf + 3])->y;
+    entry = 0.0f;
     if (par < 0) return true;
     const float4 p0 = c.nodes[4 * par], p1 = c.nodes[4 * par + 1], p2 = c.nodes[4 * par + 2];
     const bool right = reinterpret_cast<const int4*>(&c.nodes[4 * par + 3])->y == (int)leaf;
     const f3 lo = right ? f3{p1.x, p1.z, p2.z} : f3{p0.x, p0.z, p2.x};
     const f3 hi = right ? f3{p1.y, p1.w, p2.w} : f3{p0.y, p0.w, p2.y};
-    return slabHit<-1>(lo, hi, inv, oxi, t);
+    return slabHit<-1>(lo, hi, inv, oxi, t, entry);
 }
 
 // The loop state of a compact walk: the next record, the hit so far and the stack (LDS entries
@@ -602,26 +622,31 @@ MCRT_DEV void qwalk(const TraceCtx& c, const TraceRay& r, f3 inv, uint32_t* stk,
             const float th = r.mask != __float_as_int(a.w) ? triRaw(r, a, e1, e2) : __builtin_inff();   // RR_RAY_MASK
             if (th <= tc) {
                 bool boxHit;
+                float ent;
                 if (w >> 31) {
-                    boxHit = parentBoxHit(c, w & 0x7fffffffu, inv, oxi, tc);
+                    boxHit = parentBoxHit(c, w & 0x7fffffffu, inv, oxi, tc, ent);
                 } else {
                     const f3 v0 = ld3(a), v1 = v0 + ld3(e1), v2 = v0 + ld3(e2);
                     const f3 lo = f3{fminf(fminf(v0.x, v1.x), v2.x), fminf(fminf(v0.y, v1.y), v2.y),
                                      fminf(fminf(v0.z, v1.z), v2.z)};
                     const f3 hi = f3{fmaxf(fmaxf(v0.x, v1.x), v2.x), fmaxf(fmaxf(v0.y, v1.y), v2.y),
                                      fmaxf(fmaxf(v0.z, v1.z), v2.z)};
-                    boxHit = slabHit<OCT>(lo, hi, inv, oxi, tc);
+                    boxHit = slabHit<OCT>(lo, hi, inv, oxi, tc, ent);
                 }
-                if (boxHit) {
-                    if (th < t) {
-                        if (!ANY && hit >= 0 && th >= t * QTIE_LO) tieT = th;
-                        t = th;
-                        tc = ANY ? th : th * QTIE_HI;
-                        hit = (int)(w & 0x7fffffffu);
-                        if (ANY) next = QREF_DONE;
-                    } else if (!ANY && hit >= 0 && th <= tc) {
-                        tieT = t;
-                    }
+                // closest hit: a triangle X whose box entry e lies beyond its distance is ORDER-
+                // DEPENDENT in the reference, which culls the leaf at its parent once it holds a hit
+                // nearer than e (intersect_bvh2_lds.cl:128-141).  A nearer X whose box test fails
+                // here (this walk already holds such a hit) is taken provisionally with the repeat
+                // mark; an accepted X with e beyond the tie margin widens the culling distance to
+                // e, so any hit in (t_X, e] is met and marks a near tie (tests/test_tie_premise_cpu.py)
+                if (th < t && (boxHit || !ANY)) {
+                    if (!ANY && (!boxHit || (hit >= 0 && th >= t * QTIE_LO))) tieT = th;
+                    t = th;
+                    tc = ANY ? th : (boxHit && ent > th * QTIE_HI ? ent : th) * QTIE_HI;
+                    hit = (int)(w & 0x7fffffffu);
+                    if (ANY) next = QREF_DONE;
+                } else if (!ANY && hit >= 0) {   // t <= th <= tc: a near tie
+                    tieT = t;
                 }
             }
         }

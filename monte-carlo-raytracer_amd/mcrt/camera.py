@@ -106,3 +106,13 @@ def scene_camera(name, width, height, frame=0, mats=None, jitter=False):
     pos, target, fov = CAMERAS[name]
     off = taa_jitter(frame, mats=mats) if jitter else (0.0, 0.0)
     return make_camera(pos, target, width, height, fovy=fov, pixel_offset=off)
+
+
+def scene_camera_at(name, width, height, offset, frame=0, mats=None, jitter=False):
+    """scene_camera of a scene moved by `offset` (mcrt.scenes.translated)."""
+    from .scenes import CAMERAS
+    pos, target, fov = CAMERAS[name]
+    off = taa_jitter(frame, mats=mats) if jitter else (0.0, 0.0)
+    o = np.asarray(offset, np.float64)
+    return make_camera(tuple(np.asarray(pos) + o), tuple(np.asarray(target) + o), width, height, fovy=fov,
+                       pixel_offset=off)

@@ -838,6 +838,24 @@ def sponza_proxy(tris=262_267, seed=3, tex_size=1024):
     return b.build()
 
 
+def translated(scene, offset):
+    """The same scene moved by `offset` (float32 positions and light anchors; the tests of the
+    compact walk's exactness far from the world origin, where a slab test's error scales with
+    |o / d| rather than with the hit distance).  Identity shape transforms only."""
+    M = scene.shapes["toWorldTransform"]
+    if not np.array_equal(M, np.broadcast_to(np.eye(4, dtype=np.float32), M.shape)):
+        raise NotImplementedError("translated(): shapes with transforms")
+    off = np.asarray(offset, np.float32)
+    pos = scene.positions.copy()
+    pos[:, :3] += off
+    lights = scene.lights.copy()
+    if len(lights):
+        lights["p"][:, :3] += off   # point / spot positions; a directional light's disk centre
+    return Scene(scene.shapes, scene.indices, pos, scene.uvs, scene.normals, scene.tangents, scene.binormals,
+                 scene.colors, scene.textures, scene.tex_data, lights, scene.materials, sobol=scene.sobol,
+                 name=scene.name)
+
+
 CAMERAS = {
     # name: (pos, look-at, fov_y) -- perspective 45 deg, near 0.3 (PathTracingApp.cpp:387)
     "cornell": ((0.0, 1.0, 3.4), (0.0, 1.0, 0.0), 45.0),

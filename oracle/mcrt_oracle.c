@@ -1216,6 +1216,173 @@ void orc_trace_any(orc_scene* s, const mcrt_ray* rays, int n, int32_t* hits, int
 }
 
 /* ----------------------------------------------------------------------- */
+/* Premise of the compact walk's near-tie repeat (product: mcrt_traverse.h  */
+/* qwalk; checked by tests/test_tie_premise_cpu.py)                         */
+/* ----------------------------------------------------------------------- */
+/* The reference culls a leaf at its parent when the leaf box's entry (fast_intersect_bbox2,
+ * intersect_bvh2_lds.cl:54-63, the box the parent stores) exceeds the closest distance found so
+ * far (:128-141), and accepts a triangle when its Moller-Trumbore t (common.cl:177-218) is below it.
+ * The two are computed differently, so a triangle X can have t_X < e_X ("irregular"): then a hit Y
+ * with t_X < t_Y < e_X, found before X's parent is visited, culls the nearer X, and the answer
+ * depends on the visit order -- which the compact walk's outward boxes change.  The near-tie repeat
+ * (a hit within alpha = 2^-18 of the final distance sends the ray to the exact records) covers such
+ * a pair only when t_Y - t_X <= alpha t_Y.  For every ray this enumerates ALL triangle hits up to
+ * twice the reference's distance (padded boxes, no culling) with the product's arithmetic (fma
+ * dot / cross as triRaw and cl_dot; v_rcp restated as 1/x) and reports, per ray, 6 floats:
+ *   [0] the reference walk's distance t_R (+inf: no hit -- then nothing depends on the order)
+ *   [1] the largest (t_Y - t_X) / t_Y over ORDER-DEPENDENT pairs: X with t_X <= t_R (1 + alpha), Y
+ *       an acceptable hit with t_X < t_Y < e_X (-1: none); the premise is [1] <= alpha
+ *   [2] the largest (e_X - t_X) / t_X over the enumerated hits (0: none irregular)
+ *   [3] hits enumerated  [4] irregular hits among them
+ *   [5] 1 when the check is incomplete for the ray (a hit list overflow, or some X with e_X beyond
+ *       the enumerated range), else 0 */
+#define PREMISE_MAXHITS 2048
+static inline float dotG(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static inline v3 crossG(v3 a, v3 b) {
+    return V3(fmaf(a.y, b.z, b.y * -a.z), fmaf(a.z, b.x, b.z * -a.x), fmaf(a.x, b.y, b.x * -a.y));
+}
+/* the product's triRaw (mcrt_traverse.h): the distance, or +inf */
+static float triGpu(const Ray* r, const RRNode* n) {
+    v3 a = load3a(n->lmin_v0);
+    v3 e1 = vsub(load3a(n->lmax_v1), a), e2 = vsub(load3a(n->rmin_v2), a);
+    v3 s1 = crossG(r->d, e2);
+    float denom = dotG(s1, e1);
+    if (denom == 0.f) return INFINITY;
+    float invd = 1.0f / denom;
+    v3 d = vsub(r->o, a);
+    float b1 = dotG(d, s1) * invd;
+    v3 s2 = crossG(d, e1);
+    float b2 = dotG(r->d, s2) * invd;
+    float temp = dotG(e2, s2) * invd;
+    if (b1 < 0.f || b1 > 1.f || b2 < 0.f || b1 + b2 > 1.f || temp < 0.f) return INFINITY;
+    return temp;
+}
+/* the slab interval of a padded box in double (enumeration only: contains every hit point) */
+static int paddedOverlap(const float* lo, const float* hi, v3 o, v3 d, double T) {
+    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    double t0 = 0.0, t1 = T;
+    for (int a = 0; a < 3; ++a) {
+        const double pad = 1e-4 * (fabs((double)lo[a]) + fabs((double)hi[a])) + 1e-6;
+        const double l = lo[a] - pad, h = hi[a] + pad;
+        if (fabs(dd[a]) < 1e-30) {
+            if (oo[a] < l || oo[a] > h) return 0;
+            continue;
+        }
+        double u0 = (l - oo[a]) / dd[a], u1 = (h - oo[a]) / dd[a];
+        if (u0 > u1) { double s = u0; u0 = u1; u1 = s; }
+        if (u0 > t0) t0 = u0;
+        if (u1 < t1) t1 = u1;
+        if (t0 > t1) return 0;
+    }
+    return 1;
+}
+typedef struct { float t, e; int ok; } PHit;
+static void premise_one(const orc_scene* s, const Ray* r, float alpha, uint32_t* stack, float* out) {
+    const RRNode* nodes = s->nodes;
+    out[0] = INFINITY; out[1] = -1.0f; out[2] = 0.0f; out[3] = 0.0f; out[4] = 0.0f; out[5] = 0.0f;
+    /* 1. the reference walk (traceClosest with the product's triangle arithmetic) */
+    v3 inv = safe_invdir(r->d);
+    v3 oxinv = V3(-r->o.x * inv.x, -r->o.y * inv.y, -r->o.z * inv.z);
+    float tR = r->tmax;
+    int found = 0;
+    uint32_t addr = 0;
+    int sp = 0;
+    stack[sp++] = INVALID_ADDR;
+    while (addr != INVALID_ADDR) {
+        const RRNode* node = &nodes[addr];
+        if (node->addr_left != INVALID_ADDR) {
+            float a0, a1, b0, b1;
+            bbox2(node->lmin_v0, node->lmax_v1, inv, oxinv, tR, &a0, &a1);
+            bbox2(node->rmin_v2, node->rmax, inv, oxinv, tR, &b0, &b1);
+            int tc0 = a0 <= a1, tc1 = b0 <= b1;
+            int c1first = tc1 && (a0 > b0);
+            if (tc0 || tc1) {
+                uint32_t deferred;
+                if (c1first || !tc0) { addr = node->addr_right; deferred = node->addr_left; }
+                else { addr = node->addr_left; deferred = node->addr_right; }
+                if (tc0 && tc1) stack[sp++] = deferred;
+                continue;
+            }
+        } else if (r->mask != (int)node->mesh_id) {
+            float t = triGpu(r, node);
+            if (t < tR) { tR = t; found = 1; }
+        }
+        addr = stack[--sp];
+    }
+    if (!found) return;   /* no hit: every candidate was culled by tmax alone, in any order */
+    out[0] = tR;
+    /* 2. every hit up to T: padded boxes, no culling; per hit its leaf box entry e as the
+     *    reference computes it at the parent (t0 of fast_intersect_bbox2) */
+    const double T = fmin((double)r->tmax, 2.0 * (double)tR + 1e-3);
+    PHit hits[PREMISE_MAXHITS];
+    int nh = 0, incomplete = 0;
+    if (nodes[0].addr_left == INVALID_ADDR) return;   /* a root leaf has no box test */
+    sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const RRNode* node = &nodes[stack[--sp]];
+        for (int side = 0; side < 2; ++side) {
+            const float* lo = side ? node->rmin_v2 : node->lmin_v0;
+            const float* hi = side ? node->rmax : node->lmax_v1;
+            const uint32_t ch = side ? node->addr_right : node->addr_left;
+            if (!paddedOverlap(lo, hi, r->o, r->d, T)) continue;
+            const RRNode* c = &nodes[ch];
+            if (c->addr_left != INVALID_ADDR) {
+                if (sp < 4000) stack[sp++] = ch; else incomplete = 1;
+                continue;
+            }
+            if (r->mask == (int)c->mesh_id) continue;
+            const float th = triGpu(r, c);
+            if (!(th <= T)) continue;
+            float e0, e1;
+            bbox2(lo, hi, inv, oxinv, INFINITY, &e0, &e1);
+            if (nh == PREMISE_MAXHITS) { incomplete = 1; continue; }
+            /* acceptable at all: its box passes at some culling distance <= tmax (the far side and
+             * tmax do not depend on the order) */
+            hits[nh].t = th;
+            hits[nh].e = e0;
+            hits[nh].ok = e0 <= e1 && e0 <= r->tmax && th < r->tmax;
+            ++nh;
+        }
+    }
+    float worstGap = -1.0f, worstIrr = 0.0f;
+    int nirr = 0;
+    for (int i = 0; i < nh; ++i) {
+        const PHit X = hits[i];
+        if (X.e > X.t) {
+            ++nirr;
+            const float irr = (X.e - X.t) / X.t;
+            if (irr > worstIrr) worstIrr = irr;
+        }
+        if (!(X.t <= tR * (1.0f + alpha)) || !(X.e > X.t)) continue;
+        if ((double)X.e > T) incomplete = 1;
+        for (int j = 0; j < nh; ++j) {
+            const PHit Y = hits[j];
+            if (j == i || !Y.ok || !(Y.t > X.t) || !(Y.t < X.e)) continue;
+            const float gap = (Y.t - X.t) / Y.t;
+            if (gap > worstGap) worstGap = gap;
+        }
+    }
+    out[1] = worstGap;
+    out[2] = worstIrr;
+    out[3] = (float)nh;
+    out[4] = (float)nirr;
+    out[5] = (float)incomplete;
+}
+typedef struct { const orc_scene* s; const mcrt_ray* rays; float* out; float alpha; } PremiseCtx;
+static void premise_fn(void* c, int64_t i, uint32_t* stack) {
+    PremiseCtx* p = (PremiseCtx*)c;
+    Ray r = loadRay(&p->rays[i]);
+    float* o = p->out + 6 * i;
+    if (!r.active) { o[0] = INFINITY; o[1] = -1.0f; o[2] = o[3] = o[4] = o[5] = 0.0f; return; }
+    premise_one(p->s, &r, p->alpha, stack, o);
+}
+void orc_tie_premise(orc_scene* s, const mcrt_ray* rays, int n, float alpha, float* out, int threads) {
+    PremiseCtx p = {s, rays, out, alpha};
+    parallel_for(n, threads, 64, premise_fn, &p);
+}
+
+/* ----------------------------------------------------------------------- */
 /* Brute force: RRT/utils.cpp:44-189 (TestIntersections / TestOcclusions)   */
 /* ----------------------------------------------------------------------- */
 void orc_brute_closest(orc_scene* s, const mcrt_ray* rays, int n, mcrt_intersection* hits) {

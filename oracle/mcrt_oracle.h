@@ -50,6 +50,9 @@ int64_t orc_bvh_nodes(orc_scene* s, void* out, int64_t max_nodes);
 void orc_trace_closest(orc_scene* s, const mcrt_ray* rays, int n, mcrt_intersection* hits, int32_t* visits, int threads);
 void orc_trace_any(orc_scene* s, const mcrt_ray* rays, int n, int32_t* hits, int32_t* visits, int threads);
 
+/* Premise of the compact walk's near-tie repeat: 6 floats per ray (layout at orc_tie_premise in
+ * mcrt_oracle.c; tests/test_tie_premise_cpu.py). */
+void orc_tie_premise(orc_scene* s, const mcrt_ray* rays, int n, float alpha, float* out, int threads);
 /* RR UnitTest/utils.cpp brute force (world-space triangles of all shapes). */
 void orc_brute_closest(orc_scene* s, const mcrt_ray* rays, int n, mcrt_intersection* hits);
 void orc_brute_any(orc_scene* s, const mcrt_ray* rays, int n, int32_t* hits);

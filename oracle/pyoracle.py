@@ -46,6 +46,7 @@ def lib():
         L.orc_trace_closest.argtypes = [_vp, _vp, _c.c_int, _vp, _vp, _c.c_int]
         L.orc_trace_any.argtypes = [_vp, _vp, _c.c_int, _vp, _vp, _c.c_int]
         L.orc_brute_closest.argtypes = [_vp, _vp, _c.c_int, _vp]
+        L.orc_tie_premise.argtypes = [_vp, _vp, _c.c_int, _c.c_float, _vp, _c.c_int]
         L.orc_brute_any.argtypes = [_vp, _vp, _c.c_int, _vp]
         L.orc_render_frame.argtypes = [_vp, _vp, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _vp, _vp]
         L.orc_set_touched.argtypes = [_vp, _vp]
@@ -113,6 +114,14 @@ class OracleScene:
         v = np.zeros(len(rays), np.int32) if visits else None
         lib().orc_trace_any(self.h, _p(rays), len(rays), _p(out), _p(v), threads)
         return (out, v) if visits else out
+
+    def tie_premise(self, rays, alpha=2.0 ** -18, threads=8):
+        """Per ray (n, 6) float32: the reference walk's distance, the largest relative gap of an
+        order-dependent hit pair (-1: none), the largest relative irregularity of a hit's leaf box
+        entry, hits enumerated, irregular hits, incomplete flag (orc_tie_premise in mcrt_oracle.c)."""
+        out = np.zeros((len(rays), 6), np.float32)
+        lib().orc_tie_premise(self.h, _p(rays), len(rays), alpha, _p(out), threads)
+        return out
 
     def brute_closest(self, rays):
         from mcrt.types import ISECT_DTYPE

@@ -57,3 +57,28 @@ def closest_agreement(a, b, tol_dt2=1e-5):
     hit = (a["shapeid"] >= 0) & eq
     dt2 = ((a["uvwt"][hit, 3].astype(np.float64) - b["uvwt"][hit, 3]) ** 2)
     return eq.mean(), (dt2.max() if dt2.size else 0.0)
+
+
+def path_rays(oscene, cam, frame=0, max_depth=2, threads=8):
+    """The camera rays (bounce 0) and extension rays (bounce 1 ..) the oracle's PT traces for one
+    frame of `cam` (its path log: o, d, tmax of the ray traced for each bounce's hit), as RAY_DTYPE
+    arrays with mask -1 (PT rays, mcrt_kernels.hip), one per bounce."""
+    W, H = int(cam["width"][0]), int(cam["height"][0])
+    log = oscene.path_log(W, H, max_depth)
+    try:
+        oscene.render(cam, frame=frame, max_depth=max_depth, threads=threads)
+        log = log.copy()
+    finally:
+        oscene.path_log(None)
+    out = []
+    for b in range(max_depth):
+        rec = log[:, b]
+        live = rec[:, 0].view(np.int32) != -2
+        r = np.zeros(int(live.sum()), T.RAY_DTYPE)
+        r["o"][:, :3] = rec[live, 24:27]
+        r["o"][:, 3] = rec[live, 30]
+        r["d"][:, :3] = rec[live, 27:30]
+        r["extra"][:, 0] = -1
+        r["extra"][:, 1] = 1
+        out.append(r)
+    return out

@@ -13,7 +13,7 @@ import pytest
 from helpers import random_rays
 from mcrt import scenes
 from mcrt import types as T
-from mcrt.camera import scene_camera
+from mcrt.camera import scene_camera, scene_camera_at
 
 pytestmark = pytest.mark.gpu
 
@@ -36,14 +36,18 @@ def sm_small():
     return scenes.san_miguel_proxy(tris=1_000_000)
 
 
-def _frames(hip_ctx, sc, name, W, H, D, integrator=T.INTEGRATOR_PT, calls=2, batch=4, counts=False):
+FAR = (1000.0, 1000.0, 1000.0)   # the proxy moved away from the world origin (tests/test_tie_premise_cpu.py)
+
+
+def _frames(hip_ctx, sc, name, W, H, D, integrator=T.INTEGRATOR_PT, calls=2, batch=4, counts=False, offset=None):
     from mcrt import lib
     ds = lib.DeviceScene(hip_ctx, sc)
     info = ds.info()
     fb = lib.FrameBuffer(hip_ctx, W, H)
     out, retr, rays = [], 0, 0
     for c in range(calls):
-        cams = [scene_camera(name, W, H, frame=c * batch + k, jitter=True) for k in range(batch)]
+        cams = [scene_camera(name, W, H, frame=c * batch + k, jitter=True) if offset is None else
+                scene_camera_at(name, W, H, offset, frame=c * batch + k, jitter=True) for k in range(batch)]
         if counts:
             hip_ctx.set_profiling(2)
         fb.render_frames(ds, cams, frame=c * batch, max_depth=D, integrator=integrator)
@@ -61,18 +65,25 @@ def _frames(hip_ctx, sc, name, W, H, D, integrator=T.INTEGRATOR_PT, calls=2, bat
 CASES = [("mixed", 96, 64, 3), ("mixed", 64, 48, 5), ("sm", 256, 144, 2), ("sm", 256, 144, 4)]
 
 
-@pytest.mark.parametrize("name,W,H,D", CASES)
+@pytest.mark.parametrize("name,W,H,D", CASES + [("sm_far", 256, 144, 2), ("sm_far", 480, 270, 3)])
 def test_pt_frames_identical_to_64b_records(hip_ctx, sm_small, name, W, H, D):
-    sc, cam = (scenes.test_scene(), "mixed") if name == "mixed" else (sm_small, "san_miguel_proxy")
-    q, info_q, retr, rays = _with_env({"MCRT_QUANT_NODES": "1"}, lambda: _frames(hip_ctx, sc, cam, W, H, D, counts=True))
-    p, info_p, _, _ = _with_env({"MCRT_QUANT_NODES": "0"}, lambda: _frames(hip_ctx, sc, cam, W, H, D))
+    """sm_far: the proxy 1000 units from the origin, where slab tests carry errors of |o / d| ulp and
+    the reference's closest hit can depend on its visit order (mcrt_traverse.h, compact records)."""
+    off = FAR if name == "sm_far" else None
+    sc, cam = ((scenes.test_scene(), "mixed") if name == "mixed" else
+               (sm_small if off is None else scenes.translated(sm_small, off), "san_miguel_proxy"))
+    q, info_q, retr, rays = _with_env({"MCRT_QUANT_NODES": "1"},
+                                      lambda: _frames(hip_ctx, sc, cam, W, H, D, counts=True, offset=off))
+    p, info_p, _, _ = _with_env({"MCRT_QUANT_NODES": "0"}, lambda: _frames(hip_ctx, sc, cam, W, H, D, offset=off))
     assert info_q["bytes"] > info_p["bytes"], "compact records not built"
     assert np.isfinite(q).all() and q[..., :3].max() > 0
     diff = q.view(np.uint32) != p.view(np.uint32)
     assert not diff.any(), f"{int(diff.any(-1).sum())} pixels differ"
-    # near ties (two hits within 2^-18 of the distance: crossing or overlapping surfaces) are rare:
-    # 0.18 % of the 1 M-triangle proxy's extension rays
-    assert rays > 0 and retr <= max(8, rays // 100), (retr, rays)
+    # repeats (near ties: two hits within 2^-18 of the distance, crossing or overlapping surfaces;
+    # order-dependent candidates) are rare at the origin: 0.18 % of the 1 M-triangle proxy's
+    # extension rays; far from it, where flat boxes' entries carry large slab errors, more
+    lim = rays // 100 if off is None else rays // 3
+    assert rays > 0 and retr <= max(8, lim), (retr, rays)
 
 
 @pytest.mark.parametrize("cap,lanes", [("1", "64"), ("17", "64"), ("60", "8"), ("8", "48")])
@@ -115,13 +126,14 @@ def test_bdpt_capped_walks_match(hip_ctx, sm_small, cap, lanes):
     np.testing.assert_allclose(a[..., :3], b[..., :3], rtol=4e-6, atol=4e-6)
 
 
-@pytest.mark.parametrize("name", ["mixed", "sm"])
+@pytest.mark.parametrize("name", ["mixed", "sm", "sm_far"])
 def test_queries_identical_to_64b_records(hip_ctx, sm_small, name):
     """mcrt_trace_closest / mcrt_trace_any over random rays (RadeonRays' query API) with and without
-    the compact records: the same hit records bit for bit."""
+    the compact records: the same hit records bit for bit (sm_far: the proxy 1000 units from the
+    origin)."""
     import torch
     from mcrt import lib
-    sc = scenes.test_scene() if name == "mixed" else sm_small
+    sc = scenes.test_scene() if name == "mixed" else sm_small if name == "sm" else scenes.translated(sm_small, FAR)
     rays = random_rays(sc, 50_000, seed=5)
     n = len(rays)
 
