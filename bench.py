@@ -316,27 +316,21 @@ def bdpt_section(ctx, ds, cam_of, W, H, D, sampler, world, rank, steps, warmup, 
     ctx.sync()
     if world > 1:
         acc_buf, acc_s, acc_w = mdist.packed_accumulators(W * H, "cuda")
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(f0, steps)
-    if world > 1:
+
+    def end_of_job(warm):   # ONE reduce of the packed accumulators into rank 0
         fb.copy_device(1, acc_s.data_ptr())
         fb.copy_device(3, acc_w.data_ptr())
         ctx.sync()
         mdist.reduce_packed(acc_buf, dst=0)
-        if rank == 0:
+        if rank == 0 and not warm:
             torch.cuda.synchronize()
             fb.set_accumulation(acc_s.data_ptr(), acc_w.data_ptr())
-    ctx.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+
+    def sync():
+        ctx.sync()
+        torch.cuda.synchronize()
+
+    el = timed_region(lambda: run(f0, steps), end_of_job, world, sync)
     st = fb.stats()
     out = {"value": round(W * H * steps * (1 if band else world) / el / 1e6, 3), "unit": "Mpaths/s", "steps": steps,
            # the band split divides each frame (strong scaling, also its 1-rank case); --bdpt-split
@@ -441,6 +435,43 @@ def bdpt_roofline_and_cpu(scene, oracle, cam_of, W, H, D, res, target_s, quant=F
                                      f"BDPT.cl (RTBDPTPass order) + RR Bvh2/LDS traversal, {threads} threads, {el:.1f}s "
                                      f"(frame 0, {first_s:.1f}s with node marking, not timed)"}
     return out
+
+
+def timed_region(render, end_of_job, world, sync, device="cuda", trace=None):
+    """The bench contract's timed region: barrier + sync, render, the job's ONE end collective, sync +
+    barrier, max over ranks.  With N > 1 ranks the end collective runs once more BEFORE the timed
+    region, untimed and without applying its result (end_of_job(warm=True)): RCCL sets up a pair of
+    ranks' point-to-point connections on their first send/recv, and the gather is the job's only
+    send/recv (dist.barrier() is an all-reduce), so without this the first-use setup would fall inside
+    the ~24 ms N = 8 timed region.  render(): the timed steps; end_of_job(warm): the collective;
+    sync(): every device stream of this rank drained.  trace (a list): the events in order, for the
+    tests.  Returns the elapsed seconds (max over ranks)."""
+    import torch
+    import torch.distributed as dist
+    ev = trace.append if trace is not None else (lambda e: None)
+    if world > 1:
+        end_of_job(True)
+        ev("end_collective:warm")
+        sync()
+        dist.barrier()
+    sync()
+    ev("t_start")
+    t0 = time.perf_counter()
+    render()
+    ev("render")
+    if world > 1:
+        end_of_job(False)
+        ev("end_collective:timed")
+    sync()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ev("t_end")
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
 
 
 def launch_ranks(n):
@@ -690,33 +721,29 @@ def main():
             band_send, band_recv = mdist.band_buffers(H, W, args.band_rows, world, "cuda")
         else:
             acc_buf, acc_s, acc_w = mdist.packed_accumulators(W * H, "cuda")   # one buffer -> one reduce
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    run(frame0, args.steps * fps)
-    if world > 1:   # one collective: each rank's own band rows gathered to rank 0 (north star)
-        # no try/except here: a fallback taken by one rank while the others sit in the gather would
-        # hang the job; an error exits this rank and torch.distributed.run stops the others
+
+    def end_of_job(warm):
+        # one collective: each rank's own band rows gathered to rank 0 (north star).  No try/except:
+        # a fallback taken by one rank while the others sit in the gather would hang the job; an
+        # error exits this rank and torch.distributed.run stops the others.  warm: the untimed first
+        # use before the timed region, result not applied (timed_region)
         if args.end_collective == "gather":
             # rows packed straight from the frame buffer, unpacked in place on rank 0 (+ image)
-            mdist.gather_bands_fb(ctx, fb, H, W, args.band_rows, band_send, band_recv, dst=0)
+            mdist.gather_bands_fb(ctx, fb, H, W, args.band_rows, band_send, band_recv, dst=0, apply=not warm)
         else:
             fb.copy_device(1, acc_s.data_ptr())
             fb.copy_device(3, acc_w.data_ptr())
             ctx.sync()
             mdist.reduce_packed(acc_buf, dst=0)
-            if rank == 0:
+            if rank == 0 and not warm:
                 torch.cuda.synchronize()
                 fb.set_accumulation(acc_s.data_ptr(), acc_w.data_ptr())
-    ctx.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+
+    def sync():
+        ctx.sync()
+        torch.cuda.synchronize()
+
+    elapsed = timed_region(lambda: run(frame0, args.steps * fps), end_of_job, world, sync)
     if args.save_image and rank == 0:
         np.save(args.save_image, fb.read(2))
     kstats = {}

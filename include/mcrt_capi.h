@@ -521,7 +521,8 @@ MCRT_API mcrt_status mcrt_framebuffer_retrace_counts(mcrt_framebuffer fb, int32_
 /* Diagnostics: with MCRT_WAVE_CLOCK=1 in the environment, the last PT call's launches record each
  * workgroup's (start, end) on the constant 100-MHz clock (s_memrealtime, low 32 bits); which = 0
  * camera launch, 1 bounce-0 shadow + extension launch (extension workgroups), 2 last-bounce shadow
- * launch.  Copies min(max_blocks, *blocks) pairs; (0, 0) = a workgroup that had no work. */
+ * launch.  Copies min(max_blocks, *blocks) pairs; (0, 0) = a workgroup that had no work.  While
+ * MCRT_WAVE_CLOCK is set every render keeps ONE frame in flight (the buffers are per frame buffer). */
 MCRT_API mcrt_status mcrt_framebuffer_wave_clock(mcrt_framebuffer fb, int which, uint32_t* host_out, int64_t max_blocks,
                                                  int64_t* blocks);
 /* Host copy of a ray queue of the last render (the state the reference keeps in its

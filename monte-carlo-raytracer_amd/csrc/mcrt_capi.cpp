@@ -1547,6 +1547,10 @@ static bool longest_first() {
 }
 
 static int frames_in_flight(mcrt_framebuffer fb, const FrameArgs& f) {
+    // MCRT_WAVE_CLOCK=1: one frame in flight -- the clock buffers are per frame buffer, so two slots'
+    // launches in flight would write the same per-workgroup entries
+    static const bool clocks = [] { const char* e = std::getenv("MCRT_WAVE_CLOCK"); return e && std::atoi(e) != 0; }();
+    if (clocks) return 1;
     int n = fb->framesInFlight;
     if (n <= 0) n = 2;
     return std::max(1, std::min(n, MCRT_MAX_FRAMES_IN_FLIGHT));
@@ -2367,6 +2371,12 @@ MCRT_API mcrt_status mcrt_bdpt_splats_sparse(mcrt_framebuffer fb, void* d_dst, i
         total += h[r];
     }
     if (!d_dst || capacity < total) return MCRT_OK;   // sizes only (the caller grows its buffer and calls again)
+    // the caller's send buffer may still be read by an earlier call's all-to-all on another frame
+    // slot's stream (two frames in flight), and that call's unpack must read its receive buffer
+    // before this call's all-to-all (ordered after this grouping on this stream) overwrites it: wait
+    // for every other slot's completed frame, as mcrt_bdpt_splats_copy does
+    for (auto& k : fb->slot)
+        if (k.stream && k.stream != st) HIPCHK(ctx, hipStreamWaitEvent(st, k.done, 0));
     mcrt::launch_splat_group(b, off, bs.splatAux + 64, (float4*)d_dst, st);
     HIPCHK(ctx, hipGetLastError());
     return MCRT_OK;   // grouping enqueued on the frame's stream

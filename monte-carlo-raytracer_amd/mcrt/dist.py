@@ -129,19 +129,30 @@ def exchange_splats(fb, full, chunk, group=None):
 
 
 class SparseSplatBuffers:
-    """Growable device buffers of exchange_splats_sparse (send and receive records, 4 floats each)."""
+    """Growable device buffers of exchange_splats_sparse (send and receive records, 4 floats each).
+    A buffer that grows is not freed: an earlier call's all-to-all or unpack on another frame slot's
+    stream may still use it, and torch's caching allocator would hand its memory out again at once
+    (it only tracks torch's own streams).  The retired buffers are kept until release(), which the
+    caller may invoke after a device synchronisation (growth is geometric, so they are few)."""
 
     def __init__(self, device="cuda"):
         self.device = device
         self.bufs = {}
+        self.retired = []
 
     def get(self, name, records):
         import torch
         b = self.bufs.get(name)
         if b is None or b.numel() < 4 * records:
+            if b is not None:
+                self.retired.append(b)
             b = torch.empty(4 * max(records + records // 4, 1024), dtype=torch.float32, device=self.device)
             self.bufs[name] = b
         return b
+
+    def release(self):
+        """Drops the retired buffers; only after every stream that used them has completed."""
+        self.retired.clear()
 
 
 def exchange_splats_sparse(fb, bufs, group=None):
@@ -262,7 +273,7 @@ def band_buffers(height, width, band_rows, world, device):
             torch.empty(world * maxr * 5 * width, dtype=torch.float32, device=device))
 
 
-def gather_bands_fb(ctx, fb, height, width, band_rows, send, recv, dst=0, group=None):
+def gather_bands_fb(ctx, fb, height, width, band_rows, send, recv, dst=0, group=None, apply=True):
     """gather_bands without the full-frame copies: the rank's own rows are packed straight from
     its frame buffer (mcrt_framebuffer_bands_pack, on the context stream after the last
     accumulate: ONE kernel instead of two full-frame copies plus row gathers), ONE gather brings
@@ -270,7 +281,10 @@ def gather_bands_fb(ctx, fb, height, width, band_rows, send, recv, dst=0, group=
     recomputes the image (mcrt_framebuffer_bands_unpack: one kernel instead of a scatter per rank
     and a copy back).  The collective runs on torch's current stream between two host
     synchronisations, as gather_bands.  send / recv: band_buffers (recv is only used on dst).
-    Same bits as gather_bands and as one GPU rendering the whole image."""
+    Same bits as gather_bands and as one GPU rendering the whole image.  apply=False: the same pack
+    and collective on the same buffers without the unpack (bench.py runs it once before timing, so
+    the collective's first-use setup -- RCCL's peer connections -- stays out of the timed region and
+    the accumulators are untouched)."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
@@ -293,7 +307,8 @@ def gather_bands_fb(ctx, fb, height, width, band_rows, send, recv, dst=0, group=
     if rank == dst:
         if recv.is_cuda:
             torch.cuda.synchronize(recv.device)
-        fb.bands_unpack(recv.data_ptr(), maxr)
+        if apply:
+            fb.bands_unpack(recv.data_ptr(), maxr)
 
 
 def reduce_accumulators(wsum, wts, dst=0, group=None):

@@ -17,6 +17,8 @@ from mcrt import types as T
 from mcrt.camera import scene_camera
 from oracle import pyoracle as po
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 W, H, FRAMES, BAND_ROWS = 40, 36, 3, 8
 
 
@@ -382,3 +384,59 @@ def test_sparse_splat_exchange_routes_records(tmp_path, world, height):
         key = lambda a: a[np.lexsort(a.view(np.int32).T[::-1])]   # noqa: E731
         assert np.array_equal(key(g).view(np.uint32), key(want).view(np.uint32))
     assert sum(int(z["sent"]) for z in got) == sum(len(fb.rec) for fb in fbs)
+
+
+def _timed_region_worker(rank, world, port, out_path, height, width, band_rows):
+    """bench.timed_region with the PT path's end_of_job (gather_bands_fb) over gloo on the host
+    model of the frame buffer: the trace of events and rank 0's final accumulators."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(5)
+    warm_s = rng.random((height, width, 4), dtype=np.float32)   # the warm-up frames' sums
+    warm_w = rng.random((height, width), dtype=np.float32) + 0.5
+    timed_s = rng.random((height, width, 4), dtype=np.float32)  # what the timed frames add
+    timed_w = rng.random((height, width), dtype=np.float32)
+    rows = mdist.band_rows_of(height, band_rows, world, rank)
+    s = np.zeros_like(warm_s)
+    w = np.zeros_like(warm_w)
+    s[rows], w[rows] = warm_s[rows], warm_w[rows]
+    fb = _FakeBandsFB(s, w, height, width, band_rows, world, rank)
+    send, recv = mdist.band_buffers(height, width, band_rows, world, "cpu")
+    _BUFS[send.data_ptr()], _BUFS[recv.data_ptr()] = send, recv
+    trace, calls = [], []
+
+    def render():   # the timed frames accumulate into the rank's own rows
+        fb.s[rows] += timed_s[rows]
+        fb.w[rows] += timed_w[rows]
+
+    def end_of_job(warm):
+        calls.append(warm)
+        mdist.gather_bands_fb(_NoCtx(), fb, height, width, band_rows, send, recv, dst=0, apply=not warm)
+
+    el = bench.timed_region(render, end_of_job, world, lambda: None, device="cpu", trace=trace)
+    if rank == 0:
+        np.savez(out_path, s=fb.s, w=fb.w, fs=warm_s + timed_s, fw=warm_w + timed_w, el=el,
+                 trace=np.array(trace), calls=np.array(calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_warms_end_collective_before_timing(tmp_path, world):
+    """RCCL sets up point-to-point connections on first use, and the PT job's gather was
+    its first send/recv, inside the timed region.  bench.timed_region (used by bench.py's PT and BDPT
+    paths) issues the end collective once untimed before t_start -- without applying it -- and once
+    timed; rank 0's accumulators are still exactly the whole image's."""
+    out = str(tmp_path / "tr.npz")
+    mp.start_processes(_timed_region_worker, args=(world, _free_port(), out, 40, 16, 8), nprocs=world, join=True,
+                       start_method="spawn")
+    z = np.load(out)
+    assert list(z["trace"]) == ["end_collective:warm", "t_start", "render", "end_collective:timed", "t_end"]
+    assert list(z["calls"]) == [True, False]
+    assert np.array_equal(z["s"].view(np.uint32), z["fs"].view(np.uint32))
+    assert np.array_equal(z["w"].view(np.uint32), z["fw"].view(np.uint32))
+    assert float(z["el"]) > 0

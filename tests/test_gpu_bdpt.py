@@ -436,3 +436,78 @@ def test_bdpt_band_split_sparse_exchange(hip_ctx, ranks):
     for fb in fbs + [full]:
         fb.close()
     ds.close()
+
+
+def test_sparse_exchange_two_frames_in_flight(hip_ctx):
+    """The sparse splat exchange with two frames in flight and no host synchronisation between calls
+    (ADVICE r5): two band frame buffers (2 ranks emulated on one GPU) exchange their records through
+    growable mcrt.dist.SparseSplatBuffers with device copies ordered on the frame streams, as the
+    RCCL all-to-all runs (mcrt.dist.exchange_splats_sparse).  Each call's grouping must wait for the
+    other slot's call (mcrt_bdpt_splats_sparse), and a grown buffer must outlive its last use; the
+    accumulated images equal a run that synchronises the device after every step, within the splat
+    tolerance."""
+    import torch
+    from mcrt import lib
+    from mcrt import dist as mdist
+    name, W, H, D, B, calls, ranks = "mixed", 96, 64, 2, 2, 6, 2
+    ds = lib.DeviceScene(hip_ctx, build_scene(name))
+    filt = T.make_filter(T.BOX)
+    rows = [mdist.band_rows_of(H, 8, ranks, r) for r in range(ranks)]
+
+    def run(sync):
+        fbs = [lib.FrameBuffer(hip_ctx, W, H) for _ in range(ranks)]
+        bufs = [mdist.SparseSplatBuffers("cuda") for _ in range(ranks)]
+        for fb in fbs:
+            fb.set_splat_exchange(True)
+        for c in range(calls):
+            cams = [scene_camera(name, W, H, frame=c * B + k, jitter=True) for k in range(B)]
+            sends, counts, done = [], [], []
+            for r, fb in enumerate(fbs):
+                fb.render_frames(ds, cams, frame=c * B, max_depth=D, integrator=T.INTEGRATOR_BDPT, band_rows=8,
+                                 num_bands=ranks, band_index=r)
+                # the first call sizes the buffer at its minimum; later calls grow it (retired buffers)
+                send = bufs[r].get("send", 1 if c == 0 else 256 * c)
+                n = fb.bdpt_splats_sparse(send.data_ptr(), send.numel() // 4)
+                if int(n.sum()) > send.numel() // 4:
+                    send = bufs[r].get("send", int(n.sum()))
+                    n = fb.bdpt_splats_sparse(send.data_ptr(), send.numel() // 4)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.ExternalStream(fb.stream()))
+                sends.append(send)
+                counts.append(np.asarray(n, np.int64))
+                done.append(ev)
+                if sync:
+                    torch.cuda.synchronize()
+            for q, fb in enumerate(fbs):   # rank q's receive side of the all-to-all
+                total = int(sum(cnt[q] for cnt in counts))
+                recv = bufs[q].get("recv", total)
+                s = torch.cuda.ExternalStream(fb.stream())
+                at = 0
+                for r in range(ranks):
+                    s.wait_event(done[r])
+                    off = int(counts[r][:q].sum())
+                    k = int(counts[r][q])
+                    if k:
+                        with torch.cuda.stream(s):
+                            recv[4 * at:4 * (at + k)].copy_(sends[r][4 * off:4 * (off + k)])
+                    at += k
+                if sync:
+                    torch.cuda.synchronize()
+                fb.bdpt_gather_sparse(recv.data_ptr(), total)
+                fb.accumulate_frames([filt] * B, c * B)
+        hip_ctx.sync()
+        torch.cuda.synchronize()
+        out = [fb.read(0) for fb in fbs]
+        for fb in fbs:
+            fb.close()
+        return out, sum(len(b.retired) for b in bufs)
+
+    a, retired = run(False)
+    b, _ = run(True)
+    assert retired > 0   # buffers grew while earlier calls could still use them
+    for r in range(ranks):
+        x, y = a[r][rows[r], :, :3], b[r][rows[r], :, :3]
+        assert np.isfinite(x).all() and x.max() > 0
+        close = np.abs(x - y) <= REL_TOL * (np.abs(x) + np.abs(y)) + 1e-30
+        assert close.all(), (r, int((~close).sum()))
+    ds.close()
