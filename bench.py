@@ -202,29 +202,59 @@ def roofline_shadow_extend(scene, cam_of, W, H, D, batch, avg_ms, qcounts, ctx, 
     return out
 
 
-def gather_ceiling(ctx, rl, vq, avg_ms, hint_frac=0.0):
+def gather_ceiling(ctx, rl, vq, avg_ms, hint_frac=0.0, leaf_frac=None):
     """The latency roofline of the traversal launch: its node-visit rate (the launch's rays x the
     oracle's visits per query, over its HIP-event time) against the rate of a pure dependent-gather
-    probe with the same access pattern (mcrt_ctx_gather_chase: chains of 64-B records fetched as
-    four 16-B loads, links read from the record just fetched, 32 waves per CU) with its records
-    resident in L2, in the Infinity Cache, or (the tree's own size) in HBM.  A node visit also
-    does the slab / triangle arithmetic and stack work the probe leaves out.  hint_frac: the share of
-    the launch's shadow rays answered by their occluder hint (two record fetches instead of a walk)."""
+    probe with the same access pattern, 32 waves per CU, with its records resident in L2, in the
+    Infinity Cache, or (the tree's own size) in HBM.  The launch's extension rays walk the compact
+    records (mcrt_traverse.h qwalk: 32-B internal nodes, 48-B leaves fetched in one round trip), its
+    bounce-0 shadow rays the 64-B records (wave packets), so the ceiling is the time-weighted mix of
+    mcrt_ctx_gather_chase_compact (packed 32 / 48-B records, leaf_frac = the oracle's share of leaf
+    visits) and mcrt_ctx_gather_chase (64-B records as four 16-B loads).  A node visit also does the
+    slab / triangle arithmetic and stack work the probes leave out.  hint_frac: the share of the
+    launch's shadow rays answered by their occluder hint (two record fetches instead of a walk)."""
     rays = rl["rays_per_launch"]
     hinted = rays["shadow"] * hint_frac
-    visits = rays["extension"] * vq["k_extend"] + (rays["shadow"] - hinted) * vq["k_shadow"] + 2 * hinted
+    v_ext = rays["extension"] * vq["k_extend"]
+    v_sh = (rays["shadow"] - hinted) * vq["k_shadow"] + 2 * hinted
+    visits = v_ext + v_sh
     rate = visits / (avg_ms * 1e-3) / 1e9
-    out = {"unit": "G dependent 64-B record fetches / s", "node_visits_per_launch": int(visits),
-           "node_visits_per_s": round(rate, 1), "shadow_rays_hinted": round(hint_frac, 4), "ceilings": {}}
+    out = {"unit": "G dependent record fetches / s", "node_visits_per_launch": int(visits),
+           "node_visits_per_s": round(rate, 1), "shadow_rays_hinted": round(hint_frac, 4), "ceilings": {},
+           "visits": {"extension_compact": int(v_ext), "shadow_64b": int(v_sh)}}
+    if leaf_frac is not None:
+        out["extension_leaf_visit_share"] = round(leaf_frac, 4)
     try:
         for name, recs in (("l2_resident_2MiB", 32768), ("infinity_cache_resident_122MiB", 2_000_000),
                            ("hbm_tree_size", int(rl["nodes_total"]))):
-            out["ceilings"][name] = round(ctx.gather_chase_gsteps(recs, 256, 3), 1)
-        out["frac_of_l2_resident"] = round(rate / out["ceilings"]["l2_resident_2MiB"], 4)
-        out["frac_of_infinity_cache_resident"] = round(rate / out["ceilings"]["infinity_cache_resident_122MiB"], 4)
+            c64 = ctx.gather_chase_gsteps(recs, 256, 3)
+            cq = ctx.gather_chase_compact_gsteps(recs, leaf_frac if leaf_frac is not None else 0.5, 256, 3)
+            mix = visits / (v_ext / cq + v_sh / c64)   # G visits / s if every visit ran at the probes' rates
+            out["ceilings"][name] = {"chase_64b": round(c64, 1), "chase_compact": round(cq, 1), "launch_mix": round(mix, 1)}
+        for name in out["ceilings"]:
+            out["frac_of_" + name] = round(rate / out["ceilings"][name]["launch_mix"], 4)
     except Exception as e:   # noqa: BLE001 -- reported, not fatal
         log(f"[bench] gather-chase probe failed: {e}")
     return out
+
+
+def survey_8d_figure(value_mpaths, rays_per_path, vq, D):
+    """SURVEY.md §8(d)'s literal algorithmic bytes per path, B_path = 112 + sum_closest (48 + 32 + 64 V)
+    + sum_any (48 + 4 + 64 V) + sum_shade 388 + sum_bounce 132 + 72, with the line's rays per path and
+    the oracle's visits per query V, and GB/s_alg = Mpaths/s x B_path / 1000.  Reported beside the
+    roofline, not as it: 64 V prices EVERY node visit as an HBM fetch, while the walks revisit the
+    upper tree from L1 / L2 (the counters put the dominant launch's memory-side traffic at ~8x its
+    compulsory bytes but ~1/8 of 64 V), so the figure exceeds the HBM peak."""
+    n_cl, n_any, n_sh = rays_per_path["closest"], rays_per_path["any"], rays_per_path["shaded"]
+    n_prim = 1.0
+    n_ext = max(n_cl - n_prim, 0.0)
+    b = (112 + n_prim * (80 + 64 * vq["k_primary"]) + n_ext * (80 + 64 * vq["k_extend"])
+         + n_any * (52 + 64 * vq["k_shadow"]) + n_sh * 388 + n_any * 132 + 72)
+    gbs = value_mpaths * b / 1000.0
+    return {"bytes_per_path": round(b, 1), "gb_s_alg": round(gbs, 1), "frac_of_peak": round(gbs / HBM_PEAK_GBS, 3),
+            "note": "SURVEY 8(d) B_path with V = the oracle's node visits per query: every visit priced as a 64-B "
+                    "HBM fetch; the walks re-read the upper tree from L1 / L2, so this visit bandwidth exceeds the "
+                    "8 TB/s peak -- the roofline above uses the compulsory bytes and the measured traffic instead"}
 
 
 # FETCH_SIZE x 1024 is exact for the traversal's 64-B node gathers but reports half of a coalesced
@@ -828,6 +858,7 @@ def main():
             out["visits_per_query"] = {"k_primary": round(st[1] / max(st[0], 1), 2),
                                        "k_extend": round(st[3] / max(st[2], 1), 2),
                                        "k_shadow": round(st[5] / max(st[4], 1), 2)}
+            out["leaf_visit_share"] = {"k_extend": round(st[6] / max(st[3], 1), 4), "k_shadow": round(st[7] / max(st[5], 1), 4)}
             out["cpu_baseline"] = {k: v for k, v in cpu.items() if not k.startswith("_")}
             out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 4)
             out["cpu_baseline"]["fidelity"] = {
@@ -853,7 +884,9 @@ def main():
                 if "visits_per_query" in out:
                     hf = hcounts[0] / max(qcounts[0][0], 1) if hcounts else 0.0
                     out["roofline"]["gather_ceiling"] = gather_ceiling(ctx, out["roofline"], out["visits_per_query"],
-                                                                       avg_ms, hf)
+                                                                       avg_ms, hf, out["leaf_visit_share"]["k_extend"])
+                    out["roofline"]["survey_8d"] = survey_8d_figure(value, out["rays_per_path"],
+                                                                    out["visits_per_query"], D)
         if bd is not None:
             bdo = {k: v for k, v in bd.items() if not k.startswith("_")}
             if oracle_ok and sampler == T.SAMPLER_RANDOM and not args.no_cpu_baseline:

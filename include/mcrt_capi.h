@@ -287,6 +287,11 @@ MCRT_API mcrt_status mcrt_ctx_stream_copy(mcrt_ctx ctx, uint64_t bytes, int iter
  * the node-visit rate of the latency-bound traversal kernels (records ~ the tree's node count:
  * served from HBM; ~2 M: Infinity Cache; ~32 K: L2). */
 MCRT_API mcrt_status mcrt_ctx_gather_chase(mcrt_ctx ctx, uint64_t records, int steps, int iters, double* gsteps);
+/* The same probe over the compact records' layout (the per-ray walks, mcrt_traverse.h qwalk):
+ * records of 32 B (an internal node: 2 x 16-B loads) or 48 B (a leaf: 3 loads in the same round
+ * trip, its type carried in the link) packed back to back, a share leaf_frac of them leaves. */
+MCRT_API mcrt_status mcrt_ctx_gather_chase_compact(mcrt_ctx ctx, uint64_t records, double leaf_frac, int steps,
+                                                   int iters, double* gsteps);
 
 /* ------------------------------------------------------------------------ */
 /* Scene (replaces RTScene upload + RadeonRays CreateMesh/AttachShape/SetId/

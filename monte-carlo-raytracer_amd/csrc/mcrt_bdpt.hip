@@ -64,6 +64,9 @@ struct BVertex {
     int type, flags, lightIdx, materialIdx;
     const float4* planes;   // where a surface vertex's material properties live (loadUber)
     int depth;
+    Uber um;      // planes 8-12 when loaded with the vertex (loadVertexU, hasUm)
+    int umType;
+    bool hasUm;
 };
 
 // --- plane addressing ---------------------------------------------------------------------
@@ -122,6 +125,15 @@ MCRT_DEV BVertex loadVertex(const float4* base, int depth, int pix, int N) {
     v.materialIdx = h.w;
     v.planes = base;
     v.depth = depth;
+    v.hasUm = false;
+    return v;
+}
+// The vertex with its material properties, all 13 planes in one round trip (the connection kernels:
+// a strategy evaluates its vertices' BSDF and pdf several times)
+MCRT_DEV BVertex loadVertexU(const float4* base, int depth, int pix, int N) {
+    BVertex v = loadVertex(base, depth, pix, N);
+    v.um = loadUber(base, depth, pix, N, &v.umType);
+    v.hasUm = true;
     return v;
 }
 // Position / geometric normal / flags only (the "next" or "prev" vertex of a pdf evaluation)
@@ -280,14 +292,14 @@ MCRT_DEV LightLe sampleLightLe(const SceneArgs& s, const mcrt_light& light, f2 u
 // uber properties come from the vertex's planes 8-12 (the same getUberMaterialProperties values
 // the reference recomputes from the textures at every call).  Non-uber materials evaluate to 0.
 MCRT_DEV f3 evaluateMaterialV(const BVertex& v, int pix, int N, f3 wo, f3 wi, int mode) {
-    int type;
-    const Uber um = loadUber(v.planes, v.depth, pix, N, &type);
+    int type = v.umType;
+    const Uber um = v.hasUm ? v.um : loadUber(v.planes, v.depth, pix, N, &type);
     if (type != 0) return splat3(0.0f);
     return evaluateUberBSDF(um, v.fr, wo, wi, mode);
 }
 MCRT_DEV float evaluateMaterialPdfV(const BVertex& v, int pix, int N, f3 wo, f3 wi) {
-    int type;
-    const Uber um = loadUber(v.planes, v.depth, pix, N, &type);
+    int type = v.umType;
+    const Uber um = v.hasUm ? v.um : loadUber(v.planes, v.depth, pix, N, &type);
     if (type != 0) return 0.0f;
     return evaluateUberBSDF_Pdf(um, v.fr, wo, wi);
 }
@@ -402,6 +414,7 @@ MCRT_DEV BVertex createCameraVertex(f3 p, f3 throughput) {   // BDPT.cl:159-174
     v.throughput = throughput;
     v.traceErrorOffset = 0.0f;
     v.type = RT_BDPT_CAMERA_VERTEX;
+    v.hasUm = false;
     v.flags = VF_CONNECTIBLE;
     v.lightIdx = -1;
     v.materialIdx = -1;
@@ -419,6 +432,7 @@ MCRT_DEV BVertex createLightVertex(int lightIdx, f3 p, f3 n, f3 throughput, floa
     v.throughput = throughput;
     v.traceErrorOffset = RT_TRACE_OFFSET_F;
     v.type = RT_BDPT_LIGHT_VERTEX;
+    v.hasUm = false;
     v.lightIdx = lightIdx;
     v.materialIdx = -1;
     v.pdfRev = 0.0f;
@@ -693,10 +707,13 @@ MCRT_DEV void pushConn(const BdptQueue& q, int slot, f3 o, float tmax, f3 d, int
 //     slot t - 2, so its frame-to-frame read-before-write order is kept.
 // Strategies are split into four classes, one launch each, so every kernel carries only its own
 // registers: EMIT (s = 0), LIGHT (t = 1, light tracing), NEE (s = 1), GENERAL (t, s >= 2).  A wave
-// holds one strategy of one 8x8 tile (wave-uniform branches); the waves of a tile are adjacent,
-// so its vertex planes are re-read from L2.  Own strategies (t >= 2) write their slot (zero when
-// absent, not connectible or contributing nothing); strategies with a non-zero weighted
-// contribution that need visibility are queued.
+// holds one strategy of one 8x8 tile for all the call's frames (wave-uniform branches); the waves
+// of a tile are adjacent, so its vertex planes are re-read from L2.  Own strategies (t >= 2) write
+// their slot (zero when absent, not connectible or contributing nothing); strategies with a
+// non-zero weighted contribution that need visibility are queued.  (One workgroup per tile running
+// every strategy of its pixels, so each path's planes come from HBM once, measured slower: 1.02
+// against 0.74 ms per frame -- all its waves carry the heaviest class's registers, 2-3 waves per
+// SIMD, where the light classes run at 4-8; tools/experiments/bdpt_connect_tile_mispre.patch.)
 enum { CONN_EMIT = 0, CONN_LIGHT = 1, CONN_NEE = 2, CONN_GENERAL = 3 };
 
 MCRT_DEV int ownSlotOf(int t, int sI, int D) {   // index among the t >= 2 strategies in (t, s) order
@@ -720,33 +737,44 @@ MCRT_DEV void strategyOf(int k, int D, int& t, int& sI) {
     }
 }
 
-template <int CLS>
-__global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameArgs f, BdptArgs b,
-                                                             const mcrt_camera* __restrict__ camp, BdptQueue qOut,
-                                                             int numStrat) {
+// Connection rays staged in LDS, a segment per wave (no wave waits for another): one global append
+// per CONN_STAGE rays of a wave's frame loop instead of one per workgroup, frame and strategy (an
+// append to the queue's one counter sits on the appending wave's critical path: with one per wave
+// and strategy the connection launches took 1.78 ms per frame; staged, 0.836 against the
+// workgroup appends' 0.85, profiles/r06/ab/bdpt_connect).
+#define CONN_STAGE 128
+struct WaveStage {
+    float4 *o, *d, *t;   // this wave's LDS segment
+    int n;               // staged rays (wave-uniform)
+};
+MCRT_DEV void flushStage(WaveStage& ws, const BdptQueue& q) {
+    if (ws.n == 0) return;
     const int lane = threadIdx.x & 63;
-    // a wave = (tile, batch frame, strategy), strategies fastest: the strategies of one path read
-    // the same vertices (the MIS walks share every vertex below the connection), so they run in
-    // one workgroup or its neighbours, and xcdRemap keeps neighbouring workgroups on one XCD (one
-    // L2).  NEE waves walk the batch's frames in order in-thread (frame k's s = 1 strategy reads
-    // the sampled-light slot frame k - 1 wrote).
-    const int wave = xcdRemap((int)blockIdx.x, (int)gridDim.x) * (BDPT_BLOCK / 64) + (int)(threadIdx.x >> 6);
-    const int kb = CLS == CONN_NEE ? 1 : f.batch;
-    const int per = numStrat * kb;
-    const int tile = wave / per;
-    const int rem = wave - tile * per;
-    const int si = rem % numStrat;
-    int t, sI;
-    strategyOf<CLS>(si, f.maxDepth, t, sI);
-    int x = 0, y = 0;
-    const bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y) && s.numLights > 0;
-    __shared__ int ldsWave[BDPT_BLOCK / 64 + 1];
+    __builtin_amdgcn_wave_barrier();
+    int base = 0;
+    if (lane == 0) base = atomicAdd(q.count, ws.n);
+    base = __shfl(base, 0);
+    for (int i = lane; i < ws.n; i += 64) {
+        q.o[base + i] = ws.o[i];
+        q.d[base + i] = ws.d[i];
+        q.t[base + i] = ws.t[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    ws.n = 0;
+}
+
+// One strategy (t, sI) of class CLS for batch frame k of the lane's pixel (x, y): PrepareConnections
+// + the MIS weight of ConnectVertices, the own-strategy slot, and the connection ray -- appended to
+// the wave's LDS stage (ws) or with one global atomic per wave (the queue's order only decides the
+// order of the splats' float atomics).
+template <int CLS>
+MCRT_DEV void connectOne(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* camp,
+                         const BdptQueue& qOut, int t, int sI, int k, int x, int y, bool valid,
+                         WaveStage* ws = nullptr) {
     const int N0 = (int)(f.W * f.H);
     const int N = N0 * f.batch;   // plane stride
     const int D = f.maxDepth;
     const int px = y * (int)f.W + x;
-    const int kBegin = CLS == CONN_NEE ? 0 : rem / numStrat, kEnd = CLS == CONN_NEE ? f.batch : kBegin + 1;
-    for (int k = kBegin; k < kEnd; ++k) {
     const int pix = k * N0 + px;   // the path (plane index)
     const mcrt_camera& cam = camp[k];
     const int camCount = valid ? b.camCount[pix] : 0;
@@ -757,8 +785,22 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
     float rayT = 0.0f;
     int code = 0;
     if (live) {
-        BVertex cv, samp;   // samp: the sampled vertex of a t = 1 / s = 1 strategy (pt / qs in the MIS)
-        if (CLS != CONN_LIGHT && CLS != CONN_EMIT) cv = loadVertex(b.camV, t - 1, pix, N);
+        // the strategy's camera / light vertex WITH its material properties (loadVertexU) and the
+        // MIS walk's previous vertices in one round trip: the kernel is bound by its chains of
+        // dependent fetches (the BSDF and pdf evaluations re-read the material planes otherwise;
+        // 0.85 -> 0.74 ms per frame).  Fetching them before the subpath lengths are known, or the
+        // MIS walks' pdf planes with them as well, measured slower (lanes of absent strategies
+        // fetch for nothing; profiles/r06/ab/bdpt_connect)
+        BVertex cv, lv, samp;   // samp: the sampled vertex of a t = 1 / s = 1 strategy (pt / qs in the MIS)
+        BVertexPos ptPrev, qsPrev;
+        if (CLS != CONN_LIGHT && CLS != CONN_EMIT) {
+            cv = loadVertexU(b.camV, t - 1, pix, N);
+            ptPrev = loadVertexPos(b.camV, t - 2, pix, N);
+        }
+        if (CLS == CONN_LIGHT || CLS == CONN_GENERAL) {
+            lv = loadVertexU(b.lightV, sI - 1, pix, N);
+            qsPrev = loadVertexPos(b.lightV, sI - 2, pix, N);
+        }
         if (CLS == CONN_EMIT) {
             // ConnectVertices (BDPT.cl:723-731): emission of a camera vertex that is a light.  Only
             // the type word is read first: for the (many) vertices that are not lights the strategy
@@ -770,7 +812,6 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                 L = Le * cv.throughput;
             }
         } else if (CLS == CONN_LIGHT) {
-            const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
             if (isConnectible(lv.flags)) {
                 // samplePinholeCameraWi (cameras.cl:61-69)
                 f3 wi = ld3(cam.pos) - lv.fr.p;
@@ -834,7 +875,6 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
                 }
             }
         } else {
-            const BVertex lv = loadVertex(b.lightV, sI - 1, pix, N);
             if (isConnectible(cv.flags) && isConnectible(lv.flags)) {
                 const f3 lvf = evalVertex_f(lv, pix, N, cv.fr.p, TRANSPORT_MODE_IMPORTANCE);
                 const f3 cvf = evalVertex_f(cv, pix, N, lv.fr.p, TRANSPORT_MODE_RADIANCE);
@@ -866,10 +906,8 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
             BVertex pt = CLS == CONN_LIGHT ? samp : cv;
             BVertex qs;
             if (CLS == CONN_NEE) qs = samp;
-            else if (CLS == CONN_LIGHT || CLS == CONN_GENERAL) qs = loadVertex(b.lightV, sI - 1, pix, N);
-            BVertexPos ptPrev, qsPrev;
-            if (CLS != CONN_LIGHT) ptPrev = loadVertexPos(b.camV, t - 2, pix, N);
-            if (CLS == CONN_LIGHT || CLS == CONN_GENERAL) qsPrev = loadVertexPos(b.lightV, sI - 2, pix, N);
+            else if (CLS == CONN_LIGHT || CLS == CONN_GENERAL) qs = lv;
+            if (CLS == CONN_EMIT) ptPrev = loadVertexPos(b.camV, t - 2, pix, N);
             pt.flags &= ~VF_DELTA;
             if (CLS != CONN_EMIT) qs.flags &= ~VF_DELTA;
             const float ptRev = CLS != CONN_EMIT ? evalVertexPdf(s, cam, qs, pix, N, sI > 1, qsPrev.p, posOf(pt))
@@ -944,11 +982,57 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameA
     } else if (valid && CLS != CONN_LIGHT) {
         b.slots[(size_t)ownSlotOf(t, sI, D) * N + pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // strategy absent
     }
-    if (CLS != CONN_EMIT) {   // emission needs no connection ray (class-uniform: the whole block)
-        const int qslot = blockAppend<BDPT_BLOCK / 64>(qOut.count, push, ldsWave);
-        if (push) pushConn(qOut, qslot, rayO, rayT, rayD, code, L);
+    if (CLS != CONN_EMIT) {   // emission needs no connection ray (class-uniform: the whole wave)
+        const uint64_t m = __ballot(push);
+        if (m) {
+            const int lane = threadIdx.x & 63, leader = __builtin_ctzll(m), cnt = __popcll(m);
+            const int pre = __popcll(m & ((1ull << lane) - 1));
+            bool staged = false;
+            if (ws) {
+                if (ws->n + cnt > CONN_STAGE) flushStage(*ws, qOut);
+                if (push) {
+                    ws->o[ws->n + pre] = make_float4(rayO.x, rayO.y, rayO.z, rayT);
+                    ws->d[ws->n + pre] = make_float4(rayD.x, rayD.y, rayD.z, __int_as_float(code));
+                    ws->t[ws->n + pre] = make_float4(L.x, L.y, L.z, 0.0f);
+                }
+                ws->n += cnt;
+                staged = true;
+            }
+            if (!staged) {
+                int at = 0;
+                if (lane == leader) at = atomicAdd(qOut.count, cnt);
+                at = __shfl(at, leader) + pre;
+                if (push) pushConn(qOut, at, rayO, rayT, rayD, code, L);
+            }
+        }
     }
-    }
+}
+
+// The four class launches: a wave = (tile, strategy), walking the batch's frames in order (frame
+// k's s = 1 strategy reads the sampled-light slot frame k - 1 wrote), strategies fastest, so the
+// strategies of one tile run in one workgroup or its neighbours at about the same frame; each class
+// kernel carries only its own registers.  Connection rays are staged per wave in LDS.
+template <int CLS>
+__global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_connect(SceneArgs s, FrameArgs f, BdptArgs b,
+                                                             const mcrt_camera* __restrict__ camp, BdptQueue qOut,
+                                                             int numStrat) {
+    constexpr int NW = BDPT_BLOCK / 64;
+    constexpr int SEG = CLS == CONN_EMIT ? 1 : CONN_STAGE;   // emission strategies queue no rays
+    __shared__ float4 so[NW][SEG], sd[NW][SEG], st[NW][SEG];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int wave = xcdRemap((int)blockIdx.x, (int)gridDim.x) * NW + wv;
+    const int tile = wave / numStrat;
+    const int si = wave - tile * numStrat;
+    int t, sI;
+    strategyOf<CLS>(si, f.maxDepth, t, sI);
+    int x = 0, y = 0;
+    const bool valid = tile < f.numTiles && tilePixel(f, tile, lane, x, y) && s.numLights > 0;
+    if (tile >= f.numTiles) return;
+    WaveStage ws{so[wv], sd[wv], st[wv], 0};
+    for (int k = 0; k < f.batch; ++k)
+        connectOne<CLS>(s, f, b, camp, qOut, t, sI, k, x, y, valid, CLS == CONN_EMIT ? nullptr : &ws);
+    if (CLS != CONN_EMIT) flushStage(ws, qOut);
 }
 
 // Any hit over the connection queue (RR occluded_main semantics): occluded own strategies are
@@ -1139,7 +1223,7 @@ void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
         k_bdpt_connect<CONN_EMIT>, k_bdpt_connect<CONN_LIGHT>, k_bdpt_connect<CONN_NEE>, k_bdpt_connect<CONN_GENERAL>};
     for (int c = 0; c < 4; ++c) {
         if (counts[c] <= 0) continue;
-        const int64_t waves = (int64_t)f.numTiles * counts[c] * (c == CONN_NEE ? 1 : f.batch);
+        const int64_t waves = (int64_t)f.numTiles * counts[c];
         const int blocks = (int)((waves * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK);
         hipLaunchKernelGGL(kern[c], dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, q, counts[c]);
     }

@@ -644,6 +644,19 @@ MCRT_API mcrt_status mcrt_ctx_gather_chase(mcrt_ctx ctx, uint64_t records, int s
     return MCRT_OK;
 }
 
+MCRT_API mcrt_status mcrt_ctx_gather_chase_compact(mcrt_ctx ctx, uint64_t records, double leaf_frac, int steps,
+                                                   int iters, double* gsteps) {
+    if (!ctx || !gsteps || records < 64 || records > 0x3fffffffull || steps < 1 || iters < 1 || !(leaf_frac >= 0.0) ||
+        leaf_frac > 1.0)
+        return fail(ctx, MCRT_ERROR_INVALID_ARG, "bad gather-chase args");
+    hipSetDevice(ctx->device);
+    const int waves = ctx->numCUs * 32;
+    float best = 0.0f;
+    HIPCHK(ctx, mcrt::chase_compact((uint32_t)records, leaf_frac, steps, waves, iters, ctx->stream, &best));
+    *gsteps = (double)waves * 64.0 * steps / (best * 1e-3) / 1e9;
+    return MCRT_OK;
+}
+
 MCRT_API mcrt_status mcrt_ctx_reset_stats(mcrt_ctx ctx) {
     if (!ctx) return fail(nullptr, MCRT_ERROR_INVALID_ARG, "ctx is NULL");
     drain_pending(ctx);

@@ -195,6 +195,8 @@ void launch_tile_order(const uint32_t* cost, int n, uint32_t* order, hipStream_t
 hipError_t build_qnodes(const float4* nodes, uint32_t n, float4** qOut, size_t* units, hipStream_t st);
 void launch_chase_init(void* rec, uint32_t n, hipStream_t st);
 void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* sink, hipStream_t st);
+// the chase over packed 32-B / 48-B records (mcrt_ctx_gather_chase_compact): best of iters launches
+hipError_t chase_compact(uint32_t n, double leafFrac, int steps, int waves, int iters, hipStream_t st, float* bestMs);
 void launch_bdpt_start(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* cam,
                        const BdptQueue& camQ, const BdptQueue& lightQ, hipStream_t st);
 void launch_bdpt_vertex(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, int depth, const BdptQueue& qIn,

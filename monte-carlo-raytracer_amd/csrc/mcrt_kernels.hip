@@ -948,6 +948,47 @@ __global__ __launch_bounds__(64) void k_chase(const int4* __restrict__ rec, uint
     if (acc == 0xdeadbeefu) sink[0] = idx;   // never true: keeps the loads live
 }
 
+// The chase over the compact records' layout: record i is 2 (internal, 32 B) or 3 (leaf, 48 B)
+// 16-B units, packed back to back at off[i] (exclusive scan of chase_units); its link is the next
+// record's reference (unit offset << 1 | leaf bit), so a leaf's third unit is fetched in the same
+// round trip as in mcrt_traverse.h qwalk.
+MCRT_DEV uint32_t chaseHash(uint32_t i, uint32_t seed) {
+    uint32_t h = i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    return h;
+}
+__global__ void k_chase_units(uint32_t* units, uint32_t n, uint32_t leaf16) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) units[i] = 2u + ((chaseHash((uint32_t)i, 99u) & 0xffffu) < leaf16 ? 1u : 0u);
+}
+__global__ void k_chase_init_compact(int4* rec, const uint32_t* off, const uint32_t* units, uint32_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t nxt = chaseHash((uint32_t)i, 777u) % n;
+    const int ref = (int)((off[nxt] << 1) | (units[nxt] == 3u ? 1u : 0u));
+    for (uint32_t q = 0; q < units[i]; ++q) rec[off[i] + q] = make_int4((int)nxt, (int)(nxt ^ 1u), (int)(nxt ^ 2u), ref);
+}
+__global__ __launch_bounds__(64) void k_chase_compact(const int4* __restrict__ rec, const uint32_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ units, uint32_t n, int steps,
+                                                      uint32_t* sink) {
+    const uint32_t chain = blockIdx.x * 64 + threadIdx.x;
+    uint32_t h = chain * 0x9E3779B9u + 12345u;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13;
+    const uint32_t i0 = h % n;
+    uint32_t ref = (off[i0] << 1) | (units[i0] == 3u ? 1u : 0u), acc = 0;
+    for (int s = 0; s < steps; ++s) {
+        const int4* p = rec + (ref >> 1);
+        const int4 a = p[0], b = p[1];
+        int4 c;
+        asm("" : "=v"(c.x), "=v"(c.y), "=v"(c.z), "=v"(c.w));
+        if (ref & 1u) c = p[2];
+        asm volatile("" ::"v"(a.y), "v"(b.y), "v"(c.y));
+        acc += (uint32_t)(a.z ^ b.z ^ c.z);
+        ref = (uint32_t)a.w;
+    }
+    if (acc == 0xdeadbeefu) sink[0] = ref;   // never true: keeps the loads live
+}
+
 // Parent links of the flat tree's leaves (the occluder hints' box test, mcrt_traverse.h
 // hintOccludes): every internal record writes its index into word 13 of each child that is a
 // triangle leaf (mcrt_bvh.cpp leaves carry -1 there; the traversal never reads it for a leaf).
@@ -1215,6 +1256,54 @@ void launch_chase_init(void* rec, uint32_t n, hipStream_t st) {
 }
 void launch_chase(const void* rec, uint32_t n, int steps, int waves, uint32_t* sink, hipStream_t st) {
     hipLaunchKernelGGL(k_chase, dim3(waves), dim3(64), 0, st, reinterpret_cast<const int4*>(rec), n, steps, sink);
+}
+
+hipError_t chase_compact(uint32_t n, double leafFrac, int steps, int waves, int iters, hipStream_t st, float* bestMs) {
+    uint32_t *units = nullptr, *off = nullptr, *sink = nullptr, last[2] = {0, 0};
+    int4* rec = nullptr;
+    void* tmp = nullptr;
+    size_t tmpBytes = 0;
+    const uint32_t leaf16 = (uint32_t)std::min(65536.0, std::max(0.0, leafFrac * 65536.0));
+    hipError_t e = hipMalloc(&units, 4 * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&off, 4 * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&sink, 4);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_chase_units, dim3((n + 255) / 256), dim3(256), 0, st, units, n, leaf16);
+        e = rocprim::exclusive_scan(nullptr, tmpBytes, units, off, 0u, (size_t)n, rocprim::plus<uint32_t>(), st);
+    }
+    if (e == hipSuccess) e = hipMalloc(&tmp, tmpBytes);
+    if (e == hipSuccess) e = rocprim::exclusive_scan(tmp, tmpBytes, units, off, 0u, (size_t)n, rocprim::plus<uint32_t>(), st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&last[0], off + n - 1, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&last[1], units + n - 1, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipMalloc(&rec, 16 * ((size_t)last[0] + last[1]));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_chase_init_compact, dim3((n + 255) / 256), dim3(256), 0, st, rec, off, units, n);
+        hipEvent_t e0, e1;
+        hipEventCreate(&e0);
+        hipEventCreate(&e1);
+        float best = 1e30f;
+        for (int i = 0; i < iters + 1; ++i) {   // launch 0 warms caches and translations
+            hipEventRecord(e0, st);
+            hipLaunchKernelGGL(k_chase_compact, dim3(waves), dim3(64), 0, st, rec, off, units, n,
+                               i == 0 ? std::max(1, steps / 4) : steps, sink);
+            hipEventRecord(e1, st);
+            hipEventSynchronize(e1);
+            float ms = 0.0f;
+            hipEventElapsedTime(&ms, e0, e1);
+            if (i > 0 && ms < best) best = ms;
+        }
+        hipEventDestroy(e0);
+        hipEventDestroy(e1);
+        *bestMs = best;
+        e = hipGetLastError();
+    }
+    (void)hipFree(rec);
+    (void)hipFree(tmp);
+    (void)hipFree(sink);
+    (void)hipFree(off);
+    (void)hipFree(units);
+    return e;
 }
 
 void launch_leaf_parents(float4* nodes, uint32_t n, hipStream_t st) {

@@ -14,7 +14,8 @@ from . import PKG_DIR
 from . import types as T
 
 # MCRT_LIB_PATH: an alternative in-tree build of the same library (kernel tuning experiments)
-LIB_PATH = os.environ.get("MCRT_LIB_PATH") or os.path.join(os.path.dirname(PKG_DIR), "libmcrt.so")
+_DEFAULT_LIB = os.path.join(os.path.dirname(PKG_DIR), "libmcrt.so")
+LIB_PATH = os.environ.get("MCRT_LIB_PATH") or _DEFAULT_LIB
 HEADER = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), "include", "mcrt_capi.h")
 
 _c = ctypes
@@ -35,6 +36,8 @@ SIGNATURES = {
     "mcrt_ctx_stream_copy": (_c.c_int, [_vp, _c.c_uint64, _c.c_int, _c.POINTER(_c.c_double)]),
     "mcrt_ctx_get_stream": (_c.c_int, [_vp, _c.POINTER(_vp)]),
     "mcrt_ctx_gather_chase": (_c.c_int, [_vp, _c.c_uint64, _c.c_int, _c.c_int, _c.POINTER(_c.c_double)]),
+    "mcrt_ctx_gather_chase_compact": (_c.c_int, [_vp, _c.c_uint64, _c.c_double, _c.c_int, _c.c_int,
+                                                 _c.POINTER(_c.c_double)]),
     "mcrt_scene_create": (_c.c_int, [_vp, _vp, _c.POINTER(_vp)]),
     "mcrt_scene_destroy": (_c.c_int, [_vp]),
     "mcrt_scene_update_lights": (_c.c_int, [_vp, _vp, _c.c_uint32]),
@@ -110,7 +113,15 @@ def lib():
                             "(make -C monte-carlo-raytracer_amd/csrc); there is no CPU fallback")
         L = _c.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                # an older library selected with MCRT_LIB_PATH (A/B runs) may lack a later entry
+                # point: it fails when called; the in-tree library exports every one
+                # (tests/test_capi_cpu.py)
+                if LIB_PATH == _DEFAULT_LIB:
+                    raise
+                continue
             f.restype = res
             f.argtypes = args
         _lib = L
@@ -187,6 +198,14 @@ class Context:
         """Dependent 64-B gather ceiling, G steps/s (mcrt_ctx_gather_chase)."""
         g = _c.c_double()
         _check(lib().mcrt_ctx_gather_chase(self.h, records, steps, iters, _c.byref(g)), self.h)
+        return g.value
+
+    def gather_chase_compact_gsteps(self, records, leaf_frac, steps=256, iters=3):
+        """The same ceiling over packed 32-B / 48-B records, a share leaf_frac of them 48-B leaves
+        (the compact walk's layout; mcrt_ctx_gather_chase_compact), G steps/s."""
+        g = _c.c_double()
+        _check(lib().mcrt_ctx_gather_chase_compact(self.h, records, float(leaf_frac), steps, iters, _c.byref(g)),
+               self.h)
         return g.value
 
     def stream_copy_gbps(self, nbytes=2 << 30, iters=5):

@@ -1072,6 +1072,9 @@ static inline void triBarycentrics(v3 p, const float* v1, const float* v2, const
 }
 
 typedef struct { uint32_t* data; int cap; } Stack;
+/* leaf visits of the calling thread's walks (render stats [6], [7]: the traversal's leaf / internal
+ * mix, which prices the product's compact records at 48 / 32 B, bench.py gather_ceiling) */
+static _Thread_local int64_t tl_leafVisits;
 
 /* intersect_bvh2_lds.cl:66-226 (the LDS short stack + global spill is one LIFO) */
 static int traceClosest(const orc_scene* s, const Ray* r, mcrt_intersection* hit, uint32_t* stack, int* visits,
@@ -1101,6 +1104,7 @@ static int traceClosest(const orc_scene* s, const Ray* r, mcrt_intersection* hit
                 continue;
             }
         } else {
+            ++tl_leafVisits;
             if (r->mask != (int)node->mesh_id) {   /* RR_RAY_MASK */
                 float t = fastTriangle(r, node->lmin_v0, node->lmax_v1, node->rmin_v2, closest_t);
                 if (t < closest_t) { closest_t = t; closest_addr = addr; }
@@ -1150,6 +1154,7 @@ static int traceAny(const orc_scene* s, const Ray* r, uint32_t* stack, int* visi
                 continue;
             }
         } else {
+            ++tl_leafVisits;
             if (r->mask != (int)node->mesh_id) {
                 float t = fastTriangle(r, node->lmin_v0, node->lmax_v1, node->rmin_v2, closest_t);
                 if (t < closest_t) { if (visits) *visits = nv; return 1; }
@@ -1646,7 +1651,7 @@ typedef struct {
     int frame, maxDepth, sampler, W, H;
     float* radiance;
     const int32_t* rows;
-    atomic_llong stats[6];
+    atomic_llong stats[8];
 } RenderCtx;
 
 static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
@@ -1666,7 +1671,7 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
     v3 radianceAcc = V3(0, 0, 0);
     mcrt_intersection isect;
     int nv = 0;
-    int64_t nprim = 0, vprim = 0, nclosest = 0, nany = 0, vclosest = 0, vany = 0;
+    int64_t nprim = 0, vprim = 0, nclosest = 0, nany = 0, vclosest = 0, vany = 0, lclosest = 0, lany = 0;
     /* RTPrimaryRaysPass: first closest hit */
     uint8_t* const tch = s->touched;
     const int64_t NN = s->num_nodes;
@@ -1768,8 +1773,9 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
         int occl = -1;
         if (shadowSet && shadow.active) {
             int anv = 0;
+            const int64_t l0 = tl_leafVisits;
             occl = traceAny(s, &shadow, stack, &anv, tch ? tch + (b == 0 ? 2 : 3) * NN : NULL);
-            nany++; vany += anv;
+            nany++; vany += anv; lany += tl_leafVisits - l0;
             if (L) {
                 int32_t oc = occl; memcpy(&L[7], &oc, 4);
                 L[8] = shadow.o.x; L[9] = shadow.o.y; L[10] = shadow.o.z;
@@ -1782,8 +1788,9 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
         }
         radianceAcc = (b == 0) ? temp : vadd(radianceAcc, temp);
         if (b + 1 < rc->maxDepth && ray.active) {
+            const int64_t l0 = tl_leafVisits;
             traceClosest(s, &ray, &isect, stack, &nv, tch ? tch + NN : NULL);
-            nclosest++; vclosest += nv;
+            nclosest++; vclosest += nv; lclosest += tl_leafVisits - l0;
         }
     }
     float* out = &rc->radiance[4 * (size_t)bufferIdx];
@@ -1794,6 +1801,8 @@ static void renderPixel(RenderCtx* rc, int x, int y, uint32_t* stack) {
     atomic_fetch_add(&rc->stats[3], vclosest);
     atomic_fetch_add(&rc->stats[4], nany);
     atomic_fetch_add(&rc->stats[5], vany);
+    atomic_fetch_add(&rc->stats[6], lclosest);
+    atomic_fetch_add(&rc->stats[7], lany);
 }
 
 static void render_row(void* c, int64_t i, uint32_t* stack) {
@@ -1807,7 +1816,7 @@ static void render_common(orc_scene* s, const mcrt_camera* cam, int frame, int m
     RenderCtx rc;
     rc.s = s; rc.cam = cam; rc.frame = frame; rc.maxDepth = max_depth; rc.sampler = sampler;
     rc.W = (int)cam->width; rc.H = (int)cam->height; rc.radiance = radiance;
-    for (int k = 0; k < 6; ++k) atomic_init(&rc.stats[k], 0);
+    for (int k = 0; k < 8; ++k) atomic_init(&rc.stats[k], 0);
     if (rows) {
         rc.rows = rows;
         parallel_for(nrows, threads, 1, render_row, &rc);
@@ -1818,7 +1827,7 @@ static void render_common(orc_scene* s, const mcrt_camera* cam, int frame, int m
         parallel_for(nrows, threads, 1, render_row, &rc);
         free(r);
     }
-    if (stats) for (int k = 0; k < 6; ++k) stats[k] = atomic_load(&rc.stats[k]);
+    if (stats) for (int k = 0; k < 8; ++k) stats[k] = atomic_load(&rc.stats[k]);
 }
 
 void orc_render_frame(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,

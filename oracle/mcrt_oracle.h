@@ -59,8 +59,9 @@ void orc_brute_any(orc_scene* s, const mcrt_ray* rays, int n, int32_t* hits);
 
 /* One PT frame for rows [y0, y1) (GeneratePerspectiveRays + maxDepth x (PathTracing,
  * occluded, ShadowPass, intersect)).  radiance: W*H float4, rows outside untouched.
- * stats (may be NULL, 6 x int64): [0] primary closest queries, [1] their node visits,
- * [2] extension closest queries, [3] their visits, [4] any-hit queries, [5] their visits
+ * stats (may be NULL, 8 x int64): [0] primary closest queries, [1] their node visits,
+ * [2] extension closest queries, [3] their visits, [4] any-hit queries, [5] their visits,
+ * [6] leaf visits among [3], [7] leaf visits among [5]
  * (visits = RR Bvh2 node fetches of intersect_bvh2_lds.cl, the V of SURVEY.md §8d). */
 void orc_render_frame(orc_scene* s, const mcrt_camera* cam, int frame, int max_depth, int sampler,
                       int y0, int y1, int threads, float* radiance, int64_t* stats);

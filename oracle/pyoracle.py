@@ -140,7 +140,7 @@ class OracleScene:
             y1 = H
         if radiance is None:
             radiance = np.zeros((H, W, 4), np.float32)
-        stats = np.zeros(6, np.int64)
+        stats = np.zeros(8, np.int64)
         lib().orc_render_frame(self.h, _p(cam), frame, max_depth, sampler, y0, y1, threads, _p(radiance), _p(stats))
         return radiance, stats
 
@@ -175,7 +175,7 @@ class OracleScene:
         rows = np.ascontiguousarray(rows, np.int32)
         if radiance is None:
             radiance = np.zeros((H, W, 4), np.float32)
-        stats = np.zeros(6, np.int64)
+        stats = np.zeros(8, np.int64)
         lib().orc_render_rows(self.h, _p(cam), frame, max_depth, sampler, _p(rows), len(rows), threads,
                               _p(radiance), _p(stats))
         return radiance, stats
