@@ -1,9 +1,9 @@
 export TMPDIR=/tmp
 P=gpurun_out/r5rdbg; mkdir -p $P
 for D in 2 3 4; do
-  timeout -k 10 120 python3 tools/r5/dbg/refill_dbg.py $P/base_$D.npy $D || exit 3
+  timeout -k 10 120 python3 tools/archive/r5/dbg/refill_dbg.py $P/base_$D.npy $D || exit 3
   for v in refill16 refill64; do
-    MCRT_LIB_PATH=$PWD/monte-carlo-raytracer_amd/libmcrt_$v.so timeout -k 10 120 python3 tools/r5/dbg/refill_dbg.py $P/${v}_$D.npy $D || exit 3
+    MCRT_LIB_PATH=$PWD/monte-carlo-raytracer_amd/libmcrt_$v.so timeout -k 10 120 python3 tools/archive/r5/dbg/refill_dbg.py $P/${v}_$D.npy $D || exit 3
   done
 done
 python3 - $P <<'PY'
