@@ -20,6 +20,11 @@ figure of the task brief) and STEP_US of latency per collective step.
         striped over min(N - 1, 7) links: (N - 1) / N x buffer / (links x LINK) + 2 (N - 1) STEP.  The
         exchange of a call runs on its frame slot's stream while the next call renders on the other
         slot, so only the last call's exchange is exposed ("overlapped"); "serial" adds every one.
+The model has no term for a collective's first-use setup (RCCL connects a pair of ranks on their
+first send / recv): bench.py runs its end-of-job collective once before the timed region
+(bench.timed_region, tests/test_dist_cpu.py::test_bench_warms_end_collective_before_timing), and the
+BDPT band split's per-call reduce-scatters already run in its warm-up calls, so setup falls outside
+the timed region there too.
 """
 import argparse
 import json
