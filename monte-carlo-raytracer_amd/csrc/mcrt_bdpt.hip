@@ -565,6 +565,18 @@ MCRT_DEV uint32_t bounceKey(const BdptArgs& b, f3 o, f3 d) {
     return (oct << 13) | (uint32_t)((cx << 8) | (cy << 5) | cz);
 }
 
+// (connectOne below; the vertex launch runs the light-tracing strategy of each light vertex it makes)
+struct WaveStage;
+struct LightPre {   // a light vertex in registers (with its material properties) and its predecessor
+    BVertex lv;
+    BVertexPos qsPrev;
+};
+template <int CLS>
+MCRT_DEV void connectOne(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* camp,
+                         const BdptQueue& qOut, int t, int sI, int k, int x, int y, bool valid,
+                         WaveStage* ws = nullptr, const LightPre* lpre = nullptr);
+enum { CONN_EMIT = 0, CONN_LIGHT = 1, CONN_NEE = 2, CONN_GENERAL = 3 };
+
 // FINAL: the launch of depth D + 1, whose queue holds camera rays only and whose vertices all end
 // their subpath -- no BSDF sampling, so its instantiation carries far fewer registers.
 template <bool FINAL>
@@ -673,6 +685,23 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                     push = true;
                 }
             }
+            // the light-tracing strategy (t = 1, s = depth + 1) of this light vertex, from the registers
+            // that just stored it (PrepareConnections + ConnectVertices for t = 1, BDPT.cl:460-913): every
+            // input is final here -- the vertex itself, its predecessor, the pdfs below it (earlier
+            // launches) -- and nothing it reads changes later, so it equals the connection launch's
+            if (!FINAL && !isCamera && b.lightInVertex) {
+                LightPre lp;
+                lp.lv = cur;
+                lp.lv.um = um;
+                lp.lv.umType = mat.type;
+                lp.lv.hasUm = true;
+                lp.lv.planes = V;
+                lp.lv.depth = depth;
+                lp.qsPrev = prev;
+                const BdptQueue cq{b.connCount, b.connO, b.connD, b.connL};
+                connectOne<CONN_LIGHT>(s, f, b, b.cams, cq, 1, depth + 1, kf, px % (int)f.W, px / (int)f.W, true,
+                                       nullptr, &lp);
+            }
         }
     }
     // (queue order = the block's ray order: grouping the next rays by direction as the PT first
@@ -714,8 +743,6 @@ MCRT_DEV void pushConn(const BdptQueue& q, int slot, f3 o, float tmax, f3 d, int
 // every strategy of its pixels, so each path's planes come from HBM once, measured slower: 1.02
 // against 0.74 ms per frame -- all its waves carry the heaviest class's registers, 2-3 waves per
 // SIMD, where the light classes run at 4-8; tools/experiments/bdpt_connect_tile_mispre.patch.)
-enum { CONN_EMIT = 0, CONN_LIGHT = 1, CONN_NEE = 2, CONN_GENERAL = 3 };
-
 MCRT_DEV int ownSlotOf(int t, int sI, int D) {   // index among the t >= 2 strategies in (t, s) order
     int k = sI;
     for (int u = 2; u < t; ++u) k += D + 3 - u;
@@ -770,7 +797,7 @@ MCRT_DEV void flushStage(WaveStage& ws, const BdptQueue& q) {
 template <int CLS>
 MCRT_DEV void connectOne(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* camp,
                          const BdptQueue& qOut, int t, int sI, int k, int x, int y, bool valid,
-                         WaveStage* ws = nullptr) {
+                         WaveStage* ws, const LightPre* lpre) {
     const int N0 = (int)(f.W * f.H);
     const int N = N0 * f.batch;   // plane stride
     const int D = f.maxDepth;
@@ -797,7 +824,10 @@ MCRT_DEV void connectOne(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
             cv = loadVertexU(b.camV, t - 1, pix, N);
             ptPrev = loadVertexPos(b.camV, t - 2, pix, N);
         }
-        if (CLS == CONN_LIGHT || CLS == CONN_GENERAL) {
+        if (CLS == CONN_LIGHT && lpre) {   // the vertex launch's registers
+            lv = lpre->lv;
+            qsPrev = lpre->qsPrev;
+        } else if (CLS == CONN_LIGHT || CLS == CONN_GENERAL) {
             lv = loadVertexU(b.lightV, sI - 1, pix, N);
             qsPrev = loadVertexPos(b.lightV, sI - 2, pix, N);
         }
@@ -1222,7 +1252,7 @@ void launch_bdpt_connect(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
     void (*kern[4])(SceneArgs, FrameArgs, BdptArgs, const mcrt_camera*, BdptQueue, int) = {
         k_bdpt_connect<CONN_EMIT>, k_bdpt_connect<CONN_LIGHT>, k_bdpt_connect<CONN_NEE>, k_bdpt_connect<CONN_GENERAL>};
     for (int c = 0; c < 4; ++c) {
-        if (counts[c] <= 0) continue;
+        if (counts[c] <= 0 || (c == CONN_LIGHT && b.lightInVertex)) continue;   // (done by the vertex launches)
         const int64_t waves = (int64_t)f.numTiles * counts[c];
         const int blocks = (int)((waves * 64 + BDPT_BLOCK - 1) / BDPT_BLOCK);
         hipLaunchKernelGGL(kern[c], dim3(blocks), dim3(BDPT_BLOCK), 0, st, s, f, b, cam, q, counts[c]);

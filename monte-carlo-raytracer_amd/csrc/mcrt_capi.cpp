@@ -447,6 +447,12 @@ static int walk_max_bounce() {
     const char* e = std::getenv("MCRT_WALK_MAXB");
     return e ? std::atoi(e) : 0;
 }
+// BDPT: the light-tracing strategies (t = 1) evaluated by the vertex launches that create their
+// light vertices instead of by a connection launch that re-reads them (MCRT_BDPT_LIGHT_IN_VERTEX)
+static int bdpt_light_in_vertex() {
+    const char* e = std::getenv("MCRT_BDPT_LIGHT_IN_VERTEX");
+    return e ? (std::atoi(e) != 0) : 1;
+}
 static int walk_lanes() {
     const char* e = std::getenv("MCRT_WALK_LANES");
     return e ? std::min(64, std::max(0, std::atoi(e))) : 8;
@@ -1653,6 +1659,12 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         b.keyLo[a] = s->bbLo[a];
         b.keyScale[a] = ext > 0.0f ? (a == 1 ? 8.0f : 32.0f) / ext : 0.0f;
     }
+    b.cams = dCam;
+    b.connCount = fb->bdptCounters + BDPT_CNT_CONN;
+    b.connO = fb->cO;
+    b.connD = fb->cD;
+    b.connL = fb->cL;
+    b.lightInVertex = bdpt_light_in_vertex();
     BdptArgs bk = b;   // the vertex launches whose output queue is traced
     bk.extKey = bs.ekey;
     bk.extSlot = bs.eslot;

@@ -88,6 +88,12 @@ struct BdptArgs {
     int* splatListCount;
     int splatListCap;
     int splatW, splatN0, splatBpb, splatBands, splatBand;
+    // the light-tracing strategies (t = 1) evaluated by the vertex launch that creates their light
+    // vertex (lightInVertex), appending to the connection queue: the batch's cameras and that queue
+    const mcrt_camera* cams;
+    int* connCount;
+    float4 *connO, *connD, *connL;
+    int lightInVertex;
 };
 struct BdptQueue {
     int* count;
