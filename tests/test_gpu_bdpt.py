@@ -180,6 +180,36 @@ def test_bdpt_frames_in_flight(hip_ctx):
             assert close.all(), (fif, k, int((~close).sum()))
 
 
+@pytest.mark.parametrize("D", [2, 4])
+def test_light_strategies_in_vertex_launch(hip_ctx, monkeypatch, D):
+    """The light-tracing strategies (t = 1) evaluated by the vertex launches that create their light
+    vertices (the default) against the connection launch that re-reads them
+    (MCRT_BDPT_LIGHT_IN_VERTEX=0), over a batched call: the vertices, counts, own-strategy slots and
+    sampled-light planes bit-exact (t = 1 strategies write none of them); the splat plane and the
+    radiance within the splat tolerance (the placement changes the queue order of the splats' float
+    atomics only)."""
+    from mcrt import lib
+    name, W, H = "mixed", 96, 64
+    ds = lib.DeviceScene(hip_ctx, build_scene(name))
+    cams = [scene_camera(name, W, H, frame=f, jitter=True) for f in range(4)]
+    out = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("MCRT_BDPT_LIGHT_IN_VERTEX", on)
+        fb = lib.FrameBuffer(hip_ctx, W, H)
+        fb.render_frames(ds, cams, frame=0, max_depth=D, integrator=T.INTEGRATOR_BDPT)
+        out[on] = {"rad": fb.read(0), **{k: fb.read_bdpt(k) for k in lib.FrameBuffer.BDPT_READ}}
+        fb.close()
+    ds.close()
+    a, b = out["1"], out["0"]
+    for k in ("camera_vertices", "light_vertices", "camera_counts", "light_counts", "slots", "sampled_light"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    sa, sb = a["splat"].view(np.float32), b["splat"].view(np.float32)
+    assert (sb != 0).mean() > 0.01   # light-tracing splats landed
+    for x, y, k in ((sa, sb, "splat"), (a["rad"][..., :3], b["rad"][..., :3], "rad")):
+        close = np.abs(x - y) <= REL_TOL * (np.abs(x) + np.abs(y)) + 1e-30
+        assert close.all(), (k, int((~close).sum()))
+
+
 @pytest.mark.parametrize("ranks", [2, 3])
 def test_bdpt_band_split_matches_whole_frames(hip_ctx, ranks):
     """Band-split BDPT (multi-GPU, emulated on one GPU with one framebuffer per rank): rank r
