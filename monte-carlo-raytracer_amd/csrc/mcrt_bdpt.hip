@@ -735,7 +735,10 @@ MCRT_DEV void pushConn(const BdptQueue& q, int slot, f3 o, float tmax, f3 d, int
 //   * the stale sampled-light slot (BDPT.cl:585-586): strategy (t, 1) alone reads and rewrites
 //     slot t - 2, so its frame-to-frame read-before-write order is kept.
 // Strategies are split into four classes, one launch each, so every kernel carries only its own
-// registers: EMIT (s = 0), LIGHT (t = 1, light tracing), NEE (s = 1), GENERAL (t, s >= 2).  A wave
+// registers: EMIT (s = 0), LIGHT (t = 1, light tracing), NEE (s = 1), GENERAL (t, s >= 2).  LIGHT
+// runs in k_bdpt_vertex by default, from the registers that store its light vertex (lpre;
+// BdptArgs::lightInVertex, profiles/r06/ab/bdpt_connect/README.txt); moving (2, 2) into the depth-1
+// light launch as well measured slower there (its own instantiation at 150 VGPRs).  A wave
 // holds one strategy of one 8x8 tile for all the call's frames (wave-uniform branches); the waves
 // of a tile are adjacent, so its vertex planes are re-read from L2.  Own strategies (t >= 2) write
 // their slot (zero when absent, not connectible or contributing nothing); strategies with a
