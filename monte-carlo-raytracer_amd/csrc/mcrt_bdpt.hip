@@ -305,7 +305,7 @@ MCRT_DEV float evaluateMaterialPdfV(const BVertex& v, int pix, int N, f3 wo, f3 
 }
 // hasMaterialNonDeltaComponents (materials.cl:163-183)
 MCRT_DEV bool hasMaterialNonDeltaComponents(const SceneArgs& s, int materialIdx, const Frame& si) {
-    const mcrt_material mat = s.materials[materialIdx];
+    const mcrt_material mat = tableEntry(s.materials, materialIdx);
     if (mat.type != 0) return false;
     const f3 Kd = mat.uber_diffuseTexId != -1 ? readTex(s, mat.uber_diffuseTexId, si.uv).xyz : ld3(mat.uber_kd);
     const f3 Ks = mat.uber_glossyTexId != -1 ? readTex(s, mat.uber_glossyTexId, si.uv).xyz : ld3(mat.uber_ks);
@@ -606,17 +606,18 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
         float4* V = isCamera ? b.camV : b.lightV;
         const float4 hit = hits[i];
         const int shapeIdx = __float_as_int(hit.z), primIdx = __float_as_int(hit.w);
-        const mcrt_shape* shape = shapeIdx >= 0 ? &s.shapes[shapeIdx] : nullptr;
-        if (shape && shape->materialId != -1) {
+        mcrt_shape shp;
+        if (shapeIdx >= 0) shp = tableEntry(s.shapes, shapeIdx);
+        if (shapeIdx >= 0 && shp.materialId != -1) {
             (isCamera ? b.camCount : b.lightCount)[pix] = depth + 1;
             const f3 rayD = ld3(Dd);
             BVertex cur;
-            cur.fr = computeSurfaceInteraction(s, shapeIdx, primIdx, f2{hit.x, hit.y});
+            cur.fr = computeSurfaceInteraction(s, shp, shapeIdx, primIdx, f2{hit.x, hit.y});
             cur.wo = -rayD;
             const bool isBackfacing = cl_dot(cur.fr.gn, cur.wo) < 0.0f;
             cur.traceErrorOffset = isBackfacing ? -RT_TRACE_OFFSET_F : RT_TRACE_OFFSET_F;
-            const int materialIdx = shape->materialId;
-            const mcrt_material mat = s.materials[materialIdx];
+            const int materialIdx = shp.materialId;
+            const mcrt_material mat = tableEntry(s.materials, materialIdx);
             if (mat.uber_normalMapId != -1) applyNormalMapping(s, mat.uber_normalMapId, cur.fr);
             Uber um;
             if (mat.type == 0) {
@@ -640,7 +641,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
             cur.pdfRev = 0.0f;
             cur.pdfPos = 0.0f;
             cur.pdfFwd = convertVertexDensity(pdfFwd, prev.p, posOf(cur));
-            cur.lightIdx = shape->lightID;
+            cur.lightIdx = shp.lightID;
             // infinite-light correction of the first light-subpath vertex (BDPT.cl:383-393)
             if (!isCamera && depth == 1 && isInfinite(prev.flags)) {
                 const float prevPdfPos = vplane(V, 0, 3, N)[pix].w;

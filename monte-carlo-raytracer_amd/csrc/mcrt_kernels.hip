@@ -494,9 +494,9 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
     f3 add = splat3(0.0f);
     const int shapeIdx = __float_as_int(hit.z), primIdx = __float_as_int(hit.w);
     if (shapeIdx < 0 || s.numLights <= 0) return add;
-    const mcrt_shape& shape = s.shapes[shapeIdx];
+    const mcrt_shape shape = tableEntry(s.shapes, shapeIdx);
     f3 dpdu, dpdv;
-    Frame si = computeSurfaceInteraction(s, shapeIdx, primIdx, f2{hit.x, hit.y}, LOD ? &dpdu : nullptr,
+    Frame si = computeSurfaceInteraction(s, shape, shapeIdx, primIdx, f2{hit.x, hit.y}, LOD ? &dpdu : nullptr,
                                          LOD ? &dpdv : nullptr);
     TexLod lod{{0.0f, 0.0f}, {0.0f, 0.0f}, false};
     if (LOD) lod = surfaceUVDifferentials(si, dpdu, dpdv, ro, dxDir, dyDir);
@@ -506,7 +506,7 @@ MCRT_DEV f3 shadePath(const SceneArgs& s, const FrameArgs& f, int bounce, int pi
     const int materialId = shape.materialId;
     mcrt_material mat;
     if (materialId != -1) {
-        mat = s.materials[materialId];
+        mat = tableEntry(s.materials, materialId);
         if (mat.uber_normalMapId != -1) applyNormalMapping(s, mat.uber_normalMapId, si, lod);
     }
     if (bounce == 0) throughput = splat3(1.0f);

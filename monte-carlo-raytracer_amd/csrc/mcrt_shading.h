@@ -41,6 +41,26 @@ MCRT_DEV f3 cameraDir(const mcrt_camera& cam, int x, int y) {   // PathTracing.c
     return lerpDirection(ld3(cam.r00), ld3(cam.r10), ld3(cam.r11), ld3(cam.r01), uv.x, uv.y);
 }
 
+// Entry idx of a small scene table (shapes, materials, texture descriptors).  When the active lanes
+// of the wave share idx -- the camera hits of a packed wave, neighbouring pixels on one surface --
+// the entry is read with scalar loads through the constant address space (one fetch per wave, off
+// the vector-memory pipeline the shading launches are bound by); otherwise per lane.
+template <typename T>
+MCRT_DEV T tableEntry(const T* tab, int idx) {
+    static_assert(sizeof(T) % 4 == 0, "table entries are whole dwords");
+    const int u = __builtin_amdgcn_readfirstlane(idx);
+    if (__ballot(idx != u) == 0) {
+        typedef __attribute__((address_space(4))) const uint32_t ConstWord;
+        ConstWord* p = (ConstWord*)(tab + u);
+        T r;
+        uint32_t* d = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+        for (int w = 0; w < (int)(sizeof(T) / 4); ++w) d[w] = p[w];
+        return r;
+    }
+    return tab[idx];
+}
+
 
 // ---------------------------------------------------------------------------
 // shading
@@ -87,7 +107,7 @@ MCRT_DEV f4 readTexDesc(const SceneArgs& s, const mcrt_texture_desc& tex, f2 uv)
                     fmaf(m1.w - m0.w, t.y, m0.w)};
     return m * (1.0f / 255.0f);
 }
-MCRT_DEV f4 readTex(const SceneArgs& s, int texId, f2 uv) { return readTexDesc(s, s.textures[texId], uv); }
+MCRT_DEV f4 readTex(const SceneArgs& s, int texId, f2 uv) { return readTexDesc(s, tableEntry(s.textures, texId), uv); }
 
 // ---------------------------------------------------------------------------
 // Mip-mapped texture reads at camera-ray hits (opt-in, mcrt_frame_params.texture_lod).  The
@@ -151,7 +171,7 @@ MCRT_DEV f4 readTexLodDesc(const SceneArgs& s, const mcrt_texture_desc& tex, f2 
 // readTexture2Df with the LOD path switched on (textures.cl:204-209 with line 207 active)
 MCRT_DEV f4 readTexL(const SceneArgs& s, int texId, f2 uv, const TexLod& L) {
     if (!L.on) return readTex(s, texId, uv);
-    const mcrt_texture_desc tex = s.textures[texId];
+    const mcrt_texture_desc tex = tableEntry(s.textures, texId);
     return readTexLodDesc(s, tex, uv, mipLod(tex, L.duvdx, L.duvdy));
 }
 
@@ -328,12 +348,11 @@ MCRT_DEV f3 sampleTriangle(f3 p0, f3 p1, f3 p2, f2 u, f3* gn) {
 }
 
 // computeSurfaceInteraction (geometry.cl:177-215)
-MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, int shapeIdx, int primIdx, f2 barycentrics,
-                                         f3* dpduOut = nullptr, f3* dpdvOut = nullptr) {
+MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, const mcrt_shape& shape, int shapeIdx, int primIdx,
+                                         f2 barycentrics, f3* dpduOut = nullptr, f3* dpdvOut = nullptr) {
     Frame si;
-    const mcrt_shape& shape = s.shapes[shapeIdx];
     // the triangle's surface record (SceneArgs::surf): the same floats the index path gathers
-    const float4* R = s.surf + 8 * ((size_t)s.surfBase[shapeIdx] + (uint32_t)primIdx);
+    const float4* R = s.surf + 8 * ((size_t)tableEntry(s.surfBase, shapeIdx) + (uint32_t)primIdx);
     const float4 r0 = R[0], r1 = R[1], r2 = R[2], r3 = R[3], r4 = R[4], r5 = R[5];
     const f3 p0 = transformPoint3(shape.toWorldTransform, mk3(r0.x, r0.y, r0.z));
     const f3 p1 = transformPoint3(shape.toWorldTransform, mk3(r0.w, r1.x, r1.y));
@@ -353,6 +372,10 @@ MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, int shapeIdx, int p
     if (dpduOut) *dpduOut = dpdu;
     if (dpdvOut) *dpdvOut = dpdv;
     return si;
+}
+MCRT_DEV Frame computeSurfaceInteraction(const SceneArgs& s, int shapeIdx, int primIdx, f2 barycentrics,
+                                         f3* dpduOut = nullptr, f3* dpdvOut = nullptr) {
+    return computeSurfaceInteraction(s, tableEntry(s.shapes, shapeIdx), shapeIdx, primIdx, barycentrics, dpduOut, dpdvOut);
 }
 
 // The pixel's uv footprint at a camera-ray hit (computeSurfaceInteractionWithDifferentials,
