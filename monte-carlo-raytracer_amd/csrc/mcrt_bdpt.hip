@@ -303,17 +303,6 @@ MCRT_DEV float evaluateMaterialPdfV(const BVertex& v, int pix, int N, f3 wo, f3 
     if (type != 0) return 0.0f;
     return evaluateUberBSDF_Pdf(um, v.fr, wo, wi);
 }
-// hasMaterialNonDeltaComponents (materials.cl:163-183)
-MCRT_DEV bool hasMaterialNonDeltaComponents(const SceneArgs& s, int materialIdx, const Frame& si) {
-    const mcrt_material mat = tableEntry(s.materials, materialIdx);
-    if (mat.type != 0) return false;
-    const f3 Kd = mat.uber_diffuseTexId != -1 ? readTex(s, mat.uber_diffuseTexId, si.uv).xyz : ld3(mat.uber_kd);
-    const f3 Ks = mat.uber_glossyTexId != -1 ? readTex(s, mat.uber_glossyTexId, si.uv).xyz : ld3(mat.uber_ks);
-    const f3 op = mat.uber_opacityTexId != -1 ? readTex(s, mat.uber_opacityTexId, si.uv).xyz : ld3(mat.uber_opacity);
-    const f3 kd = Kd * op, ks = Ks * op;
-    return !isBlack(kd) || !isBlack(ks);
-}
-
 // computeShadingNormalCorrection (BDPT.cl:23-36).  The reference's compiled kernels evaluate
 // this division correctly rounded (its accuracy metadata is dropped when the select of the
 // three return values is folded), in GenerateSecondaryVertices and PrepareConnections alike.
@@ -620,8 +609,9 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
             const mcrt_material mat = tableEntry(s.materials, materialIdx);
             if (mat.uber_normalMapId != -1) applyNormalMapping(s, mat.uber_normalMapId, cur.fr);
             Uber um;
+            bool nonDelta = false;   // hasMaterialNonDeltaComponents, from uberProps' texture reads
             if (mat.type == 0) {
-                um = uberProps(s, mat, cur.fr.uv);
+                um = uberProps(s, mat, cur.fr.uv, TexLod{{0, 0}, {0, 0}, false}, &nonDelta);
             } else {
                 um.Kd = um.Ks = um.Kr = um.opacity = splat3(0.0f);
                 um.Kt = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -650,7 +640,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                 storePdfFwd(V, 0, pix, N, 0.0f);
             }
             if (FINAL || depth == D + (isCamera ? 1 : 0)) {   // subpath complete (BDPT.cl:395-403)
-                if (hasMaterialNonDeltaComponents(s, materialIdx, cur.fr)) cur.flags |= VF_CONNECTIBLE;
+                if (nonDelta) cur.flags |= VF_CONNECTIBLE;
                 storeVertex(V, depth, pix, N, cur);
             } else {
                 Sampler sampler = makeSampler(f.sampler, (uint32_t)px, f.frame + kf, depth + (D + 1) * (isCamera ? 1 : 0),

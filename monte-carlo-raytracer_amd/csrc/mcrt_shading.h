@@ -193,18 +193,29 @@ MCRT_DEV void cameraDiffDirs(const mcrt_camera& cam, int x, int y, f3& dx, f3& d
 }
 
 // KRN/materials.cl:76-91 (getUberMaterialProperties)
-MCRT_DEV Uber uberProps(const SceneArgs& s, const mcrt_material& material, f2 uv, const TexLod& L = TexLod{{0, 0}, {0, 0}, false}) {
+// nonDelta (BDPT): hasMaterialNonDeltaComponents (materials.cl:163-183) of the same material at the
+// same uv, from these texture reads instead of a second set
+MCRT_DEV Uber uberProps(const SceneArgs& s, const mcrt_material& material, f2 uv, const TexLod& L = TexLod{{0, 0}, {0, 0}, false},
+                        bool* nonDelta = nullptr) {
     Uber u;
     const f4 Kd_opacity = material.uber_diffuseTexId != -1 ? readTexL(s, material.uber_diffuseTexId, uv, L) : f4{1.0f, 1.0f, 1.0f, 1.0f};
     u.Kd = Kd_opacity.xyz * ld3(material.uber_kd);
-    u.Ks = (material.uber_glossyTexId != -1 ? readTexL(s, material.uber_glossyTexId, uv, L).xyz : splat3(1.0f)) * ld3(material.uber_ks);
+    const f3 glossy = material.uber_glossyTexId != -1 ? readTexL(s, material.uber_glossyTexId, uv, L).xyz : splat3(1.0f);
+    u.Ks = glossy * ld3(material.uber_ks);
     u.Kr = (material.uber_specReflectionTexId != -1 ? readTexL(s, material.uber_specReflectionTexId, uv, L).xyz : splat3(1.0f)) *
            ld3(material.uber_kr);
     u.Kt.xyz = (material.uber_transmissionTexId != -1 ? readTexL(s, material.uber_transmissionTexId, uv, L).xyz : splat3(1.0f)) *
                ld3(material.uber_kt);
     u.Kt.w = material.uber_kt.w;
-    u.opacity = (material.uber_opacityTexId != -1 ? readTexL(s, material.uber_opacityTexId, uv, L).xyz : splat3(1.0f)) *
-                ld3(material.uber_opacity) * Kd_opacity.w;
+    const f3 opTex = material.uber_opacityTexId != -1 ? readTexL(s, material.uber_opacityTexId, uv, L).xyz : splat3(1.0f);
+    u.opacity = opTex * ld3(material.uber_opacity) * Kd_opacity.w;
+    if (nonDelta) {
+        const f3 Kd = material.uber_diffuseTexId != -1 ? Kd_opacity.xyz : ld3(material.uber_kd);
+        const f3 Ks = material.uber_glossyTexId != -1 ? glossy : ld3(material.uber_ks);
+        const f3 op = material.uber_opacityTexId != -1 ? opTex : ld3(material.uber_opacity);
+        const f3 kd = Kd * op, ks = Ks * op;
+        *nonDelta = !isBlack(kd) || !isBlack(ks);
+    }
     u.roughness = material.uber_roughnessTexId != -1 ? readTexL(s, material.uber_roughnessTexId, uv, L).xy
                                                       : f2{material.uber_roughness.x, material.uber_roughness.y};
     u.eta = material.uber_iorTexId != -1 ? readTexL(s, material.uber_iorTexId, uv, L).x : material.uber_eta;
