@@ -199,9 +199,10 @@ SCALE_CASES = {
     ],
 }
 BDPT_VERTEX_STRIDE = 17   # vertex records kept for every 17th pixel (the full arrays are ~0.5 GB at 960x540)
-# cases whose FULL vertex arrays are also written (raw .npy beside the job's npz, ~3.5 GB at 1080p), so
-# every pixel's vertices are compared: config 4's integrator at the bench's size
-FULL_VERTEX_CASES = ("sm_bdpt_1080p",)
+# cases whose FULL vertex arrays are also written (raw .npy beside the job's npz, ~3.5 GB at 1080p D = 2,
+# ~1.6 GB at 960x540 D = 5), so every pixel's vertices are compared: config 4's integrator at the bench's
+# size and the depth-5 case
+FULL_VERTEX_CASES = ("sm_bdpt_1080p", "sm_bdpt_540p_d5")
 
 
 def full_vertex_path(out_path, key, which):

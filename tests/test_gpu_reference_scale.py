@@ -14,9 +14,9 @@
   * config 3: Sponza proxy (16 x 1024^2 mip-mapped textures) 1920x1080, PT -- bit-exact;
   * config 4: San-Miguel proxy BDPT at 1920x1080 (the bench's BDPT object), frames 0 and 1 in sequence from fresh buffers
     (BDPT.cl) -- vertex counts bit-exact, every defined field of the vertices of EVERY pixel
-    bit-exact (the job writes the reference's full vertex arrays beside its npz; the 960x540
-    depth-5 case compares every 17th pixel plus three full rows and a 64 x 64 block,
-    clref_job.bdpt_vertex_sel), radiance within 4e-6 relative (splat atomics, tests/test_gpu_bdpt.py) and
+    bit-exact (the job writes the reference's full vertex arrays beside its npz, for the 960x540
+    depth-5 case too; other BDPT cases compare every 17th pixel plus three full rows and a 64 x 64
+    block, clref_job.bdpt_vertex_sel), radiance within 4e-6 relative (splat atomics, tests/test_gpu_bdpt.py) and
     bit-exact where no light-tracing splat landed;
   * SURVEY §8(d)'s depth-5 sensitivity run on the headline scene: PT at 1920x1080 (frames 0 and 1
     bit-exact) and BDPT at 960x540 (as config 4 above), maxDepth 5;
@@ -116,7 +116,8 @@ def test_full_size_config_matches_reference(hip_ctx, clref_scale, variant, case)
                 bad.append(f"{nm} counts differ at {int((a != b).sum())} pixels")
         for which, depths, counts in (("camera_vertices", D + 2, cc), ("light_vertices", D + 1, lc)):
             full = full_vertex_path(_JOB_PATHS.get(variant, ""), key, which)
-            if key in FULL_VERTEX_CASES and os.path.exists(full):   # every pixel's vertices
+            if key in FULL_VERTEX_CASES:   # every pixel's vertices (the job wrote the full arrays)
+                assert os.path.exists(full), f"{key}: the reference job wrote no full {which} array"
                 theirs = np.load(full, mmap_mode="r").view(po.REF_VERTEX_DTYPE).reshape(N, depths)
                 bad += compare_vertices(our_planes(fb.read_bdpt(which), depths, N), theirs, counts, depths, N, which)
                 continue
