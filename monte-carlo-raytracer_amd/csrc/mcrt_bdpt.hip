@@ -618,7 +618,10 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                 um.roughness = f2{0.0f, 0.0f};
                 um.eta = 0.0f;
             }
-            storeUber(V, depth, pix, N, um, mat.type);
+            // the material planes are read only by connection strategies that fetch this vertex: none
+            // fetches a camera vertex of depth D + 1, nor -- with the light-tracing strategies evaluated
+            // here -- a light vertex of depth D (a (t >= 2, s = D + 1) strategy would exceed the depth)
+            if (!FINAL && !(b.lightInVertex && !isCamera && depth == D)) storeUber(V, depth, pix, N, um, mat.type);
             const int mode = isCamera ? TRANSPORT_MODE_RADIANCE : TRANSPORT_MODE_IMPORTANCE;
             const BVertexPos prev = loadVertexPos(V, depth - 1, pix, N);
             float pdfFwd = Dd.w;

@@ -184,7 +184,7 @@ def test_bdpt_frames_in_flight(hip_ctx):
 def test_light_strategies_in_vertex_launch(hip_ctx, monkeypatch, D):
     """The light-tracing strategies (t = 1) evaluated by the vertex launches that create their light
     vertices (the default) against the connection launch that re-reads them
-    (MCRT_BDPT_LIGHT_IN_VERTEX=0), over a batched call: the vertices, counts, own-strategy slots and
+    (MCRT_BDPT_LIGHT_IN_VERTEX=0), over a batched call: the vertex fields, counts, own-strategy slots and
     sampled-light planes bit-exact (t = 1 strategies write none of them); the splat plane and the
     radiance within the splat tolerance (the placement changes the queue order of the splats' float
     atomics only)."""
@@ -201,7 +201,12 @@ def test_light_strategies_in_vertex_launch(hip_ctx, monkeypatch, D):
         fb.close()
     ds.close()
     a, b = out["1"], out["0"]
-    for k in ("camera_vertices", "light_vertices", "camera_counts", "light_counts", "slots", "sampled_light"):
+    N = W * H * len(cams)
+    for k, depths in (("camera_vertices", D + 2), ("light_vertices", D + 1)):
+        # the vertex fields (planes 0-7); the material planes of a light vertex of depth D are read only
+        # by the connection launch's light-tracing class, so the default placement leaves them unwritten
+        np.testing.assert_array_equal(our_planes(a[k], depths, N)[:, :8], our_planes(b[k], depths, N)[:, :8], err_msg=k)
+    for k in ("camera_counts", "light_counts", "slots", "sampled_light"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     sa, sb = a["splat"].view(np.float32), b["splat"].view(np.float32)
     assert (sb != 0).mean() > 0.01   # light-tracing splats landed
