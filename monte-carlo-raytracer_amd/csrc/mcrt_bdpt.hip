@@ -560,10 +560,17 @@ struct LightPre {   // a light vertex in registers (with its material properties
     BVertex lv;
     BVertexPos qsPrev;
 };
+struct ConnOut {   // a strategy's connection ray, appended by the caller (the vertex launch: per workgroup)
+    bool push;
+    f3 o, d, L;
+    float t;
+    int code;
+};
 template <int CLS>
 MCRT_DEV void connectOne(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* camp,
                          const BdptQueue& qOut, int t, int sI, int k, int x, int y, bool valid,
-                         WaveStage* ws = nullptr, const LightPre* lpre = nullptr);
+                         WaveStage* ws = nullptr, const LightPre* lpre = nullptr, ConnOut* cout = nullptr);
+MCRT_DEV void pushConn(const BdptQueue& q, int slot, f3 o, float tmax, f3 d, int code, f3 c);
 enum { CONN_EMIT = 0, CONN_LIGHT = 1, CONN_NEE = 2, CONN_GENERAL = 3 };
 
 // FINAL: the launch of depth D + 1, whose queue holds camera rays only and whose vertices all end
@@ -585,6 +592,8 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
     f3 no = splat3(0.0f), nd = splat3(0.0f), ntp = splat3(0.0f);
     float nPdf = 0.0f;
     int tag = 0;
+    ConnOut lightRay;   // this light vertex's t = 1 connection ray (appended after the bounce ray)
+    lightRay.push = false;
     const float4 O = i < n ? qIn.o[i] : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
     tag = __float_as_int(O.w);
     if (tag >= 0) {   // tag -1: a start-queue slot outside the image
@@ -694,7 +703,7 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
                 lp.qsPrev = prev;
                 const BdptQueue cq{b.connCount, b.connO, b.connD, b.connL};
                 connectOne<CONN_LIGHT>(s, f, b, b.cams, cq, 1, depth + 1, kf, px % (int)f.W, px / (int)f.W, true,
-                                       nullptr, &lp);
+                                       nullptr, &lp, &lightRay);
             }
         }
     }
@@ -709,6 +718,14 @@ __global__ __launch_bounds__(BDPT_BLOCK) void k_bdpt_vertex(SceneArgs s, FrameAr
             b.extKey[slot] = bounceKey(b, no, nd);
             b.extSlot[slot] = (uint32_t)slot;
         }
+    }
+    // the light-tracing connection rays: one append per workgroup (a per-wave append on the queue's
+    // one counter serialises across the XCDs)
+    if (b.lightInVertex) {
+        const int cs = blockAppend<BDPT_BLOCK / 64>(b.connCount, lightRay.push, ldsWave);
+        if (lightRay.push)
+            pushConn(BdptQueue{b.connCount, b.connO, b.connD, b.connL}, cs, lightRay.o, lightRay.t, lightRay.d,
+                     lightRay.code, lightRay.L);
     }
 }
 
@@ -794,7 +811,7 @@ MCRT_DEV void flushStage(WaveStage& ws, const BdptQueue& q) {
 template <int CLS>
 MCRT_DEV void connectOne(const SceneArgs& s, const FrameArgs& f, const BdptArgs& b, const mcrt_camera* camp,
                          const BdptQueue& qOut, int t, int sI, int k, int x, int y, bool valid,
-                         WaveStage* ws, const LightPre* lpre) {
+                         WaveStage* ws, const LightPre* lpre, ConnOut* cout) {
     const int N0 = (int)(f.W * f.H);
     const int N = N0 * f.batch;   // plane stride
     const int D = f.maxDepth;
@@ -1008,6 +1025,15 @@ MCRT_DEV void connectOne(const SceneArgs& s, const FrameArgs& f, const BdptArgs&
         L = c;
     } else if (valid && CLS != CONN_LIGHT) {
         b.slots[(size_t)ownSlotOf(t, sI, D) * N + pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // strategy absent
+    }
+    if (cout) {   // the caller appends
+        cout->push = push;
+        cout->o = rayO;
+        cout->d = rayD;
+        cout->L = L;
+        cout->t = rayT;
+        cout->code = code;
+        return;
     }
     if (CLS != CONN_EMIT) {   // emission needs no connection ray (class-uniform: the whole wave)
         const uint64_t m = __ballot(push);
