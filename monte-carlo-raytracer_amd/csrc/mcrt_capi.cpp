@@ -1673,8 +1673,11 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
     // rank of a band split would otherwise sort 8 x its own rays at N = 8
     const int bandQ = f.numTiles * 64 * B;   // this rank's paths: a start queue holds at most one ray each
     const int nSort = (int)std::min((size_t)2 * N, (size_t)2 * (size_t)bandQ);
-    auto clearKeys = [&]() {   // unwritten slots sort last (stable sort: after the written ones)
-        return hipMemsetAsync(bs.ekey, 0xFF, 4 * (size_t)nSort, st);
+    // the queue traced at round D + 1 holds camera rays only (the light subpaths end at depth D): at
+    // most one per path, so it is sorted (and its keys cleared) over bandQ slots, not 2 x bandQ
+    auto sortRange = [&](int tracedAt) { return tracedAt == D + 1 ? std::min(nSort, bandQ) : nSort; };
+    auto clearKeys = [&](int n) {   // unwritten slots sort last (stable sort: after the written ones)
+        return hipMemsetAsync(bs.ekey, 0xFF, 4 * (size_t)n, st);
     };
     b.depth0Const = bs.constStride == N && bs.constBand[0] == f.bandRows && bs.constBand[1] == f.numBands &&
                     bs.constBand[2] == f.bandIndex ? 1 : 0;
@@ -1743,7 +1746,7 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
                                  fb->bHits + NQ, bandQ, bandQ, st, bs.lperm);   // grids sized to the band
         if (wcap > 0) mcrt::launch_walk_resume(tl, lightQ.o, lightQ.d, fb->bHits + NQ, bandQ, st);
     }
-    HIPCHK(ctx, clearKeys());   // queue 1 is traced (D >= 1)
+    HIPCHK(ctx, clearKeys(sortRange(2)));   // queue 1 is traced (D >= 1), at round 2
     {
         Timed t(ctx, K_BDPT_VERTEX, camQ.count, 0, st);
         mcrt::launch_bdpt_vertex(sa, f, bk, 1, camQ, fb->bHits, queue(1), bandQ, st);
@@ -1756,15 +1759,16 @@ static mcrt_status render_bdpt(mcrt_scene s, mcrt_framebuffer fb, const mcrt_cam
         const BdptQueue qIn = queue(d - 1), qOut = queue(d);
         {
             Timed t(ctx, K_EXTEND, qIn.count, 0, st);
-            HIPCHK(ctx, mcrt::bdpt_light_sort(bs.ekey, bs.ekey2, bs.eslot, bs.eperm, nSort, bs.sortTmp,
+            const int nQ = sortRange(d);
+            HIPCHK(ctx, mcrt::bdpt_light_sort(bs.ekey, bs.ekey2, bs.eslot, bs.eperm, nQ, bs.sortTmp,
                                               bs.sortTmpBytes, st, 16));
             TraceCtx te = tce;
             te.suspendCount = wcap > 0 ? bs.suspendCnt + d : nullptr;
-            mcrt::launch_extend(te, qIn.count, qIn.o, qIn.d, fb->bHits, nSort, st, bs.eperm);
-            if (wcap > 0) mcrt::launch_walk_resume(te, qIn.o, qIn.d, fb->bHits, nSort, st);
+            mcrt::launch_extend(te, qIn.count, qIn.o, qIn.d, fb->bHits, nQ, st, bs.eperm);
+            if (wcap > 0) mcrt::launch_walk_resume(te, qIn.o, qIn.d, fb->bHits, nQ, st);
         }
         const bool traced = d <= D;   // queue d is traced by the next round
-        if (traced) HIPCHK(ctx, clearKeys());
+        if (traced) HIPCHK(ctx, clearKeys(sortRange(d + 1)));
         Timed t(ctx, K_BDPT_VERTEX, qIn.count, 0, st);
         mcrt::launch_bdpt_vertex(sa, f, traced ? bk : b, d, qIn, fb->bHits, qOut, nSort, st);
     }
