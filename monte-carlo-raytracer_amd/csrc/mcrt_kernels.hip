@@ -1213,7 +1213,13 @@ void launch_shadow_extend(const TraceCtx& c, const int* extCount, const float4* 
 }
 void launch_walk_resume(const TraceCtx& c, const float4* qO, const float4* qD, float4* hits, int maxExt,
                         hipStream_t st) {
-    hipLaunchKernelGGL(k_walk_resume, dim3(maxExt > 0 ? (maxExt + 63) / 64 : 1), dim3(64), 0, st, c, qO, qD, hits);
+    // a stopping wave suspends at most walkLanes of its lanes, so the list holds at most walkLanes per
+    // 64 queue slots: the grid covers that bound, not the queue's capacity (workgroups past the
+    // device-side count exit at once, but each still costs a dispatch: ~0.2 ns, tools/probe/empty_blocks.hip)
+    const int64_t waves = (maxExt + 63) / 64;
+    const int64_t bound = (waves * std::max(1, std::min(64, c.walkLanes)) + 63) / 64;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(waves, bound));
+    hipLaunchKernelGGL(k_walk_resume, dim3(blocks), dim3(64), 0, st, c, qO, qD, hits);
 }
 void launch_shade0(const SceneArgs& s, const FrameArgs& f, const mcrt_camera* cam, const float4* hits,
                    float4* radiance, const QueueArgs& q, hipStream_t st) {
