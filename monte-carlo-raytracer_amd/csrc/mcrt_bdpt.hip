@@ -8,9 +8,11 @@
 //   for d in 1..D+1:
 //     k_extend            closest hit over the queue (camera and light rays together)
 //     k_bdpt_vertex       GenerateSecondaryVertices (BDPT.cl:317-458) for every queued ray: the
-//                         surface vertex at depth d and, unless the subpath is done, its next ray
+//                         surface vertex at depth d and, unless the subpath is done, its next ray;
+//                         for a light vertex also its light-tracing strategy (t = 1, below) from the
+//                         registers that store it (BdptArgs::lightInVertex)
 //   k_bdpt_connect        PrepareConnections (BDPT.cl:460-646) fused with the visibility-independent
-//                         part of ConnectVertices (BDPT.cl:671-913): every (t, s) strategy's
+//                         part of ConnectVertices (BDPT.cl:671-913): every other (t, s) strategy's
 //                         unweighted contribution AND its MIS weight, so only strategies with a
 //                         non-zero weighted contribution emit a connection ray (compacted queue)
 //   k_bdpt_vis            any hit over the connection queue: an occluded own strategy is zeroed
@@ -23,7 +25,9 @@
 //     0 p.xyz|traceErrorOffset  1 gn.xyz|pdfFwd  2 sn.xyz|pdfRev  3 wo.xyz|pdfPos
 //     4 sdpdu.xyz|uv.x  5 sdpdv.xyz|uv.y  6 throughput.xyz|-  7 int4(type, flags, lightIdx, materialIdx)
 //     8-12 the vertex's uber-material properties (getUberMaterialProperties at its uv, computed
-//     once by k_bdpt_vertex): Kd|eta, Ks|Kt.w, Kr|alpha.x, Kt.xyz|alpha.y, opacity|material type.
+//     once by k_bdpt_vertex): Kd|eta, Ks|Kt.w, Kr|alpha.x, Kt.xyz|alpha.y, opacity|material type --
+//     written only where a connection strategy fetches them (not for camera depth D + 1, nor for
+//     light depth D while the light-tracing strategies run in the vertex launch).
 //   (the reference's 240-B RTBDPTVertex holds the first 8 planes' fields plus unused
 //   differentials, and re-reads up to 8 textures per material evaluation instead of plane 8-12).
 //   vertex counts: int x N per subpath.  sampled light vertex of the s = 1 strategy, persistent across
